@@ -1,0 +1,166 @@
+"""Benchmark: Z^2_2 photon x trial evaluations per second (BASELINE.json metric, config 3).
+
+One step = one complete Z^2_2 search of the config-3 workload per GPU: 1e7 synthetic pulsed
+photons (T = 1e6 s, p = 0.1, f0 = 7.123456789 Hz, seed 0) against 1e6 trial frequencies
+spaced 1/(10T), inputs resident in HBM, followed by the search's one exchange step (every
+rank's best trial gathered so that all ranks agree on the global best, ties -> lowest index).
+With N ranks each rank searches its own 1e6-trial slice of an N*1e6 grid (weak scaling);
+``value`` = all ranks' evaluations / max-over-ranks time.
+
+Also reported: the dominant kernel's roofline (algorithmic FLOP per launch / measured launch
+time: 8 real FLOP per photon x trial x harmonic, the complex multiply-accumulate of the
+factorised search), and the CPU oracle (oracle/liborc.so, OpenMP over trials) on
+a bounded sample of the same workload.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_F32_TFLOPS = 157.3  # MI355X_MICROARCH.md: peak FP32 vector = FP32-input MFMA (spec)
+FLOP_PER_EVAL_HARM = 8.0
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--photons", type=int, default=10_000_000)
+    p.add_argument("--trials", type=int, default=1_000_000, help="trial frequencies per GPU")
+    p.add_argument("--nharm", type=int, default=2)
+    p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    return p.parse_args()
+
+
+def cpu_baseline(t, f0, df, nharm, budget_s):
+    """Oracle (fp64 C restatement of periodsearch.py:57-71, OpenMP over trials) on a bounded sample."""
+    from oracle import oracle as O
+    threads = min(16, os.cpu_count() or 1)
+    O.set_threads(threads)
+    n = min(t.size, 1_000_000)
+    ts = np.ascontiguousarray(t[:n])
+    m = 64
+    while True:
+        f = f0 + (np.arange(m) - m // 2) * df
+        t1 = time.perf_counter()
+        O.search(ts, f, nharm)
+        el = time.perf_counter() - t1
+        if el >= budget_s or m >= 1 << 20:
+            break
+        m = int(m * min(16.0, max(2.0, 1.2 * budget_s / max(el, 1e-3))))
+    rate = n * m / el
+    return {"value": rate, "unit": "photon*trial evals/s", "cores": threads, "kind": "port",
+            "sample": "%d photons x %d trials of the same workload, Z^2_%d, oracle/liborc.so fp64, %.1f s" % (
+                n, m, nharm, el)}
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    from crimp_amd import ops
+    from crimp_amd.synth import pulsed_events
+
+    span, f0 = 1.0e6, 7.123456789
+    t_h = pulsed_events(a.photons, span, f0, pulsed_frac=0.1, seed=0)
+    df = 1.0 / (10.0 * span)
+    M = a.trials
+    g0 = rank * M - (world * M) // 2          # this rank's slice of the N*M grid centred on f0
+    f_h = f0 + (np.arange(M) + g0) * df
+    t = torch.as_tensor(t_h, device=dev)
+    f = torch.as_tensor(f_h, device=dev)
+    out = torch.empty(M, dtype=torch.float64, device=dev)
+    t0 = (t_h[0] + t_h[-1]) / 2
+    best = torch.zeros(2, dtype=torch.float64, device=dev)
+    gathered = torch.zeros(world, 2, dtype=torch.float64, device=dev)
+
+    def step():
+        ops.search(t, t0, f, a.nharm, 0, out=out)
+        i = torch.argmax(out)
+        best[0] = out[i]
+        best[1] = (i + (g0 + (world * M) // 2)).to(torch.float64)  # global trial index
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, best)
+        else:
+            gathered[0] = best
+        return gathered
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    t1 = time.perf_counter()
+    for k in range(a.steps):
+        evs[k][0].record(stream)
+        g = step()
+        evs[k][1].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t1
+    elt = torch.tensor([el], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elt, op=dist.ReduceOp.MAX)
+    el = float(elt.item())
+    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in evs]))
+    gb = g.cpu().numpy()
+    order = np.lexsort((gb[:, 1], -gb[:, 0]))
+    best_idx = int(gb[order[0], 1])
+
+    evals = float(a.photons) * M * world * a.steps
+    value = evals / el
+    if rank == 0:
+        flop = FLOP_PER_EVAL_HARM * a.nharm * float(a.photons) * M
+        achieved = flop / (kern_ms * 1e-3) / 1e12
+        rec = {
+            "metric": "Z^2_2 photon*trial evals/sec (node)",
+            "value": value,
+            "unit": "photon*trial evals/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": el / a.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32 MFMA/sincos, f64 phase+sums",
+            "data": "synthetic (seeded Poisson pulsed events, crimp_amd/synth.py)",
+            "config": {"workload": "config3: synthetic %d photons x %d trials/GPU, Z^2_%d" % (a.photons, M, a.nharm),
+                       "photons": a.photons, "trials_per_gpu": M, "nharm": a.nharm, "span_s": span, "f0": f0,
+                       "trial_step_hz": df, "parallelism": "trial-sharded dp%d + all_gather(best)" % world,
+                       "best_trial_index": best_idx, "best_power": float(gb[order[0], 0]),
+                       "search_path": os.environ.get("CRIMP_SEARCH", "auto")},
+            "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s",
+                         "frac": achieved / PEAK_F32_TFLOPS, "traffic": None,
+                         "kernel_ms": kern_ms,
+                         "note": "8 FLOP per photon*trial*harmonic; time = HIP events around the search call"},
+        }
+        if not a.no_cpu:
+            rec["cpu_baseline"] = cpu_baseline(t_h, f0, df, a.nharm, a.cpu_seconds)
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,151 @@
+"""ctypes binding of libcrimp_hip.so (include/crimp_hip.h).
+
+The shipped path has no CPU fallback: if the library is missing, cannot be
+loaded, or no HIP device is visible, every hot-path call raises
+``CrimpNativeError``. Buffers may be NumPy arrays (host; the library stages them)
+or torch CUDA tensors (device; passed by pointer on torch's current stream).
+"""
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libcrimp_hip.so")
+
+FLAG_DEVICE_PTRS = 1
+FLAG_SYNC = 2
+FLAG_FORCE_DIRECT = 4
+FLAG_FORCE_MFMA = 8
+FLAG_HW_SINCOS = 16
+
+STAT_Z2 = 0
+STAT_H = 1
+
+MODEL_IDS = {"fourier": 0, "cauchy": 1, "vonmises": 2}
+MAX_GLITCH = 32
+MAX_WAVE = 64
+MAX_COMP = 16
+
+
+class CrimpNativeError(RuntimeError):
+    """Raised when the HIP library is unavailable or a native call fails."""
+
+
+class TimingModel(ctypes.Structure):
+    _fields_ = [("pepoch", ctypes.c_double), ("f", ctypes.c_double * 13), ("n_glitch", ctypes.c_int32),
+                ("glitch", (ctypes.c_double * 7) * MAX_GLITCH), ("n_wave", ctypes.c_int32),
+                ("wave_epoch", ctypes.c_double), ("wave_om", ctypes.c_double),
+                ("wave_ab", (ctypes.c_double * 2) * MAX_WAVE)]
+
+
+class Template(ctypes.Structure):
+    _fields_ = [("model", ctypes.c_int32), ("ncomp", ctypes.c_int32), ("amp", ctypes.c_double * MAX_COMP),
+                ("loc", ctypes.c_double * MAX_COMP), ("wid", ctypes.c_double * MAX_COMP),
+                ("i0", ctypes.c_double * MAX_COMP), ("amp_shift", ctypes.c_double)]
+
+
+EXPORTS = ("crimp_version", "crimp_last_error", "crimp_device_count", "crimp_calcphase", "crimp_search",
+           "crimp_toa_points", "crimp_toa_grid", "crimp_binphases")
+
+_lib = None
+_lock = threading.Lock()
+_dev_ok = None
+
+
+def load(require_device=True):
+    """Load the library (and, by default, insist on a visible HIP device)."""
+    global _lib, _dev_ok
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise CrimpNativeError("libcrimp_hip.so not built (%s); run __graft_entry__.build()" % LIB_PATH)
+            try:
+                L = ctypes.CDLL(LIB_PATH)
+            except OSError as e:  # pragma: no cover - environment specific
+                raise CrimpNativeError("cannot load %s: %s" % (LIB_PATH, e))
+            P = ctypes.c_void_p
+            i64, i32, u32 = ctypes.c_int64, ctypes.c_int32, ctypes.c_uint32
+            L.crimp_version.restype = ctypes.c_int
+            L.crimp_last_error.restype = ctypes.c_char_p
+            L.crimp_device_count.argtypes = [ctypes.POINTER(i32)]
+            L.crimp_calcphase.argtypes = [P, i64, ctypes.POINTER(TimingModel), i32, P, P, u32, P]
+            L.crimp_search.argtypes = [P, i64, ctypes.c_double, P, i64, P, i64, i32, i32, i64, i64, P, u32, P]
+            L.crimp_toa_points.argtypes = [P, P, i64, ctypes.POINTER(Template), P, P, P, i64, P, u32, P]
+            L.crimp_toa_grid.argtypes = [P, P, i64, ctypes.POINTER(Template), P, i64, P, i64, P, P, u32, P]
+            L.crimp_binphases.argtypes = [P, P, i64, P, i32, P, u32, P]
+            for name in EXPORTS:
+                if name != "crimp_last_error":
+                    getattr(L, name).restype = ctypes.c_int
+            _lib = L
+        if require_device and not _dev_ok:
+            n = ctypes.c_int32(0)
+            _lib.crimp_device_count(ctypes.byref(n))
+            if n.value < 1:
+                raise CrimpNativeError("no HIP device visible: the CRIMP hot path runs only on the GPU "
+                                       "(there is no CPU fallback)")
+            _dev_ok = True
+    return _lib
+
+
+def check(rc):
+    if rc != 0:
+        msg = _lib.crimp_last_error().decode(errors="replace") if _lib is not None else "library not loaded"
+        raise CrimpNativeError("libcrimp_hip: %s (status %d)" % (msg, rc))
+
+
+# ------------------------------------------------------------------ buffer helpers
+def _is_torch(a):
+    return type(a).__module__.startswith("torch") and hasattr(a, "data_ptr")
+
+
+class Buffers:
+    """Collects the pointers for one call; all-host or all-device (torch CUDA) arrays."""
+
+    def __init__(self):
+        self.keep = []
+        self.device = None
+
+    def arg(self, a, dtype, writable=False, allow_none=False):
+        if a is None:
+            if allow_none:
+                return None
+            raise ValueError("missing array argument")
+        if _is_torch(a):
+            import torch
+            if not a.is_cuda:
+                a = a.cpu().numpy()
+            else:
+                tdt = {np.float64: torch.float64, np.int64: torch.int64}[np.dtype(dtype).type]
+                if a.dtype != tdt or not a.is_contiguous():
+                    if writable:
+                        raise ValueError("output tensors must be contiguous %s" % tdt)
+                    a = a.to(tdt).contiguous()
+                self._mode(True)
+                self.keep.append(a)
+                return ctypes.c_void_p(a.data_ptr())
+        arr = np.asarray(a)
+        if writable:
+            if arr.dtype != dtype or not arr.flags.c_contiguous or not arr.flags.writeable:
+                raise ValueError("output arrays must be writable C-contiguous %s" % np.dtype(dtype))
+        else:
+            arr = np.ascontiguousarray(arr, dtype=dtype)
+        self._mode(False)
+        self.keep.append(arr)
+        return ctypes.c_void_p(arr.ctypes.data)
+
+    def _mode(self, dev):
+        if self.device is None:
+            self.device = dev
+        elif self.device != dev:
+            raise ValueError("mix of host arrays and device tensors in one call")
+
+    def flags(self, extra=0):
+        return (FLAG_DEVICE_PTRS if self.device else 0) | extra
+
+    def stream(self):
+        if self.device:
+            import torch
+            return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        return None

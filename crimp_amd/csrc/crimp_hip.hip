@@ -1,0 +1,996 @@
+// crimp_hip.hip -- MI355X (gfx950) kernels + C-ABI for CRIMP's photon hot path.
+//
+// Entry points are declared (with the reference routine each replaces) in
+// include/crimp_hip.h. Layout of this file:
+//   1. runtime helpers (errors, stream-ordered scratch, staging of host buffers)
+//   2. fp32 sin/cos in revolutions (polynomial and hardware v_sin/v_cos)
+//   3. calcphase            -- HBM-bound fp64 phase folding
+//   4. periodicity search   -- direct VALU kernel (any trial grid) + finalize
+//   5. ToA likelihood scan  -- fp64 point evaluator, fp32 brute grid, binning
+//   6. C-ABI
+// The factorised MFMA search kernel for arithmetic-progression grids lives in
+// search_mfma.h and is included below.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/crimp_hip.h"
+
+#define CRIMP_VERSION 1
+
+// ============================================================== 1. runtime helpers
+static thread_local std::string g_err;
+static std::mutex g_mutex;
+
+static int set_err(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                               \
+    do {                                                                                           \
+        hipError_t e_ = (expr);                                                                    \
+        if (e_ != hipSuccess)                                                                      \
+            return set_err(CRIMP_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));     \
+    } while (0)
+
+#define ARGCHK(cond, msg)                                                                          \
+    do {                                                                                           \
+        if (!(cond)) return set_err(CRIMP_ERR_ARG, msg);                                           \
+    } while (0)
+
+// Stream-ordered scratch allocation (hipMallocAsync pool); freed in the destructor on the
+// same stream, so buffers of an async device-pointer call live exactly as long as its kernels.
+struct Scratch {
+    hipStream_t s;
+    std::vector<void*> ptrs;
+    explicit Scratch(hipStream_t st) : s(st) {}
+    ~Scratch() {
+        for (void* p : ptrs) (void)hipFreeAsync(p, s);
+    }
+    template <typename T>
+    hipError_t alloc(T** out, size_t count) {
+        void* p = nullptr;
+        size_t bytes = std::max<size_t>(count * sizeof(T), 16);
+        hipError_t e = hipMallocAsync(&p, bytes, s);
+        if (e != hipSuccess) return e;
+        ptrs.push_back(p);
+        *out = static_cast<T*>(p);
+        return hipSuccess;
+    }
+};
+
+// An input array: either the caller's device pointer or a staged copy of a host array.
+template <typename T>
+static hipError_t stage_in(Scratch& sc, const T* src, size_t count, bool dev, const T** out) {
+    if (dev || src == nullptr || count == 0) {
+        *out = src;
+        return hipSuccess;
+    }
+    T* d = nullptr;
+    hipError_t e = sc.alloc(&d, count);
+    if (e != hipSuccess) return e;
+    e = hipMemcpyAsync(d, src, count * sizeof(T), hipMemcpyHostToDevice, sc.s);
+    *out = d;
+    return e;
+}
+
+template <typename T>
+static hipError_t stage_out(Scratch& sc, T* dst, size_t count, bool dev, T** out) {
+    if (dev || dst == nullptr) {
+        *out = dst;
+        return hipSuccess;
+    }
+    return sc.alloc(out, count);
+}
+
+template <typename T>
+static hipError_t copy_back(hipStream_t s, T* host, const T* devp, size_t count, bool dev) {
+    if (dev || host == nullptr || count == 0) return hipSuccess;
+    return hipMemcpyAsync(host, devp, count * sizeof(T), hipMemcpyDeviceToHost, s);
+}
+
+static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// ============================================================== 2. sin/cos in revolutions
+// r in [-0.5, 0.5] revolutions -> sin(2*pi*r), cos(2*pi*r).
+// Polynomial form: quarter-turn reduction y = r - q/4 (exact), |y| <= 1/8, Taylor series of
+// sin/cos(2*pi*y) to degree 9/10 (truncation < 2e-9), then an exact quadrant rotation.
+__device__ __forceinline__ void sincos_rev_poly(float r, float& s, float& c) {
+    const float q = __builtin_rintf(4.0f * r);
+    const float y = __builtin_fmaf(-0.25f, q, r);
+    const float y2 = y * y;
+    const float S1 = 6.28318530717958647692f, S3 = -41.3417022403997f, S5 = 81.6052492760750f,
+                S7 = -76.7058597530613f, S9 = 42.0587782776566f;
+    const float C2 = -19.7392088021787f, C4 = 64.9393940226683f, C6 = -85.4568172844813f,
+                C8 = 60.2446397079094f, C10 = -26.4262625987960f;
+    float sp = __builtin_fmaf(y2, S9, S7);
+    sp = __builtin_fmaf(y2, sp, S5);
+    sp = __builtin_fmaf(y2, sp, S3);
+    sp = __builtin_fmaf(y2, sp, S1);
+    sp *= y;
+    float cp = __builtin_fmaf(y2, C10, C8);
+    cp = __builtin_fmaf(y2, cp, C6);
+    cp = __builtin_fmaf(y2, cp, C4);
+    cp = __builtin_fmaf(y2, cp, C2);
+    cp = __builtin_fmaf(y2, cp, 1.0f);
+    const int iq = ((int)q) & 3;
+    const float s_a = (iq & 1) ? cp : sp;
+    const float c_a = (iq & 1) ? sp : cp;
+    s = (iq & 2) ? -s_a : s_a;
+    c = ((iq + 1) & 2) ? -c_a : c_a;
+}
+
+// Hardware transcendental: v_sin_f32 / v_cos_f32 take revolutions (D = sin(2*pi*S0)).
+__device__ __forceinline__ void sincos_rev_hw(float r, float& s, float& c) {
+    s = __builtin_amdgcn_sinf(r);
+    c = __builtin_amdgcn_cosf(r);
+}
+
+template <bool HW>
+__device__ __forceinline__ void sincos_rev(float r, float& s, float& c) {
+    if (HW)
+        sincos_rev_hw(r, s, c);
+    else
+        sincos_rev_poly(r, s, c);
+}
+
+// ============================================================== 3. calcphase
+struct CPModel {
+    double pepoch;
+    double coef[13];  // (1/n!) * F_{n-1}, exactly as calcphase.py:84 forms it
+    int32_t nterms;   // highest n with a non-zero coefficient
+    int32_t parts;
+    int32_t n_glitch;
+    int32_t n_wave;
+    double glitch[CRIMP_MAX_GLITCH][7];
+    double wave_epoch, wave_om, f0;
+    double wave_ab[CRIMP_MAX_WAVE][2];
+};
+
+__device__ __forceinline__ double cp_one(const CPModel* __restrict__ M, double t) {
+    double te = 0.0;
+    if (M->parts & 1) {
+        // calcphase.py:80-85: te = sum_{n=1}^{13} coef_n * dt**n, summed in increasing n.
+        const double dt = (t - M->pepoch) * 86400.0;
+        double dn = dt;
+        const int nt = M->nterms;
+        for (int k = 0; k < nt; ++k) {
+            te += M->coef[k] * dn;
+            dn *= dt;
+        }
+    }
+    double gl = 0.0;
+    if (M->parts & 2) {
+        // calcphase.py:98-124
+        for (int j = 0; j < M->n_glitch; ++j) {
+            const double* g = M->glitch[j];
+            if (t >= g[0]) {
+                const double dts = (t - g[0]) * 86400.0;
+                const double ex = (g[6] == 0.0) ? 0.0 : (g[6] * 86400.0) * (1.0 - exp(-(t - g[0]) / g[6]));
+                gl += (((g[1] + g[2] * dts) + (0.5 * g[3]) * (dts * dts)) + ((1.0 / 6.0) * g[4]) * (dts * dts * dts)) +
+                      g[5] * ex;
+            }
+        }
+    }
+    double wv = 0.0;
+    if ((M->parts & 4) && M->n_wave > 0) {
+        // calcphase.py:138-149
+        for (int j = 1; j <= M->n_wave; ++j) {
+            const double arg = (j * M->wave_om) * (t - M->wave_epoch);
+            wv += (M->wave_ab[j - 1][0] * sin(arg)) + (M->wave_ab[j - 1][1] * cos(arg));
+        }
+        wv *= M->f0;
+    }
+    return te + gl + wv;
+}
+
+// Two photons per thread, 16-byte loads and stores (24 B of HBM traffic per photon).
+__global__ __launch_bounds__(256) void k_calcphase_vec(const double2* __restrict__ t, int64_t npair,
+                                                       const CPModel* __restrict__ M, double2* __restrict__ total,
+                                                       double2* __restrict__ folded) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < npair; i += (int64_t)gridDim.x * blockDim.x) {
+        const double2 tv = t[i];
+        double2 tot;
+        tot.x = cp_one(M, tv.x);
+        tot.y = cp_one(M, tv.y);
+        total[i] = tot;
+        if (folded) {
+            double2 fo;
+            fo.x = tot.x - floor(tot.x);
+            fo.y = tot.y - floor(tot.y);
+            folded[i] = fo;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_calcphase_scalar(const double* __restrict__ t, int64_t n,
+                                                          const CPModel* __restrict__ M, double* __restrict__ total,
+                                                          double* __restrict__ folded) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const double tot = cp_one(M, t[i]);
+        total[i] = tot;
+        if (folded) folded[i] = tot - floor(tot);
+    }
+}
+
+// ============================================================== 4. periodicity search
+// dt[i] = t[i] - t0 (periodsearch.py: self.time - self.t0); dt2 = dt*dt for the 2-D grid.
+__global__ __launch_bounds__(256) void k_search_prep(const double* __restrict__ t, int64_t n, double t0,
+                                                     double* __restrict__ dt, double* __restrict__ dt2) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const double d = t[i] - t0;
+        dt[i] = d;
+        if (dt2) dt2[i] = d * d;
+    }
+}
+
+// Direct kernel: one lane per trial, every photon of its split broadcast to the wave through
+// the scalar data path. Harmonics k0 .. k0+G-1 of one pass: fp64 phase, centred fractional
+// cycle, fp32 sin/cos in revolutions, angle-addition for k>k0, fp32 sums over 32-photon blocks
+// folded into fp64. part layout: [split][2*m][count] (C_k at 2(k-1), S_k at 2(k-1)+1).
+constexpr int kSearchBlock = 256;
+constexpr int kSearchFold = 32;
+
+template <int G, bool TWOD, bool FIRST, bool HW>
+__global__ __launch_bounds__(kSearchBlock) void k_search_direct(
+    const double* __restrict__ dt, const double* __restrict__ dt2, int64_t n, int64_t chunk,
+    const double* __restrict__ freq, int64_t nf, const double* __restrict__ c2row, int64_t first, int64_t count,
+    int k0, int ncomp, double* __restrict__ part) {
+    const int64_t t = (int64_t)blockIdx.x * kSearchBlock + threadIdx.x;
+    const int64_t split = blockIdx.y;
+    const int64_t tt = t < count ? t : count - 1;
+    const int64_t g = first + tt;
+    const int64_t row = TWOD ? g / nf : 0;
+    const double f = freq[g - row * nf];
+    const double c2 = TWOD ? c2row[row] : 0.0;
+    const double kf = (double)k0;
+    const int64_t i0 = split * chunk;
+    const int64_t i1 = i0 + chunk < n ? i0 + chunk : n;
+
+    double C[G], S[G];
+#pragma unroll
+    for (int k = 0; k < G; ++k) C[k] = S[k] = 0.0;
+
+    for (int64_t ib = i0; ib < i1; ib += kSearchFold) {
+        float pc[G], ps[G];
+#pragma unroll
+        for (int k = 0; k < G; ++k) pc[k] = ps[k] = 0.0f;
+        const int64_t ie = ib + kSearchFold < i1 ? ib + kSearchFold : i1;
+#pragma unroll 4
+        for (int64_t i = ib; i < ie; ++i) {
+            const double d = dt[i];
+            const double ph = TWOD ? fma(f, d, c2 * dt2[i]) : f * d;
+            float s1, c1;
+            sincos_rev<HW>((float)(ph - rint(ph)), s1, c1);
+            float s, c;
+            if (FIRST) {
+                s = s1;
+                c = c1;
+            } else {
+                const double pk = ph * kf;
+                sincos_rev<HW>((float)(pk - rint(pk)), s, c);
+            }
+            pc[0] += c;
+            ps[0] += s;
+#pragma unroll
+            for (int k = 1; k < G; ++k) {
+                const float cn = __builtin_fmaf(c, c1, -s * s1);
+                const float sn = __builtin_fmaf(s, c1, c * s1);
+                c = cn;
+                s = sn;
+                pc[k] += c;
+                ps[k] += s;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+            C[k] += (double)pc[k];
+            S[k] += (double)ps[k];
+        }
+    }
+    if (t < count) {
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+            const int comp = 2 * (k0 - 1 + k);
+            part[(split * ncomp + comp) * count + t] = C[k];
+            part[(split * ncomp + comp + 1) * count + t] = S[k];
+        }
+    }
+}
+
+// Z^2 = (2/n) sum_k (C_k^2 + S_k^2)            (periodsearch.py:66-69)
+// H   = max_k (cumsum_k[(C^2+S^2)(2/n)] - 4(k-1)) (periodsearch.py:118-123)
+__global__ __launch_bounds__(256) void k_search_finalize(const double* __restrict__ part, int64_t count, int splits,
+                                                         int m, int stat, double n, double* __restrict__ out) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= count) return;
+    const int ncomp = 2 * m;
+    double zsum = 0.0, cum = 0.0, best = -INFINITY;
+    const double w = 2.0 / n;
+    for (int k = 0; k < m; ++k) {
+        double c = 0.0, s = 0.0;
+        for (int sp = 0; sp < splits; ++sp) {
+            c += part[((int64_t)sp * ncomp + 2 * k) * count + t];
+            s += part[((int64_t)sp * ncomp + 2 * k + 1) * count + t];
+        }
+        const double z = c * c + s * s;
+        if (stat == CRIMP_STAT_Z2) {
+            zsum += z;
+        } else {
+            cum += z * w;
+            const double v = cum - 4.0 * (double)k;
+            best = v > best ? v : best;
+        }
+    }
+    out[t] = (stat == CRIMP_STAT_Z2) ? zsum * w : best;
+}
+
+#include "search_mfma.h"
+
+// ============================================================== 5. ToA likelihood scan
+struct TplDev {
+    int32_t model, K;
+    double amp[CRIMP_MAX_COMP];   // amp_j * ampShift (fourier), amp_j*ampShift/(2 pi) * sinh(w) (cauchy),
+                                  // amp_j*ampShift/(2 pi I0(1/w^2)) (vonmises)
+    double loc[CRIMP_MAX_COMP];   // ph_j or cen_j
+    double ch[CRIMP_MAX_COMP];    // cosh(wid_j) (cauchy)
+    double kap[CRIMP_MAX_COMP];   // 1/wid_j^2 (vonmises)
+};
+
+constexpr int kPtsPerGroup = 4;
+constexpr int kPtsBlock = 256;
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+__device__ __forceinline__ double wave_min(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o));
+    return v;
+}
+
+// One block per group of <= 4 points of one interval; lanes stride the photons. fp64.
+// Coefficient table per point (LDS): fourier  a_j = A cos(ph_j - j phi), b_j = -A sin(ph_j - j phi)
+//                                    cauchy/vm a_j = cos(cen_j + phi),   b_j = sin(cen_j + phi)
+__global__ __launch_bounds__(kPtsBlock) void k_toa_points(const double* __restrict__ x,
+                                                          const int64_t* __restrict__ offsets,
+                                                          const TplDev* __restrict__ T,
+                                                          const int64_t* __restrict__ grp_int,
+                                                          const int64_t* __restrict__ grp_first,
+                                                          const int32_t* __restrict__ grp_np,
+                                                          const double* __restrict__ pt_norm,
+                                                          const double* __restrict__ pt_phi, double* __restrict__ out) {
+    __shared__ double coef[kPtsPerGroup][2][CRIMP_MAX_COMP];
+    __shared__ double red[kPtsBlock / 64][kPtsPerGroup][8];
+    const int gi = blockIdx.x;
+    const int64_t iv = grp_int[gi];
+    const int64_t p0 = grp_first[gi];
+    const int np = grp_np[gi];
+    const int model = T->model, K = T->K;
+    const int tid = threadIdx.x;
+    if (tid < kPtsPerGroup * K) {
+        const int p = tid / K, j = tid % K;
+        const double phi = p < np ? pt_phi[p0 + p] : 0.0;
+        if (model == CRIMP_MODEL_FOURIER) {
+            const double d = T->loc[j] - (double)(j + 1) * phi;
+            coef[p][0][j] = T->amp[j] * cos(d);
+            coef[p][1][j] = -T->amp[j] * sin(d);
+        } else {
+            const double d = T->loc[j] + phi;
+            coef[p][0][j] = cos(d);
+            coef[p][1][j] = sin(d);
+        }
+    }
+    __syncthreads();
+    double nrm[kPtsPerGroup];
+#pragma unroll
+    for (int p = 0; p < kPtsPerGroup; ++p) nrm[p] = p < np ? pt_norm[p0 + p] : 1.0;
+    double acc[kPtsPerGroup][7];
+#pragma unroll
+    for (int p = 0; p < kPtsPerGroup; ++p) {
+#pragma unroll
+        for (int q = 0; q < 6; ++q) acc[p][q] = 0.0;
+        acc[p][6] = INFINITY;
+    }
+    const int64_t a = offsets[iv], b = offsets[iv + 1];
+    for (int64_t i = a + tid; i < b; i += kPtsBlock) {
+        const double xv = x[i];
+        double s1, c1;
+        if (model == CRIMP_MODEL_FOURIER)
+            sincospi(2.0 * xv, &s1, &c1);
+        else
+            sincos(xv, &s1, &c1);
+#pragma unroll
+        for (int p = 0; p < kPtsPerGroup; ++p) {
+            if (p >= np) break;
+            double h = 0.0, h1 = 0.0, h2 = 0.0;
+            if (model == CRIMP_MODEL_FOURIER) {
+                double cj = c1, sj = s1;
+                for (int j = 0; j < K; ++j) {
+                    const double al = coef[p][0][j], be = coef[p][1][j];
+                    const double tj = al * cj + be * sj;
+                    const double jj = (double)(j + 1);
+                    h += tj;
+                    h2 -= jj * jj * tj;
+                    h1 += jj * (al * sj - be * cj);
+                    const double cn = cj * c1 - sj * s1;
+                    sj = sj * c1 + cj * s1;
+                    cj = cn;
+                }
+            } else {
+                for (int j = 0; j < K; ++j) {
+                    const double C = coef[p][0][j], S = coef[p][1][j];
+                    const double cu = c1 * C + s1 * S;  // cos(x - cen - phi)
+                    const double su = s1 * C - c1 * S;  // sin(x - cen - phi)
+                    if (model == CRIMP_MODEL_CAUCHY) {
+                        const double iD = 1.0 / (T->ch[j] - cu);
+                        const double v = T->amp[j] * iD;           // amp' = a*sinh(w)
+                        const double dvdu = -v * su * iD;
+                        const double d2 = -v * iD * (cu - 2.0 * su * su * iD);
+                        h += v;
+                        h1 -= dvdu;
+                        h2 += d2;
+                    } else {
+                        const double kp = T->kap[j];
+                        const double v = T->amp[j] * exp(kp * cu);
+                        h += v;
+                        h1 += kp * su * v;
+                        h2 += (-kp * cu + kp * kp * su * su) * v;
+                    }
+                }
+            }
+            const double mv = nrm[p] + h;
+            const double q = 1.0 / mv;
+            acc[p][0] += log(mv);
+            acc[p][1] += q;
+            acc[p][2] += h1 * q;
+            acc[p][3] -= q * q;
+            acc[p][4] -= h1 * q * q;
+            acc[p][5] += h2 * q - h1 * h1 * q * q;
+            acc[p][6] = fmin(acc[p][6], mv);
+        }
+    }
+    const int wid = tid >> 6, lane = tid & 63;
+#pragma unroll
+    for (int p = 0; p < kPtsPerGroup; ++p) {
+#pragma unroll
+        for (int q = 0; q < 6; ++q) {
+            const double v = wave_sum(acc[p][q]);
+            if (lane == 0) red[wid][p][q] = v;
+        }
+        const double v = wave_min(acc[p][6]);
+        if (lane == 0) red[wid][p][6] = v;
+    }
+    __syncthreads();
+    if (tid < kPtsPerGroup * 7) {
+        const int p = tid / 7, q = tid % 7;
+        if (p < np) {
+            double v = red[0][p][q];
+            for (int w = 1; w < kPtsBlock / 64; ++w) v = (q == 6) ? fmin(v, red[w][p][q]) : v + red[w][p][q];
+            out[(p0 + p) * 8 + q] = v;
+            if (q == 0) out[(p0 + p) * 8 + 7] = (double)(b - a);
+        }
+    }
+}
+
+// Brute grid (fp32 model and log2, fp64 fold every 32 photons). One lane per phShift value,
+// photons of a 128-photon tile broadcast from LDS; NN norms per lane.
+constexpr int kGridBlock = 128;
+constexpr int kGridNN = 20;
+constexpr int kGridKMax = 8;
+
+template <int KMAX>
+__global__ __launch_bounds__(kGridBlock) void k_toa_grid(const double* __restrict__ x,
+                                                         const int64_t* __restrict__ offsets,
+                                                         const TplDev* __restrict__ T, const double* __restrict__ norm,
+                                                         int nnorm, int a0, int na, const double* __restrict__ phi,
+                                                         int nphi, int64_t chunk, int nint,
+                                                         double* __restrict__ lnsum, double* __restrict__ hmin) {
+    __shared__ float basis[kGridBlock][2 * KMAX];
+    const int tid = threadIdx.x;
+    const int bphi = blockIdx.x * kGridBlock + tid;
+    const int64_t iv = blockIdx.y;
+    const int64_t split = blockIdx.z;
+    const int model = T->model, K = T->K;
+    const double ph = phi[bphi < nphi ? bphi : nphi - 1];
+    float ca[KMAX], cb[KMAX], amp[KMAX], chj[KMAX], kpj[KMAX];
+#pragma unroll
+    for (int j = 0; j < KMAX; ++j) {
+        ca[j] = cb[j] = amp[j] = chj[j] = kpj[j] = 0.0f;
+        if (j < K) {
+            if (model == CRIMP_MODEL_FOURIER) {
+                const double d = T->loc[j] - (double)(j + 1) * ph;
+                ca[j] = (float)(T->amp[j] * cos(d));
+                cb[j] = (float)(-T->amp[j] * sin(d));
+            } else {
+                const double d = T->loc[j] + ph;
+                ca[j] = (float)cos(d);
+                cb[j] = (float)sin(d);
+                amp[j] = (float)T->amp[j];
+                chj[j] = (float)T->ch[j];
+                kpj[j] = (float)(T->kap[j] * 1.4426950408889634);  // exp(k*cu) = exp2(k*log2e*cu)
+            }
+        }
+    }
+    float nr[kGridNN];
+#pragma unroll
+    for (int a = 0; a < kGridNN; ++a) nr[a] = (a < na) ? (float)norm[iv * nnorm + a0 + a] : 1.0f;
+    double acc[kGridNN];
+#pragma unroll
+    for (int a = 0; a < kGridNN; ++a) acc[a] = 0.0;
+    float hmn = INFINITY;
+    const int64_t beg = offsets[iv] + split * chunk;
+    const int64_t end = std::min<int64_t>(offsets[iv + 1], beg + chunk);
+    for (int64_t base = beg; base < end; base += kGridBlock) {
+        const int cnt = (int)std::min<int64_t>(kGridBlock, end - base);
+        __syncthreads();
+        if (tid < cnt) {
+            const double xv = x[base + tid];
+            double rv = (model == CRIMP_MODEL_FOURIER) ? xv : xv * 0.15915494309189533577;  // cycles
+            rv -= rint(rv);
+            float s1, c1;
+            sincos_rev_poly((float)rv, s1, c1);
+            if (model == CRIMP_MODEL_FOURIER) {
+                float cj = c1, sj = s1;
+#pragma unroll
+                for (int j = 0; j < KMAX; ++j) {
+                    basis[tid][2 * j] = cj;
+                    basis[tid][2 * j + 1] = sj;
+                    const float cn = __builtin_fmaf(cj, c1, -sj * s1);
+                    sj = __builtin_fmaf(sj, c1, cj * s1);
+                    cj = cn;
+                }
+            } else {
+                basis[tid][0] = c1;
+                basis[tid][1] = s1;
+            }
+        }
+        __syncthreads();
+        for (int i0 = 0; i0 < cnt; i0 += 32) {
+            float pa[kGridNN];
+#pragma unroll
+            for (int a = 0; a < kGridNN; ++a) pa[a] = 0.0f;
+            const int i1 = std::min(cnt, i0 + 32);
+            for (int i = i0; i < i1; ++i) {
+                float h = 0.0f;
+                if (model == CRIMP_MODEL_FOURIER) {
+#pragma unroll
+                    for (int j = 0; j < KMAX; ++j)
+                        if (j < K) h = __builtin_fmaf(ca[j], basis[i][2 * j], __builtin_fmaf(cb[j], basis[i][2 * j + 1], h));
+                } else {
+                    const float cx = basis[i][0], sx = basis[i][1];
+#pragma unroll
+                    for (int j = 0; j < KMAX; ++j) {
+                        if (j < K) {
+                            const float cu = __builtin_fmaf(cx, ca[j], sx * cb[j]);
+                            if (model == CRIMP_MODEL_CAUCHY)
+                                h += amp[j] * __builtin_amdgcn_rcpf(chj[j] - cu);
+                            else
+                                h += amp[j] * __builtin_amdgcn_exp2f(kpj[j] * cu);
+                        }
+                    }
+                }
+                hmn = fminf(hmn, h);
+#pragma unroll
+                for (int a = 0; a < kGridNN; ++a) pa[a] += __builtin_amdgcn_logf(nr[a] + h);
+            }
+#pragma unroll
+            for (int a = 0; a < kGridNN; ++a) acc[a] += (double)pa[a];
+        }
+    }
+    if (bphi < nphi) {
+#pragma unroll
+        for (int a = 0; a < kGridNN; ++a)
+            if (a < na) lnsum[((split * nint + iv) * nnorm + a0 + a) * nphi + bphi] = acc[a];
+        if (a0 == 0) hmin[(split * nint + iv) * nphi + bphi] = (double)hmn;
+    }
+}
+
+// np.histogram(x, bins=edges) for uniform edges (numpy/lib/_histograms_impl.py semantics).
+__global__ __launch_bounds__(256) void k_binphases(const double* __restrict__ x, const int64_t* __restrict__ offsets,
+                                                   const double* __restrict__ edges, int nb,
+                                                   unsigned long long* __restrict__ counts) {
+    __shared__ unsigned int cnt[256];
+    const int64_t iv = blockIdx.x;
+    for (int b = threadIdx.x; b < nb; b += blockDim.x) cnt[b] = 0;
+    __syncthreads();
+    const double first = edges[0], last = edges[nb];
+    const double denom = last - first;
+    for (int64_t i = offsets[iv] + threadIdx.x; i < offsets[iv + 1]; i += blockDim.x) {
+        const double v = x[i];
+        if (!(v >= first && v <= last)) continue;
+        int64_t idx = (int64_t)(((v - first) / denom) * (double)nb);
+        if (idx == nb) idx -= 1;
+        if (v < edges[idx]) idx -= 1;
+        if (v >= edges[idx + 1] && idx != nb - 1) idx += 1;
+        atomicAdd(&cnt[idx], 1u);
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < nb; b += blockDim.x) counts[iv * nb + b] = cnt[b];
+}
+
+// ============================================================== 6. C-ABI
+static hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+extern "C" int crimp_version(void) { return CRIMP_VERSION; }
+
+extern "C" const char* crimp_last_error(void) { return g_err.c_str(); }
+
+extern "C" int crimp_device_count(int32_t* count) {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (count) *count = (e == hipSuccess) ? n : 0;
+    if (e != hipSuccess) return set_err(CRIMP_ERR_NODEV, std::string("hipGetDeviceCount: ") + hipGetErrorString(e));
+    return CRIMP_OK;
+}
+
+static int finish(hipStream_t s, uint32_t flags) {
+    HIPCHK(hipGetLastError());
+    if (!(flags & CRIMP_FLAG_DEVICE_PTRS) || (flags & CRIMP_FLAG_SYNC)) HIPCHK(hipStreamSynchronize(s));
+    return CRIMP_OK;
+}
+
+extern "C" int crimp_calcphase(const double* t_mjd, int64_t n, const crimp_timing_model* model, int32_t parts,
+                               double* total, double* folded, uint32_t flags, void* stream) {
+    ARGCHK(n >= 0, "n < 0");
+    ARGCHK(model != nullptr && total != nullptr && (t_mjd != nullptr || n == 0), "null argument");
+    ARGCHK(model->n_glitch >= 0 && model->n_glitch <= CRIMP_MAX_GLITCH, "n_glitch out of range");
+    ARGCHK(model->n_wave >= 0 && model->n_wave <= CRIMP_MAX_WAVE, "n_wave out of range");
+    if (n == 0) return CRIMP_OK;
+    std::lock_guard<std::mutex> lk(g_mutex);
+    const bool dev = flags & CRIMP_FLAG_DEVICE_PTRS;
+    hipStream_t s = as_stream(stream);
+    CPModel hm{};
+    hm.pepoch = model->pepoch;
+    hm.nterms = 0;
+    double fact = 1.0;
+    for (int k = 0; k < 13; ++k) {
+        fact *= (double)(k + 1);
+        hm.coef[k] = (1.0 / fact) * model->f[k];
+        if (model->f[k] != 0.0) hm.nterms = k + 1;
+    }
+    hm.parts = parts;
+    hm.n_glitch = model->n_glitch;
+    std::memcpy(hm.glitch, model->glitch, sizeof(hm.glitch));
+    hm.n_wave = model->n_wave;
+    hm.wave_epoch = model->wave_epoch;
+    hm.wave_om = model->wave_om;
+    hm.f0 = model->f[0];
+    std::memcpy(hm.wave_ab, model->wave_ab, sizeof(hm.wave_ab));
+    {
+        Scratch sc(s);
+        CPModel* dm = nullptr;
+        HIPCHK(sc.alloc(&dm, 1));
+        HIPCHK(hipMemcpyAsync(dm, &hm, sizeof(CPModel), hipMemcpyHostToDevice, s));
+        const double* dt = nullptr;
+        double *dtot = nullptr, *dfol = nullptr;
+        HIPCHK(stage_in(sc, t_mjd, (size_t)n, dev, &dt));
+        HIPCHK(stage_out(sc, total, (size_t)n, dev, &dtot));
+        HIPCHK(stage_out(sc, folded, (size_t)n, dev, &dfol));
+        const bool vec = ((reinterpret_cast<uintptr_t>(dt) | reinterpret_cast<uintptr_t>(dtot) |
+                           reinterpret_cast<uintptr_t>(dfol)) & 15u) == 0 && (n % 2 == 0);
+        const int blocks = (int)std::min<int64_t>(cdiv(vec ? n / 2 : n, 256), 256 * 16);
+        if (vec)
+            k_calcphase_vec<<<blocks, 256, 0, s>>>(reinterpret_cast<const double2*>(dt), n / 2, dm,
+                                                     reinterpret_cast<double2*>(dtot), reinterpret_cast<double2*>(dfol));
+        else
+            k_calcphase_scalar<<<blocks, 256, 0, s>>>(dt, n, dm, dtot, dfol);
+        HIPCHK(hipGetLastError());
+        HIPCHK(copy_back(s, total, dtot, (size_t)n, dev));
+        HIPCHK(copy_back(s, folded, dfol, (size_t)n, dev));
+    }
+    return finish(s, flags);
+}
+
+// Launch the direct kernel for one harmonic group.
+template <bool TWOD, bool HW>
+static void launch_direct(int G, bool firstk, dim3 grid, hipStream_t s, const double* dt, const double* dt2,
+                          int64_t n, int64_t chunk, const double* fr, int64_t nf, const double* c2, int64_t first,
+                          int64_t count, int k0, int ncomp, double* part) {
+#define CRIMP_LD(GG, FF) \
+    k_search_direct<GG, TWOD, FF, HW><<<grid, kSearchBlock, 0, s>>>(dt, dt2, n, chunk, fr, nf, c2, first, count, k0, ncomp, part)
+    if (firstk) {
+        if (G == 8) CRIMP_LD(8, true); else if (G == 4) CRIMP_LD(4, true); else if (G == 2) CRIMP_LD(2, true); else CRIMP_LD(1, true);
+    } else {
+        if (G == 8) CRIMP_LD(8, false); else if (G == 4) CRIMP_LD(4, false); else if (G == 2) CRIMP_LD(2, false); else CRIMP_LD(1, false);
+    }
+#undef CRIMP_LD
+}
+
+extern "C" int crimp_search(const double* t, int64_t n, double t0, const double* freq, int64_t nf,
+                            const double* log10_negfdot, int64_t nfd, int32_t nharm, int32_t stat, int64_t first,
+                            int64_t count, double* out, uint32_t flags, void* stream) {
+    ARGCHK(n >= 1, "need at least one photon (periodsearch.py:54 reads time[0], time[-1])");
+    ARGCHK(nf >= 1, "need at least one trial frequency");
+    ARGCHK(nharm >= 1 && nharm <= 256, "nbrHarm must be in 1..256");
+    ARGCHK(stat == CRIMP_STAT_Z2 || stat == CRIMP_STAT_H, "unknown statistic");
+    ARGCHK(t != nullptr && freq != nullptr && out != nullptr, "null argument");
+    const bool twod = log10_negfdot != nullptr && nfd > 0;
+    const int64_t total = (twod ? nfd : 1) * nf;
+    ARGCHK(first >= 0 && count >= 0 && first + count <= total, "trial range outside the grid");
+    if (count == 0) return CRIMP_OK;
+    std::lock_guard<std::mutex> lk(g_mutex);
+    const bool dev = flags & CRIMP_FLAG_DEVICE_PTRS;
+    hipStream_t s = as_stream(stream);
+    {
+        Scratch sc(s);
+        const double *dtm = nullptr, *dfr = nullptr;
+        double* dout = nullptr;
+        HIPCHK(stage_in(sc, t, (size_t)n, dev, &dtm));
+        HIPCHK(stage_in(sc, freq, (size_t)nf, dev, &dfr));
+        HIPCHK(stage_out(sc, out, (size_t)count, dev, &dout));
+        // fdot term per row, formed on the host exactly as periodsearch.py:271: 0.5*(-1*10**fd)
+        double* dc2 = nullptr;
+        if (twod) {
+            std::vector<double> fdh((size_t)nfd), c2h((size_t)nfd);
+            if (dev) {
+                HIPCHK(hipMemcpyAsync(fdh.data(), log10_negfdot, nfd * sizeof(double), hipMemcpyDeviceToHost, s));
+                HIPCHK(hipStreamSynchronize(s));
+            } else {
+                std::memcpy(fdh.data(), log10_negfdot, nfd * sizeof(double));
+            }
+            for (int64_t r = 0; r < nfd; ++r) c2h[r] = 0.5 * (-1.0 * std::pow(10.0, fdh[r]));
+            HIPCHK(sc.alloc(&dc2, (size_t)nfd));
+            HIPCHK(hipMemcpyAsync(dc2, c2h.data(), nfd * sizeof(double), hipMemcpyHostToDevice, s));
+            // c2h must stay alive until the copy has been consumed
+            HIPCHK(hipStreamSynchronize(s));
+        }
+        double *ddt = nullptr, *ddt2 = nullptr;
+        HIPCHK(sc.alloc(&ddt, (size_t)n));
+        if (twod) HIPCHK(sc.alloc(&ddt2, (size_t)n));
+        k_search_prep<<<(int)std::min<int64_t>(cdiv(n, 256), 4096), 256, 0, s>>>(dtm, n, t0, ddt, ddt2);
+        HIPCHK(hipGetLastError());
+
+        int rc = -1;
+        if (!(flags & CRIMP_FLAG_FORCE_DIRECT)) {
+            rc = mfma_search(sc, s, ddt, ddt2, n, dfr, nf, dc2, twod, nharm, stat, first, count, dout, flags);
+            if (rc < 0) return rc;  // error already recorded
+        }
+        if (rc != 1) {  // factorised path declined (grid not an arithmetic progression, too small, ...)
+            if (flags & CRIMP_FLAG_FORCE_MFMA) return set_err(CRIMP_ERR_ARG, "factorised search not applicable");
+            const int64_t tblocks = cdiv(count, kSearchBlock);
+            int64_t splits = std::max<int64_t>(1, std::min<int64_t>(cdiv(2048, tblocks), cdiv(n, 2048)));
+            int64_t chunk = cdiv(cdiv(n, splits), kSearchFold) * kSearchFold;
+            splits = cdiv(n, chunk);
+            const int ncomp = 2 * nharm;
+            double* part = nullptr;
+            HIPCHK(sc.alloc(&part, (size_t)(splits * ncomp * count)));
+            dim3 grid((unsigned)tblocks, (unsigned)splits);
+            const bool hw = flags & CRIMP_FLAG_HW_SINCOS;
+            int k0 = 1;
+            while (k0 <= nharm) {
+                const int rem = nharm - k0 + 1;
+                const int G = rem >= 8 ? 8 : rem >= 4 ? 4 : rem >= 2 ? 2 : 1;
+                if (twod) {
+                    if (hw) launch_direct<true, true>(G, k0 == 1, grid, s, ddt, ddt2, n, chunk, dfr, nf, dc2, first, count, k0, ncomp, part);
+                    else launch_direct<true, false>(G, k0 == 1, grid, s, ddt, ddt2, n, chunk, dfr, nf, dc2, first, count, k0, ncomp, part);
+                } else {
+                    if (hw) launch_direct<false, true>(G, k0 == 1, grid, s, ddt, ddt2, n, chunk, dfr, nf, dc2, first, count, k0, ncomp, part);
+                    else launch_direct<false, false>(G, k0 == 1, grid, s, ddt, ddt2, n, chunk, dfr, nf, dc2, first, count, k0, ncomp, part);
+                }
+                HIPCHK(hipGetLastError());
+                k0 += G;
+            }
+            k_search_finalize<<<(unsigned)cdiv(count, 256), 256, 0, s>>>(part, count, (int)splits, nharm, stat,
+                                                                       (double)n, dout);
+            HIPCHK(hipGetLastError());
+        }
+        HIPCHK(copy_back(s, out, dout, (size_t)count, dev));
+    }
+    return finish(s, flags);
+}
+
+static int make_tpl(const crimp_template* tpl, TplDev* T) {
+    ARGCHK(tpl != nullptr, "null template");
+    ARGCHK(tpl->ncomp >= 1 && tpl->ncomp <= CRIMP_MAX_COMP, "ncomp out of range");
+    ARGCHK(tpl->model >= 0 && tpl->model <= 2, "unknown template model");
+    std::memset(T, 0, sizeof(*T));
+    T->model = tpl->model;
+    T->K = tpl->ncomp;
+    const double twopi = 6.283185307179586476925286766559;
+    for (int j = 0; j < tpl->ncomp; ++j) {
+        const double a = tpl->amp[j] * tpl->amp_shift;
+        T->loc[j] = tpl->loc[j];
+        if (tpl->model == CRIMP_MODEL_FOURIER) {
+            T->amp[j] = a;
+        } else if (tpl->model == CRIMP_MODEL_CAUCHY) {
+            T->amp[j] = (a / twopi) * std::sinh(tpl->wid[j]);
+            T->ch[j] = std::cosh(tpl->wid[j]);
+        } else {
+            T->amp[j] = a / (twopi * tpl->i0[j]);
+            T->kap[j] = 1.0 / (tpl->wid[j] * tpl->wid[j]);
+        }
+    }
+    return CRIMP_OK;
+}
+
+extern "C" int crimp_toa_points(const double* x, const int64_t* offsets, int64_t nint, const crimp_template* tpl,
+                                const int64_t* pt_interval, const double* pt_norm, const double* pt_phi, int64_t npts,
+                                double* out, uint32_t flags, void* stream) {
+    ARGCHK(nint >= 1 && npts >= 0, "bad sizes");
+    ARGCHK(x != nullptr && offsets != nullptr && pt_interval != nullptr && pt_norm != nullptr && pt_phi != nullptr &&
+               out != nullptr,
+           "null argument");
+    TplDev T;
+    int rc = make_tpl(tpl, &T);
+    if (rc) return rc;
+    if (npts == 0) return CRIMP_OK;
+    std::lock_guard<std::mutex> lk(g_mutex);
+    const bool dev = flags & CRIMP_FLAG_DEVICE_PTRS;
+    hipStream_t s = as_stream(stream);
+    // groups of <= 4 consecutive points sharing an interval (host needs the interval ids)
+    std::vector<int64_t> pint((size_t)npts), hoff((size_t)nint + 1);
+    if (dev) {
+        HIPCHK(hipMemcpyAsync(pint.data(), pt_interval, npts * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(hoff.data(), offsets, (nint + 1) * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+    } else {
+        std::memcpy(pint.data(), pt_interval, npts * sizeof(int64_t));
+        std::memcpy(hoff.data(), offsets, (nint + 1) * sizeof(int64_t));
+    }
+    for (int64_t i = 0; i < nint; ++i) ARGCHK(hoff[i + 1] >= hoff[i] && hoff[i] >= 0, "offsets must be non-decreasing");
+    std::vector<int64_t> gint, gfirst;
+    std::vector<int32_t> gnp;
+    for (int64_t p = 0; p < npts;) {
+        ARGCHK(pint[p] >= 0 && pint[p] < nint, "point interval out of range");
+        int64_t q = p + 1;
+        while (q < npts && q - p < kPtsPerGroup && pint[q] == pint[p]) ++q;
+        gint.push_back(pint[p]);
+        gfirst.push_back(p);
+        gnp.push_back((int32_t)(q - p));
+        p = q;
+    }
+    const int64_t ng = (int64_t)gint.size();
+    {
+        Scratch sc(s);
+        const double *dx = nullptr, *dn = nullptr, *dp = nullptr;
+        const int64_t* doff = nullptr;
+        double* dout = nullptr;
+        HIPCHK(stage_in(sc, x, (size_t)hoff[nint], dev, &dx));
+        HIPCHK(stage_in(sc, offsets, (size_t)nint + 1, dev, &doff));
+        HIPCHK(stage_in(sc, pt_norm, (size_t)npts, dev, &dn));
+        HIPCHK(stage_in(sc, pt_phi, (size_t)npts, dev, &dp));
+        HIPCHK(stage_out(sc, out, (size_t)npts * 8, dev, &dout));
+        TplDev* dT = nullptr;
+        int64_t *dgi = nullptr, *dgf = nullptr;
+        int32_t* dgn = nullptr;
+        HIPCHK(sc.alloc(&dT, 1));
+        HIPCHK(sc.alloc(&dgi, (size_t)ng));
+        HIPCHK(sc.alloc(&dgf, (size_t)ng));
+        HIPCHK(sc.alloc(&dgn, (size_t)ng));
+        HIPCHK(hipMemcpyAsync(dT, &T, sizeof(T), hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(dgi, gint.data(), ng * sizeof(int64_t), hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(dgf, gfirst.data(), ng * sizeof(int64_t), hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(dgn, gnp.data(), ng * sizeof(int32_t), hipMemcpyHostToDevice, s));
+        k_toa_points<<<(unsigned)ng, kPtsBlock, 0, s>>>(dx, doff, dT, dgi, dgf, dgn, dn, dp, dout);
+        HIPCHK(hipGetLastError());
+        HIPCHK(copy_back(s, out, dout, (size_t)npts * 8, dev));
+        HIPCHK(hipStreamSynchronize(s));  // host vectors above are read by queued copies
+    }
+    return finish(s, flags);
+}
+
+extern "C" int crimp_toa_grid(const double* x, const int64_t* offsets, int64_t nint, const crimp_template* tpl,
+                              const double* norm, int64_t nnorm, const double* phi, int64_t nphi, double* lnsum,
+                              double* hmin, uint32_t flags, void* stream) {
+    ARGCHK(nint >= 1 && nnorm >= 1 && nphi >= 1, "bad sizes");
+    ARGCHK(nphi <= (1 << 24) && nnorm <= (1 << 20), "grid too large");
+    ARGCHK(x != nullptr && offsets != nullptr && norm != nullptr && phi != nullptr && lnsum != nullptr &&
+               hmin != nullptr,
+           "null argument");
+    TplDev T;
+    int rc = make_tpl(tpl, &T);
+    if (rc) return rc;
+    ARGCHK(T.K <= kGridKMax, "brute grid supports at most 8 template components");
+    std::lock_guard<std::mutex> lk(g_mutex);
+    const bool dev = flags & CRIMP_FLAG_DEVICE_PTRS;
+    hipStream_t s = as_stream(stream);
+    std::vector<int64_t> hoff((size_t)nint + 1);
+    if (dev) {
+        HIPCHK(hipMemcpyAsync(hoff.data(), offsets, (nint + 1) * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+    } else {
+        std::memcpy(hoff.data(), offsets, (nint + 1) * sizeof(int64_t));
+    }
+    int64_t maxn = 0;
+    for (int64_t i = 0; i < nint; ++i) {
+        ARGCHK(hoff[i + 1] >= hoff[i] && hoff[i] >= 0, "offsets must be non-decreasing");
+        maxn = std::max(maxn, hoff[i + 1] - hoff[i]);
+    }
+    {
+        Scratch sc(s);
+        const double *dx = nullptr, *dnrm = nullptr, *dphi = nullptr;
+        const int64_t* doff = nullptr;
+        HIPCHK(stage_in(sc, x, (size_t)hoff[nint], dev, &dx));
+        HIPCHK(stage_in(sc, offsets, (size_t)nint + 1, dev, &doff));
+        HIPCHK(stage_in(sc, norm, (size_t)(nint * nnorm), dev, &dnrm));
+        HIPCHK(stage_in(sc, phi, (size_t)nphi, dev, &dphi));
+        const int64_t pblocks = cdiv(nphi, kGridBlock);
+        int64_t splits = std::max<int64_t>(1, std::min<int64_t>(cdiv(2048, pblocks * nint), cdiv(std::max<int64_t>(maxn, 1), 1024)));
+        splits = std::min<int64_t>(splits, 65535);
+        int64_t chunk = cdiv(std::max<int64_t>(maxn, 1), splits);
+        chunk = cdiv(chunk, kGridBlock) * kGridBlock;
+        splits = cdiv(std::max<int64_t>(maxn, 1), chunk);
+        double *pl = nullptr, *ph = nullptr;
+        HIPCHK(sc.alloc(&pl, (size_t)(splits * nint * nnorm * nphi)));
+        HIPCHK(sc.alloc(&ph, (size_t)(splits * nint * nphi)));
+        TplDev* dT = nullptr;
+        HIPCHK(sc.alloc(&dT, 1));
+        HIPCHK(hipMemcpyAsync(dT, &T, sizeof(T), hipMemcpyHostToDevice, s));
+        ARGCHK(nint <= 65535, "at most 65535 intervals per brute-grid call");
+        dim3 grid((unsigned)pblocks, (unsigned)nint, (unsigned)splits);
+        for (int64_t a0 = 0; a0 < nnorm; a0 += kGridNN) {
+            const int na = (int)std::min<int64_t>(kGridNN, nnorm - a0);
+            k_toa_grid<kGridKMax><<<grid, kGridBlock, 0, s>>>(dx, doff, dT, dnrm, (int)nnorm, (int)a0, na, dphi,
+                                                              (int)nphi, chunk, (int)nint, pl, ph);
+            HIPCHK(hipGetLastError());
+        }
+        // combine splits on the host in a fixed order (deterministic)
+        std::vector<double> hl((size_t)(splits * nint * nnorm * nphi)), hh((size_t)(splits * nint * nphi));
+        HIPCHK(hipMemcpyAsync(hl.data(), pl, hl.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(hh.data(), ph, hh.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        const int64_t L = nint * nnorm * nphi, H = nint * nphi;
+        std::vector<double> rl((size_t)L), rh((size_t)H);
+        for (int64_t k = 0; k < L; ++k) {
+            double v = 0.0;
+            for (int64_t sp = 0; sp < splits; ++sp) v += hl[(size_t)(sp * L + k)];
+            rl[(size_t)k] = v * 0.69314718055994530942;  // log2 -> ln
+        }
+        for (int64_t k = 0; k < H; ++k) {
+            double v = INFINITY;
+            for (int64_t sp = 0; sp < splits; ++sp) v = std::min(v, hh[(size_t)(sp * H + k)]);
+            rh[(size_t)k] = v;
+        }
+        if (dev) {
+            HIPCHK(hipMemcpyAsync(lnsum, rl.data(), L * sizeof(double), hipMemcpyHostToDevice, s));
+            HIPCHK(hipMemcpyAsync(hmin, rh.data(), H * sizeof(double), hipMemcpyHostToDevice, s));
+            HIPCHK(hipStreamSynchronize(s));
+        } else {
+            std::memcpy(lnsum, rl.data(), L * sizeof(double));
+            std::memcpy(hmin, rh.data(), H * sizeof(double));
+        }
+    }
+    return finish(s, flags);
+}
+
+extern "C" int crimp_binphases(const double* x, const int64_t* offsets, int64_t nint, const double* edges,
+                               int32_t nbins, int64_t* counts, uint32_t flags, void* stream) {
+    ARGCHK(nint >= 1 && nbins >= 1 && nbins <= 256, "bad sizes (nbins must be 1..256)");
+    ARGCHK(x != nullptr && offsets != nullptr && edges != nullptr && counts != nullptr, "null argument");
+    ARGCHK(nint <= 2147483647LL, "too many intervals");
+    std::lock_guard<std::mutex> lk(g_mutex);
+    const bool dev = flags & CRIMP_FLAG_DEVICE_PTRS;
+    hipStream_t s = as_stream(stream);
+    int64_t ntot = 0;
+    if (dev) {
+        HIPCHK(hipMemcpyAsync(&ntot, offsets + nint, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+    } else {
+        ntot = offsets[nint];
+    }
+    {
+        Scratch sc(s);
+        const double *dx = nullptr, *de = nullptr;
+        const int64_t* doff = nullptr;
+        int64_t* dc = nullptr;
+        HIPCHK(stage_in(sc, x, (size_t)ntot, dev, &dx));
+        HIPCHK(stage_in(sc, offsets, (size_t)nint + 1, dev, &doff));
+        HIPCHK(stage_in(sc, edges, (size_t)nbins + 1, dev, &de));
+        HIPCHK(stage_out(sc, counts, (size_t)(nint * nbins), dev, &dc));
+        k_binphases<<<(unsigned)nint, 256, 0, s>>>(dx, doff, de, nbins, reinterpret_cast<unsigned long long*>(dc));
+        HIPCHK(hipGetLastError());
+        HIPCHK(copy_back(s, counts, dc, (size_t)(nint * nbins), dev));
+    }
+    return finish(s, flags);
+}

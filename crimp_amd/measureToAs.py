@@ -1,0 +1,225 @@
+"""Drop-in ``measureToAs`` / ``measureToA_*`` / ``measuretoas`` CLI on the MI355X.
+
+Same signatures, return values, output text file and CLI flags as CRIMP v2.3.0
+``measureToAs.py`` (:64-251 ToA loop, :254-693 per-template fits, :698-806
+initial parameters, :951-1003 CLI). The per-interval likelihood work runs in
+batches on the device (crimp_amd/toafit.py); the loop body keeps the
+reference's order of operations and its text formatting (``str()`` of each value,
+tab-separated, 13 columns, :161-162, :222-226).
+
+Not implemented in this build (raise ``NotImplementedError``): ``varyAmps`` and
+``readvaryparam`` and the .tim writer ``timFile``
+(§8f row 2).
+"""
+import argparse
+import math
+import sys
+
+import numpy as np
+
+from .calcphase import calcphase
+from .ephemTmjd import ephemTmjd
+from .eventfile import EvtFileOps
+from .logging_utils import configure_logging, get_logger
+from .periodsearch import PeriodSearch
+from .readPPtemplate import readPPtemplate
+from .toafit import ToAFitter
+
+logger = get_logger(__name__)
+
+
+class Param:
+    """Minimal stand-in for an lmfit Parameter (value / min / max / vary / brute_step)."""
+
+    def __init__(self, name, value, vary=True, min=-np.inf, max=np.inf, brute_step=None):  # noqa: A002
+        self.name, self.value, self.vary, self.min, self.max, self.brute_step = name, value, vary, min, max, brute_step
+
+    def __float__(self):
+        return float(min(max(self.value, self.min), self.max))
+
+    def __repr__(self):
+        return "<Param %s=%r vary=%s bounds=[%r, %r]>" % (self.name, self.value, self.vary, self.min, self.max)
+
+
+def defineinitialfitparam(tempModPP, readvaryparam=False):
+    """Initial parameters and number of free parameters (measureToAs.py:698-806)."""
+    if readvaryparam:
+        raise NotImplementedError("readvaryparam=True is not implemented in this build")
+    model = tempModPP["model"]
+    K = len([k for k in tempModPP if k.startswith("amp_")])
+    n0 = tempModPP["norm"]["value"]
+    p = {"norm": Param("norm", n0, True, n0 / 100, 500)}
+    if model == "fourier":
+        for k in range(1, K + 1):
+            p["amp_%d" % k] = Param("amp_%d" % k, tempModPP["amp_%d" % k]["value"], False)
+            p["ph_%d" % k] = Param("ph_%d" % k, tempModPP["ph_%d" % k]["value"], False)
+        p["phShift"] = Param("phShift", 0, True, -np.pi, np.pi, 0.05)
+        p["ampShift"] = Param("ampShift", 1, False, 0, 100)
+    elif model in ("vonmises", "cauchy"):
+        for k in range(1, K + 1):
+            for nm in ("amp", "cen", "wid"):
+                key = "%s_%d" % (nm, k)
+                p[key] = Param(key, tempModPP[key]["value"], False)
+        p["phShift"] = Param("phShift", 0, True, -1.5 * np.pi, 1.5 * np.pi, 0.05)
+        p["ampShift"] = Param("ampShift", 1, False, -np.pi, np.pi)
+    else:
+        raise ValueError("Unknown template model. Only fourier, cauchy, or vonmises are supported")
+    return p, 2
+
+
+def _check_opts(varyAmps, readvaryparam):
+    if varyAmps:
+        raise NotImplementedError("varyAmps=True is not implemented in this build")
+    if readvaryparam:
+        raise NotImplementedError("readvaryparam=True is not implemented in this build")
+
+
+def _single(model, tempModPP, phases, exposureInt, phShiftRes, nbrBins, varyAmps, brutemin, readvaryparam,
+            plotLLs, plotPPs):
+    _check_opts(varyAmps, readvaryparam)
+    if str(tempModPP["model"]).lower() != model:
+        raise ValueError("template model %s used with measureToA_%s" % (tempModPP["model"], model))
+    x = np.ascontiguousarray(np.ravel(phases), dtype=np.float64)
+    fit = ToAFitter(x, np.array([0, x.size]), np.array([float(exposureInt)]), tempModPP, phShiftRes, nbrBins)
+    r = fit.fit(brutemin=brutemin)
+    if plotLLs or plotPPs:
+        logger.warning("plotPPs/plotLLs are diagnostic plots and are not produced by this build")
+    return {"phShi": float(r["phShi"][0]), "phShi_LL": float(r["phShi_LL"][0]), "phShi_UL": float(r["phShi_UL"][0]),
+            "reducedChi2": float(r["reducedChi2"][0])}
+
+
+def measureToA_fourier(tempModPP, cycleFoldedPhases, exposureInt, outFile='', phShiftRes=1000, nbrBins=15,
+                       varyAmps=False, brutemin=False, plotPPs=False, plotLLs=False, readvaryparam=False):
+    """Fourier-template ToA (measureToAs.py:254-403); phases in cycles [0,1)."""
+    return _single("fourier", tempModPP, cycleFoldedPhases, exposureInt, phShiftRes, nbrBins, varyAmps, brutemin,
+                   readvaryparam, plotLLs, plotPPs)
+
+
+def measureToA_cauchy(tempModPP, cycleFoldedPhases, exposureInt, outFile='', phShiftRes=1000, nbrBins=15,
+                      varyAmps=False, brutemin=False, plotPPs=False, plotLLs=False, readvaryparam=False):
+    """Wrapped-Cauchy ToA (measureToAs.py:406-548); phases in radians [0,2pi)."""
+    return _single("cauchy", tempModPP, cycleFoldedPhases, exposureInt, phShiftRes, nbrBins, varyAmps, brutemin,
+                   readvaryparam, plotLLs, plotPPs)
+
+
+def measureToA_vonmises(tempModPP, cycleFoldedPhases, exposureInt, outFile='', phShiftRes=1000, nbrBins=15,
+                        varyAmps=False, brutemin=False, plotPPs=False, plotLLs=False, readvaryparam=False):
+    """von Mises ToA (measureToAs.py:551-693); phases in radians [0,2pi)."""
+    return _single("vonmises", tempModPP, cycleFoldedPhases, exposureInt, phShiftRes, nbrBins, varyAmps, brutemin,
+                   readvaryparam, plotLLs, plotPPs)
+
+
+HEADER = ('ToA \t ToA_mid \t ToA_start \t ToA_end \t ToA_lenInt \t ToA_exp \t nbr_events \t count_rate \t phShift'
+          ' \t phShift_LL \t phShift_UL \t Hpower \t redChi2\n')
+
+
+def measure_intervals(TIMEMJD, timMod, tempModPP, starts, ends, exposures, phShiftRes=1000, nbrBins=15,
+                      brutemin=False):
+    """Batched core of measureToAs on in-memory arrays: per interval ToA_mid, fit dict entries, H power."""
+    tmpl = readPPtemplate(tempModPP) if isinstance(tempModPP, str) else tempModPP
+    model = str(tmpl["model"]).lower()
+    sel, mids, offs = [], [], [0]
+    for a, b in zip(starts, ends):
+        t = TIMEMJD[(TIMEMJD >= a) & (TIMEMJD <= b)]  # measureToAs.py:173-174
+        mids.append(((t[-1] - t[0]) / 2) + t[0])       # :182 (IndexError on an empty interval, as the reference)
+        sel.append(t)
+        offs.append(offs[-1] + t.size)
+    allt = np.concatenate(sel)
+    _, folded = calcphase(allt, timMod)
+    if model in ("cauchy", "vonmises"):
+        folded = folded * (2 * np.pi)                  # :195, :200
+    fit = ToAFitter(folded, np.array(offs), np.asarray(exposures, dtype=np.float64), tmpl, phShiftRes, nbrBins)
+    res = fit.fit(brutemin=brutemin)
+    hp = []
+    for t, mid in zip(sel, mids):
+        eph = ephemTmjd(mid, timMod)
+        hp.append(PeriodSearch(t * 86400, np.atleast_1d(eph["freqAtTmjd"]), nbrHarm=5).htest()[0])  # :210-212
+    res["ToA_mid"] = np.array(mids)
+    res["htestPow"] = np.array(hp)
+    return res
+
+
+def measureToAs(evtFile, timMod, tempModPP, toagtifile, eneLow=0.5, eneHigh=10., toaStart=0, toaEnd=None,
+                phShiftRes=1000, nbrBins=15, varyAmps=False, readvaryparam=False, brutemin=False, plotPPs=False,
+                plotLLs=False, toaFile='ToAs', timFile=None):
+    """ToAs of every interval of ``toagtifile`` (measureToAs.py:64-251)."""
+    import pandas as pd
+    _check_opts(varyAmps, readvaryparam)
+    logger.info("\n Running measureToAs with input parameters: evtFile: %s timMod: %s tempModPP: %s toagtifile: %s"
+                " eneLow: %s eneHigh: %s toaStart: %s toaEnd: %s phShiftRes: %s brutemin: %s toaFile: %s",
+                evtFile, timMod, tempModPP, toagtifile, eneLow, eneHigh, toaStart, toaEnd, phShiftRes, brutemin,
+                toaFile)
+    ef = EvtFileOps(evtFile).build_time_energy_df().filtenergy(eneLow=eneLow, eneHigh=eneHigh)
+    TIMEMJD = ef.time_energy_df["TIME"].to_numpy()
+    iv = pd.read_csv(toagtifile, sep=r'\s+', comment='#')
+    st, en = iv['ToA_tstart'].to_numpy(), iv['ToA_tend'].to_numpy()
+    lenInt, expo = iv['ToA_lenInt'].to_numpy(), iv['ToA_exposure'].to_numpy()
+    events, rate = iv['Events'].to_numpy(), iv['ct_rate'].to_numpy()
+    toaEnd = np.size(en) if toaEnd is None else toaEnd + 1  # :147-150 (inclusive end)
+    rng = list(range(toaStart, toaEnd))
+    tmpl = readPPtemplate(tempModPP)
+    logger.info('\n Using best fit model of template {} to measure ToAs'.format(tmpl["model"]))
+    for ii in rng:
+        print('ToA {}'.format(ii))
+    res = measure_intervals(TIMEMJD, timMod, tmpl, st[rng], en[rng], expo[rng], phShiftRes, nbrBins, brutemin)
+    with open(toaFile + '.txt', "w+") as f:
+        f.write(HEADER)
+        for k, ii in enumerate(rng):
+            f.write(str(ii) + '\t' + str(res["ToA_mid"][k]) + '\t' + str(st[ii]) + '\t' + str(en[ii]) + '\t' +
+                    str(lenInt[ii]) + '\t' + str(expo[ii]) + '\t' + str(events[ii]) + '\t' + str(rate[ii]) + '\t' +
+                    str(res["phShi"][k]) + '\t' + str(res["phShi_LL"][k]) + '\t' + str(res["phShi_UL"][k]) + '\t' +
+                    str(res["htestPow"][k]) + '\t' + str(res["reducedChi2"][k]) + '\n')
+    logger.info('\n Wrote ToA properties to {}.txt'.format(toaFile))
+    if timFile is not None:
+        raise NotImplementedError("the .tim writer (timFile) is not implemented in this build")
+    _plot_residuals(res, toaFile)
+    return pd.read_csv(toaFile + '.txt', sep=r'\s+', comment='#')
+
+
+def _plot_residuals(res, outFile):
+    try:
+        import matplotlib
+        matplotlib.use("Agg")
+        import matplotlib.pyplot as plt
+    except Exception:  # pragma: no cover - plotting is optional
+        return
+    fig, ax = plt.subplots(1, figsize=(7, 5))
+    ax.errorbar(res["ToA_mid"], res["phShi"] / (2 * math.pi),
+                yerr=(res["phShi_LL"] / (2 * math.pi), res["phShi_UL"] / (2 * math.pi)), fmt='ok')
+    ax.set_xlabel('Time (MJD)')
+    ax.set_ylabel(r'$\Delta\phi$ (cycles)')
+    fig.tight_layout()
+    fig.savefig(str(outFile) + '_phaseResiduals.pdf', format='pdf')
+    plt.close(fig)
+
+
+def main(argv=None):
+    p = argparse.ArgumentParser(description="Script to measure ToAs from event file")
+    p.add_argument("evtFile", help="Name of a barycentered event file", type=str)
+    p.add_argument("timMod", help="Timing model, Tempo2 .par file should work", type=str)
+    p.add_argument("tempModPP", help="Parameters of template pulse profile", type=str)
+    p.add_argument("toagtifile", help=".txt file with ToA interval information", type=str)
+    p.add_argument("-el", "--enelow", type=float, default=0.5)
+    p.add_argument("-eh", "--enehigh", type=float, default=10)
+    p.add_argument("-ts", "--toaStart", type=int, default=0)
+    p.add_argument("-te", "--toaEnd", type=int, default=None)
+    p.add_argument("-pr", "--phShiftRes", type=int, default=1000)
+    p.add_argument("-nb", "--nbrBins", type=int, default=15)
+    p.add_argument("-va", "--varyAmps", default=False, action=argparse.BooleanOptionalAction)
+    p.add_argument("-rv", "--readvaryparam", default=False, action=argparse.BooleanOptionalAction)
+    p.add_argument("-bm", "--brutemin", default=False, action=argparse.BooleanOptionalAction)
+    p.add_argument("-pp", "--plotPPs", default=False, action=argparse.BooleanOptionalAction)
+    p.add_argument("-ll", "--plotLLs", default=False, action=argparse.BooleanOptionalAction)
+    p.add_argument("-tf", "--toaFile", type=str, default='ToAs')
+    p.add_argument("-mf", "--timFile", type=str, default=None)
+    p.add_argument("-v", "--verbose", action="count", default=0)
+    a = p.parse_args(argv)
+    configure_logging(console_level=("WARNING", "INFO", "DEBUG")[min(a.verbose, 2)],
+                      file_path=f"{a.toaFile}.log", file_level="INFO", force=True)
+    measureToAs(a.evtFile, a.timMod, a.tempModPP, a.toagtifile, a.enelow, a.enehigh, a.toaStart, a.toaEnd,
+                a.phShiftRes, a.nbrBins, a.varyAmps, a.readvaryparam, a.brutemin, a.plotPPs, a.plotLLs, a.toaFile,
+                a.timFile)
+
+
+if __name__ == '__main__':
+    sys.exit(main())

@@ -1,0 +1,173 @@
+"""Thin typed wrappers over the C-ABI (one per entry point of include/crimp_hip.h).
+
+Arrays are NumPy (host; staged by the library, synchronous) or torch CUDA tensors
+(device; enqueued on torch's current stream). Outputs are allocated here when not
+given. These are the only functions that touch the native library.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from . import _native as N
+
+
+def _modeltm(tm):
+    """Pack a timing-model dict (values or {value, flag}) into crimp_timing_model."""
+    def val(x):
+        if isinstance(x, dict) and "value" in x and "flag" in x:  # readtimingmodel.py:309-321
+            return x["value"]
+        return x
+    d = {k: val(v) for k, v in tm.items()}
+    m = N.TimingModel()
+    m.pepoch = float(d["PEPOCH"])
+    for i in range(13):
+        m.f[i] = float(d.get("F%d" % i, 0.0))
+    ngl = sum(1 for k in d if k.startswith("GLEP_"))  # calcphase.py:94
+    if ngl > N.MAX_GLITCH:
+        raise ValueError("at most %d glitches supported" % N.MAX_GLITCH)
+    m.n_glitch = ngl
+    for j in range(1, ngl + 1):
+        row = [d["GLEP_%d" % j]] + [d.get("%s_%d" % (b, j), 0.0) for b in ("GLPH", "GLF0", "GLF1", "GLF2", "GLF0D", "GLTD")]
+        for c in range(7):
+            m.glitch[j - 1][c] = float(row[c])
+    nw = sum(1 for k in d if k.startswith("WAVE"))  # calcphase.py:135
+    if nw:
+        nharm = nw - 2  # calcphase.py:142 assumes WAVEEPOCH and WAVE_OM are present
+        if nharm > N.MAX_WAVE:
+            raise ValueError("at most %d wave harmonics supported" % N.MAX_WAVE)
+        m.wave_epoch = float(d["WAVEEPOCH"])
+        m.wave_om = float(d["WAVE_OM"])
+        m.n_wave = max(nharm, 0)
+        for j in range(1, nharm + 1):
+            m.wave_ab[j - 1][0] = float(d["WAVE%d" % j]["A"])
+            m.wave_ab[j - 1][1] = float(d["WAVE%d" % j]["B"])
+    return m
+
+
+def calcphase(t_mjd, timing_model_dict, parts=7, total=None, folded=None, want_folded=True):
+    L = N.load()
+    b = N.Buffers()
+    tp = b.arg(t_mjd, np.float64)
+    n = int(t_mjd.numel() if N._is_torch(t_mjd) else np.size(t_mjd))
+    if total is None:
+        total = _empty_like_input(t_mjd, n, b)
+    if folded is None and want_folded:
+        folded = _empty_like_input(t_mjd, n, b)
+    op = b.arg(total, np.float64, writable=True)
+    fp = b.arg(folded, np.float64, writable=True) if folded is not None else None
+    m = _modeltm(timing_model_dict)
+    N.check(L.crimp_calcphase(tp, n, ctypes.byref(m), int(parts), op, fp, b.flags(), b.stream()))
+    return total, folded
+
+
+def _empty_like_input(a, n, b, dtype=np.float64):
+    if b.device:
+        import torch
+        return torch.empty(n, dtype=torch.float64 if dtype == np.float64 else torch.int64, device=a.device)
+    return np.empty(n, dtype=dtype)
+
+
+def search_flags():
+    """Extra search flags from the environment (CRIMP_SEARCH=direct|mfma, CRIMP_SINCOS=hw)."""
+    f = 0
+    mode = os.environ.get("CRIMP_SEARCH", "").lower()
+    if mode == "direct":
+        f |= N.FLAG_FORCE_DIRECT
+    elif mode == "mfma":
+        f |= N.FLAG_FORCE_MFMA
+    if os.environ.get("CRIMP_SINCOS", "").lower() == "hw":
+        f |= N.FLAG_HW_SINCOS
+    return f
+
+
+def search(t, t0, freq, nharm, stat, log10_negfdot=None, first=0, count=None, out=None, flags=0):
+    """Z^2 / H over the fd-outer grid; computes flat trials [first, first+count)."""
+    L = N.load()
+    b = N.Buffers()
+    tp = b.arg(t, np.float64)
+    fp = b.arg(freq, np.float64)
+    dp = b.arg(log10_negfdot, np.float64, allow_none=True)
+    n = int(t.numel() if N._is_torch(t) else np.size(t))
+    nf = int(freq.numel() if N._is_torch(freq) else np.size(freq))
+    nfd = 0 if log10_negfdot is None else int(log10_negfdot.numel() if N._is_torch(log10_negfdot)
+                                               else np.size(log10_negfdot))
+    total = (nfd if nfd else 1) * nf
+    if count is None:
+        count = total - first
+    if out is None:
+        out = _empty_like_input(t, count, b)
+    op = b.arg(out, np.float64, writable=True)
+    N.check(L.crimp_search(tp, n, float(t0), fp, nf, dp, nfd, int(nharm), int(stat), int(first), int(count), op,
+                           b.flags(flags | search_flags()), b.stream()))
+    return out
+
+
+def make_template(model, amps, locs, wids=None, amp_shift=1.0):
+    """crimp_template from arrays (model in {'fourier','cauchy','vonmises'})."""
+    from scipy.special import i0
+    t = N.Template()
+    t.model = N.MODEL_IDS[model]
+    K = len(amps)
+    if not 1 <= K <= N.MAX_COMP:
+        raise ValueError("template needs 1..%d components" % N.MAX_COMP)
+    t.ncomp = K
+    for j in range(K):
+        t.amp[j] = float(amps[j])
+        t.loc[j] = float(locs[j])
+        if wids is not None:
+            t.wid[j] = float(wids[j])
+            t.i0[j] = float(i0(1.0 / float(wids[j]) ** 2)) if model == "vonmises" else 1.0
+    t.amp_shift = float(amp_shift)
+    return t
+
+
+def toa_points(x, offsets, tpl, pt_interval, pt_norm, pt_phi):
+    """[npts, 8] sums (see crimp_toa_points) in fp64 on host."""
+    L = N.load()
+    b = N.Buffers()
+    xp = b.arg(x, np.float64)
+    op = b.arg(offsets, np.int64)
+    ip = b.arg(pt_interval, np.int64)
+    npp = b.arg(pt_norm, np.float64)
+    pp = b.arg(pt_phi, np.float64)
+    npts = int(pt_norm.numel() if N._is_torch(pt_norm) else np.size(pt_norm))
+    nint = int((offsets.numel() if N._is_torch(offsets) else np.size(offsets)) - 1)
+    out = _empty_like_input(x, npts * 8, b)
+    outp = b.arg(out, np.float64, writable=True)
+    N.check(L.crimp_toa_points(xp, op, nint, ctypes.byref(tpl), ip, npp, pp, npts, outp, b.flags(), b.stream()))
+    return out.reshape(npts, 8)
+
+
+def toa_grid(x, offsets, tpl, norms, phis):
+    """lnsum [nint, nnorm, nphi], hmin [nint, nphi] of the brute grid (fp64 accumulation)."""
+    L = N.load()
+    b = N.Buffers()
+    xp = b.arg(x, np.float64)
+    op = b.arg(offsets, np.int64)
+    nint = int((offsets.numel() if N._is_torch(offsets) else np.size(offsets)) - 1)
+    norms = np.asarray(norms, dtype=np.float64) if not N._is_torch(norms) else norms
+    nnorm = int(norms.shape[-1])
+    np_ = b.arg(norms, np.float64)
+    pp = b.arg(phis, np.float64)
+    nphi = int(phis.numel() if N._is_torch(phis) else np.size(phis))
+    ln = _empty_like_input(x, nint * nnorm * nphi, b)
+    hm = _empty_like_input(x, nint * nphi, b)
+    lp = b.arg(ln, np.float64, writable=True)
+    hp = b.arg(hm, np.float64, writable=True)
+    N.check(L.crimp_toa_grid(xp, op, nint, ctypes.byref(tpl), np_, nnorm, pp, nphi, lp, hp, b.flags(), b.stream()))
+    return ln.reshape(nint, nnorm, nphi), hm.reshape(nint, nphi)
+
+
+def binphases_counts(x, offsets, edges):
+    L = N.load()
+    b = N.Buffers()
+    xp = b.arg(x, np.float64)
+    op = b.arg(offsets, np.int64)
+    ep = b.arg(edges, np.float64)
+    nint = int((offsets.numel() if N._is_torch(offsets) else np.size(offsets)) - 1)
+    nb = int((edges.numel() if N._is_torch(edges) else np.size(edges)) - 1)
+    out = _empty_like_input(x, nint * nb, b, dtype=np.int64)
+    cp = b.arg(out, np.int64, writable=True)
+    N.check(L.crimp_binphases(xp, op, nint, ep, nb, cp, b.flags(), b.stream()))
+    return out.reshape(nint, nb)

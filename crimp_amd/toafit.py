@@ -1,0 +1,310 @@
+"""Batched ToA phase-shift fits on the MI355X (the measureToA_* driver).
+
+Restates, for every ToA interval at once, what CRIMP v2.3.0
+``measureToAs.py:254-403`` (Fourier), ``:406-548`` (Cauchy) and ``:551-693``
+(von Mises) do with lmfit, targeting the same optimum rather than lmfit's
+iterates:
+
+1. optional brute grid (``-bm``): lmfit's ``brute`` over norm x phShift with
+   scipy's ``mgrid`` lattices -- 20 norms on [norm0/100, 500] and phShift =
+   k*0.05 - bound (126 points for Fourier, 189 for Cauchy / von Mises), LL on the
+   device (``crimp_toa_grid``, fp32 model/log, fp64 sums), first maximum in
+   norm-outer order as scipy.optimize.brute picks it;
+2. the local maximum of the extended LL in (norm, phShift) from the brute point
+   (or from (norm0, 0) without ``-bm``, where lmfit starts Nelder-Mead): a damped
+   2-D Newton ascent on fp64 device sums (``crimp_toa_points``: LL, gradient and
+   Hessian in one pass over the photons);
+3. the 1-sigma scan: phShift = best -/+ k*2*pi/phShiftRes with lmfit's clip-to-
+   bound behaviour, norm re-profiled (1-D Newton) at every step, stop at the first
+   LLmax - LL > 0.5*chi2.ppf(0.6827, 1); sigma = (k+1)*step + step/2, capped at
+   phShiftRes/2 steps (:330-376);
+4. redChi2 from the ``binphases`` profile (device histogram, numpy.histogram
+   edge semantics) against the best-fit curve, dof = nbrBins - 2 (:385-393).
+
+Only ``readvaryparam=False, varyAmps=False`` (the CLI defaults) are implemented.
+"""
+import math
+
+import numpy as np
+
+from . import ops
+from ._native import _is_torch
+
+CHI2_1SIG_1DOF = 0.500021713558733  # 0.5 * scipy.stats.chi2.ppf(0.6827, 1)   (measureToAs.py:324)
+TWO_PI = 2.0 * math.pi
+
+
+def _vals(tmpl, prefix, K):
+    out = []
+    for j in range(1, K + 1):
+        v = tmpl["%s_%d" % (prefix, j)]
+        out.append(float(v["value"] if isinstance(v, dict) else v))
+    return out
+
+
+class ToAFitter:
+    """Fits all intervals of one concatenated folded-phase array together."""
+
+    def __init__(self, x, offsets, exposure, tmpl, ph_shift_res=1000, nbr_bins=15, device=None):
+        self.model = str(tmpl["model"]).lower()
+        if self.model not in ("fourier", "cauchy", "vonmises"):
+            raise ValueError("Unknown template model. Only fourier, cauchy, or vonmises are supported")
+        K = len([k for k in tmpl if k.startswith("amp_")])
+        self.K = K
+        amps = _vals(tmpl, "amp", K)
+        if self.model == "fourier":
+            locs, wids = _vals(tmpl, "ph", K), None
+        else:
+            locs, wids = _vals(tmpl, "cen", K), _vals(tmpl, "wid", K)
+        self.amps = np.array(amps)
+        self.tpl = ops.make_template(self.model, amps, locs, wids, 1.0)
+        self.tmpl = tmpl
+        nv = tmpl["norm"]
+        self.norm0 = float(nv["value"] if isinstance(nv, dict) else nv)
+        self.lo, self.hi = self.norm0 / 100.0, 500.0                          # measureToAs.py:715-716, :757-758
+        self.pb = math.pi if self.model == "fourier" else 1.5 * math.pi       # :722, :767
+        self.res = int(ph_shift_res)
+        self.nbins = int(nbr_bins)
+        self.E = np.asarray(exposure, dtype=np.float64).reshape(-1)
+        off = np.asarray(offsets.cpu().numpy() if _is_torch(offsets) else offsets, dtype=np.int64)
+        self.offsets_h = off
+        self.nint = off.size - 1
+        if self.E.size != self.nint:
+            raise ValueError("one exposure per interval required")
+        self.N = np.diff(off).astype(np.float64)
+        if np.any(self.N <= 0):
+            raise IndexError("a ToA interval holds no photons (measureToAs.py:182 would fail on TIME_toa[-1])")
+        self.x_h = None if _is_torch(x) else np.ascontiguousarray(x, dtype=np.float64)
+        self.x, self.offsets = self._to_device(x, off, device)
+
+    # ------------------------------------------------------------------ device plumbing
+    def _to_device(self, x, off, device):
+        if _is_torch(x):
+            import torch
+            return x.reshape(-1).to(torch.float64).contiguous(), torch.as_tensor(off, device=x.device)
+        try:
+            import torch
+            if torch.cuda.is_available():
+                dev = torch.device(device if device is not None else "cuda")
+                return (torch.as_tensor(np.ascontiguousarray(x, dtype=np.float64), device=dev),
+                        torch.as_tensor(off, device=dev))
+        except ImportError:  # pragma: no cover
+            pass
+        return np.ascontiguousarray(x, dtype=np.float64), off
+
+    def _arr(self, a, dtype):
+        if _is_torch(self.x):
+            import torch
+            return torch.as_tensor(np.ascontiguousarray(a, dtype=dtype), device=self.x.device)
+        return np.ascontiguousarray(a, dtype=dtype)
+
+    # ------------------------------------------------------------------ evaluations
+    def _F(self, n):
+        return n if self.model == "fourier" else TWO_PI * n + self.amps.sum()
+
+    def evaluate(self, iv, n, phi):
+        """LL, gradient (2) and Hessian (3) of the reference extended LL at points."""
+        iv = np.asarray(iv, dtype=np.int64)
+        n = np.asarray(n, dtype=np.float64)
+        phi = np.asarray(phi, dtype=np.float64)
+        s = ops.toa_points(self.x, self.offsets, self.tpl, self._arr(iv, np.int64), self._arr(n, np.float64),
+                           self._arr(phi, np.float64))
+        if _is_torch(s):
+            s = s.cpu().numpy()
+        s = np.asarray(s)
+        N, E = s[:, 7], self.E[iv]
+        F = self._F(n)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            if self.model == "fourier":
+                ll = -n * E + N * np.log(n * E) + (s[:, 0] - N * np.log(n))
+            else:
+                ll = -F * E / TWO_PI + N * np.log(F * E / TWO_PI) + (s[:, 0] - N * np.log(F))
+        ll = np.where(s[:, 6] / F > 0, ll, -np.inf)
+        g = np.stack([-E + s[:, 1], s[:, 2]], axis=1)
+        H = np.stack([s[:, 3], s[:, 4], s[:, 5]], axis=1)
+        return ll, g, H
+
+    # ------------------------------------------------------------------ step 1: brute grid
+    def brute(self):
+        nphi = int(math.ceil((2 * self.pb) / (0.05 * 1.0)))
+        phis = np.arange(nphi) * 0.05 + (-self.pb)                            # numpy mgrid lattice
+        norms = np.arange(20) * ((self.hi - self.lo) / float(20 - 1)) + self.lo
+        ln, hmin = ops.toa_grid(self.x, self.offsets, self.tpl, self._arr(np.tile(norms, (self.nint, 1)), np.float64),
+                                self._arr(phis, np.float64))
+        if _is_torch(ln):
+            ln, hmin = ln.cpu().numpy(), hmin.cpu().numpy()
+        N = self.N[:, None, None]
+        E = self.E[:, None, None]
+        nn = norms[None, :, None]
+        F = self._F(nn)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            if self.model == "fourier":
+                ll = -nn * E + N * np.log(nn * E) + (ln - N * np.log(nn))
+            else:
+                ll = -F * E / TWO_PI + N * np.log(F * E / TWO_PI) + (ln - N * np.log(F))
+        valid = (hmin[:, None, :] + nn) > 0
+        ll = np.where(valid & np.isfinite(ll), ll, -np.inf)
+        flat = ll.reshape(self.nint, -1)
+        idx = np.argmax(flat, axis=1)                                          # first maximum, norm-outer
+        a, b = np.unravel_index(idx, (20, nphi))
+        return norms[a], phis[b]
+
+    # ------------------------------------------------------------------ step 2: 2-D ascent
+    def maximise(self, n0, phi0, max_iter=60):
+        n = np.array(n0, dtype=np.float64)
+        phi = np.array(phi0, dtype=np.float64)
+        iv_all = np.arange(self.nint)
+        ll, g, H = self.evaluate(iv_all, n, phi)
+        active = np.ones(self.nint, dtype=bool)
+        for _ in range(max_iter):
+            act = np.nonzero(active)[0]
+            if act.size == 0:
+                break
+            dn, dp = self._newton_step(n[act], g[act], H[act])
+            t = np.ones(act.size)
+            pending = np.ones(act.size, dtype=bool)
+            new_n, new_p = n[act].copy(), phi[act].copy()
+            new_ll, new_g, new_H = ll[act].copy(), g[act].copy(), H[act].copy()
+            for _ls in range(40):
+                idx = np.nonzero(pending)[0]
+                if idx.size == 0:
+                    break
+                tn = np.clip(n[act][idx] + t[idx] * dn[idx], self.lo, self.hi)
+                tp = np.clip(phi[act][idx] + t[idx] * dp[idx], -self.pb, self.pb)
+                l2, g2, H2 = self.evaluate(act[idx], tn, tp)
+                ok = np.isfinite(l2) & (l2 >= ll[act][idx] - 1e-12 * np.abs(ll[act][idx]))
+                acc = idx[ok]
+                new_n[acc], new_p[acc] = tn[ok], tp[ok]
+                new_ll[acc], new_g[acc], new_H[acc] = l2[ok], g2[ok], H2[ok]
+                pending[acc] = False
+                t[idx[~ok]] *= 0.5
+            moved_n = np.abs(new_n - n[act])
+            moved_p = np.abs(new_p - phi[act])
+            n[act], phi[act] = new_n, new_p
+            ll[act], g[act], H[act] = new_ll, new_g, new_H
+            done = (moved_p < 1e-12) & (moved_n < 1e-12 * np.maximum(1.0, np.abs(new_n)))
+            done |= pending  # line search exhausted: at the (numerical) optimum
+            active[act[done]] = False
+        return n, phi, ll
+
+    def _newton_step(self, n, g, H):
+        hnn, hnp, hpp = H[:, 0], H[:, 1], H[:, 2]
+        # shift the Hessian to be negative definite (Levenberg damping), then solve
+        tr = hnn + hpp
+        det = hnn * hpp - hnp * hnp
+        lam_max = 0.5 * tr + np.sqrt(np.maximum(0.25 * tr * tr - det, 0.0))   # largest eigenvalue
+        shift = np.where(lam_max < 0, 0.0, lam_max * 1.5 + 1e-6 * (np.abs(hnn) + np.abs(hpp)) + 1e-12)
+        a, c = hnn - shift, hpp - shift
+        det2 = a * c - hnp * hnp
+        dn = -(c * g[:, 0] - hnp * g[:, 1]) / det2
+        dp = -(a * g[:, 1] - hnp * g[:, 0]) / det2
+        # trust region: at most 0.05 rad in phShift and half the norm per step
+        sc = np.minimum(1.0, 0.05 / np.maximum(np.abs(dp), 1e-300))
+        sc = np.minimum(sc, 0.5 * np.abs(n) / np.maximum(np.abs(dn), 1e-300))
+        return dn * sc, dp * sc
+
+    def profile_norm(self, iv, phi, n_start, max_iter=30):
+        """max over norm in [lo, hi] of LL(norm, phi) at fixed phi (1-D Newton, concave)."""
+        iv = np.asarray(iv)
+        n = np.clip(np.array(n_start, dtype=np.float64), self.lo, self.hi)
+        ll, g, H = self.evaluate(iv, n, phi)
+        for _ in range(max_iter):
+            bad = ~np.isfinite(ll)
+            step = np.where(H[:, 0] < 0, -g[:, 0] / np.where(H[:, 0] < 0, H[:, 0], -1.0), 0.1 * n)
+            step = np.clip(step, -0.5 * n, 0.5 * n)
+            step = np.where(bad, 0.5 * n, step)  # infeasible: model <= 0 somewhere, raise the norm
+            nn = np.clip(n + step, self.lo, self.hi)
+            l2, g2, H2 = self.evaluate(iv, nn, phi)
+            worse = np.isfinite(ll) & (~np.isfinite(l2) | (l2 < ll - 1e-12 * np.abs(ll)))
+            if np.any(worse):  # damp the few overshoots
+                nn[worse] = np.clip(n[worse] + 0.25 * step[worse], self.lo, self.hi)
+                l3, g3, H3 = self.evaluate(iv[worse], nn[worse], phi[worse])
+                l2[worse], g2[worse], H2[worse] = l3, g3, H3
+            conv = np.abs(nn - n) <= 1e-13 * np.maximum(1.0, n)
+            n, ll, g, H = nn, l2, g2, H2
+            if np.all(conv):
+                break
+        return n, ll
+
+    # ------------------------------------------------------------------ step 3: error scan
+    def _scan_phases(self, phi_hat, side, ks):
+        """phShift values the lmfit loop evaluates at steps ks (clip-to-bound semantics)."""
+        step = TWO_PI / self.res
+        target = phi_hat[:, None] + side * ks[None, :] * step
+        if self.model == "fourier":
+            # the first step past +-pi is clipped to the bound; later steps move the bound (:332-334, :357-359)
+            past = (target <= -math.pi) if side < 0 else (target >= math.pi)
+            first = np.where(past.any(axis=1), past.argmax(axis=1), -1)
+            cur = target.copy()
+            rows = np.nonzero(first >= 0)[0]
+            cur[rows, first[rows]] = -math.pi if side < 0 else math.pi
+            return cur
+        return np.clip(target, -self.pb, self.pb)
+
+    def error_scan(self, phi_hat, n_hat, ll_max):
+        step = TWO_PI / self.res
+        kcap = self.res / 2.0
+        out = {}
+        for side in (-1, 1):
+            kk_final = np.full(self.nint, -1, dtype=np.int64)
+            k0 = 1
+            batch = 12
+            while True:
+                todo = np.nonzero(kk_final < 0)[0]
+                if todo.size == 0:
+                    break
+                ks = np.arange(k0, k0 + batch)
+                phis = self._scan_phases(phi_hat[todo], side, ks)
+                iv = np.repeat(todo, ks.size)
+                nprof, llk = self.profile_norm(iv, phis.reshape(-1), np.repeat(n_hat[todo], ks.size))
+                diff = (ll_max[todo][:, None] - llk.reshape(todo.size, ks.size))
+                cross = diff > CHI2_1SIG_1DOF
+                # the loop stops at the first crossing, or once kk (= k+1) exceeds phShiftRes/2
+                stop = cross | ((ks[None, :] + 1) > kcap)
+                hit = stop.any(axis=1)
+                first = stop.argmax(axis=1)
+                kk_final[todo[hit]] = ks[first[hit]] + 1
+                k0 += batch
+                batch = min(batch * 2, 256)
+            out[side] = kk_final * step + step / 2
+        return out[-1], out[1]
+
+    # ------------------------------------------------------------------ step 4: redChi2
+    def reduced_chi2(self, n_hat, phi_hat, nfree=2):
+        upper = 1.0 if self.model == "fourier" else TWO_PI
+        edges = np.linspace(0, upper, self.nbins + 1, endpoint=True)
+        cts = ops.binphases_counts(self.x, self.offsets, self._arr(edges, np.float64))
+        if _is_torch(cts):
+            cts = cts.cpu().numpy()
+        cts = np.asarray(cts, dtype=np.float64)
+        pp = np.linspace(0, upper, self.nbins, endpoint=False) + (upper / self.nbins) / 2
+        rate = cts / (self.E[:, None] / self.nbins)
+        err = np.sqrt(cts) / (self.E[:, None] / self.nbins)
+        model = self.curve(n_hat[:, None], phi_hat[:, None], pp[None, :])
+        with np.errstate(divide="ignore", invalid="ignore"):
+            chi2 = np.sum(np.divide((model - rate) ** 2, err ** 2), axis=1)
+        return np.divide(chi2, self.nbins - nfree)
+
+    def curve(self, n, phi, xx):
+        y = np.zeros(np.broadcast(n, xx).shape) + n
+        t = self.tpl
+        for j in range(self.K):
+            if self.model == "fourier":
+                y = y + t.amp[j] * np.cos((j + 1) * 2 * np.pi * xx + t.loc[j] - (j + 1) * phi)
+            elif self.model == "cauchy":
+                y = y + (t.amp[j] / (2 * np.pi)) * (np.sinh(t.wid[j]) / (np.cosh(t.wid[j]) - np.cos(xx - t.loc[j] - phi)))
+            else:
+                y = y + (t.amp[j] / (2 * np.pi * t.i0[j])) * np.exp((1 / t.wid[j] ** 2) * np.cos(xx - t.loc[j] - phi))
+        return y
+
+    # ------------------------------------------------------------------ driver
+    def fit(self, brutemin=False):
+        if brutemin:
+            n0, p0 = self.brute()
+        else:
+            n0, p0 = np.full(self.nint, self.norm0), np.zeros(self.nint)
+        n_hat, phi_hat, ll_max = self.maximise(n0, p0)
+        lo_err, up_err = self.error_scan(phi_hat, n_hat, ll_max)
+        rchi2 = self.reduced_chi2(n_hat, phi_hat)
+        return {"phShi": phi_hat, "phShi_LL": lo_err, "phShi_UL": up_err, "reducedChi2": rchi2, "norm": n_hat,
+                "LLmax": ll_max}

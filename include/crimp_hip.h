@@ -1,0 +1,125 @@
+/*
+ * crimp_hip.h -- C-ABI of the MI355X-native CRIMP photon hot path (libcrimp_hip.so).
+ *
+ * The reference (georgeyounes/CRIMP v2.3.0) is pure Python with no FFI; its
+ * "operator API" is the Python functions listed per entry point below. Each entry
+ * point replaces the NumPy inner loops of one of them; the Python drop-ins in
+ * crimp_amd/ keep the reference signatures and call these through ctypes.
+ *
+ * Conventions (all entry points):
+ *   - return 0 (CRIMP_OK) or a negative status; crimp_last_error() gives the text
+ *     (thread-local, valid until the next call on the same thread);
+ *   - every buffer is caller-owned; with CRIMP_FLAG_DEVICE_PTRS all array
+ *     arguments are device pointers on the current HIP device, otherwise they are
+ *     host pointers and the library stages them through device memory itself;
+ *   - `stream` is a hipStream_t (NULL = the null stream). Host-pointer calls are
+ *     synchronous; device-pointer calls return after enqueueing unless
+ *     CRIMP_FLAG_SYNC is given;
+ *   - calls are serialised per device (internal mutex); the ctypes layer releases
+ *     the GIL around them.
+ */
+#ifndef CRIMP_HIP_H
+#define CRIMP_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CRIMP_OK 0
+#define CRIMP_ERR_ARG (-1)
+#define CRIMP_ERR_HIP (-2)
+#define CRIMP_ERR_NODEV (-3)
+
+#define CRIMP_FLAG_DEVICE_PTRS 1u  /* array arguments are device pointers */
+#define CRIMP_FLAG_SYNC 2u         /* synchronise the stream before returning */
+#define CRIMP_FLAG_FORCE_DIRECT 4u /* periodicity search: never use the factorised MFMA kernel */
+#define CRIMP_FLAG_FORCE_MFMA 8u   /* periodicity search: fail unless the factorised kernel applies */
+#define CRIMP_FLAG_HW_SINCOS 16u   /* direct search: hardware v_sin/v_cos instead of the polynomial */
+
+#define CRIMP_STAT_Z2 0 /* Z^2_m  (periodsearch.py:57-71, :73-106) */
+#define CRIMP_STAT_H 1  /* H-test (periodsearch.py:109-125)         */
+
+#define CRIMP_MODEL_FOURIER 0  /* templatemodels.py:24-121, x in cycles  */
+#define CRIMP_MODEL_CAUCHY 1   /* templatemodels.py:124-226, x in rad    */
+#define CRIMP_MODEL_VONMISES 2 /* templatemodels.py:229-329, x in rad    */
+
+#define CRIMP_MAX_GLITCH 32
+#define CRIMP_MAX_WAVE 64
+#define CRIMP_MAX_COMP 16
+
+/* Values of a .par timing model as calcphase consumes them
+ * (readtimingmodel.py:212-233; calcphase.py:73-149). */
+typedef struct crimp_timing_model {
+    double pepoch;                          /* PEPOCH (MJD) */
+    double f[13];                           /* F0..F12; absent ones 0 */
+    int32_t n_glitch;                       /* glitches 1..n (count of GLEP_ keys, calcphase.py:94) */
+    double glitch[CRIMP_MAX_GLITCH][7];     /* GLEP, GLPH, GLF0, GLF1, GLF2, GLF0D, GLTD */
+    int32_t n_wave;                         /* WAVE harmonics used = (#WAVE* keys) - 2 (calcphase.py:142) */
+    double wave_epoch, wave_om;             /* WAVEEPOCH (MJD), WAVE_OM (rad/day) */
+    double wave_ab[CRIMP_MAX_WAVE][2];      /* WAVEj A, B */
+} crimp_timing_model;
+
+/* A pulse-profile template (readPPtemplate.py:15-166) with its fixed shape. */
+typedef struct crimp_template {
+    int32_t model;                   /* CRIMP_MODEL_* */
+    int32_t ncomp;                   /* harmonics / components, 1..CRIMP_MAX_COMP */
+    double amp[CRIMP_MAX_COMP];      /* amp_j */
+    double loc[CRIMP_MAX_COMP];      /* ph_j (fourier) or cen_j (cauchy, vonmises) */
+    double wid[CRIMP_MAX_COMP];      /* wid_j (cauchy, vonmises) */
+    double i0[CRIMP_MAX_COMP];       /* scipy.special.i0(1/wid_j^2) (vonmises) */
+    double amp_shift;                /* ampShift (1 unless varied) */
+} crimp_template;
+
+/* Library identification. */
+int crimp_version(void);
+const char* crimp_last_error(void);
+int crimp_device_count(int32_t* count);
+
+/* calcphase(timeMJD, timMod) -> (total, folded)   [calcphase.py:152-176]
+ * parts: bit0 Taylor expansion (:73-85), bit1 glitches (:87-126), bit2 waves (:128-149);
+ * 7 = calcphase(). folded may be NULL. */
+int crimp_calcphase(const double* t_mjd, int64_t n, const crimp_timing_model* model, int32_t parts,
+                    double* total, double* folded, uint32_t flags, void* stream);
+
+/* PeriodSearch(time, freq, nbrHarm).ztest()/.htest()/.twod_ztest(freq_dot)
+ *   [periodsearch.py:40-125]
+ * t: photon times (s) [n]; t0: (t[0]+t[n-1])/2 as periodsearch.py:54 (passed explicitly so that
+ * shards of one search share it); freq [nf] (Hz); log10_negfdot [nfd] or NULL (1-D); the trial
+ * grid is fd-outer/f-inner (periodsearch.py:264-278) and this call computes flat trials
+ * [first, first+count) of it into out[count]. stat = CRIMP_STAT_Z2 or CRIMP_STAT_H (the latter
+ * over the 2-D grid is this library's extension). */
+int crimp_search(const double* t, int64_t n, double t0, const double* freq, int64_t nf,
+                 const double* log10_negfdot, int64_t nfd, int32_t nharm, int32_t stat, int64_t first,
+                 int64_t count, double* out, uint32_t flags, void* stream);
+
+/* Fourier|WrappedCauchy|VonMises(theta, x).loglikelihood{FS,CA,VM}normalized(exposure) and its
+ * (norm, phShift) derivatives at arbitrary points   [templatemodels.py:98-121, 201-226, 306-329].
+ * x: folded phases of all intervals concatenated, interval i = x[offsets[i] : offsets[i+1]]
+ * (cycles for fourier, radians otherwise). Point p is (pt_interval[p], pt_norm[p], pt_phi[p]).
+ * out[p*8 + 0..7] = { sum ln(norm + h), sum q, sum h' q, -sum q^2, -sum h' q^2,
+ *                     sum (h'' q - h'^2 q^2), min(norm + h), N }   with q = 1/(norm + h),
+ * h = model - norm, primes = d/dphShift. fp64 throughout. Host assembles the reference LL. */
+int crimp_toa_points(const double* x, const int64_t* offsets, int64_t nint, const crimp_template* tpl,
+                     const int64_t* pt_interval, const double* pt_norm, const double* pt_phi, int64_t npts,
+                     double* out, uint32_t flags, void* stream);
+
+/* lmfit 'brute' grid of measureToA_* (measureToAs.py:292-295, defineinitialfitparam :698-806):
+ * for every interval i, norm a, phShift b:
+ *   lnsum[(i*nnorm + a)*nphi + b] = sum_photons ln(norm[i*nnorm+a] + h(x; phi[b]))
+ *   hmin[i*nphi + b]              = min_photons h(x; phi[b])
+ * fp32 model + logarithm, fp64 accumulation. */
+int crimp_toa_grid(const double* x, const int64_t* offsets, int64_t nint, const crimp_template* tpl,
+                   const double* norm, int64_t nnorm, const double* phi, int64_t nphi, double* lnsum,
+                   double* hmin, uint32_t flags, void* stream);
+
+/* binphases(phases, nbrBins) counts per interval   [binphases.py:9-39]:
+ * np.histogram(x, bins=edges) semantics with edges[nbins+1] (numpy.linspace). counts[i*nbins+b]. */
+int crimp_binphases(const double* x, const int64_t* offsets, int64_t nint, const double* edges, int32_t nbins,
+                    int64_t* counts, uint32_t flags, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CRIMP_HIP_H */

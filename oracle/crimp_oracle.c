@@ -1,0 +1,272 @@
+/*
+ * crimp_oracle.c -- CPU restatement of CRIMP's photon hot path (TEST INFRASTRUCTURE).
+ *
+ * This file is the parity CHECKER, never the product: only tests/, the
+ * __graft_entry__.smoke() check and bench.py's cpu_baseline leg may load it.
+ * The shipped path (crimp_amd/, libcrimp_hip.so) must never link or call it.
+ *
+ * Plain fp64 C, one function per reference routine, each citing the reference
+ * file:line it restates (paths relative to georgeyounes/CRIMP v2.3.0, src/crimp/).
+ * Pinned against the reference's own outputs: tests/golden/ fixtures were produced
+ * by importing the reference (tests/golden/gen_golden.py) and the worked-example
+ * table data/ToAs_2259.txt rows 35-41.
+ *
+ * OpenMP parallelises the trial axis of the periodicity searches (the CPU
+ * baseline timed by bench.py); every per-trial sum is computed serially in
+ * photon order, so results do not depend on the thread count.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define ORC_PI 3.141592653589793238462643383279502884
+
+/* ------------------------------------------------------------------------ */
+/* Timing model (values of the .par dictionary, readtimingmodel.py:212-233)  */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+    double pepoch;
+    double f[13];              /* F0..F12, missing ones are 0 (readtimingmodel.py:64-65) */
+    int32_t n_glitch;
+    double glitch[32][7];      /* GLEP, GLPH, GLF0, GLF1, GLF2, GLF0D, GLTD (calcphase.py:99-110) */
+    int32_t n_wave;            /* number of WAVEj harmonics used (calcphase.py:135,142) */
+    double wave_epoch, wave_om;
+    double wave_ab[64][2];
+} orc_model;
+
+int orc_max_threads(void) {
+#ifdef _OPENMP
+    return omp_get_max_threads();
+#else
+    return 1;
+#endif
+}
+
+void orc_set_threads(int n) {
+#ifdef _OPENMP
+    if (n > 0) omp_set_num_threads(n);
+#else
+    (void)n;
+#endif
+}
+
+/* calcphase.py:73-85  phases_te = sum_{n=1..13} (1/n!) F_{n-1} dt^n, dt=(t-PEPOCH)*86400,
+ * summed in increasing n with dt**n as in the reference (pow). */
+static double te_phase(const orc_model* m, double t) {
+    double dt = (t - m->pepoch) * 86400.0;
+    double acc = 0.0, fact = 1.0;
+    for (int n = 1; n <= 13; ++n) {
+        fact *= (double)n;
+        acc += (1.0 / fact) * m->f[n - 1] * pow(dt, (double)n);
+    }
+    return acc;
+}
+
+/* calcphase.py:87-126 (glitches): mask t >= GLEP; GLTD == 0 disables the exp term (:115). */
+static double gl_phase(const orc_model* m, double t) {
+    double acc = 0.0;
+    for (int j = 0; j < m->n_glitch; ++j) {
+        const double* g = m->glitch[j];
+        if (!(t >= g[0])) continue;
+        double dts = (t - g[0]) * 86400.0;
+        double ex = (g[6] == 0.0) ? 0.0 : (g[6] * 86400.0) * (1.0 - exp(-(t - g[0]) / g[6]));
+        acc += g[1] + g[2] * dts + 0.5 * g[3] * dts * dts + (1.0 / 6.0) * g[4] * dts * dts * dts + g[5] * ex;
+    }
+    return acc;
+}
+
+/* calcphase.py:128-149 (waves): F0 * sum_j (A_j sin(j*om*(t-EPOCH)) + B_j cos(...)). */
+static double wave_phase(const orc_model* m, double t) {
+    if (m->n_wave <= 0) return 0.0;
+    double acc = 0.0;
+    for (int j = 1; j <= m->n_wave; ++j) {
+        double arg = j * m->wave_om * (t - m->wave_epoch);
+        acc += m->wave_ab[j - 1][0] * sin(arg) + m->wave_ab[j - 1][1] * cos(arg);
+    }
+    return acc * m->f[0];
+}
+
+/* calcphase.py:152-176: total = te + gl + wav; folded = total - floor(total).
+ * parts: bit0 te, bit1 glitches, bit2 waves (Phases.taylorexpansion/.glitches/.waves). */
+void orc_calcphase(const double* t, int64_t n, const orc_model* m, int parts, double* total, double* folded) {
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; ++i) {
+        double te = (parts & 1) ? te_phase(m, t[i]) : 0.0;
+        double gl = (parts & 2) ? gl_phase(m, t[i]) : 0.0;
+        double wv = (parts & 4) ? wave_phase(m, t[i]) : 0.0;
+        double tot = te + gl + wv;
+        total[i] = tot;
+        if (folded) folded[i] = tot - floor(tot);
+    }
+}
+
+/* periodsearch.py:57-71 (ztest), :73-106 (twod_ztest), :109-125 (htest).
+ * The argument is built exactly as the reference does:
+ *   1-D: 2*(kk+1)*pi*f*(t-t0)
+ *   2-D: 2*(kk+1)*pi*(f*(t-t0) + (0.5*(-1*10**fd))*(t-t0)**2)
+ * stat 0 = Z^2_m; stat 1 = H (max of cumsum(Z^2_k) - 4*(k-1)).
+ * out is [nfd*nf] with fd outer, f inner (periodsearch.py:264-278). nfd==0 => 1-D. */
+void orc_search(const double* time, int64_t n, double t0, const double* freq, int64_t nf,
+                const double* fd, int64_t nfd, int nharm, int stat, double* out) {
+    int64_t rows = nfd > 0 ? nfd : 1;
+    int64_t total = rows * nf;
+#pragma omp parallel
+    {
+        double* z = (double*)malloc(sizeof(double) * (size_t)(nharm > 0 ? nharm : 1));
+#pragma omp for schedule(dynamic, 1)
+        for (int64_t idx = 0; idx < total; ++idx) {
+            int64_t r = idx / nf, j = idx % nf;
+            double f = freq[j];
+            double c2 = nfd > 0 ? 0.5 * (-1.0 * pow(10.0, fd[r])) : 0.0;
+            for (int k = 0; k < nharm; ++k) {
+                double pre = 2.0 * (double)(k + 1) * ORC_PI;
+                double sc = 0.0, ss = 0.0;
+                if (nfd > 0) {
+                    for (int64_t i = 0; i < n; ++i) {
+                        double dt = time[i] - t0;
+                        double a = pre * (f * dt + c2 * (dt * dt));
+                        sc += cos(a);
+                        ss += sin(a);
+                    }
+                } else {
+                    double pf = pre * f;
+                    for (int64_t i = 0; i < n; ++i) {
+                        double a = pf * (time[i] - t0);
+                        sc += cos(a);
+                        ss += sin(a);
+                    }
+                }
+                z[k] = sc * sc + ss * ss;
+            }
+            double res;
+            if (stat == 0) {
+                double s = 0.0;
+                for (int k = 0; k < nharm; ++k) s += z[k];
+                res = s * (2.0 / (double)n);
+            } else {
+                double cum = 0.0, best = -INFINITY;
+                for (int k = 0; k < nharm; ++k) {
+                    cum += z[k] * (2.0 / (double)n);
+                    double v = cum - 4.0 * (double)k;
+                    if (v > best) best = v;
+                }
+                res = best;
+            }
+            out[idx] = res;
+        }
+        free(z);
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* Unbinned extended likelihoods (templatemodels.py:98-121, 201-226, 306-329) */
+/* ------------------------------------------------------------------------ */
+/* model: 0 fourier (x in cycles), 1 wrapped cauchy, 2 von mises (x in radians).
+ * p1 = amp_j, p2 = ph_j (fourier) or cen_j, p3 = wid_j (cauchy/vm), i0k = I0(1/wid^2) for VM.
+ *
+ * All three reduce to LL(n, phi) = -n*E + sum_i ln(n + a*h_i(phi)) + C(n-independent) with
+ * the reference's exact constant terms restored below, so this routine also returns the
+ * first and second derivatives in (n, phi) used by the profile fits:
+ *   out[0] = LL (reference formula), out[1] = dLL/dn, out[2] = dLL/dphi,
+ *   out[3] = d2/dn2, out[4] = d2/dn dphi, out[5] = d2/dphi2, out[6] = min(model/norm-factor)
+ * LL is -inf when any model value <= 0 (templatemodels.py:113-115,220-222,324-326). */
+static void h_terms(int model, int K, const double* p1, const double* p2, const double* p3, const double* i0k,
+                    double amps, double x, double phi, double* h, double* h1, double* h2) {
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+    for (int j = 0; j < K; ++j) {
+        if (model == 0) {
+            double jj = (double)(j + 1);
+            double arg = jj * 2.0 * ORC_PI * x + p2[j] - jj * phi;
+            double a = p1[j] * amps;
+            double c = cos(arg), s = sin(arg);
+            s0 += a * c;
+            s1 += a * jj * s;          /* d/dphi of cos(arg) = +j sin(arg) */
+            s2 += -a * jj * jj * c;
+        } else if (model == 1) {
+            double a = p1[j] * amps / (2.0 * ORC_PI);
+            double sh = sinh(p3[j]), ch = cosh(p3[j]);
+            double u = x - p2[j] - phi;
+            double cu = cos(u), su = sin(u);
+            double D = ch - cu;
+            double v = a * sh / D;
+            /* dv/du = -a sh su / D^2 ; du/dphi = -1 */
+            double dvdu = -a * sh * su / (D * D);
+            double d2vdu2 = -a * sh * (cu / (D * D) - 2.0 * su * su / (D * D * D));
+            s0 += v;
+            s1 += -dvdu;
+            s2 += d2vdu2;
+        } else {
+            double kap = 1.0 / (p3[j] * p3[j]);
+            double b = p1[j] * amps / (2.0 * ORC_PI * i0k[j]);
+            double u = x - p2[j] - phi;
+            double cu = cos(u), su = sin(u);
+            double v = b * exp(kap * cu);
+            double dvdu = -kap * su * v;
+            double d2vdu2 = (-kap * cu + kap * kap * su * su) * v;
+            s0 += v;
+            s1 += -dvdu;
+            s2 += d2vdu2;
+        }
+    }
+    *h = s0;
+    *h1 = s1;
+    *h2 = s2;
+}
+
+void orc_toa_eval(const double* x, int64_t n, double exposure, int model, int K, const double* p1,
+                  const double* p2, const double* p3, const double* i0k, double amps, double norm, double phi,
+                  double* out) {
+    double lsum = 0.0, g_n = 0.0, g_p = 0.0, h_nn = 0.0, h_np = 0.0, h_pp = 0.0, mn = INFINITY;
+    double atot = 0.0;
+    for (int j = 0; j < K; ++j) atot += p1[j] * amps;
+    /* normalising factor: fourier -> norm ; cauchy/vm -> 2*pi*norm + sum(amp*ampShift) */
+    double F = (model == 0) ? norm : 2.0 * ORC_PI * norm + atot;
+    for (int64_t i = 0; i < n; ++i) {
+        double h, h1, h2;
+        h_terms(model, K, p1, p2, p3, i0k, amps, x[i], phi, &h, &h1, &h2);
+        double mv = norm + h;
+        double r = mv / F;
+        if (r < mn) mn = r;
+        lsum += log(r);
+        double q = 1.0 / mv;
+        g_n += q;
+        g_p += h1 * q;
+        h_nn -= q * q;
+        h_np -= h1 * q * q;
+        h_pp += h2 * q - h1 * h1 * q * q;
+    }
+    double ll;
+    if (mn <= 0.0) {
+        ll = -INFINITY;
+    } else if (model == 0) {
+        ll = -norm * exposure + (double)n * log(norm * exposure) + lsum;
+    } else {
+        ll = -F * exposure / (2.0 * ORC_PI) + (double)n * log(F * exposure / (2.0 * ORC_PI)) + lsum;
+    }
+    out[0] = ll;
+    out[1] = -exposure + g_n;
+    out[2] = g_p;
+    out[3] = h_nn;
+    out[4] = h_np;
+    out[5] = h_pp;
+    out[6] = mn;
+}
+
+/* Batched brute grid (lmfit brute over norm x phShift, measureToAs.py:292-295):
+ * ll[a*nphi + b] = LL(norm_grid[a], phi_grid[b]). */
+void orc_toa_grid(const double* x, int64_t n, double exposure, int model, int K, const double* p1,
+                  const double* p2, const double* p3, const double* i0k, double amps, const double* norms,
+                  int64_t nn, const double* phis, int64_t np_, double* ll) {
+#pragma omp parallel for collapse(2) schedule(dynamic, 1)
+    for (int64_t a = 0; a < nn; ++a)
+        for (int64_t b = 0; b < np_; ++b) {
+            double o[7];
+            orc_toa_eval(x, n, exposure, model, K, p1, p2, p3, i0k, amps, norms[a], phis[b], o);
+            ll[a * np_ + b] = o[0];
+        }
+}

@@ -1,0 +1,249 @@
+"""Generate the golden fixtures under tests/golden/ from the CRIMP reference.
+
+Run HERE (the build container), never on the GPU box:
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py
+
+It imports the importable reference modules from /root/reference/src (SURVEY.md
+§8c: periodsearch, calcphase, templatemodels, ephemTmjd, readtimingmodel,
+readPPtemplate, binphases) and records inputs + outputs as plain arrays (.npz,
+allow_pickle=False) and JSON. Nothing of the reference's source travels; only
+these vectors and the reference's own data files (par / template / interval /
+golden ToA tables) are copied.
+
+The event arrays come from a raw big-endian read of the bundled
+data/1e2259_ni1020600110.fits EVENTS table (TIME >f8 @0, PI >i2 @33, 39-byte
+rows), which SURVEY.md §4 shows reproduces data/ToAs_2259.txt ToA_mid bit-exactly.
+"""
+import json
+import os
+import shutil
+import sys
+
+import numpy as np
+
+REF = "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REF, "src"))
+sys.path.insert(0, os.path.abspath(os.path.join(HERE, "..", "..")))
+sys.dont_write_bytecode = True
+
+from crimp.periodsearch import PeriodSearch  # noqa: E402
+from crimp.calcphase import calcphase  # noqa: E402
+from crimp.templatemodels import Fourier, WrappedCauchy, VonMises  # noqa: E402
+from crimp.ephemTmjd import ephemTmjd  # noqa: E402
+from crimp.readtimingmodel import ReadTimingModel  # noqa: E402
+from crimp.readPPtemplate import readPPtemplate  # noqa: E402
+from crimp.binphases import binphases  # noqa: E402
+
+from crimp_amd.synth import pulsed_events  # noqa: E402
+
+
+def raw_events(path):
+    """Minimal FITS EVENTS reader used only to build the fixture."""
+    buf = open(path, "rb").read()
+    pos = 0
+    hdus = []
+    while pos < len(buf):
+        cards = {}
+        while True:
+            block = buf[pos:pos + 2880].decode("ascii")
+            pos += 2880
+            done = False
+            for i in range(0, 2880, 80):
+                card = block[i:i + 80]
+                key = card[:8].strip()
+                if key == "END":
+                    done = True
+                    break
+                if card[8:10] == "= ":
+                    val = card[10:].split("/")[0].strip()
+                    cards[key] = val
+            if done:
+                break
+        naxis = int(cards.get("NAXIS", 0))
+        size = 0
+        if naxis:
+            size = abs(int(cards.get("BITPIX", 8))) // 8
+            for a in range(1, naxis + 1):
+                size *= int(cards["NAXIS%d" % a])
+            size += int(cards.get("PCOUNT", 0))
+        hdus.append((cards, pos))
+        pos += ((size + 2879) // 2880) * 2880
+    for cards, start in hdus:
+        if cards.get("EXTNAME", "").strip("' ") == "EVENTS":
+            w = int(cards["NAXIS1"])
+            nrow = int(cards["NAXIS2"])
+            rows = np.frombuffer(buf, dtype=np.uint8, count=w * nrow, offset=start).reshape(nrow, w)
+            time = rows[:, 0:8].copy().view(">f8").ravel().astype(np.float64)
+            pi = rows[:, 33:35].copy().view(">i2").ravel().astype(np.int16)
+            mjdref = float(cards["MJDREFI"]) + float(cards["MJDREFF"])
+            return time, pi, int(cards["MJDREFI"]), float(cards["MJDREFF"]), mjdref
+    raise RuntimeError("no EVENTS HDU")
+
+
+def main():
+    out = {}
+    # ---------------------------------------------------------------- data files
+    for fn in ("1e2259.par", "1e2259_template.txt", "timIntToAs_1e2259.txt", "ToAs_2259.txt", "ToAs_2259.tim"):
+        shutil.copyfile(os.path.join(REF, "data", fn), os.path.join(HERE, fn))
+
+    # ---------------------------------------------------------------- events
+    time, pi, mjdrefi, mjdreff, mjdref = raw_events(os.path.join(REF, "data", "1e2259_ni1020600110.fits"))
+    np.savez_compressed(os.path.join(HERE, "events_1e2259.npz"), TIME=time, PI=pi,
+                        MJDREFI=np.int64(mjdrefi), MJDREFF=np.float64(mjdreff))
+    tmjd = time / 86400 + mjdref
+    ene = pi.astype(np.float64) * 0.01
+    keep = (ene >= 1.0) & (ene <= 5.0)
+    t15 = tmjd[keep]
+    print("events", time.size, "1-5 keV", t15.size)
+    par = os.path.join(REF, "data", "1e2259.par")
+    tmpl = os.path.join(REF, "data", "1e2259_template.txt")
+
+    # ---------------------------------------------------------------- PeriodSearch, config 1
+    x = t15 * 86400.0
+    T = x[-1] - x[0]
+    F0 = ReadTimingModel(par).readfulltimingmodel()[0]["F0"]
+    freq = F0 + np.arange(-200, 200) / (10.0 * T)
+    ps = PeriodSearch(x, freq, nbrHarm=2)
+    z2 = ps.ztest()
+    ps20 = PeriodSearch(x, freq, nbrHarm=20)
+    h20 = ps20.htest()
+    fsub = freq[180:220]
+    fd = np.array([-16.0, -14.0, -13.0, -12.5])
+    z2d, _ = PeriodSearch(x, fsub, nbrHarm=2).twod_ztest(fd)
+    print("config1 ztest argmax", int(np.argmax(z2)), z2.max(), "htest argmax", int(np.argmax(h20)), h20.max())
+    np.savez_compressed(os.path.join(HERE, "periodsearch_1e2259.npz"), time=x, freq=freq, z2_m2=z2, h_m20=h20,
+                        fsub=fsub, fd=fd, z2d_m2=z2d)
+
+    # ---------------------------------------------------------------- PeriodSearch, synthetic small cases
+    cases = {}
+    ev = pulsed_events(6000, 2.0e4, 3.3, pulsed_frac=0.2, fdot=-2e-10, seed=11)
+    fr = 3.3 + (np.arange(-96, 96) / (10.0 * 2.0e4))
+    for m in (1, 2, 3, 5):
+        cases["z_m%d" % m] = PeriodSearch(ev, fr, nbrHarm=m).ztest()
+    for m in (1, 5, 20):
+        cases["h_m%d" % m] = PeriodSearch(ev, fr, nbrHarm=m).htest()
+    fdd = np.array([-11.0, -9.7, -9.5, -9.0])
+    cases["z2d_m2"], _ = PeriodSearch(ev, fr[64:128], nbrHarm=2).twod_ztest(fdd)
+    cases["z2d_m3"], _ = PeriodSearch(ev, fr[64:128], nbrHarm=3).twod_ztest(fdd)
+    # non-uniform trial grid + unsorted photon list (t0 uses first/last element, not min/max)
+    rng = np.random.default_rng(5)
+    fr_nu = np.sort(3.3 + rng.uniform(-4e-4, 4e-4, size=77))
+    ev_perm = ev.copy()
+    rng.shuffle(ev_perm)
+    cases["z_nonuniform_m2"] = PeriodSearch(ev_perm, fr_nu, nbrHarm=2).ztest()
+    cases["h_nonuniform_m4"] = PeriodSearch(ev_perm, fr_nu, nbrHarm=4).htest()
+    # edge cases: one and two photons, one trial
+    cases["z_n1"] = PeriodSearch(ev[:1], fr[:8], nbrHarm=2).ztest()
+    cases["z_n2"] = PeriodSearch(ev[:2], fr[:8], nbrHarm=2).ztest()
+    cases["h_n2"] = PeriodSearch(ev[:2], fr[:8], nbrHarm=3).htest()
+    cases["z_m1trial"] = PeriodSearch(ev, fr[100:101], nbrHarm=2).ztest()
+    np.savez_compressed(os.path.join(HERE, "periodsearch_synth.npz"), time=ev, time_perm=ev_perm, freq=fr,
+                        freq_nu=fr_nu, fd=fdd, **cases)
+
+    # ---------------------------------------------------------------- calcphase
+    tsl = t15[:10000]
+    tot_par, fold_par = calcphase(tsl, par)
+    tot_s, fold_s = calcphase(float(t15[123]), par)
+    tm = {
+        "PEPOCH": 58140.0, "F0": 0.14328254547263483, "F1": -9.7e-15, "F2": 1.4e-23, "F3": -2.0e-31,
+        "F4": 0.0, "F5": 0.0, "F6": 0.0, "F7": 0.0, "F8": 0.0, "F9": 0.0, "F10": 0.0, "F11": 0.0, "F12": 0.0,
+        "GLEP_1": 58142.0, "GLPH_1": 0.1, "GLF0_1": 1.2e-7, "GLF1_1": -3.0e-15, "GLF2_1": 1.0e-23,
+        "GLF0D_1": 2.0e-8, "GLTD_1": 30.0,
+        "GLEP_2": 58144.5, "GLPH_2": -0.05, "GLF0_2": 4.0e-8, "GLF1_2": 0.0, "GLF2_2": 0.0,
+        "GLF0D_2": 1.0e-8, "GLTD_2": 0.0,
+        "WAVEEPOCH": 58140.5, "WAVE_OM": 0.0123,
+        "WAVE1": {"A": 0.01, "B": -0.02}, "WAVE2": {"A": 0.003, "B": 0.004}, "WAVE3": {"A": -0.001, "B": 0.0005},
+    }
+    tm_flags = {k: ({"value": v, "flag": 1} if isinstance(v, float) and k.startswith("F") else v)
+                for k, v in tm.items()}
+    tot_d, fold_d = calcphase(tsl, tm_flags)
+    t2d = tsl[:600].reshape(20, 30)
+    tot_2d, fold_2d = calcphase(t2d, tm)
+    np.savez_compressed(os.path.join(HERE, "calcphase.npz"), t=tsl, total_par=tot_par, folded_par=fold_par,
+                        t_scalar=np.float64(t15[123]), total_scalar=np.float64(tot_s), folded_scalar=np.float64(fold_s),
+                        total_dict=tot_d, folded_dict=fold_d, t2d=t2d, total_2d=tot_2d, folded_2d=fold_2d)
+    with open(os.path.join(HERE, "timing_model_dict.json"), "w") as fh:
+        json.dump(tm, fh, indent=1)
+
+    # ---------------------------------------------------------------- ToA intervals 35-41
+    import pandas as pd
+    iv = pd.read_csv(os.path.join(REF, "data", "timIntToAs_1e2259.txt"), sep=r"\s+", comment="#")
+    gold = pd.read_csv(os.path.join(REF, "data", "ToAs_2259.txt"), sep=r"\s+", comment="#")
+    tmpl_d = readPPtemplate(tmpl)
+    toa = {"ids": [], "mid": [], "n": [], "h5": [], "freq": [], "fdot": [], "ll_points": []}
+    fold_all = []
+    offs = [0]
+    ll_norm, ll_phi, ll_val, ll_toa = [], [], [], []
+    for ii in range(35, 42):
+        m = (t15 >= iv["ToA_tstart"][ii]) & (t15 <= iv["ToA_tend"][ii])
+        tt = t15[m]
+        mid = ((tt[-1] - tt[0]) / 2) + tt[0]
+        _, fold = calcphase(tt, par)
+        eph = ephemTmjd(mid, par)
+        h5 = PeriodSearch(tt * 86400, np.atleast_1d(eph["freqAtTmjd"]), nbrHarm=5).htest()[0]
+        toa["ids"].append(ii)
+        toa["mid"].append(float(mid))
+        toa["n"].append(int(tt.size))
+        toa["h5"].append(float(h5))
+        toa["freq"].append(float(eph["freqAtTmjd"]))
+        toa["fdot"].append(float(eph["freqdotAtTmjd"]))
+        fold_all.append(fold)
+        offs.append(offs[-1] + fold.size)
+        g = gold[gold["ToA"] == ii].iloc[0]
+        E = float(iv["ToA_exposure"][ii])
+        for nv in (g["phShift"] * 0 + 14.0, 16.598081, 17.06, 19.5):
+            for ph in (float(g["phShift"]), 0.0, 1.0, -2.5, 3.1):
+                theta = {"norm": nv, "ampShift": 1.0, "phShift": ph}
+                for j in range(1, 7):
+                    theta["amp_%d" % j] = tmpl_d["amp_%d" % j]["value"]
+                    theta["ph_%d" % j] = tmpl_d["ph_%d" % j]["value"]
+                ll_norm.append(nv)
+                ll_phi.append(ph)
+                ll_toa.append(ii)
+                ll_val.append(Fourier(theta, fold).loglikelihoodFSnormalized(E))
+    # an invalid (negative model) point: tiny norm -> -inf
+    theta = {"norm": 0.5, "ampShift": 1.0, "phShift": 0.0}
+    for j in range(1, 7):
+        theta["amp_%d" % j] = tmpl_d["amp_%d" % j]["value"]
+        theta["ph_%d" % j] = tmpl_d["ph_%d" % j]["value"]
+    ll_inf = Fourier(theta, fold_all[0]).loglikelihoodFSnormalized(600.0)
+    bp = binphases(fold_all[0], 15)
+    np.savez_compressed(os.path.join(HERE, "toa_1e2259.npz"), folded=np.concatenate(fold_all),
+                        offsets=np.array(offs, dtype=np.int64), ids=np.array(toa["ids"]), mid=np.array(toa["mid"]),
+                        n=np.array(toa["n"]), h5=np.array(toa["h5"]), freq=np.array(toa["freq"]),
+                        fdot=np.array(toa["fdot"]),
+                        ll_norm=np.array(ll_norm), ll_phi=np.array(ll_phi), ll_toa=np.array(ll_toa),
+                        ll_val=np.array(ll_val), ll_inf=np.float64(ll_inf),
+                        bp_ppBins=bp["ppBins"], bp_cts=bp["ctsBins"], bp_err=bp["ctsBinsErr"])
+    print("ToA ids", toa["ids"], "n", toa["n"], "h5", toa["h5"])
+
+    # ---------------------------------------------------------------- Cauchy / von Mises LL (synthetic templates)
+    rng = np.random.default_rng(7)
+    xr = np.sort(rng.uniform(0, 2 * np.pi, size=3000))
+    tc = {"norm": 5.0, "ampShift": 1.0, "phShift": 0.3, "amp_1": 6.0, "cen_1": 1.0, "wid_1": 0.4,
+          "amp_2": 3.0, "cen_2": 4.0, "wid_2": 0.9}
+    cau = [WrappedCauchy(dict(tc, phShift=p, norm=nv), xr).loglikelihoodCAnormalized(250.0)
+           for p in (-4.0, -0.5, 0.3, 2.2) for nv in (3.0, 5.0, 8.0)]
+    vm = [VonMises(dict(tc, phShift=p, norm=nv), xr).loglikelihoodVMnormalized(250.0)
+          for p in (-4.0, -0.5, 0.3, 2.2) for nv in (3.0, 5.0, 8.0)]
+    four_curve = Fourier(dict(norm=2.0, ampShift=1.3, phShift=0.2, amp_1=0.5, ph_1=0.1, amp_2=0.25, ph_2=-1.0),
+                         np.linspace(0, 1, 15, endpoint=False)).fourseries()
+    np.savez_compressed(os.path.join(HERE, "templatemodels.npz"), x=xr, cauchy=np.array(cau), vonmises=np.array(vm),
+                        four_curve=four_curve)
+    with open(os.path.join(HERE, "cauchy_vm_theta.json"), "w") as fh:
+        json.dump(tc, fh)
+
+    # ---------------------------------------------------------------- readers (parsed dicts)
+    def plain(d):
+        return {k: (plain(v) if isinstance(v, dict) else (v.item() if hasattr(v, "item") else v))
+                for k, v in d.items()}
+    with open(os.path.join(HERE, "parsed.json"), "w") as fh:
+        json.dump({"par": plain(ReadTimingModel(par).readfulltimingmodel()[0]),
+                   "template": plain(readPPtemplate(tmpl))}, fh, indent=1)
+    print("done")
+
+
+if __name__ == "__main__":
+    main()

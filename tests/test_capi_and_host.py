@@ -1,0 +1,123 @@
+"""CPU-side checks: the C-ABI library loads and exports the header's symbols; host logic
+(readers, event ingestion, scan-phase sequence) matches the reference's fixtures."""
+import json
+import os
+import re
+
+import numpy as np
+import pandas as pd
+import pytest
+
+from conftest import ROOT, gold, gpath
+
+
+def _declared():
+    src = open(os.path.join(ROOT, "include", "crimp_hip.h")).read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(crimp_\w+)\s*\(", src, re.M)))
+
+
+def test_library_exports_every_declared_symbol():
+    from crimp_amd import _native
+    L = _native.load(require_device=False)
+    names = _declared()
+    assert set(names) == set(_native.EXPORTS)
+    for n in names:
+        assert hasattr(L, n), n
+    assert L.crimp_version() >= 1
+
+
+def test_hot_path_fails_loudly_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from crimp_amd import _native
+    from crimp_amd.periodsearch import PeriodSearch
+    with pytest.raises(_native.CrimpNativeError):
+        PeriodSearch(np.arange(10.0), np.array([0.1]), 2).ztest()
+
+
+def test_readtimingmodel_matches_reference():
+    from crimp_amd.readtimingmodel import ReadTimingModel
+    ref = json.load(open(gpath("parsed.json")))["par"]
+    got = ReadTimingModel(gpath("1e2259.par")).readfulltimingmodel()[0]
+    assert set(got) == set(ref)
+    for k in ref:
+        assert float(got[k]) == ref[k], k
+
+
+def test_readpptemplate_matches_reference():
+    from crimp_amd.readPPtemplate import readPPtemplate
+    ref = json.load(open(gpath("parsed.json")))["template"]
+    got = readPPtemplate(gpath("1e2259_template.txt"))
+    assert list(got) == list(ref)
+    for k, v in ref.items():
+        if isinstance(v, dict):
+            assert float(got[k]["value"]) == v["value"] and got[k]["vary"] == v["vary"], k
+        else:
+            assert got[k] == v, k
+
+
+def test_eventfile_roundtrip_and_toa_mid(tmp_path):
+    """Raw FITS ingestion: TIME/86400+MJDREF and PI*0.01 reproduce ToA_mid of ToAs 35-41 bit-exactly."""
+    from crimp_amd.eventfile import EvtFileOps, write_events_fits
+    ev = gold("events_1e2259.npz")
+    p = str(tmp_path / "ev.fits")
+    write_events_fits(p, ev["TIME"], ev["PI"], int(ev["MJDREFI"]), float(ev["MJDREFF"]))
+    ef = EvtFileOps(p).build_time_energy_df().filtenergy(1.0, 5.0)
+    t = ef.time_energy_df["TIME"].to_numpy()
+    assert t.size == 68877
+    iv = pd.read_csv(gpath("timIntToAs_1e2259.txt"), sep=r"\s+", comment="#")
+    ref = pd.read_csv(gpath("ToAs_2259.txt"), sep=r"\s+", comment="#")
+    for ii in range(35, 42):
+        tt = t[(t >= iv["ToA_tstart"][ii]) & (t <= iv["ToA_tend"][ii])]
+        mid = ((tt[-1] - tt[0]) / 2) + tt[0]
+        assert str(mid) == str(ref[ref["ToA"] == ii]["ToA_mid"].iloc[0])
+
+
+def test_eventfile_reads_bundled_fits_if_present():
+    from crimp_amd.eventfile import EvtFileOps
+    p = "/root/reference/data/1e2259_ni1020600110.fits"
+    if not os.path.exists(p):
+        pytest.skip("reference data not mounted")
+    ev = gold("events_1e2259.npz")
+    ef = EvtFileOps(p)
+    df = ef.build_time_energy_df().time_energy_df
+    assert np.array_equal(df["TIME"].to_numpy(), ev["TIME"] / 86400 + (int(ev["MJDREFI"]) + float(ev["MJDREFF"])))
+    kw, gti = ef.readGTI()
+    assert kw["TELESCOPE"] == "NICER" and gti.shape[1] == 2
+
+
+def test_binphases_host_matches_reference():
+    from crimp_amd.binphases import binphases
+    g = gold("toa_1e2259.npz")
+    x = g["folded"][g["offsets"][0]:g["offsets"][1]]
+    b = binphases(x, 15)
+    assert np.array_equal(b["ctsBins"], g["bp_cts"]) and np.array_equal(b["ppBins"], g["bp_ppBins"])
+
+
+def test_ephemtmjd_matches_reference():
+    from crimp_amd.ephemTmjd import ephemTmjd
+    g = gold("toa_1e2259.npz")
+    for mid, f, fd in zip(g["mid"], g["freq"], g["fdot"]):
+        e = ephemTmjd(mid, gpath("1e2259.par"))
+        assert e["freqAtTmjd"] == f and e["freqdotAtTmjd"] == fd
+
+
+def test_error_scan_phase_sequence_clip_semantics():
+    """lmfit clips a stepped phShift to [-pi, pi] once, then the loop moves the bound (measureToAs.py:332-334)."""
+    from crimp_amd.toafit import ToAFitter
+    tm = {"model": "fourier", "norm": {"value": 10.0}, "amp_1": {"value": 1.0}, "ph_1": {"value": 0.0}}
+    fit = ToAFitter.__new__(ToAFitter)
+    fit.model, fit.res, fit.pb = "fourier", 1000, np.pi
+    step = 2 * np.pi / 1000
+    phi = np.array([-np.pi + 2.5 * step, 0.3])
+    ks = np.arange(1, 6)
+    seq = fit._scan_phases(phi, -1, ks)
+    exp0 = phi[0] - ks * step
+    exp0[2] = -np.pi  # third step is the first past the bound: evaluated at the bound itself
+    np.testing.assert_array_equal(seq[0], exp0)
+    np.testing.assert_array_equal(seq[1], phi[1] - ks * step)
+    fit.model, fit.pb = "cauchy", 1.5 * np.pi
+    seq = fit._scan_phases(np.array([1.5 * np.pi - step]), 1, ks)
+    np.testing.assert_array_equal(seq[0], np.minimum(1.5 * np.pi - step + ks * step, 1.5 * np.pi))
+    del tm

@@ -1,0 +1,294 @@
+"""HIP path (through the C-ABI) against the oracle and the reference's golden vectors.
+
+Tolerances (BASELINE.json north_star): Z^2/H powers within 1e-6 relative -- stated per bin
+relative to max(|ref|, mean(ref)) because a relative error on a near-zero noise bin is
+ill-conditioned for any fp32 kernel -- best-trial index bit-exact, ToA phase shifts within
+1e-4 cycles; calcphase within 1e-9 cycles; LL within 1e-9 relative (fp64 kernel).
+"""
+import json
+import math
+
+import numpy as np
+import pandas as pd
+import pytest
+
+from conftest import gold, gpath
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-6
+
+
+def close_z(got, ref, rtol=RTOL):
+    got, ref = np.asarray(got), np.asarray(ref)
+    scale = np.maximum(np.abs(ref), np.mean(np.abs(ref)))
+    err = np.abs(got - ref) / scale
+    assert err.max() <= rtol, "max scaled error %.3g at %d" % (err.max(), int(err.argmax()))
+    return err.max()
+
+
+def test_z2_h_config1_golden(gpu):
+    from crimp_amd.periodsearch import PeriodSearch
+    g = gold("periodsearch_1e2259.npz")
+    z = PeriodSearch(g["time"], g["freq"], 2).ztest()
+    assert int(np.argmax(z)) == 200
+    close_z(z, g["z2_m2"])
+    h = PeriodSearch(g["time"], g["freq"], 20).htest()
+    assert int(np.argmax(h)) == 200
+    close_z(h, g["h_m20"])
+    arr, df = PeriodSearch(g["time"], g["fsub"], 2).twod_ztest(g["fd"])
+    np.testing.assert_array_equal(arr[:, :2], g["z2d_m2"][:, :2])
+    close_z(arr[:, 2], g["z2d_m2"][:, 2])
+    assert list(df.columns) == ["Freq", "Freq_dot", "Z2pow"]
+
+
+def test_search_synthetic_golden_and_edges(gpu):
+    from crimp_amd.periodsearch import PeriodSearch
+    g = gold("periodsearch_synth.npz")
+    t, f = g["time"], g["freq"]
+    for m in (1, 2, 3, 5):
+        z = PeriodSearch(t, f, m).ztest()
+        close_z(z, g["z_m%d" % m])
+        assert np.argmax(z) == np.argmax(g["z_m%d" % m])
+    for m in (1, 5, 20):
+        close_z(PeriodSearch(t, f, m).htest(), g["h_m%d" % m])
+    close_z(PeriodSearch(t, f[64:128], 2).twod_ztest(g["fd"])[0][:, 2], g["z2d_m2"][:, 2])
+    close_z(PeriodSearch(t, f[64:128], 3).twod_ztest(g["fd"])[0][:, 2], g["z2d_m3"][:, 2])
+    close_z(PeriodSearch(g["time_perm"], g["freq_nu"], 2).ztest(), g["z_nonuniform_m2"])
+    close_z(PeriodSearch(g["time_perm"], g["freq_nu"], 4).htest(), g["h_nonuniform_m4"])
+    close_z(PeriodSearch(t[:1], f[:8], 2).ztest(), g["z_n1"])
+    close_z(PeriodSearch(t[:2], f[:8], 2).ztest(), g["z_n2"])
+    close_z(PeriodSearch(t[:2], f[:8], 3).htest(), g["h_n2"])
+    close_z(PeriodSearch(t, f[100:101], 2).ztest(), g["z_m1trial"])
+    assert PeriodSearch(t, f[:0], 2).ztest().size == 0
+    with pytest.raises(IndexError):
+        PeriodSearch(t[:0], f, 2)
+
+
+@pytest.mark.parametrize("mode", ["direct", "auto"])
+def test_search_vs_oracle_larger(gpu, mode, monkeypatch):
+    from crimp_amd.periodsearch import PeriodSearch
+    from crimp_amd.synth import pulsed_events
+    if mode == "direct":
+        monkeypatch.setenv("CRIMP_SEARCH", "direct")
+    t = pulsed_events(200000, 2.0e5, 7.123456789, pulsed_frac=0.05, seed=4)
+    f = 7.123456789 + (np.arange(-1024, 1024) / (10 * 2.0e5))
+    z = PeriodSearch(t, f, 2).ztest()
+    zr = O.search(t, f, 2)
+    assert int(np.argmax(z)) == int(np.argmax(zr))
+    close_z(z, zr)
+    fd = np.array([-13.0, -12.0, -11.5])
+    a = PeriodSearch(t, f[512:1536], 3).twod_htest(fd)[0][:, 2]
+    ar = O.search(t, f[512:1536], 3, freq_dot=fd, stat="h")
+    assert int(np.argmax(a)) == int(np.argmax(ar))
+    close_z(a, ar)
+
+
+def test_search_sharded_ranges_equal_full(gpu):
+    """A search split into flat-trial ranges (what each rank computes) equals the unsplit search."""
+    from crimp_amd import ops
+    from crimp_amd.synth import pulsed_events
+    t = pulsed_events(50000, 1.0e5, 3.0, pulsed_frac=0.1, seed=9)
+    f = 3.0 + np.arange(-300, 300) / 1.0e6
+    fd = np.array([-12.0, -11.0])
+    t0 = (t[0] + t[-1]) / 2
+    full = ops.search(t, t0, f, 2, 0, log10_negfdot=fd)
+    parts = [ops.search(t, t0, f, 2, 0, log10_negfdot=fd, first=a, count=b - a)
+             for a, b in ((0, 333), (333, 901), (901, 1200))]
+    np.testing.assert_array_equal(np.concatenate(parts), full)
+
+
+def test_sincos_variants_accuracy_report(gpu, monkeypatch, capsys):
+    """Hardware v_sin/v_cos vs the polynomial in the direct kernel (reported; polynomial must pass)."""
+    from crimp_amd.periodsearch import PeriodSearch
+    from crimp_amd.synth import pulsed_events
+    t = pulsed_events(300000, 3.0e5, 5.0, pulsed_frac=0.02, seed=12)
+    f = 5.0 + np.arange(-512, 512) / 3.0e6
+    zr = O.search(t, f, 2)
+    monkeypatch.setenv("CRIMP_SEARCH", "direct")
+    errs = {}
+    for hw in ("", "hw"):
+        monkeypatch.setenv("CRIMP_SINCOS", hw)
+        z = PeriodSearch(t, f, 2).ztest()
+        scale = np.maximum(np.abs(zr), zr.mean())
+        errs[hw or "poly"] = float((np.abs(z - zr) / scale).max())
+    with capsys.disabled():
+        print("\n[sincos] max scaled Z2 error: %s" % errs)
+    assert errs["poly"] <= RTOL
+
+
+def test_calcphase_golden(gpu):
+    from crimp_amd.calcphase import calcphase, Phases
+    g = gold("calcphase.npz")
+    tot, fol = calcphase(g["t"], gpath("1e2259.par"))
+    assert np.max(np.abs(tot - g["total_par"])) <= 1e-9
+    d = np.abs(fol - g["folded_par"])
+    assert np.max(np.minimum(d, 1 - d)) <= 1e-9
+    tm = json.load(open(gpath("timing_model_dict.json")))
+    tot, fol = calcphase(g["t"], tm)
+    assert np.max(np.abs(tot - g["total_dict"])) <= 1e-9
+    ts, fs = calcphase(float(g["t_scalar"]), gpath("1e2259.par"))
+    assert isinstance(ts, float) and abs(ts - float(g["total_scalar"])) <= 1e-9
+    t2, f2 = calcphase(g["t2d"], tm)
+    assert t2.shape == (20, 30) and np.max(np.abs(t2 - g["total_2d"])) <= 1e-9
+    ph = Phases(g["t"][:100], tm)
+    te, gl, wv = ph.taylorexpansion(), ph.glitches(), ph.waves()
+    np.testing.assert_allclose(te + gl + wv, g["total_dict"][:100], rtol=0, atol=1e-9)
+    with pytest.raises(TypeError):
+        Phases(g["t"], 3.0)
+
+
+def test_fourier_ll_golden_points(gpu):
+    from crimp_amd.templatemodels import Fourier
+    g = gold("toa_1e2259.npz")
+    iv = pd.read_csv(gpath("timIntToAs_1e2259.txt"), sep=r"\s+", comment="#")
+    tm = json.load(open(gpath("parsed.json")))["template"]
+    for k in range(g["ll_val"].size):
+        i = int(np.nonzero(g["ids"] == g["ll_toa"][k])[0][0])
+        x = g["folded"][g["offsets"][i]:g["offsets"][i + 1]]
+        th = {"norm": g["ll_norm"][k], "ampShift": 1.0, "phShift": g["ll_phi"][k]}
+        for j in range(1, 7):
+            th["amp_%d" % j] = tm["amp_%d" % j]["value"]
+            th["ph_%d" % j] = tm["ph_%d" % j]["value"]
+        ll = Fourier(th, x).loglikelihoodFSnormalized(float(iv["ToA_exposure"][g["ll_toa"][k]]))
+        assert abs(ll - g["ll_val"][k]) <= 1e-9 * abs(g["ll_val"][k])
+    th["norm"], th["phShift"] = 0.5, 0.0
+    assert Fourier(th, g["folded"][:g["offsets"][1]]).loglikelihoodFSnormalized(600.0) == -np.inf
+
+
+def test_cauchy_vonmises_ll_golden(gpu):
+    from crimp_amd.templatemodels import WrappedCauchy, VonMises
+    g = gold("templatemodels.npz")
+    tc = json.load(open(gpath("cauchy_vm_theta.json")))
+    i = 0
+    for p in (-4.0, -0.5, 0.3, 2.2):
+        for nv in (3.0, 5.0, 8.0):
+            th = dict(tc, phShift=p, norm=nv)
+            assert abs(WrappedCauchy(th, g["x"]).loglikelihoodCAnormalized(250.0) - g["cauchy"][i]) <= 1e-9 * abs(
+                g["cauchy"][i])
+            assert abs(VonMises(th, g["x"]).loglikelihoodVMnormalized(250.0) - g["vonmises"][i]) <= 1e-9 * abs(
+                g["vonmises"][i])
+            i += 1
+
+
+def test_toa_points_derivatives_vs_oracle(gpu):
+    from crimp_amd import ops
+    g = gold("templatemodels.npz")
+    tc = json.load(open(gpath("cauchy_vm_theta.json")))
+    x = g["x"]
+    for model in ("cauchy", "vonmises"):
+        tarr = O.template_arrays(dict(tc, model=model))
+        tpl = ops.make_template(model, tarr[2], tarr[3], tarr[4])
+        s = ops.toa_points(x, np.array([0, x.size]), tpl, np.zeros(3, np.int64), np.array([4.0, 5.0, 6.0]),
+                           np.array([0.1, -1.0, 2.0]))
+        for p, (nv, ph) in enumerate(((4.0, 0.1), (5.0, -1.0), (6.0, 2.0))):
+            o = O.toa_eval(x, 250.0, tarr, nv, ph)
+            np.testing.assert_allclose([s[p, 1] - 250.0, s[p, 2], s[p, 3], s[p, 4], s[p, 5]], o[1:6], rtol=1e-9)
+
+
+def test_brute_grid_vs_oracle(gpu):
+    from crimp_amd import ops
+    g = gold("toa_1e2259.npz")
+    tm = json.load(open(gpath("parsed.json")))["template"]
+    tarr = O.template_arrays(tm)
+    tpl = ops.make_template("fourier", tarr[2], tarr[3])
+    x, off = g["folded"], g["offsets"]
+    norms = np.linspace(0.17, 500, 20)
+    phis = np.arange(126) * 0.05 - np.pi
+    ln, hmin = ops.toa_grid(x, off, tpl, np.tile(norms, (off.size - 1, 1)), phis)
+    for i in (0, 6):
+        xi = x[off[i]:off[i + 1]]
+        E = 600.0
+        ref = O.toa_grid(xi, E, tarr, norms, phis)
+        N = xi.size
+        got = -norms[:, None] * E + N * np.log(norms[:, None] * E) + ln[i] - N * np.log(norms[:, None])
+        got = np.where(hmin[i][None, :] + norms[:, None] > 0, got, -np.inf)
+        fin = np.isfinite(ref)
+        assert np.array_equal(fin, np.isfinite(got))
+        np.testing.assert_allclose(got[fin], ref[fin], rtol=2e-7, atol=0.05)
+        assert np.unravel_index(np.argmax(got), got.shape) == np.unravel_index(np.argmax(ref), ref.shape)
+
+
+def test_binphases_device_counts(gpu):
+    from crimp_amd import ops
+    g = gold("toa_1e2259.npz")
+    x, off = g["folded"], g["offsets"]
+    edges = np.linspace(0, 1, 16)
+    c = ops.binphases_counts(x, off, edges)
+    for i in range(off.size - 1):
+        assert np.array_equal(c[i], np.histogram(x[off[i]:off[i + 1]], bins=edges)[0])
+    assert np.array_equal(c[0], g["bp_cts"])
+
+
+def _golden_rows():
+    g = gold("toa_1e2259.npz")
+    iv = pd.read_csv(gpath("timIntToAs_1e2259.txt"), sep=r"\s+", comment="#")
+    ref = pd.read_csv(gpath("ToAs_2259.txt"), sep=r"\s+", comment="#")
+    return g, iv, ref
+
+
+def test_toa_fits_match_reference_and_oracle(gpu):
+    """Config 2: ToAs 35-41 of the worked example, batched on the device."""
+    from crimp_amd.toafit import ToAFitter
+    from crimp_amd.readPPtemplate import readPPtemplate
+    g, iv, ref = _golden_rows()
+    tm = readPPtemplate(gpath("1e2259_template.txt"))
+    E = iv["ToA_exposure"].to_numpy()[g["ids"]]
+    r = ToAFitter(g["folded"], g["offsets"], E, tm).fit(brutemin=True)
+    for i, tid in enumerate(g["ids"]):
+        row = ref[ref["ToA"] == tid].iloc[0]
+        x = g["folded"][g["offsets"][i]:g["offsets"][i + 1]]
+        o = O.fit_toa(x, E[i], tm, brutemin=True)
+        assert abs(r["phShi"][i] - row["phShift"]) / (2 * math.pi) < 1e-4
+        assert abs(r["phShi"][i] - o["phShi"]) / (2 * math.pi) < 1e-6
+        assert r["phShi_LL"][i] == pytest.approx(row["phShift_LL"], abs=1e-12)
+        assert r["phShi_UL"][i] == pytest.approx(row["phShift_UL"], abs=1e-12)
+        assert r["reducedChi2"][i] == pytest.approx(row["redChi2"], rel=5e-4)
+        assert r["reducedChi2"][i] == pytest.approx(o["reducedChi2"], rel=1e-6)
+
+
+def test_toa_fit_without_brute_and_other_templates(gpu):
+    from crimp_amd.measureToAs import measureToA_fourier, measureToA_cauchy, measureToA_vonmises
+    from crimp_amd.readPPtemplate import readPPtemplate
+    g, iv, ref = _golden_rows()
+    tm = readPPtemplate(gpath("1e2259_template.txt"))
+    x = g["folded"][g["offsets"][2]:g["offsets"][3]]
+    E = float(iv["ToA_exposure"][37])
+    r = measureToA_fourier(tm, x, E)
+    o = O.fit_toa(x, E, tm, brutemin=False)
+    assert abs(r["phShi"] - o["phShi"]) / (2 * math.pi) < 1e-6
+    assert r["phShi_LL"] == o["phShi_LL"] and r["phShi_UL"] == o["phShi_UL"]
+    tc = json.load(open(gpath("cauchy_vm_theta.json")))
+    gx = gold("templatemodels.npz")["x"]
+    for fn, model in ((measureToA_cauchy, "cauchy"), (measureToA_vonmises, "vonmises")):
+        t = {"model": model, "norm": {"value": 5.0, "vary": True}}
+        for j in (1, 2):
+            for nm in ("amp", "cen", "wid"):
+                t["%s_%d" % (nm, j)] = {"value": tc["%s_%d" % (nm, j)], "vary": True}
+        r = fn(t, gx, 250.0, brutemin=True)
+        o = O.fit_toa(gx, 250.0, t, brutemin=True)
+        assert abs(r["phShi"] - o["phShi"]) / (2 * math.pi) < 1e-6, model
+        assert r["phShi_LL"] == o["phShi_LL"] and r["phShi_UL"] == o["phShi_UL"], model
+
+
+def test_measuretoas_end_to_end(gpu, tmp_path):
+    """measureToAs on a FITS file written from the bundled events: the golden table rows 35-41."""
+    from crimp_amd.eventfile import write_events_fits
+    from crimp_amd.measureToAs import measureToAs
+    ev = gold("events_1e2259.npz")
+    p = str(tmp_path / "ev.fits")
+    write_events_fits(p, ev["TIME"], ev["PI"], int(ev["MJDREFI"]), float(ev["MJDREFF"]))
+    out = str(tmp_path / "ToAs")
+    tab = measureToAs(p, gpath("1e2259.par"), gpath("1e2259_template.txt"), gpath("timIntToAs_1e2259.txt"),
+                      eneLow=1, eneHigh=5, toaStart=35, toaEnd=41, brutemin=True, toaFile=out)
+    ref = pd.read_csv(gpath("ToAs_2259.txt"), sep=r"\s+", comment="#")
+    ref = ref[(ref["ToA"] >= 35) & (ref["ToA"] <= 41)].reset_index(drop=True)
+    assert list(tab.columns) == list(ref.columns)
+    for c in ("ToA", "ToA_mid", "ToA_start", "ToA_end", "ToA_lenInt", "ToA_exp", "nbr_events", "count_rate",
+              "phShift_LL", "phShift_UL"):
+        np.testing.assert_array_equal(tab[c].to_numpy(), ref[c].to_numpy(), err_msg=c)
+    assert np.all(np.abs(tab["phShift"] - ref["phShift"]) / (2 * np.pi) < 1e-4)
+    g = gold("toa_1e2259.npz")
+    np.testing.assert_allclose(tab["Hpower"].to_numpy(), g["h5"], rtol=1e-6)
+    lines = open(out + ".txt").read().splitlines()
+    assert lines[0] == open(gpath("ToAs_2259.txt")).read().splitlines()[0]

@@ -1,0 +1,93 @@
+"""The oracle (CPU restatement, test infrastructure) pinned against the reference's own outputs."""
+import json
+import math
+
+import numpy as np
+import pandas as pd
+import pytest
+
+from conftest import gold, gpath
+from oracle import oracle as O
+
+
+def test_periodsearch_config1():
+    g = gold("periodsearch_1e2259.npz")
+    z = O.search(g["time"], g["freq"], 2)
+    assert int(np.argmax(z)) == 200 == int(np.argmax(g["z2_m2"]))
+    np.testing.assert_allclose(z, g["z2_m2"], rtol=1e-11)
+    h = O.search(g["time"], g["freq"], 20, stat="h")
+    assert int(np.argmax(h)) == 200
+    np.testing.assert_allclose(h, g["h_m20"], rtol=1e-11)
+    zd = O.search(g["time"], g["fsub"], 2, freq_dot=g["fd"])
+    np.testing.assert_allclose(zd, g["z2d_m2"][:, 2], rtol=1e-11)
+
+
+def test_periodsearch_synthetic_cases():
+    g = gold("periodsearch_synth.npz")
+    t, f = g["time"], g["freq"]
+    for m in (1, 2, 3, 5):
+        np.testing.assert_allclose(O.search(t, f, m), g["z_m%d" % m], rtol=1e-10)
+    for m in (1, 5, 20):
+        np.testing.assert_allclose(O.search(t, f, m, stat="h"), g["h_m%d" % m], rtol=1e-10, atol=1e-9)
+    np.testing.assert_allclose(O.search(t, f[64:128], 2, freq_dot=g["fd"]), g["z2d_m2"][:, 2], rtol=1e-10)
+    np.testing.assert_allclose(O.search(g["time_perm"], g["freq_nu"], 2), g["z_nonuniform_m2"], rtol=1e-10)
+    np.testing.assert_allclose(O.search(g["time_perm"], g["freq_nu"], 4, stat="h"), g["h_nonuniform_m4"],
+                               rtol=1e-10, atol=1e-9)
+    np.testing.assert_allclose(O.search(t[:1], f[:8], 2), g["z_n1"], rtol=1e-12)
+    np.testing.assert_allclose(O.search(t[:2], f[:8], 2), g["z_n2"], rtol=1e-12)
+    np.testing.assert_allclose(O.search(t[:2], f[:8], 3, stat="h"), g["h_n2"], rtol=1e-12)
+    np.testing.assert_allclose(O.search(t, f[100:101], 2), g["z_m1trial"], rtol=1e-10)
+
+
+def test_calcphase():
+    g = gold("calcphase.npz")
+    tot, fol = O.calcphase(g["t"], gpath("1e2259.par"))
+    assert np.array_equal(tot, g["total_par"]) and np.array_equal(fol, g["folded_par"])
+    tm = json.load(open(gpath("timing_model_dict.json")))
+    tot, fol = O.calcphase(g["t"], tm)
+    np.testing.assert_allclose(tot, g["total_dict"], rtol=0, atol=1e-9)
+    np.testing.assert_allclose(fol, g["folded_dict"], rtol=0, atol=1e-9)
+
+
+def test_fourier_ll_points():
+    g = gold("toa_1e2259.npz")
+    iv = pd.read_csv(gpath("timIntToAs_1e2259.txt"), sep=r"\s+", comment="#")
+    tm = json.load(open(gpath("parsed.json")))["template"]
+    tarr = O.template_arrays(tm)
+    for k in range(g["ll_val"].size):
+        i = int(np.nonzero(g["ids"] == g["ll_toa"][k])[0][0])
+        x = g["folded"][g["offsets"][i]:g["offsets"][i + 1]]
+        ll = O.toa_eval(np.sort(x), float(iv["ToA_exposure"][g["ll_toa"][k]]), tarr, g["ll_norm"][k],
+                        g["ll_phi"][k])[0]
+        assert abs(ll - g["ll_val"][k]) <= 1e-9 * abs(g["ll_val"][k])
+    x0 = g["folded"][g["offsets"][0]:g["offsets"][1]]
+    assert O.toa_eval(x0, 600.0, tarr, 0.5, 0.0)[0] == -np.inf == g["ll_inf"]
+
+
+def test_cauchy_vonmises_ll():
+    g = gold("templatemodels.npz")
+    tc = json.load(open(gpath("cauchy_vm_theta.json")))
+    i = 0
+    for p in (-4.0, -0.5, 0.3, 2.2):
+        for nv in (3.0, 5.0, 8.0):
+            for model, key in (("cauchy", "cauchy"), ("vonmises", "vonmises")):
+                tarr = O.template_arrays(dict(tc, model=model))
+                ll = O.toa_eval(g["x"], 250.0, tarr, nv, p)[0]
+                assert abs(ll - g[key][i]) <= 1e-9 * abs(g[key][i]), (model, p, nv)
+            i += 1
+
+
+def test_toa_fit_matches_reference_table():
+    """data/ToAs_2259.txt rows 35-41: phShift within 1e-4 cycles, LL/UL exact, redChi2 ~2e-4."""
+    g = gold("toa_1e2259.npz")
+    iv = pd.read_csv(gpath("timIntToAs_1e2259.txt"), sep=r"\s+", comment="#")
+    ref = pd.read_csv(gpath("ToAs_2259.txt"), sep=r"\s+", comment="#")
+    tm = json.load(open(gpath("parsed.json")))["template"]
+    for i, tid in enumerate(g["ids"]):
+        x = g["folded"][g["offsets"][i]:g["offsets"][i + 1]]
+        r = O.fit_toa(x, float(iv["ToA_exposure"][tid]), tm, brutemin=True)
+        row = ref[ref["ToA"] == tid].iloc[0]
+        assert abs(r["phShi"] - row["phShift"]) / (2 * math.pi) < 1e-4
+        assert r["phShi_LL"] == pytest.approx(row["phShift_LL"], abs=1e-12)
+        assert r["phShi_UL"] == pytest.approx(row["phShift_UL"], abs=1e-12)
+        assert r["reducedChi2"] == pytest.approx(row["redChi2"], rel=5e-4)

@@ -1,0 +1,35 @@
+#!/bin/bash
+# One GPU session: parity tests, smoke, a short bench, and a rocprofv3 kernel-trace profile.
+# Every GPU step has its own time limit; a fault/abort/timeout ends the script (no retries).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+stop_on_fault() {  # rc 0 ok, 1 = test failures (not a fault); anything else: stop here
+    local rc=$1 name=$2
+    echo "[$name] rc=$rc" | tee -a "$OUT/steps.log"
+    if [ "$rc" -ne 0 ] && [ "$rc" -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit "$rc"; fi
+}
+STEPS=${STEPS:-tests,smoke,bench,prof}
+if [[ $STEPS == *tests* ]]; then
+  timeout -k 10 900 python -m pytest tests -m gpu -q -rs -x ${PYTEST_ARGS:-} > "$OUT/pytest_gpu.log" 2>&1
+  stop_on_fault $? pytest
+  tail -5 "$OUT/pytest_gpu.log"
+fi
+if [[ $STEPS == *smoke* ]]; then
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
+  stop_on_fault $? smoke
+  tail -2 "$OUT/smoke.log"
+fi
+if [[ $STEPS == *bench* ]]; then
+  timeout -k 10 600 python bench.py ${BENCH_ARGS:---steps 3 --warmup 1} > "$OUT/bench.log" 2>&1
+  stop_on_fault $? bench
+  tail -1 "$OUT/bench.log"
+fi
+if [[ $STEPS == *prof* ]]; then
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
+      python bench.py ${PROF_ARGS:---steps 2 --warmup 1 --no-cpu} > "$OUT/prof.log" 2>&1
+  stop_on_fault $? rocprof
+  find "$OUT/prof" -name "*stats*" | head
+fi
