@@ -16,6 +16,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -46,28 +47,62 @@ static int set_err(int code, const std::string& msg) {
         if (!(cond)) return set_err(CRIMP_ERR_ARG, msg);                                           \
     } while (0)
 
-// Stream-ordered scratch allocation (hipMallocAsync pool); freed in the destructor on the
-// same stream, so buffers of an async device-pointer call live exactly as long as its kernels.
+// CRIMP_DEBUG=1: poison every scratch allocation with 0xFF (NaN) bytes before use.
+static int debug_level() {
+    static int lvl = -1;
+    if (lvl < 0) {
+        const char* e = getenv("CRIMP_DEBUG");
+        lvl = e ? atoi(e) : 0;
+    }
+    return lvl;
+}
+
+// Device scratch: a small caching allocator (hipMalloc'd blocks reused across calls). Every
+// entry point synchronises its stream before returning and calls are serialised by g_mutex, so
+// a block handed back at the end of a call is idle when the next call takes it.
+struct Block {
+    void* p;
+    size_t bytes;
+    int dev;
+    bool busy;
+};
+static std::vector<Block> g_blocks;
+
 struct Scratch {
     hipStream_t s;
-    std::vector<void*> ptrs;
-    explicit Scratch(hipStream_t st) : s(st) {}
+    int dev = 0;
+    std::vector<size_t> held;
+    explicit Scratch(hipStream_t st) : s(st) { (void)hipGetDevice(&dev); }
     ~Scratch() {
-        for (void* p : ptrs) (void)hipFreeAsync(p, s);
+        for (size_t i : held) g_blocks[i].busy = false;
     }
     template <typename T>
     hipError_t alloc(T** out, size_t count) {
-        void* p = nullptr;
-        size_t bytes = std::max<size_t>(count * sizeof(T), 16);
-        hipError_t e = hipMallocAsync(&p, bytes, s);
-        if (e != hipSuccess) return e;
-        ptrs.push_back(p);
-        *out = static_cast<T*>(p);
+        const size_t bytes = (std::max<size_t>(count * sizeof(T), 16) + 255) & ~size_t(255);
+        size_t pick = (size_t)-1;
+        for (size_t i = 0; i < g_blocks.size(); ++i) {
+            const Block& b = g_blocks[i];
+            if (!b.busy && b.dev == dev && b.bytes >= bytes && b.bytes <= 2 * bytes + (1u << 20) &&
+                (pick == (size_t)-1 || b.bytes < g_blocks[pick].bytes))
+                pick = i;
+        }
+        if (pick == (size_t)-1) {
+            void* p = nullptr;
+            hipError_t e = hipMalloc(&p, bytes);
+            if (e != hipSuccess) return e;
+            g_blocks.push_back(Block{p, bytes, dev, false});
+            pick = g_blocks.size() - 1;
+        }
+        g_blocks[pick].busy = true;
+        held.push_back(pick);
+        *out = static_cast<T*>(g_blocks[pick].p);
+        if (debug_level() > 0) return hipMemset(g_blocks[pick].p, 0xFF, g_blocks[pick].bytes);
         return hipSuccess;
     }
 };
 
-// An input array: either the caller's device pointer or a staged copy of a host array.
+// Host staging uses blocking copies: inputs are copied before any kernel of the call is queued,
+// outputs after the stream has drained.
 template <typename T>
 static hipError_t stage_in(Scratch& sc, const T* src, size_t count, bool dev, const T** out) {
     if (dev || src == nullptr || count == 0) {
@@ -77,9 +112,8 @@ static hipError_t stage_in(Scratch& sc, const T* src, size_t count, bool dev, co
     T* d = nullptr;
     hipError_t e = sc.alloc(&d, count);
     if (e != hipSuccess) return e;
-    e = hipMemcpyAsync(d, src, count * sizeof(T), hipMemcpyHostToDevice, sc.s);
     *out = d;
-    return e;
+    return hipMemcpy(d, src, count * sizeof(T), hipMemcpyHostToDevice);
 }
 
 template <typename T>
@@ -94,7 +128,17 @@ static hipError_t stage_out(Scratch& sc, T* dst, size_t count, bool dev, T** out
 template <typename T>
 static hipError_t copy_back(hipStream_t s, T* host, const T* devp, size_t count, bool dev) {
     if (dev || host == nullptr || count == 0) return hipSuccess;
-    return hipMemcpyAsync(host, devp, count * sizeof(T), hipMemcpyDeviceToHost, s);
+    hipError_t e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return e;
+    return hipMemcpy(host, devp, count * sizeof(T), hipMemcpyDeviceToHost);
+}
+
+// blocking host <-> device copies of small host-side tables
+static hipError_t h2d(void* d, const void* h, size_t bytes) { return hipMemcpy(d, h, bytes, hipMemcpyHostToDevice); }
+static hipError_t d2h(hipStream_t s, void* h, const void* d, size_t bytes) {
+    hipError_t e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return e;
+    return hipMemcpy(h, d, bytes, hipMemcpyDeviceToHost);
 }
 
 static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
@@ -635,8 +679,9 @@ extern "C" int crimp_device_count(int32_t* count) {
 }
 
 static int finish(hipStream_t s, uint32_t flags) {
+    (void)flags;
     HIPCHK(hipGetLastError());
-    if (!(flags & CRIMP_FLAG_DEVICE_PTRS) || (flags & CRIMP_FLAG_SYNC)) HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(hipStreamSynchronize(s));  // every call returns with its stream drained (scratch reuse)
     return CRIMP_OK;
 }
 
@@ -671,7 +716,7 @@ extern "C" int crimp_calcphase(const double* t_mjd, int64_t n, const crimp_timin
         Scratch sc(s);
         CPModel* dm = nullptr;
         HIPCHK(sc.alloc(&dm, 1));
-        HIPCHK(hipMemcpyAsync(dm, &hm, sizeof(CPModel), hipMemcpyHostToDevice, s));
+        HIPCHK(h2d(dm, &hm, sizeof(CPModel)));
         const double* dt = nullptr;
         double *dtot = nullptr, *dfol = nullptr;
         HIPCHK(stage_in(sc, t_mjd, (size_t)n, dev, &dt));
@@ -700,11 +745,21 @@ static void launch_direct(int G, bool firstk, dim3 grid, hipStream_t s, const do
 #define CRIMP_LD(GG, FF) \
     k_search_direct<GG, TWOD, FF, HW><<<grid, kSearchBlock, 0, s>>>(dt, dt2, n, chunk, fr, nf, c2, first, count, k0, ncomp, part)
     if (firstk) {
-        if (G == 8) CRIMP_LD(8, true); else if (G == 4) CRIMP_LD(4, true); else if (G == 2) CRIMP_LD(2, true); else CRIMP_LD(1, true);
+        if (G == 4) CRIMP_LD(4, true); else if (G == 3) CRIMP_LD(3, true); else if (G == 2) CRIMP_LD(2, true); else CRIMP_LD(1, true);
     } else {
-        if (G == 8) CRIMP_LD(8, false); else if (G == 4) CRIMP_LD(4, false); else if (G == 2) CRIMP_LD(2, false); else CRIMP_LD(1, false);
+        if (G == 4) CRIMP_LD(4, false); else if (G == 3) CRIMP_LD(3, false); else if (G == 2) CRIMP_LD(2, false); else CRIMP_LD(1, false);
     }
 #undef CRIMP_LD
+}
+
+// Harmonic groups of the direct kernel. Inside a group harmonics come from the group's first
+// harmonic (exact fp64 phase) by angle addition with the fundamental. The fp32 sin/cos error is
+// periodic in the quarter turn, so a harmonic k = 0 (mod 4) reached by angle addition from the
+// fundamental inherits a coherent bias (its e^{-ik theta} error component sums over photons);
+// groups therefore start at k = 1 and at every multiple of 4: {1,2,3}, {4..7}, {8..11}, ...
+static int direct_group(int k0, int m) {
+    const int rem = m - k0 + 1;
+    return k0 == 1 ? (rem < 3 ? rem : 3) : (rem < 4 ? rem : 4);
 }
 
 extern "C" int crimp_search(const double* t, int64_t n, double t0, const double* freq, int64_t nf,
@@ -734,14 +789,14 @@ extern "C" int crimp_search(const double* t, int64_t n, double t0, const double*
         if (twod) {
             std::vector<double> fdh((size_t)nfd), c2h((size_t)nfd);
             if (dev) {
-                HIPCHK(hipMemcpyAsync(fdh.data(), log10_negfdot, nfd * sizeof(double), hipMemcpyDeviceToHost, s));
+                HIPCHK(d2h(s, fdh.data(), log10_negfdot, nfd * sizeof(double)));
                 HIPCHK(hipStreamSynchronize(s));
             } else {
                 std::memcpy(fdh.data(), log10_negfdot, nfd * sizeof(double));
             }
             for (int64_t r = 0; r < nfd; ++r) c2h[r] = 0.5 * (-1.0 * std::pow(10.0, fdh[r]));
             HIPCHK(sc.alloc(&dc2, (size_t)nfd));
-            HIPCHK(hipMemcpyAsync(dc2, c2h.data(), nfd * sizeof(double), hipMemcpyHostToDevice, s));
+            HIPCHK(h2d(dc2, c2h.data(), nfd * sizeof(double)));
             // c2h must stay alive until the copy has been consumed
             HIPCHK(hipStreamSynchronize(s));
         }
@@ -769,8 +824,7 @@ extern "C" int crimp_search(const double* t, int64_t n, double t0, const double*
             const bool hw = flags & CRIMP_FLAG_HW_SINCOS;
             int k0 = 1;
             while (k0 <= nharm) {
-                const int rem = nharm - k0 + 1;
-                const int G = rem >= 8 ? 8 : rem >= 4 ? 4 : rem >= 2 ? 2 : 1;
+                const int G = direct_group(k0, nharm);
                 if (twod) {
                     if (hw) launch_direct<true, true>(G, k0 == 1, grid, s, ddt, ddt2, n, chunk, dfr, nf, dc2, first, count, k0, ncomp, part);
                     else launch_direct<true, false>(G, k0 == 1, grid, s, ddt, ddt2, n, chunk, dfr, nf, dc2, first, count, k0, ncomp, part);
@@ -831,8 +885,8 @@ extern "C" int crimp_toa_points(const double* x, const int64_t* offsets, int64_t
     // groups of <= 4 consecutive points sharing an interval (host needs the interval ids)
     std::vector<int64_t> pint((size_t)npts), hoff((size_t)nint + 1);
     if (dev) {
-        HIPCHK(hipMemcpyAsync(pint.data(), pt_interval, npts * sizeof(int64_t), hipMemcpyDeviceToHost, s));
-        HIPCHK(hipMemcpyAsync(hoff.data(), offsets, (nint + 1) * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        HIPCHK(d2h(s, pint.data(), pt_interval, npts * sizeof(int64_t)));
+        HIPCHK(d2h(s, hoff.data(), offsets, (nint + 1) * sizeof(int64_t)));
         HIPCHK(hipStreamSynchronize(s));
     } else {
         std::memcpy(pint.data(), pt_interval, npts * sizeof(int64_t));
@@ -868,10 +922,10 @@ extern "C" int crimp_toa_points(const double* x, const int64_t* offsets, int64_t
         HIPCHK(sc.alloc(&dgi, (size_t)ng));
         HIPCHK(sc.alloc(&dgf, (size_t)ng));
         HIPCHK(sc.alloc(&dgn, (size_t)ng));
-        HIPCHK(hipMemcpyAsync(dT, &T, sizeof(T), hipMemcpyHostToDevice, s));
-        HIPCHK(hipMemcpyAsync(dgi, gint.data(), ng * sizeof(int64_t), hipMemcpyHostToDevice, s));
-        HIPCHK(hipMemcpyAsync(dgf, gfirst.data(), ng * sizeof(int64_t), hipMemcpyHostToDevice, s));
-        HIPCHK(hipMemcpyAsync(dgn, gnp.data(), ng * sizeof(int32_t), hipMemcpyHostToDevice, s));
+        HIPCHK(h2d(dT, &T, sizeof(T)));
+        HIPCHK(h2d(dgi, gint.data(), ng * sizeof(int64_t)));
+        HIPCHK(h2d(dgf, gfirst.data(), ng * sizeof(int64_t)));
+        HIPCHK(h2d(dgn, gnp.data(), ng * sizeof(int32_t)));
         k_toa_points<<<(unsigned)ng, kPtsBlock, 0, s>>>(dx, doff, dT, dgi, dgf, dgn, dn, dp, dout);
         HIPCHK(hipGetLastError());
         HIPCHK(copy_back(s, out, dout, (size_t)npts * 8, dev));
@@ -897,7 +951,7 @@ extern "C" int crimp_toa_grid(const double* x, const int64_t* offsets, int64_t n
     hipStream_t s = as_stream(stream);
     std::vector<int64_t> hoff((size_t)nint + 1);
     if (dev) {
-        HIPCHK(hipMemcpyAsync(hoff.data(), offsets, (nint + 1) * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        HIPCHK(d2h(s, hoff.data(), offsets, (nint + 1) * sizeof(int64_t)));
         HIPCHK(hipStreamSynchronize(s));
     } else {
         std::memcpy(hoff.data(), offsets, (nint + 1) * sizeof(int64_t));
@@ -926,7 +980,7 @@ extern "C" int crimp_toa_grid(const double* x, const int64_t* offsets, int64_t n
         HIPCHK(sc.alloc(&ph, (size_t)(splits * nint * nphi)));
         TplDev* dT = nullptr;
         HIPCHK(sc.alloc(&dT, 1));
-        HIPCHK(hipMemcpyAsync(dT, &T, sizeof(T), hipMemcpyHostToDevice, s));
+        HIPCHK(h2d(dT, &T, sizeof(T)));
         ARGCHK(nint <= 65535, "at most 65535 intervals per brute-grid call");
         dim3 grid((unsigned)pblocks, (unsigned)nint, (unsigned)splits);
         for (int64_t a0 = 0; a0 < nnorm; a0 += kGridNN) {
@@ -937,8 +991,8 @@ extern "C" int crimp_toa_grid(const double* x, const int64_t* offsets, int64_t n
         }
         // combine splits on the host in a fixed order (deterministic)
         std::vector<double> hl((size_t)(splits * nint * nnorm * nphi)), hh((size_t)(splits * nint * nphi));
-        HIPCHK(hipMemcpyAsync(hl.data(), pl, hl.size() * sizeof(double), hipMemcpyDeviceToHost, s));
-        HIPCHK(hipMemcpyAsync(hh.data(), ph, hh.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+        HIPCHK(d2h(s, hl.data(), pl, hl.size() * sizeof(double)));
+        HIPCHK(d2h(s, hh.data(), ph, hh.size() * sizeof(double)));
         HIPCHK(hipStreamSynchronize(s));
         const int64_t L = nint * nnorm * nphi, H = nint * nphi;
         std::vector<double> rl((size_t)L), rh((size_t)H);
@@ -953,8 +1007,8 @@ extern "C" int crimp_toa_grid(const double* x, const int64_t* offsets, int64_t n
             rh[(size_t)k] = v;
         }
         if (dev) {
-            HIPCHK(hipMemcpyAsync(lnsum, rl.data(), L * sizeof(double), hipMemcpyHostToDevice, s));
-            HIPCHK(hipMemcpyAsync(hmin, rh.data(), H * sizeof(double), hipMemcpyHostToDevice, s));
+            HIPCHK(h2d(lnsum, rl.data(), L * sizeof(double)));
+            HIPCHK(h2d(hmin, rh.data(), H * sizeof(double)));
             HIPCHK(hipStreamSynchronize(s));
         } else {
             std::memcpy(lnsum, rl.data(), L * sizeof(double));
@@ -974,7 +1028,7 @@ extern "C" int crimp_binphases(const double* x, const int64_t* offsets, int64_t 
     hipStream_t s = as_stream(stream);
     int64_t ntot = 0;
     if (dev) {
-        HIPCHK(hipMemcpyAsync(&ntot, offsets + nint, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        HIPCHK(d2h(s, &ntot, offsets + nint, sizeof(int64_t)));
         HIPCHK(hipStreamSynchronize(s));
     } else {
         ntot = offsets[nint];

@@ -12,9 +12,10 @@
  *   - every buffer is caller-owned; with CRIMP_FLAG_DEVICE_PTRS all array
  *     arguments are device pointers on the current HIP device, otherwise they are
  *     host pointers and the library stages them through device memory itself;
- *   - `stream` is a hipStream_t (NULL = the null stream). Host-pointer calls are
- *     synchronous; device-pointer calls return after enqueueing unless
- *     CRIMP_FLAG_SYNC is given;
+ *   - `stream` is a hipStream_t (NULL = the null stream); kernels are queued on it
+ *     and every call returns with that stream drained (host staging copies are
+ *     blocking), so results are ready on return -- CRIMP_FLAG_SYNC is accepted and
+ *     implied;
  *   - calls are serialised per device (internal mutex); the ctypes layer releases
  *     the GIL around them.
  */

@@ -33,3 +33,29 @@ if [[ $STEPS == *prof* ]]; then
   stop_on_fault $? rocprof
   find "$OUT/prof" -name "*stats*" | head
 fi
+if [[ $STEPS == *k4* ]]; then
+  timeout -k 10 300 python tools/diag_k4.py > "$OUT/k4.log" 2>&1
+  stop_on_fault $? k4
+  cat "$OUT/k4.log"
+fi
+if [[ $STEPS == *harm* ]]; then
+  timeout -k 10 600 python tools/diag_harm.py > "$OUT/harm.log" 2>&1
+  stop_on_fault $? harm
+  cat "$OUT/harm.log"
+fi
+if [[ $STEPS == *diag* ]]; then
+  timeout -k 10 600 python tools/diag_search.py > "$OUT/diag.log" 2>&1
+  stop_on_fault $? diag
+  cat "$OUT/diag.log"
+fi
+if [[ $STEPS == *repeat* ]]; then
+  timeout -k 10 300 python tools/diag_repeat.py > "$OUT/repeat.log" 2>&1
+  stop_on_fault $? repeat
+  cat "$OUT/repeat.log"
+  CRIMP_DEBUG=1 timeout -k 10 300 python tools/diag_repeat.py > "$OUT/repeat_dbg.log" 2>&1
+  stop_on_fault $? repeat_dbg
+  cat "$OUT/repeat_dbg.log"
+  AMD_SERIALIZE_KERNEL=3 AMD_SERIALIZE_COPY=3 timeout -k 10 300 python tools/diag_repeat.py > "$OUT/repeat_ser.log" 2>&1
+  stop_on_fault $? repeat_ser
+  cat "$OUT/repeat_ser.log"
+fi
