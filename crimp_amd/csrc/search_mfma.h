@@ -18,6 +18,71 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr int kMfmaChunk = 32;
 constexpr int kTile = 1024;
 
+// sin/cos(2*pi*r) rotated by qadd quarter turns (exact: the rotation is folded into the quadrant
+// index of sincos_rev_poly, so the fp32 phase is never offset).
+__device__ __forceinline__ void sincos_rev_q(float r, int qadd, float& s, float& c) {
+    const float q = __builtin_rintf(4.0f * r);
+    const float y = __builtin_fmaf(-0.25f, q, r);
+    const float y2 = y * y;
+    float sp = __builtin_fmaf(y2, 42.0587782776566f, -76.7058597530613f);
+    sp = __builtin_fmaf(y2, sp, 81.6052492760750f);
+    sp = __builtin_fmaf(y2, sp, -41.3417022403997f);
+    sp = __builtin_fmaf(y2, sp, 6.28318530717958647692f);
+    sp *= y;
+    float cp = __builtin_fmaf(y2, -26.4262625987960f, 60.2446397079094f);
+    cp = __builtin_fmaf(y2, cp, -85.4568172844813f);
+    cp = __builtin_fmaf(y2, cp, 64.9393940226683f);
+    cp = __builtin_fmaf(y2, cp, -19.7392088021787f);
+    cp = __builtin_fmaf(y2, cp, 1.0f);
+    const int iq = ((int)q + qadd) & 3;
+    const float s_a = (iq & 1) ? cp : sp;
+    const float c_a = (iq & 1) ? sp : cp;
+    s = (iq & 2) ? -s_a : s_a;
+    c = ((iq + 1) & 2) ? -c_a : c_a;
+}
+
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+    return __hiloint2double(hi, lo);
+}
+
+// One photon of one wave's tile: operands of harmonics k0 .. k0+G-1 and their 2G MFMAs.
+// Lane l supplies A[a = l&31][h = l>>5] and B[h][b = l&31]; with U' = U*i^h and V' = V*(-i)^h:
+//   Re-product operand A = (Re U', Im U'), B = Re V'   (h=0: Ur | Ui, Vr;  h=1: -Ui | Ur, Vi).
+// FIRST groups take harmonic 2 by squaring (unbiased: the sin/cos error is quarter-turn periodic);
+// later groups evaluate every harmonic from its own fp64 phase.
+template <int G, bool FIRST>
+__device__ __forceinline__ void mfma_photon(double phu, double phv, int h, int k0, f32x16 (&re)[G], f32x16 (&im)[G]) {
+    if (FIRST) {
+        float us, uc, vs, vc;
+        sincos_rev_q((float)(phu - rint(phu)), h, us, uc);
+        sincos_rev_q((float)(phv - rint(phv)), 3 * h, vs, vc);
+        re[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(uc, vc, re[0], 0, 0, 0);
+        im[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(us, vc, im[0], 0, 0, 0);
+        if (G > 1) {
+            const float c2u = __builtin_fmaf(uc, uc, -us * us), s2u = 2.0f * uc * us;
+            const float c2v = __builtin_fmaf(vc, vc, -vs * vs), s2v = 2.0f * vc * vs;
+            const float are = h ? s2u : c2u;
+            const float aim = h ? -c2u : s2u;
+            const float bop = h ? -s2v : c2v;
+            re[G - 1] = __builtin_amdgcn_mfma_f32_32x32x2f32(are, bop, re[G - 1], 0, 0, 0);
+            im[G - 1] = __builtin_amdgcn_mfma_f32_32x32x2f32(aim, bop, im[G - 1], 0, 0, 0);
+        }
+    } else {
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const double kf = (double)(k0 + g);
+            const double pu = phu * kf, pv = phv * kf;
+            float us, uc, vs, vc;
+            sincos_rev_q((float)(pu - rint(pu)), h, us, uc);
+            sincos_rev_q((float)(pv - rint(pv)), 3 * h, vs, vc);
+            re[g] = __builtin_amdgcn_mfma_f32_32x32x2f32(uc, vc, re[g], 0, 0, 0);
+            im[g] = __builtin_amdgcn_mfma_f32_32x32x2f32(us, vc, im[g], 0, 0, 0);
+        }
+    }
+}
+
 template <int G, bool TWOD, bool FIRST>
 __global__ __launch_bounds__(256, 2) void k_search_mfma(
     const double* __restrict__ dt, const double* __restrict__ dt2, int64_t n, int64_t chunk,
@@ -31,13 +96,12 @@ __global__ __launch_bounds__(256, 2) void k_search_mfma(
     const int64_t frow = gt / tiles_per_row;
     const int64_t c0 = (gt - frow * tiles_per_row) * kTile;
     const int a = lane & 31;
-    const bool hi = lane >= 32;
+    const int h = lane >> 5;
     int64_t ca = c0 + a;
     ca = ca < nf ? ca : nf - 1;
     const double fa = freq[ca];
     const double gb = (double)(32 * a) * delta;
     const double c2 = TWOD ? c2row[frow] : 0.0;
-    const double kf = (double)k0;
     const int64_t split = blockIdx.y;
     const int64_t i0 = split * chunk;
     const int64_t i1 = i0 + chunk < n ? i0 + chunk : n;
@@ -49,43 +113,28 @@ __global__ __launch_bounds__(256, 2) void k_search_mfma(
         for (int r = 0; r < 16; ++r) Cr[g][r] = Ci[g][r] = 0.0;
 
     for (int64_t ib = i0; ib < i1; ib += kMfmaChunk) {
+        const int cnt = (int)(i1 - ib < kMfmaChunk ? i1 - ib : kMfmaChunk);
+        // the chunk's photon times: one coalesced load, then broadcast with v_readlane
+        const double dtv = a < cnt ? dt[ib + a] : 0.0;
+        const double d2v = TWOD ? (a < cnt ? dt2[ib + a] : 0.0) : 0.0;
         f32x16 re[G], im[G];
 #pragma unroll
         for (int g = 0; g < G; ++g) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) re[g][r] = im[g][r] = 0.0f;
         }
-        const int64_t ie = ib + kMfmaChunk < i1 ? ib + kMfmaChunk : i1;
-        for (int64_t i = ib; i < ie; ++i) {
-            const double d = dt[i];
-            const double phu1 = TWOD ? fma(fa, d, c2 * dt2[i]) : fa * d;
-            const double phv1 = gb * d;
-            float su1, cu1, sv1, cv1;
-            sincos_rev_poly((float)(phu1 - rint(phu1)), su1, cu1);
-            sincos_rev_poly((float)(phv1 - rint(phv1)), sv1, cv1);
-            float su, cu, sv, cv;
-            if (FIRST) {
-                su = su1; cu = cu1; sv = sv1; cv = cv1;
-            } else {
-                const double phu = phu1 * kf, phv = phv1 * kf;
-                sincos_rev_poly((float)(phu - rint(phu)), su, cu);
-                sincos_rev_poly((float)(phv - rint(phv)), sv, cv);
-            }
+        if (cnt == kMfmaChunk) {
 #pragma unroll
-            for (int g = 0; g < G; ++g) {
-                const float bop = hi ? sv : cv;
-                const float are = hi ? -su : cu;
-                const float aim = hi ? cu : su;
-                re[g] = __builtin_amdgcn_mfma_f32_32x32x2f32(are, bop, re[g], 0, 0, 0);
-                im[g] = __builtin_amdgcn_mfma_f32_32x32x2f32(aim, bop, im[g], 0, 0, 0);
-                if (g + 1 < G) {  // next harmonic by angle addition with the fundamental
-                    const float cun = __builtin_fmaf(cu, cu1, -su * su1);
-                    su = __builtin_fmaf(su, cu1, cu * su1);
-                    cu = cun;
-                    const float cvn = __builtin_fmaf(cv, cv1, -sv * sv1);
-                    sv = __builtin_fmaf(sv, cv1, cv * sv1);
-                    cv = cvn;
-                }
+            for (int p = 0; p < kMfmaChunk; ++p) {
+                const double d = readlane_d(dtv, p);
+                const double phu = TWOD ? fma(fa, d, c2 * readlane_d(d2v, p)) : fa * d;
+                mfma_photon<G, FIRST>(phu, gb * d, h, k0, re, im);
+            }
+        } else {
+            for (int p = 0; p < cnt; ++p) {
+                const double d = readlane_d(dtv, p);
+                const double phu = TWOD ? fma(fa, d, c2 * readlane_d(d2v, p)) : fa * d;
+                mfma_photon<G, FIRST>(phu, gb * d, h, k0, re, im);
             }
         }
 #pragma unroll
@@ -100,7 +149,7 @@ __global__ __launch_bounds__(256, 2) void k_search_mfma(
     // D[row][col] of the 32x32 tile: col = lane&31 (b), row = (r&3) + 8*(r>>2) + 4*(lane>>5) (a)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-        const int ra = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int ra = (r & 3) + 8 * (r >> 2) + 4 * h;
         const int64_t c = c0 + ra + 32 * a;
         const int64_t t = frow * nf + c - first;
         if (c < nf && t >= 0 && t < count) {
@@ -192,9 +241,8 @@ static int mfma_search(Scratch& sc, hipStream_t s, const double* dt, const doubl
     if (e != hipSuccess) return set_err(CRIMP_ERR_HIP, std::string("mfma_search alloc: ") + hipGetErrorString(e));
     dim3 grid((unsigned)cdiv(nt, 4), (unsigned)splits);
     for (int k0 = 1; k0 <= nharm;) {
-        // groups {1,2}, {3}, {4,5}, {6,7}, {8,9}, ...: never reach k = 0 (mod 4) by angle addition
-        // from the fundamental (see direct_group in crimp_hip.hip)
-        const int G = ((nharm - k0 + 1) >= 2 && (k0 & 3) != 3) ? 2 : 1;
+        // groups {1,2}, {3,4}, {5,6}, ...: harmonic 2 by squaring, later ones from exact phases
+        const int G = (nharm - k0 + 1) >= 2 ? 2 : 1;
         if (twod)
             launch_mfma<true>(G, k0 == 1, grid, s, dt, dt2, n, chunk, freq, nf, c2, delta, tf, nt, tpr, first, count, k0,
                               ncomp, part);
