@@ -24,6 +24,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PEAK_F32_TFLOPS = 157.3  # MI355X_MICROARCH.md: peak FP32 vector = FP32-input MFMA (spec)
+# HBM bytes per k_search_mfma launch of this workload from rocprofv3 PMC passes
+# (profiles/r1/search_mfma_pmc_summary.json): (2 x FETCH_SIZE + WRITE_SIZE) KB x 1024, FETCH_SIZE
+# doubled per the gfx950 correction in MI355X_MICROARCH.md (HBM section).
+PMC_TRAFFIC_BYTES = (2 * 588447.5625 + 153453.875) * 1024
 FLOP_PER_EVAL_HARM = 8.0
 
 
@@ -37,7 +41,51 @@ def parse():
     p.add_argument("--nharm", type=int, default=2)
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--toa-intervals", type=int, default=1250, help="ToA intervals per GPU (config 5: 1e4 over 8)")
+    p.add_argument("--toa-photons", type=int, default=100_000)
+    p.add_argument("--no-toa", action="store_true", help="skip the ToA-fit throughput leg")
     return p.parse_args()
+
+
+# 1E 2259+586 Fourier template (data/1e2259_template.txt), config 5 draws intervals from it
+T2259 = {"model": "fourier", "norm": {"value": 17.060771467236613},
+         "amp": [1.508994969593123, 4.055594828231136, 1.4384785819368275, 0.3505348524380939,
+                 0.19725727340744187, 0.3483402644535841],
+         "ph": [-0.4071967961461897, -0.8051383329477251, 0.5157949575544241, 1.9295783704947946,
+                -0.1917798112304259, 0.8297144204463391]}
+
+
+def toa_leg(a, dev, world, rank):
+    """Config 5 (per GPU): intervals x photons drawn from the 1e2259 template with random true shifts,
+    brute grid + exact MLE + 1-sigma scan + redChi2 per interval (measureToA_fourier -bm), timed."""
+    import torch
+    import torch.distributed as dist
+    from crimp_amd.synth import template_intervals_torch
+    from crimp_amd.toafit import ToAFitter
+    tm = {"model": "fourier", "norm": T2259["norm"]}
+    for j, (am, ph) in enumerate(zip(T2259["amp"], T2259["ph"]), start=1):
+        tm["amp_%d" % j] = {"value": am}
+        tm["ph_%d" % j] = {"value": ph}
+    x, off, E, shifts = template_intervals_torch(a.toa_intervals, a.toa_photons, T2259["norm"]["value"],
+                                                 T2259["amp"], T2259["ph"], seed=2 + rank, device=dev)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    res = ToAFitter(x, off, E, tm).fit(brutemin=True)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t1
+    elt = torch.tensor([el], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elt, op=dist.ReduceOp.MAX)
+    d = np.angle(np.exp(1j * (res["phShi"] - shifts)))  # recovered vs true shift, wrapped
+    return {"toa_fits_per_s": a.toa_intervals * world / float(elt.item()),
+            "toa_config": "config5: %d intervals/GPU x %d photons, Fourier K=6 (1e2259), brute+MLE+1-sigma scan"
+                          % (a.toa_intervals, a.toa_photons),
+            "toa_seconds": float(elt.item()),
+            "toa_shift_recovery_rms_cycles": float(np.sqrt(np.mean(d ** 2)) / (2 * np.pi)),
+            "toa_median_sigma_cycles": float(np.median(res["phShi_LL"]) / (2 * np.pi)),
+            "toa_cpu_reference_fits_per_s": 0.42}
 
 
 def cpu_baseline(t, f0, df, nharm, budget_s):
@@ -151,12 +199,21 @@ def main():
                        "best_trial_index": best_idx, "best_power": float(gb[order[0], 0]),
                        "search_path": os.environ.get("CRIMP_SEARCH", "auto")},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / PEAK_F32_TFLOPS, "traffic": None,
+                         "frac": achieved / PEAK_F32_TFLOPS,
+                         "traffic": PMC_TRAFFIC_BYTES if (a.photons, M, a.nharm) == (10_000_000, 1_000_000, 2)
+                         else None,
                          "kernel_ms": kern_ms,
                          "note": "8 FLOP per photon*trial*harmonic; time = HIP events around the search call"},
         }
         if not a.no_cpu:
             rec["cpu_baseline"] = cpu_baseline(t_h, f0, df, a.nharm, a.cpu_seconds)
+    if not a.no_toa:
+        del t, f, out
+        torch.cuda.empty_cache()
+        toa = toa_leg(a, dev, world, rank)
+        if rank == 0:
+            rec.update(toa)
+    if rank == 0:
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -71,3 +71,40 @@ def template_intervals(n_int, n_per, norm, amps, phs, seed=2):
     offsets = np.arange(n_int + 1, dtype=np.int64) * n_per
     exposure = np.full(n_int, n_per / norm)
     return x, offsets, exposure, shifts
+
+
+def template_intervals_torch(n_int, n_per, norm, amps, phs, seed=2, device="cuda"):
+    """Device-side version of ``template_intervals`` for large benchmark workloads (config 5):
+    rejection sampling of every interval at once with torch; returns device tensors
+    (x [n_int*n_per] fp64, offsets [n_int+1] int64) and host arrays (exposure, true shifts)."""
+    import torch
+    g = torch.Generator(device=device)
+    g.manual_seed(int(seed))
+    amps_t = torch.tensor(amps, dtype=torch.float64, device=device)
+    phs_t = torch.tensor(phs, dtype=torch.float64, device=device)
+    j = torch.arange(1, len(amps) + 1, dtype=torch.float64, device=device)
+    shifts = (torch.rand(n_int, generator=g, device=device, dtype=torch.float64) * 2 - 1) * np.pi
+    ymax = norm + float(np.sum(np.abs(amps)))
+    out = torch.empty(n_int, n_per, dtype=torch.float64, device=device)
+    step = max(1, int(2.0e8 // (2 * n_per * (len(amps) + 3))))  # bound the temporaries (~1.6 GB)
+    for c0 in range(0, n_int, step):
+        c1 = min(n_int, c0 + step)
+        m = c1 - c0
+        filled = torch.zeros(m, dtype=torch.int64, device=device)
+        rows = torch.arange(m, device=device)
+        sh = shifts[c0:c1]
+        while int(filled.min()) < n_per:
+            want = n_per * 2
+            x = torch.rand(m, want, generator=g, device=device, dtype=torch.float64)
+            y = torch.rand(m, want, generator=g, device=device, dtype=torch.float64) * ymax
+            arg = 2 * np.pi * x[..., None] * j + phs_t - j * sh[:, None, None]
+            curve = norm + (amps_t * torch.cos(arg)).sum(-1)
+            keep = y < curve
+            rank = torch.cumsum(keep, dim=1) - 1 + filled[:, None]
+            ok = keep & (rank < n_per)
+            r_idx = rows[:, None].expand(-1, want)[ok]
+            out[c0:c1][r_idx, rank[ok]] = x[ok]
+            filled = torch.clamp(filled + keep.sum(1), max=n_per)
+            del x, y, arg, curve
+    offsets = torch.arange(n_int + 1, dtype=torch.int64, device=device) * n_per
+    return out.reshape(-1), offsets, np.full(n_int, n_per / norm), shifts.cpu().numpy()
