@@ -8,8 +8,7 @@ reference's order of operations and its text formatting (``str()`` of each value
 tab-separated, 13 columns, :161-162, :222-226).
 
 Not implemented in this build (raise ``NotImplementedError``): ``varyAmps`` and
-``readvaryparam`` and the .tim writer ``timFile``
-(§8f row 2).
+``readvaryparam``.
 """
 import argparse
 import math
@@ -23,6 +22,7 @@ from .eventfile import EvtFileOps
 from .logging_utils import configure_logging, get_logger
 from .periodsearch import PeriodSearch
 from .readPPtemplate import readPPtemplate
+from .timfile import phshiftTotimfile
 from .toafit import ToAFitter
 
 logger = get_logger(__name__)
@@ -170,8 +170,9 @@ def measureToAs(evtFile, timMod, tempModPP, toagtifile, eneLow=0.5, eneHigh=10.,
                     str(res["phShi"][k]) + '\t' + str(res["phShi_LL"][k]) + '\t' + str(res["phShi_UL"][k]) + '\t' +
                     str(res["htestPow"][k]) + '\t' + str(res["reducedChi2"][k]) + '\n')
     logger.info('\n Wrote ToA properties to {}.txt'.format(toaFile))
-    if timFile is not None:
-        raise NotImplementedError("the .tim writer (timFile) is not implemented in this build")
+    if timFile is not None:  # measureToAs.py:238-240
+        phshiftTotimfile(toaFile + '.txt', timMod, timFile, tempModPP=tempModPP)
+        logger.info('\n Wrote timfile {}.tim'.format(timFile))
     _plot_residuals(res, toaFile)
     return pd.read_csv(toaFile + '.txt', sep=r'\s+', comment='#')
 

@@ -121,3 +121,27 @@ def test_error_scan_phase_sequence_clip_semantics():
     seq = fit._scan_phases(np.array([1.5 * np.pi - step]), 1, ks)
     np.testing.assert_array_equal(seq[0], np.minimum(1.5 * np.pi - step + ks * step, 1.5 * np.pi))
     del tm
+
+
+def test_tim_writer_matches_reference_tim(tmp_path):
+    """phshiftTotimfile on the reference's ToA table reproduces data/ToAs_2259.tim (all 84 rows); the
+    current writer prefixes each data line with one space (timfile.py:159), the committed file predates it."""
+    from crimp_amd.timfile import phshiftTotimfile, readtimfile
+    out = str(tmp_path / "x")
+    tab = phshiftTotimfile(gpath("ToAs_2259.txt"), gpath("1e2259.par"), out, tempModPP="1e2259_template.txt")
+    got = open(out + ".tim").read().splitlines()
+    ref = open(gpath("ToAs_2259.tim")).read().splitlines()
+    assert got[0] == ref[0] == "FORMAT 1" and len(got) == len(ref) == 85
+    for a, b in zip(got[1:], ref[1:]):
+        assert a == " " + b
+    back = readtimfile(gpath("ToAs_2259.tim"))
+    np.testing.assert_allclose(back["pulse_ToA"].to_numpy(), tab["TOA"].to_numpy(), rtol=2e-16, atol=0)
+    assert list(back.columns[:5]) == ["template", "frequency", "pulse_ToA", "pulse_ToA_err", "time_ref"]
+    with pytest.raises(FileExistsError):
+        phshiftTotimfile(gpath("ToAs_2259.txt"), gpath("1e2259.par"), out)
+
+
+def test_ephem_integer_rotation_lands_on_integer_phase():
+    from crimp_amd.ephemIntegerRotation import ephemIntegerRotation
+    e = ephemIntegerRotation(58144.25468778948, gpath("1e2259.par"))
+    assert abs(e["phase_residual_from_integer"]) < 1e-6 and e["Tmjd_intRotation"] <= 58144.25468778948
