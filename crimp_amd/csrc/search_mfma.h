@@ -177,17 +177,6 @@ static bool freq_is_progression(const std::vector<double>& f, double* delta) {
     return true;
 }
 
-static int g_num_cus = 0;
-static int num_cus() {
-    if (g_num_cus == 0) {
-        int dev = 0;
-        hipDeviceProp_t p;
-        if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&p, dev) == hipSuccess)
-            g_num_cus = p.multiProcessorCount;
-        if (g_num_cus <= 0) g_num_cus = 256;
-    }
-    return g_num_cus;
-}
 
 template <bool TWOD>
 static void launch_mfma(int G, bool firstk, dim3 grid, hipStream_t s, const double* dt, const double* dt2, int64_t n,
@@ -220,19 +209,11 @@ static int mfma_search(Scratch& sc, hipStream_t s, const double* dt, const doubl
     const int64_t tf = (first / nf) * tpr + (first % nf) / kTile;
     const int64_t tl = (last / nf) * tpr + (last % nf) / kTile;
     const int64_t nt = tl - tf + 1;
-    // photon splits: fill the resident wave slots (2 waves/SIMD at this kernel's VGPR budget) in
-    // as few rounds as possible
-    const int64_t slots = (int64_t)num_cus() * 4 * 2;
-    int64_t best_s = 1;
-    double best_cost = 1e300;
-    for (int64_t sp = 1; sp <= 16; ++sp) {
-        if (sp > 1 && cdiv(n, sp) < 256) break;
-        const double cost = (double)cdiv(nt * sp, slots) / (double)sp;
-        if (cost < best_cost - 1e-12) {
-            best_cost = cost;
-            best_s = sp;
-        }
-    }
+    // photon splits depend on the photon count alone, so that every trial's value is bit-identical
+    // however the grid is partitioned (tiles are already aligned to absolute trial indices): a
+    // sharded search returns exactly what one unsharded call returns. 16 splits of >= 64k photons
+    // fill the 2048 resident wave slots from ~128 tiles up at a tail cost <= 1/16 of a round.
+    const int64_t best_s = std::min<int64_t>(16, std::max<int64_t>(1, n / 65536));
     int64_t chunk = cdiv(cdiv(n, best_s), kMfmaChunk) * kMfmaChunk;
     const int64_t splits = cdiv(n, chunk);
     const int ncomp = 2 * nharm;
