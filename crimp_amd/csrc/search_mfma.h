@@ -6,9 +6,9 @@
 //                                         V_b = exp(2*pi*i*k*(32*b*delta)*dt),
 // so the harmonic sums over photons are a complex matrix product
 //     C_ab + i S_ab = sum_i U_ai V_bi,
-// computed as two real 32x32x2 f32 MFMAs per photon and harmonic (K=2 = the (re, im) pair):
-//     Re = [Ur, -Ui] . [Vr; Vi],   Im = [Ui, Ur] . [Vr; Vi].
-// U and V cost 64 sin/cos per photon per wave instead of 1024 for the direct kernel; the phases
+// computed with real 32x32x2 f32 MFMAs whose K=2 index runs over a pair of photons, four per pair
+// and harmonic: Re += Ur.Vr + Ui.(-Vi), Im += Ui.Vr + Ur.Vi.
+// U and V cost 32+32 sin/cos per photon per wave instead of 1024 for the direct kernel; the phases
 // are fp64 and reduced to a centred fractional cycle before the fp32 sin/cos, the MFMA chain
 // accumulates kMfmaChunk photons in fp32 (exact fp32 fma chain) before folding into fp64.
 // One wave owns one tile and one photon range (split); results go to the same part[] layout as
@@ -18,9 +18,8 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr int kMfmaChunk = 32;
 constexpr int kTile = 1024;
 
-// sin/cos(2*pi*r) rotated by qadd quarter turns (exact: the rotation is folded into the quadrant
-// index of sincos_rev_poly, so the fp32 phase is never offset).
-__device__ __forceinline__ void sincos_rev_q(float r, int qadd, float& s, float& c) {
+// sin/cos(2*pi*r), |r| <= 1/2: quarter-turn reduction + the polynomials of sincos_rev_poly.
+__device__ __forceinline__ void sincos_rev_f(float r, float& s, float& c) {
     const float q = __builtin_rintf(4.0f * r);
     const float y = __builtin_fmaf(-0.25f, q, r);
     const float y2 = y * y;
@@ -34,7 +33,7 @@ __device__ __forceinline__ void sincos_rev_q(float r, int qadd, float& s, float&
     cp = __builtin_fmaf(y2, cp, 64.9393940226683f);
     cp = __builtin_fmaf(y2, cp, -19.7392088021787f);
     cp = __builtin_fmaf(y2, cp, 1.0f);
-    const int iq = ((int)q + qadd) & 3;
+    const int iq = (int)q & 3;
     const float s_a = (iq & 1) ? cp : sp;
     const float c_a = (iq & 1) ? sp : cp;
     s = (iq & 2) ? -s_a : s_a;
@@ -47,40 +46,77 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
     return __hiloint2double(hi, lo);
 }
 
-// One photon of one wave's tile: operands of harmonics k0 .. k0+G-1 and their 2G MFMAs.
-// Lane l supplies A[a = l&31][h = l>>5] and B[h][b = l&31]; with U' = U*i^h and V' = V*(-i)^h:
-//   Re-product operand A = (Re U', Im U'), B = Re V'   (h=0: Ur | Ui, Vr;  h=1: -Ui | Ur, Vi).
-// FIRST groups take harmonic 2 by squaring (unbiased: the sin/cos error is quarter-turn periodic);
-// later groups evaluate every harmonic from its own fp64 phase.
+// One photon PAIR of one wave's tile: operands of harmonics k0 .. k0+G-1 and their 4G MFMAs.
+// The MFMA's K=2 index is the photon of the pair: lane l = (a = l&31, h = l>>5) evaluates U_a and
+// V_a of photon 2q+h only (no sin/cos is computed twice), and the complex product is split into
+// real MFMAs:  Re += Ur.Vr + Ui.(-Vi),  Im += Ui.Vr + Ur.Vi.  `live` zeroes the missing photon of
+// an odd tail. FIRST groups take harmonic 2 by squaring (unbiased: the sin/cos error is quarter-turn
+// periodic); later groups evaluate every harmonic from its own fp64 phase.
+template <int G>
+__device__ __forceinline__ void mfma_pair_ops(float uc, float us, float vc, float vs, int g, f32x16 (&re)[G],
+                                              f32x16 (&im)[G]) {
+    re[g] = __builtin_amdgcn_mfma_f32_32x32x2f32(uc, vc, re[g], 0, 0, 0);
+    im[g] = __builtin_amdgcn_mfma_f32_32x32x2f32(us, vc, im[g], 0, 0, 0);
+    re[g] = __builtin_amdgcn_mfma_f32_32x32x2f32(us, -vs, re[g], 0, 0, 0);
+    im[g] = __builtin_amdgcn_mfma_f32_32x32x2f32(uc, vs, im[g], 0, 0, 0);
+}
+
 template <int G, bool FIRST>
-__device__ __forceinline__ void mfma_photon(double phu, double phv, int h, int k0, f32x16 (&re)[G], f32x16 (&im)[G]) {
+__device__ __forceinline__ void mfma_pair(double phu, double phv, float live, int k0, f32x16 (&re)[G],
+                                          f32x16 (&im)[G]) {
     if (FIRST) {
         float us, uc, vs, vc;
-        sincos_rev_q((float)(phu - rint(phu)), h, us, uc);
-        sincos_rev_q((float)(phv - rint(phv)), 3 * h, vs, vc);
-        re[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(uc, vc, re[0], 0, 0, 0);
-        im[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(us, vc, im[0], 0, 0, 0);
+        sincos_rev_f((float)(phu - rint(phu)), us, uc);
+        sincos_rev_f((float)(phv - rint(phv)), vs, vc);
+        us *= live;
+        uc *= live;
         if (G > 1) {
             const float c2u = __builtin_fmaf(uc, uc, -us * us), s2u = 2.0f * uc * us;
             const float c2v = __builtin_fmaf(vc, vc, -vs * vs), s2v = 2.0f * vc * vs;
-            const float are = h ? s2u : c2u;
-            const float aim = h ? -c2u : s2u;
-            const float bop = h ? -s2v : c2v;
-            re[G - 1] = __builtin_amdgcn_mfma_f32_32x32x2f32(are, bop, re[G - 1], 0, 0, 0);
-            im[G - 1] = __builtin_amdgcn_mfma_f32_32x32x2f32(aim, bop, im[G - 1], 0, 0, 0);
+            re[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(uc, vc, re[0], 0, 0, 0);
+            im[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(us, vc, im[0], 0, 0, 0);
+            re[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(c2u, c2v, re[1], 0, 0, 0);
+            im[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(s2u, c2v, im[1], 0, 0, 0);
+            re[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(us, -vs, re[0], 0, 0, 0);
+            im[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(uc, vs, im[0], 0, 0, 0);
+            re[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(s2u, -s2v, re[1], 0, 0, 0);
+            im[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(c2u, s2v, im[1], 0, 0, 0);
+        } else {
+            mfma_pair_ops<G>(uc, us, vc, vs, 0, re, im);
         }
     } else {
+        float us[G], uc[G], vs[G], vc[G];
 #pragma unroll
         for (int g = 0; g < G; ++g) {
             const double kf = (double)(k0 + g);
             const double pu = phu * kf, pv = phv * kf;
-            float us, uc, vs, vc;
-            sincos_rev_q((float)(pu - rint(pu)), h, us, uc);
-            sincos_rev_q((float)(pv - rint(pv)), 3 * h, vs, vc);
-            re[g] = __builtin_amdgcn_mfma_f32_32x32x2f32(uc, vc, re[g], 0, 0, 0);
-            im[g] = __builtin_amdgcn_mfma_f32_32x32x2f32(us, vc, im[g], 0, 0, 0);
+            sincos_rev_f((float)(pu - rint(pu)), us[g], uc[g]);
+            sincos_rev_f((float)(pv - rint(pv)), vs[g], vc[g]);
+            us[g] *= live;
+            uc[g] *= live;
+        }
+        if (G > 1) {
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                re[g] = __builtin_amdgcn_mfma_f32_32x32x2f32(uc[g], vc[g], re[g], 0, 0, 0);
+                im[g] = __builtin_amdgcn_mfma_f32_32x32x2f32(us[g], vc[g], im[g], 0, 0, 0);
+            }
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                re[g] = __builtin_amdgcn_mfma_f32_32x32x2f32(us[g], -vs[g], re[g], 0, 0, 0);
+                im[g] = __builtin_amdgcn_mfma_f32_32x32x2f32(uc[g], vs[g], im[g], 0, 0, 0);
+            }
+        } else {
+            mfma_pair_ops<G>(uc[0], us[0], vc[0], vs[0], 0, re, im);
         }
     }
+}
+
+// lane-indexed fetch of a double held by lane `src` of the wave (ds_bpermute, LDS crossbar)
+__device__ __forceinline__ double bperm_d(double v, int src) {
+    const int lo = __builtin_amdgcn_ds_bpermute(src << 2, __double2loint(v));
+    const int hi = __builtin_amdgcn_ds_bpermute(src << 2, __double2hiint(v));
+    return __hiloint2double(hi, lo);
 }
 
 template <int G, bool TWOD, bool FIRST>
@@ -114,7 +150,7 @@ __global__ __launch_bounds__(256, 2) void k_search_mfma(
 
     for (int64_t ib = i0; ib < i1; ib += kMfmaChunk) {
         const int cnt = (int)(i1 - ib < kMfmaChunk ? i1 - ib : kMfmaChunk);
-        // the chunk's photon times: one coalesced load, then broadcast with v_readlane
+        // the chunk's photon times: one coalesced load; lane (a, h) then fetches photon 2q+h's
         const double dtv = a < cnt ? dt[ib + a] : 0.0;
         const double d2v = TWOD ? (a < cnt ? dt2[ib + a] : 0.0) : 0.0;
         f32x16 re[G], im[G];
@@ -125,16 +161,18 @@ __global__ __launch_bounds__(256, 2) void k_search_mfma(
         }
         if (cnt == kMfmaChunk) {
 #pragma unroll
-            for (int p = 0; p < kMfmaChunk; ++p) {
-                const double d = readlane_d(dtv, p);
-                const double phu = TWOD ? fma(fa, d, c2 * readlane_d(d2v, p)) : fa * d;
-                mfma_photon<G, FIRST>(phu, gb * d, h, k0, re, im);
+            for (int q = 0; q < kMfmaChunk / 2; ++q) {
+                const int src = 2 * q + h;
+                const double d = bperm_d(dtv, src);
+                const double phu = TWOD ? fma(fa, d, c2 * bperm_d(d2v, src)) : fa * d;
+                mfma_pair<G, FIRST>(phu, gb * d, 1.0f, k0, re, im);
             }
         } else {
-            for (int p = 0; p < cnt; ++p) {
-                const double d = readlane_d(dtv, p);
-                const double phu = TWOD ? fma(fa, d, c2 * readlane_d(d2v, p)) : fa * d;
-                mfma_photon<G, FIRST>(phu, gb * d, h, k0, re, im);
+            for (int q = 0; 2 * q < cnt; ++q) {
+                const int src = 2 * q + h;
+                const double d = bperm_d(dtv, src);
+                const double phu = TWOD ? fma(fa, d, c2 * bperm_d(d2v, src)) : fa * d;
+                mfma_pair<G, FIRST>(phu, gb * d, src < cnt ? 1.0f : 0.0f, k0, re, im);
             }
         }
 #pragma unroll
