@@ -111,10 +111,89 @@ void orc_calcphase(const double* t, int64_t n, const orc_model* m, int parts, do
  *   2-D: 2*(kk+1)*pi*(f*(t-t0) + (0.5*(-1*10**fd))*(t-t0)**2)
  * stat 0 = Z^2_m; stat 1 = H (max of cumsum(Z^2_k) - 4*(k-1)).
  * out is [nfd*nf] with fd outer, f inner (periodsearch.py:264-278). nfd==0 => 1-D. */
+/* Harmonic sums of one trial over photons [i0, i1) (the inner loops of periodsearch.py:66-69,
+ * :97-100 and :118-121). */
+static void trial_sums(const double* time, int64_t i0, int64_t i1, double t0, double f, double c2, int twod,
+                       int k, double* sc_out, double* ss_out) {
+    double pre = 2.0 * (double)(k + 1) * ORC_PI;
+    double sc = 0.0, ss = 0.0;
+    if (twod) {
+        for (int64_t i = i0; i < i1; ++i) {
+            double dt = time[i] - t0;
+            double a = pre * (f * dt + c2 * (dt * dt));
+            sc += cos(a);
+            ss += sin(a);
+        }
+    } else {
+        double pf = pre * f;
+        for (int64_t i = i0; i < i1; ++i) {
+            double a = pf * (time[i] - t0);
+            sc += cos(a);
+            ss += sin(a);
+        }
+    }
+    *sc_out = sc;
+    *ss_out = ss;
+}
+
+static double combine(const double* z, int nharm, int stat, int64_t n) {
+    if (stat == 0) {
+        double s = 0.0;
+        for (int k = 0; k < nharm; ++k) s += z[k];
+        return s * (2.0 / (double)n);
+    }
+    double cum = 0.0, best = -INFINITY;
+    for (int k = 0; k < nharm; ++k) {
+        cum += z[k] * (2.0 / (double)n);
+        double v = cum - 4.0 * (double)k;
+        if (v > best) best = v;
+    }
+    return best;
+}
+
+/* Few trials over many photons (the full-size parity checks: 1e8 photons, a handful of trials):
+ * parallel over (trial, harmonic, photon block) with a FIXED block count, blocks summed in
+ * order, so the result does not depend on the thread count either. */
+#define ORC_PBLOCKS 256
+static void orc_search_photon_blocked(const double* time, int64_t n, double t0, const double* freq, int64_t nf,
+                                      const double* fd, int64_t nfd, int nharm, int stat, double* out) {
+    int64_t rows = nfd > 0 ? nfd : 1;
+    int64_t total = rows * nf;
+    int64_t nb = ORC_PBLOCKS, bs = (n + nb - 1) / nb;
+    double* part = (double*)malloc(sizeof(double) * 2 * (size_t)(total * nharm * nb));
+#pragma omp parallel for collapse(3) schedule(dynamic, 1)
+    for (int64_t idx = 0; idx < total; ++idx)
+        for (int k = 0; k < nharm; ++k)
+            for (int64_t b = 0; b < nb; ++b) {
+                int64_t r = idx / nf, j = idx % nf;
+                double c2 = nfd > 0 ? 0.5 * (-1.0 * pow(10.0, fd[r])) : 0.0;
+                int64_t i0 = b * bs, i1 = i0 + bs < n ? i0 + bs : n;
+                double* o = part + 2 * ((idx * nharm + k) * nb + b);
+                if (i0 >= i1) { o[0] = o[1] = 0.0; continue; }
+                trial_sums(time, i0, i1, t0, freq[j], c2, nfd > 0, k, o, o + 1);
+            }
+    double* z = (double*)malloc(sizeof(double) * (size_t)nharm);
+    for (int64_t idx = 0; idx < total; ++idx) {
+        for (int k = 0; k < nharm; ++k) {
+            double sc = 0.0, ss = 0.0;
+            const double* o = part + 2 * ((idx * nharm + k) * nb);
+            for (int64_t b = 0; b < nb; ++b) { sc += o[2 * b]; ss += o[2 * b + 1]; }
+            z[k] = sc * sc + ss * ss;
+        }
+        out[idx] = combine(z, nharm, stat, n);
+    }
+    free(z);
+    free(part);
+}
+
 void orc_search(const double* time, int64_t n, double t0, const double* freq, int64_t nf,
                 const double* fd, int64_t nfd, int nharm, int stat, double* out) {
     int64_t rows = nfd > 0 ? nfd : 1;
     int64_t total = rows * nf;
+    if (total < 64 && n >= (1 << 22)) {
+        orc_search_photon_blocked(time, n, t0, freq, nf, fd, nfd, nharm, stat, out);
+        return;
+    }
 #pragma omp parallel
     {
         double* z = (double*)malloc(sizeof(double) * (size_t)(nharm > 0 ? nharm : 1));
