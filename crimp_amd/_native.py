@@ -19,6 +19,7 @@ FLAG_SYNC = 2
 FLAG_FORCE_DIRECT = 4
 FLAG_FORCE_MFMA = 8
 FLAG_HW_SINCOS = 16
+FLAG_MFMA_F16 = 32
 
 STAT_Z2 = 0
 STAT_H = 1

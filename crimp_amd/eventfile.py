@@ -86,10 +86,16 @@ def read_table(raw, hdr, start):
         rep = int(form[:i]) if i else 1
         code = form[i]
         name = str(hdr.get("TTYPE%d" % c, "COL%d" % c)).strip()
-        if code == "X":
+        if code == "X":  # bit array -> bool[rep] per row, as astropy returns it
             nbytes = (rep + 7) // 8
-            cols[name] = rows[:, off:off + nbytes].copy()
+            bits = np.unpackbits(rows[:, off:off + nbytes], axis=1)[:, :rep].astype(bool)
+            cols[name] = bits.ravel() if rep == 1 else bits
             off += nbytes
+            continue
+        if code == "L":  # logical 'T'/'F' bytes -> bool
+            lg = rows[:, off:off + rep] == ord("T")
+            cols[name] = lg.ravel() if rep == 1 else lg
+            off += rep
             continue
         dt, sz = _CODES[code]
         nbytes = sz * rep
@@ -187,6 +193,66 @@ class EvtFileOps:
         mask = self.time_energy_df["TIME"].between(lo, hi)
         self.time_energy_df = self.time_energy_df.loc[mask].copy()
         return self
+
+
+    def read_fpmsel(self):
+        """NICER FPM_SEL extension condensed to selected / on detector counts per time stamp
+        (eventfile.py:149-183): DataFrame TIME (MJD), TOTFPMSEL, TOTFPMON."""
+        import pandas as pd
+        kw = self.readEF()
+        if kw["TELESCOPE"] != "NICER":
+            raise ValueError("No FPM selection is possible for non-NICER observations")
+        hdr, start = self._hdu("FPM_SEL")
+        cols = read_table(self._raw, hdr, start)
+        time = cols["TIME"] / 86400 + kw["MJDREF"]
+        sel = np.asarray(cols["FPM_SEL"]).reshape(len(time), -1).sum(axis=1).astype(np.float64)
+        on = np.asarray(cols["FPM_ON"]).reshape(len(time), -1).sum(axis=1).astype(np.float64)
+        table = pd.DataFrame({"TIME": time, "FPM_SEL": list(cols["FPM_SEL"]), "FPM_ON": list(cols["FPM_ON"])})
+        condensed = pd.DataFrame(np.vstack((time, sel, on)).T, columns=["TIME", "TOTFPMSEL", "TOTFPMON"])
+        return table, condensed
+
+
+def _card(k, v):
+    if isinstance(v, str):
+        return ("%-8s= '%-8s'" % (k, v)).ljust(80)
+    if isinstance(v, bool):
+        return ("%-8s= %20s" % (k, "T" if v else "F")).ljust(80)
+    return ("%-8s= %20s" % (k, repr(v) if isinstance(v, float) else v)).ljust(80)
+
+
+def _block(cards):
+    s = "".join(cards) + "END".ljust(80)
+    s = s.ljust(((len(s) + 2879) // 2880) * 2880)
+    return s.encode("ascii")
+
+
+def write_fits(path, tables, primary=None):
+    """Write BINTABLE extensions: ``tables`` is a list of (extname, [(col, tform, array)], {keyword: value}).
+    Supports D/E/J/I/B/K scalars or vectors and L (bool) vectors -- enough for test inputs."""
+    out = [_block([_card("SIMPLE", True), _card("BITPIX", 8), _card("NAXIS", 0), _card("EXTEND", True)]
+                  + [_card(k, v) for k, v in (primary or {}).items()])]
+    codes = {"D": ">f8", "E": ">f4", "J": ">i4", "I": ">i2", "B": "u1", "K": ">i8", "L": "S1"}
+    for extname, cols, kws in tables:
+        n = len(cols[0][2])
+        fields = []
+        for name, tform, arr in cols:
+            rep = int(tform[:-1] or 1)
+            code = tform[-1]
+            fields.append((name, codes[code], (rep,)) if rep > 1 else (name, codes[code]))
+        rec = np.zeros(n, dtype=fields)
+        for name, tform, arr in cols:
+            a = np.asarray(arr)
+            rec[name] = np.where(a, b"T", b"F") if tform[-1] == "L" else a
+        cards = [_card("XTENSION", "BINTABLE"), _card("BITPIX", 8), _card("NAXIS", 2),
+                 _card("NAXIS1", rec.dtype.itemsize), _card("NAXIS2", n), _card("PCOUNT", 0), _card("GCOUNT", 1),
+                 _card("TFIELDS", len(cols)), _card("EXTNAME", extname)]
+        for i, (name, tform, _) in enumerate(cols, start=1):
+            cards += [_card("TTYPE%d" % i, name), _card("TFORM%d" % i, tform)]
+        cards += [_card(k, v) for k, v in kws.items()]
+        data = rec.tobytes()
+        out += [_block(cards), data + b"\0" * (((len(data) + 2879) // 2880) * 2880 - len(data))]
+    with open(path, "wb") as fh:
+        fh.write(b"".join(out))
 
 
 def write_events_fits(path, time, pi, mjdrefi, mjdreff, telescope="NICER"):

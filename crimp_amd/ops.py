@@ -69,7 +69,7 @@ def _empty_like_input(a, n, b, dtype=np.float64):
 
 
 def search_flags():
-    """Extra search flags from the environment (CRIMP_SEARCH=direct|mfma, CRIMP_SINCOS=hw)."""
+    """Extra search flags from the environment (CRIMP_SEARCH=direct|mfma, CRIMP_SINCOS=hw, CRIMP_MFMA=f16)."""
     f = 0
     mode = os.environ.get("CRIMP_SEARCH", "").lower()
     if mode == "direct":
@@ -78,6 +78,8 @@ def search_flags():
         f |= N.FLAG_FORCE_MFMA
     if os.environ.get("CRIMP_SINCOS", "").lower() == "hw":
         f |= N.FLAG_HW_SINCOS
+    if os.environ.get("CRIMP_MFMA", "").lower() == "f16":
+        f |= N.FLAG_MFMA_F16
     return f
 
 

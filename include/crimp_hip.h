@@ -38,6 +38,7 @@ extern "C" {
 #define CRIMP_FLAG_FORCE_DIRECT 4u /* periodicity search: never use the factorised MFMA kernel */
 #define CRIMP_FLAG_FORCE_MFMA 8u   /* periodicity search: fail unless the factorised kernel applies */
 #define CRIMP_FLAG_HW_SINCOS 16u   /* direct search: hardware v_sin/v_cos instead of the polynomial */
+#define CRIMP_FLAG_MFMA_F16 32u    /* factorised search: f16 hi/lo split operands on the f16 MFMA */
 
 #define CRIMP_STAT_Z2 0 /* Z^2_m  (periodsearch.py:57-71, :73-106) */
 #define CRIMP_STAT_H 1  /* H-test (periodsearch.py:109-125)         */

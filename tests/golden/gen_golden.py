@@ -82,8 +82,46 @@ def raw_events(path):
     raise RuntimeError("no EVENTS HDU")
 
 
+def raw_gti(path):
+    """GTI START/STOP (raw seconds, 16-byte rows of two >f8) of the bundled observation: the
+    input of the interval builder (buildtimeintervalsToAs.py:114, eventfile.py:188-236)."""
+    buf = open(path, "rb").read()
+    pos = 0
+    while pos < len(buf):
+        cards, done = {}, False
+        while not done:
+            block = buf[pos:pos + 2880].decode("ascii")
+            pos += 2880
+            for i in range(0, 2880, 80):
+                card = block[i:i + 80]
+                if card[:8].strip() == "END":
+                    done = True
+                    break
+                if card[8:10] == "= ":
+                    cards[card[:8].strip()] = card[10:].split("/")[0].strip()
+        naxis = int(cards.get("NAXIS", 0))
+        size = abs(int(cards.get("BITPIX", 8))) // 8 if naxis else 0
+        for a in range(1, naxis + 1):
+            size *= int(cards["NAXIS%d" % a])
+        if naxis:
+            size += int(cards.get("PCOUNT", 0))
+        if cards.get("EXTNAME", "").strip("' ") == "GTI":
+            nrow = int(cards["NAXIS2"])
+            rows = np.frombuffer(buf, dtype=">f8", count=2 * nrow, offset=pos).reshape(nrow, 2)
+            return rows[:, 0].astype(np.float64), rows[:, 1].astype(np.float64)
+        pos += ((size + 2879) // 2880) * 2880
+    raise RuntimeError("no GTI HDU")
+
+
+def gti_fixture():
+    start, stop = raw_gti(os.path.join(REF, "data", "1e2259_ni1020600110.fits"))
+    np.savez_compressed(os.path.join(HERE, "gti_1e2259.npz"), START=start, STOP=stop)
+    print("gti rows", start.size)
+
+
 def main():
     out = {}
+    gti_fixture()
     # ---------------------------------------------------------------- data files
     for fn in ("1e2259.par", "1e2259_template.txt", "timIntToAs_1e2259.txt", "ToAs_2259.txt", "ToAs_2259.tim"):
         shutil.copyfile(os.path.join(REF, "data", fn), os.path.join(HERE, fn))
@@ -246,4 +284,7 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["gti"]:
+        gti_fixture()
+    else:
+        main()
