@@ -23,11 +23,12 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-PEAK_F32_TFLOPS = 157.3  # MI355X_MICROARCH.md: peak FP32 vector = FP32-input MFMA (spec)
-# HBM bytes per k_search_mfma launch of this workload from rocprofv3 PMC passes
-# (profiles/r1/search_mfma_pmc_summary.json): (2 x FETCH_SIZE + WRITE_SIZE) KB x 1024, FETCH_SIZE
-# doubled per the gfx950 correction in MI355X_MICROARCH.md (HBM section).
-PMC_TRAFFIC_BYTES = (2 * 588447.5625 + 153453.875) * 1024
+PEAK_F32_TFLOPS = 157.3         # MI355X_MICROARCH.md: FP32-input MFMA = FP32 vector peak
+PEAK_F16_DENSE_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16/F16 dense (no 2:1 sparsity)
+SPLIT_PRODUCTS = 4              # f16 hi/lo split: one fp32-exact product = four f16 products
+# HBM bytes per harmonic-sum launch of this workload from rocprofv3 PMC passes (profiles/): (2 x FETCH_SIZE
+# + WRITE_SIZE) KB x 1024, FETCH_SIZE doubled per the gfx950 correction in MI355X_MICROARCH.md (HBM section).
+PMC_TRAFFIC_BYTES = {"f16": None, "f32": (2 * 588447.5625 + 153453.875) * 1024}
 FLOP_PER_EVAL_HARM = 8.0
 
 
@@ -122,6 +123,7 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
     from crimp_amd import ops
+    from crimp_amd import _native as N
     from crimp_amd.synth import pulsed_events
 
     span, f0 = 1.0e6, 7.123456789
@@ -137,8 +139,11 @@ def main():
     best = torch.zeros(2, dtype=torch.float64, device=dev)
     gathered = torch.zeros(world, 2, dtype=torch.float64, device=dev)
 
+    kms = []
+
     def step():
-        ops.search(t, t0, f, a.nharm, 0, out=out)
+        ops.search(t, t0, f, a.nharm, 0, out=out, flags=N.FLAG_TIME_KERNELS)
+        kms.append(N.load().crimp_last_kernel_ms())
         i = torch.argmax(out)
         best[0] = out[i]
         best[1] = (i + (g0 + (world * M) // 2)).to(torch.float64)  # global trial index
@@ -150,6 +155,7 @@ def main():
 
     for _ in range(a.warmup):
         step()
+    kms.clear()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -170,7 +176,8 @@ def main():
     if world > 1:
         dist.all_reduce(elt, op=dist.ReduceOp.MAX)
     el = float(elt.item())
-    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in evs]))
+    step_ms = float(np.mean([s.elapsed_time(e) for s, e in evs]))
+    kern_ms = float(np.mean(kms))  # hipEvents around the harmonic-sum kernels, on the stream they run on
     gb = g.cpu().numpy()
     order = np.lexsort((gb[:, 1], -gb[:, 0]))
     best_idx = int(gb[order[0], 1])
@@ -180,6 +187,8 @@ def main():
     if rank == 0:
         flop = FLOP_PER_EVAL_HARM * a.nharm * float(a.photons) * M
         achieved = flop / (kern_ms * 1e-3) / 1e12
+        variant = "f32" if os.environ.get("CRIMP_MFMA", "").lower() == "f32" else "f16"
+        peak = PEAK_F32_TFLOPS if variant == "f32" else PEAK_F16_DENSE_TFLOPS / SPLIT_PRODUCTS
         rec = {
             "metric": "Z^2_2 photon*trial evals/sec (node)",
             "value": value,
@@ -191,19 +200,23 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32 MFMA/sincos, f64 phase+sums",
+            "dtype": ("f32-input MFMA" if variant == "f32" else "f16 hi/lo-split MFMA (fp32-exact products)")
+                     + ", f32 sin/cos, f64 phase + sums",
             "data": "synthetic (seeded Poisson pulsed events, crimp_amd/synth.py)",
             "config": {"workload": "config3: synthetic %d photons x %d trials/GPU, Z^2_%d" % (a.photons, M, a.nharm),
                        "photons": a.photons, "trials_per_gpu": M, "nharm": a.nharm, "span_s": span, "f0": f0,
                        "trial_step_hz": df, "parallelism": "trial-sharded dp%d + all_gather(best)" % world,
                        "best_trial_index": best_idx, "best_power": float(gb[order[0], 0]),
                        "search_path": os.environ.get("CRIMP_SEARCH", "auto")},
-            "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / PEAK_F32_TFLOPS,
-                         "traffic": PMC_TRAFFIC_BYTES if (a.photons, M, a.nharm) == (10_000_000, 1_000_000, 2)
-                         else None,
-                         "kernel_ms": kern_ms,
-                         "note": "8 FLOP per photon*trial*harmonic; time = HIP events around the search call"},
+            "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+                         "frac": achieved / peak,
+                         "traffic": PMC_TRAFFIC_BYTES[variant]
+                         if (a.photons, M, a.nharm) == (10_000_000, 1_000_000, 2) else None,
+                         "kernel_ms": kern_ms, "step_ms": step_ms,
+                         "note": "achieved = 8 FLOP (one complex MAC) per photon*trial*harmonic / mean duration of the "
+                                 "harmonic-sum kernels (hipEvents in libcrimp_hip on their stream); peak = "
+                                 + ("FP32-input MFMA" if variant == "f32" else
+                                    "F16 dense MFMA / 4 (four f16 products per fp32-exact product)")},
         }
         if not a.no_cpu:
             rec["cpu_baseline"] = cpu_baseline(t_h, f0, df, a.nharm, a.cpu_seconds)

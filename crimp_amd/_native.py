@@ -19,7 +19,9 @@ FLAG_SYNC = 2
 FLAG_FORCE_DIRECT = 4
 FLAG_FORCE_MFMA = 8
 FLAG_HW_SINCOS = 16
-FLAG_MFMA_F16 = 32
+FLAG_MFMA_F32 = 32
+FLAG_MFMA_T2 = 64
+FLAG_TIME_KERNELS = 128
 
 STAT_Z2 = 0
 STAT_H = 1
@@ -47,8 +49,8 @@ class Template(ctypes.Structure):
                 ("i0", ctypes.c_double * MAX_COMP), ("amp_shift", ctypes.c_double)]
 
 
-EXPORTS = ("crimp_version", "crimp_last_error", "crimp_device_count", "crimp_calcphase", "crimp_search",
-           "crimp_toa_points", "crimp_toa_grid", "crimp_binphases")
+EXPORTS = ("crimp_version", "crimp_last_error", "crimp_last_kernel_ms", "crimp_device_count", "crimp_calcphase",
+           "crimp_search", "crimp_toa_points", "crimp_toa_grid", "crimp_binphases")
 
 _lib = None
 _lock = threading.Lock()
@@ -70,6 +72,7 @@ def load(require_device=True):
             i64, i32, u32 = ctypes.c_int64, ctypes.c_int32, ctypes.c_uint32
             L.crimp_version.restype = ctypes.c_int
             L.crimp_last_error.restype = ctypes.c_char_p
+            L.crimp_last_kernel_ms.restype = ctypes.c_double
             L.crimp_device_count.argtypes = [ctypes.POINTER(i32)]
             L.crimp_calcphase.argtypes = [P, i64, ctypes.POINTER(TimingModel), i32, P, P, u32, P]
             L.crimp_search.argtypes = [P, i64, ctypes.c_double, P, i64, P, i64, i32, i32, i64, i64, P, u32, P]
@@ -77,7 +80,7 @@ def load(require_device=True):
             L.crimp_toa_grid.argtypes = [P, P, i64, ctypes.POINTER(Template), P, i64, P, i64, P, P, u32, P]
             L.crimp_binphases.argtypes = [P, P, i64, P, i32, P, u32, P]
             for name in EXPORTS:
-                if name != "crimp_last_error":
+                if name not in ("crimp_last_error", "crimp_last_kernel_ms"):
                     getattr(L, name).restype = ctypes.c_int
             _lib = L
         if require_device and not _dev_ok:

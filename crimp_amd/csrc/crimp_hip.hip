@@ -30,6 +30,31 @@
 static thread_local std::string g_err;
 static std::mutex g_mutex;
 
+// CRIMP_FLAG_TIME_KERNELS: hipEvents around the harmonic-sum kernels of the last search (ms)
+static double g_last_kernel_ms = -1.0;
+struct KernelTimer {
+    hipEvent_t a = nullptr, b = nullptr;
+    hipStream_t s;
+    bool on;
+    KernelTimer(hipStream_t st, bool enable) : s(st), on(enable) {
+        if (on && (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess)) on = false;
+    }
+    void start() {
+        if (on) (void)hipEventRecord(a, s);
+    }
+    void stop() {
+        if (!on) return;
+        (void)hipEventRecord(b, s);
+        float ms = -1.0f;
+        if (hipEventSynchronize(b) == hipSuccess && hipEventElapsedTime(&ms, a, b) == hipSuccess)
+            g_last_kernel_ms = ms;
+    }
+    ~KernelTimer() {
+        if (a) (void)hipEventDestroy(a);
+        if (b) (void)hipEventDestroy(b);
+    }
+};
+
 static int set_err(int code, const std::string& msg) {
     g_err = msg;
     return code;
@@ -666,6 +691,8 @@ __global__ __launch_bounds__(256) void k_binphases(const double* __restrict__ x,
 // ============================================================== 6. C-ABI
 static hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+extern "C" double crimp_last_kernel_ms(void) { return g_last_kernel_ms; }
+
 extern "C" int crimp_version(void) { return CRIMP_VERSION; }
 
 extern "C" const char* crimp_last_error(void) { return g_err.c_str(); }
@@ -823,6 +850,8 @@ extern "C" int crimp_search(const double* t, int64_t n, double t0, const double*
             dim3 grid((unsigned)tblocks, (unsigned)splits);
             const bool hw = flags & CRIMP_FLAG_HW_SINCOS;
             int k0 = 1;
+            KernelTimer kt(s, flags & CRIMP_FLAG_TIME_KERNELS);
+            kt.start();
             while (k0 <= nharm) {
                 const int G = direct_group(k0, nharm);
                 if (twod) {
@@ -835,6 +864,7 @@ extern "C" int crimp_search(const double* t, int64_t n, double t0, const double*
                 HIPCHK(hipGetLastError());
                 k0 += G;
             }
+            kt.stop();
             k_search_finalize<<<(unsigned)cdiv(count, 256), 256, 0, s>>>(part, count, (int)splits, nharm, stat,
                                                                        (double)n, dout);
             HIPCHK(hipGetLastError());

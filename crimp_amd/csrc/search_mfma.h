@@ -19,23 +19,20 @@ constexpr int kMfmaChunk = 32;
 constexpr int kTile = 1024;
 
 // sin/cos(2*pi*r), |r| <= 1/2: quarter-turn reduction + the polynomials of sincos_rev_poly.
-// SC scales both outputs by a power of two at no cost (folded into the coefficients).
-template <int SC = 1>
 __device__ __forceinline__ void sincos_rev_f(float r, float& s, float& c) {
-    constexpr float k = (float)SC;
     const float q = __builtin_rintf(4.0f * r);
     const float y = __builtin_fmaf(-0.25f, q, r);
     const float y2 = y * y;
-    float sp = __builtin_fmaf(y2, k * 42.0587782776566f, k * -76.7058597530613f);
-    sp = __builtin_fmaf(y2, sp, k * 81.6052492760750f);
-    sp = __builtin_fmaf(y2, sp, k * -41.3417022403997f);
-    sp = __builtin_fmaf(y2, sp, k * 6.28318530717958647692f);
+    float sp = __builtin_fmaf(y2, 42.0587782776566f, -76.7058597530613f);
+    sp = __builtin_fmaf(y2, sp, 81.6052492760750f);
+    sp = __builtin_fmaf(y2, sp, -41.3417022403997f);
+    sp = __builtin_fmaf(y2, sp, 6.28318530717958647692f);
     sp *= y;
-    float cp = __builtin_fmaf(y2, k * -26.4262625987960f, k * 60.2446397079094f);
-    cp = __builtin_fmaf(y2, cp, k * -85.4568172844813f);
-    cp = __builtin_fmaf(y2, cp, k * 64.9393940226683f);
-    cp = __builtin_fmaf(y2, cp, k * -19.7392088021787f);
-    cp = __builtin_fmaf(y2, cp, k);
+    float cp = __builtin_fmaf(y2, -26.4262625987960f, 60.2446397079094f);
+    cp = __builtin_fmaf(y2, cp, -85.4568172844813f);
+    cp = __builtin_fmaf(y2, cp, 64.9393940226683f);
+    cp = __builtin_fmaf(y2, cp, -19.7392088021787f);
+    cp = __builtin_fmaf(y2, cp, 1.0f);
     const int iq = (int)q & 3;
     const float s_a = (iq & 1) ? cp : sp;
     const float c_a = (iq & 1) ? sp : cp;
@@ -115,79 +112,6 @@ __device__ __forceinline__ void mfma_pair(double phu, double phv, float live, in
     }
 }
 
-// ---- f16 split-precision variant: every fp32 operand x is carried as hi + lo, two f16 values
-// (hi = RN_f16(x), lo = RN_f16(x - hi); |x - hi - lo| <= 2^-22 |x|). The operands are scaled by
-// kS16 = 2^12 (in the sin/cos coefficients) so that lo stays a normal f16 (|x - hi| >= 2^-14
-// whenever |x| >= 2^-3 unscaled would otherwise be subnormal and flushed); the accumulators carry
-// 2^24 and the final store rescales exactly.
-// and the four products hi.hi + hi.lo + lo.hi + lo.lo of each real product fill the K = 16 of a
-// v_mfma_f32_32x32x16_f16 together with the complex structure: lane (a, h) holds the 8 K-values
-// of photon 2q+h. Re: A = [uc_h uc_h uc_l uc_l us_h us_h us_l us_l], B = [vc_h vc_l vc_h vc_l
-// -vs_h -vs_l -vs_h -vs_l]; Im: A = [us.. uc..] (the same dwords reordered), B with +vs. f16
-// products are exact in the fp32 accumulator, so one pair and harmonic costs two 32-cycle MFMAs
-// instead of four 64-cycle f32 ones.
-typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ uint32_t pk16(_Float16 a, _Float16 b) {
-    f16x2 v = {a, b};
-    return __builtin_bit_cast(uint32_t, v);
-}
-
-__device__ __forceinline__ f16x8 frag(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t d3) {
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-    u32x4 v = {d0, d1, d2, d3};
-    return __builtin_bit_cast(f16x8, v);
-}
-
-// One harmonic of one photon pair: operands (uc, us) of U_a and (vc, vs) of V_a for this lane's
-// photon, split and packed, then the Re and Im MFMAs.
-__device__ __forceinline__ void mfma16_harm(float uc, float us, float vc, float vs, f32x16& re, f32x16& im) {
-    // Materialise the four fp32 values first: otherwise the compiler fuses a producing multiply into
-    // the f16 conversion (v_fma_mix*, no intermediate fp32 rounding) for one use of `hi` and not
-    // the other, and hi + lo no longer equals x (seen as a 1e-5 error on squared harmonics).
-    asm volatile("" : "+v"(uc), "+v"(us), "+v"(vc), "+v"(vs));
-    const _Float16 uch = (_Float16)uc, ush = (_Float16)us, vch = (_Float16)vc, vsh = (_Float16)vs;
-    const _Float16 ucl = (_Float16)(uc - (float)uch), usl = (_Float16)(us - (float)ush);
-    const _Float16 vcl = (_Float16)(vc - (float)vch), vsl = (_Float16)(vs - (float)vsh);
-    const uint32_t a0 = pk16(uch, uch), a1 = pk16(ucl, ucl), a2 = pk16(ush, ush), a3 = pk16(usl, usl);
-    const uint32_t bc = pk16(vch, vcl), bs = pk16(vsh, vsl), bn = bs ^ 0x80008000u;
-    re = __builtin_amdgcn_mfma_f32_32x32x16_f16(frag(a0, a1, a2, a3), frag(bc, bc, bn, bn), re, 0, 0, 0);
-    im = __builtin_amdgcn_mfma_f32_32x32x16_f16(frag(a2, a3, a0, a1), frag(bc, bc, bs, bs), im, 0, 0, 0);
-}
-
-constexpr int kS16 = 4096;
-
-template <int G, bool FIRST>
-__device__ __forceinline__ void mfma16_pair(double phu, double phv, float live, int k0, f32x16 (&re)[G],
-                                            f32x16 (&im)[G]) {
-    if (FIRST) {
-        float us, uc, vs, vc;
-        sincos_rev_f<kS16>((float)(phu - rint(phu)), us, uc);
-        sincos_rev_f<kS16>((float)(phv - rint(phv)), vs, vc);
-        us *= live;
-        uc *= live;
-        mfma16_harm(uc, us, vc, vs, re[0], im[0]);
-        if (G > 1) {
-            // harmonic 2 by squaring; (2^12 x)^2 * 2^-12 keeps the 2^12 scale (exact power-of-two steps)
-            constexpr float inv = 1.0f / (float)kS16;
-            const float c2u = __builtin_fmaf(uc, uc * inv, -(us * inv) * us), s2u = (2.0f * inv * uc) * us;
-            const float c2v = __builtin_fmaf(vc, vc * inv, -(vs * inv) * vs), s2v = (2.0f * inv * vc) * vs;
-            mfma16_harm(c2u, s2u, c2v, s2v, re[1], im[1]);
-        }
-    } else {
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            const double kf = (double)(k0 + g);
-            const double pu = phu * kf, pv = phv * kf;
-            float us, uc, vs, vc;
-            sincos_rev_f<kS16>((float)(pu - rint(pu)), us, uc);
-            sincos_rev_f<kS16>((float)(pv - rint(pv)), vs, vc);
-            mfma16_harm(uc * live, us * live, vc, vs, re[g], im[g]);
-        }
-    }
-}
-
 // lane-indexed fetch of a double held by lane `src` of the wave (ds_bpermute, LDS crossbar)
 __device__ __forceinline__ double bperm_d(double v, int src) {
     const int lo = __builtin_amdgcn_ds_bpermute(src << 2, __double2loint(v));
@@ -195,7 +119,7 @@ __device__ __forceinline__ double bperm_d(double v, int src) {
     return __hiloint2double(hi, lo);
 }
 
-template <int G, bool TWOD, bool FIRST, bool F16>
+template <int G, bool TWOD, bool FIRST>
 __global__ __launch_bounds__(256, 2) void k_search_mfma(
     const double* __restrict__ dt, const double* __restrict__ dt2, int64_t n, int64_t chunk,
     const double* __restrict__ freq, int64_t nf, const double* __restrict__ c2row, double delta,
@@ -241,20 +165,14 @@ __global__ __launch_bounds__(256, 2) void k_search_mfma(
                 const int src = 2 * q + h;
                 const double d = bperm_d(dtv, src);
                 const double phu = TWOD ? fma(fa, d, c2 * bperm_d(d2v, src)) : fa * d;
-                if constexpr (F16)
-                    mfma16_pair<G, FIRST>(phu, gb * d, 1.0f, k0, re, im);
-                else
-                    mfma_pair<G, FIRST>(phu, gb * d, 1.0f, k0, re, im);
+                mfma_pair<G, FIRST>(phu, gb * d, 1.0f, k0, re, im);
             }
         } else {
             for (int q = 0; 2 * q < cnt; ++q) {
                 const int src = 2 * q + h;
                 const double d = bperm_d(dtv, src);
                 const double phu = TWOD ? fma(fa, d, c2 * bperm_d(d2v, src)) : fa * d;
-                if constexpr (F16)
-                    mfma16_pair<G, FIRST>(phu, gb * d, src < cnt ? 1.0f : 0.0f, k0, re, im);
-                else
-                    mfma_pair<G, FIRST>(phu, gb * d, src < cnt ? 1.0f : 0.0f, k0, re, im);
+                mfma_pair<G, FIRST>(phu, gb * d, src < cnt ? 1.0f : 0.0f, k0, re, im);
             }
         }
 #pragma unroll
@@ -276,13 +194,14 @@ __global__ __launch_bounds__(256, 2) void k_search_mfma(
 #pragma unroll
             for (int g = 0; g < G; ++g) {
                 const int comp = 2 * (k0 - 1 + g);
-                constexpr double sc = F16 ? 1.0 / ((double)kS16 * (double)kS16) : 1.0;
-                part[(split * ncomp + comp) * count + t] = Cr[g][r] * sc;
-                part[(split * ncomp + comp + 1) * count + t] = Ci[g][r] * sc;
+                part[(split * ncomp + comp) * count + t] = Cr[g][r];
+                part[(split * ncomp + comp + 1) * count + t] = Ci[g][r];
             }
         }
     }
 }
+
+#include "search_mfma16.h"
 
 // Uniform-grid check on the host copy of freq: |f_j - (f_0 + j*delta)| <= 16 ulp(max|f|).
 static bool freq_is_progression(const std::vector<double>& f, double* delta) {
@@ -299,32 +218,19 @@ static bool freq_is_progression(const std::vector<double>& f, double* delta) {
 }
 
 
-template <bool TWOD, bool F16>
-static void launch_mfma_p(int G, bool firstk, dim3 grid, hipStream_t s, const double* dt, const double* dt2, int64_t n,
-                          int64_t chunk, const double* fr, int64_t nf, const double* c2, double delta, int64_t tf,
-                          int64_t nt, int64_t tpr, int64_t first, int64_t count, int k0, int ncomp, double* part) {
+template <bool TWOD>
+static void launch_mfma(int G, bool firstk, dim3 grid, hipStream_t s, const double* dt, const double* dt2, int64_t n,
+                        int64_t chunk, const double* fr, int64_t nf, const double* c2, double delta, int64_t tf,
+                        int64_t nt, int64_t tpr, int64_t first, int64_t count, int k0, int ncomp, double* part) {
 #define CRIMP_LM(GG, FF)                                                                                           \
-    k_search_mfma<GG, TWOD, FF, F16><<<grid, 256, 0, s>>>(dt, dt2, n, chunk, fr, nf, c2, delta, tf, nt, tpr, first,  \
-                                                          count, k0, ncomp, part)
+    k_search_mfma<GG, TWOD, FF><<<grid, 256, 0, s>>>(dt, dt2, n, chunk, fr, nf, c2, delta, tf, nt, tpr, first, count, \
+                                                     k0, ncomp, part)
     if (G == 2) {
         if (firstk) CRIMP_LM(2, true); else CRIMP_LM(2, false);
     } else {
         if (firstk) CRIMP_LM(1, true); else CRIMP_LM(1, false);
     }
 #undef CRIMP_LM
-}
-
-template <bool TWOD>
-static void launch_mfma(bool f16, int G, bool firstk, dim3 grid, hipStream_t s, const double* dt, const double* dt2,
-                        int64_t n, int64_t chunk, const double* fr, int64_t nf, const double* c2, double delta,
-                        int64_t tf, int64_t nt, int64_t tpr, int64_t first, int64_t count, int k0, int ncomp,
-                        double* part) {
-    if (f16)
-        launch_mfma_p<TWOD, true>(G, firstk, grid, s, dt, dt2, n, chunk, fr, nf, c2, delta, tf, nt, tpr, first, count,
-                                  k0, ncomp, part);
-    else
-        launch_mfma_p<TWOD, false>(G, firstk, grid, s, dt, dt2, n, chunk, fr, nf, c2, delta, tf, nt, tpr, first,
-                                   count, k0, ncomp, part);
 }
 
 // Returns 1 when the factorised kernel produced `out`, 0 when it declines, <0 on error.
@@ -338,10 +244,13 @@ static int mfma_search(Scratch& sc, hipStream_t s, const double* dt, const doubl
     double delta = 0.0;
     if (!freq_is_progression(fh, &delta)) return 0;
 
-    const int64_t tpr = cdiv(nf, kTile);
+    // variant: f16 hi/lo split on the f16 MFMA (default; one or two tiles per wave) or f32-input MFMA
+    const int variant = (flags & CRIMP_FLAG_MFMA_F32) ? 0 : ((flags & CRIMP_FLAG_MFMA_T2) ? 2 : 1);
+    const int64_t wtile = kTile * (variant == 2 ? 2 : 1);
+    const int64_t tpr = cdiv(nf, wtile);
     const int64_t last = first + count - 1;
-    const int64_t tf = (first / nf) * tpr + (first % nf) / kTile;
-    const int64_t tl = (last / nf) * tpr + (last % nf) / kTile;
+    const int64_t tf = (first / nf) * tpr + (first % nf) / wtile;
+    const int64_t tl = (last / nf) * tpr + (last % nf) / wtile;
     const int64_t nt = tl - tf + 1;
     // photon splits depend on the photon count alone, so that every trial's value is bit-identical
     // however the grid is partitioned (tiles are already aligned to absolute trial indices): a
@@ -355,20 +264,25 @@ static int mfma_search(Scratch& sc, hipStream_t s, const double* dt, const doubl
     e = sc.alloc(&part, (size_t)(splits * ncomp * count));
     if (e != hipSuccess) return set_err(CRIMP_ERR_HIP, std::string("mfma_search alloc: ") + hipGetErrorString(e));
     dim3 grid((unsigned)cdiv(nt, 4), (unsigned)splits);
-    const bool f16 = (flags & CRIMP_FLAG_MFMA_F16) != 0;
+    KernelTimer kt(s, flags & CRIMP_FLAG_TIME_KERNELS);
+    kt.start();
     for (int k0 = 1; k0 <= nharm;) {
         // groups {1,2}, {3,4}, {5,6}, ...: harmonic 2 by squaring, later ones from exact phases
         const int G = (nharm - k0 + 1) >= 2 ? 2 : 1;
-        if (twod)
-            launch_mfma<true>(f16, G, k0 == 1, grid, s, dt, dt2, n, chunk, freq, nf, c2, delta, tf, nt, tpr, first, count, k0,
-                              ncomp, part);
-        else
-            launch_mfma<false>(f16, G, k0 == 1, grid, s, dt, dt2, n, chunk, freq, nf, c2, delta, tf, nt, tpr, first, count,
-                               k0, ncomp, part);
+#define CRIMP_ARGS G, k0 == 1, grid, s, dt, dt2, n, chunk, freq, nf, c2, delta, tf, nt, tpr, first, count, k0, ncomp, part
+        if (variant == 0) {
+            if (twod) launch_mfma<true>(CRIMP_ARGS); else launch_mfma<false>(CRIMP_ARGS);
+        } else if (variant == 1) {
+            if (twod) launch_mfma16<true, 1>(CRIMP_ARGS); else launch_mfma16<false, 1>(CRIMP_ARGS);
+        } else {
+            if (twod) launch_mfma16<true, 2>(CRIMP_ARGS); else launch_mfma16<false, 2>(CRIMP_ARGS);
+        }
+#undef CRIMP_ARGS
         e = hipGetLastError();
         if (e != hipSuccess) return set_err(CRIMP_ERR_HIP, std::string("k_search_mfma: ") + hipGetErrorString(e));
         k0 += G;
     }
+    kt.stop();
     k_search_finalize<<<(unsigned)cdiv(count, 256), 256, 0, s>>>(part, count, (int)splits, nharm, stat, (double)n,
                                                                out);
     e = hipGetLastError();

@@ -69,7 +69,7 @@ def _empty_like_input(a, n, b, dtype=np.float64):
 
 
 def search_flags():
-    """Extra search flags from the environment (CRIMP_SEARCH=direct|mfma, CRIMP_SINCOS=hw, CRIMP_MFMA=f16)."""
+    """Extra search flags from the environment (CRIMP_SEARCH=direct|mfma, CRIMP_SINCOS=hw, CRIMP_MFMA=f32|t2)."""
     f = 0
     mode = os.environ.get("CRIMP_SEARCH", "").lower()
     if mode == "direct":
@@ -78,8 +78,11 @@ def search_flags():
         f |= N.FLAG_FORCE_MFMA
     if os.environ.get("CRIMP_SINCOS", "").lower() == "hw":
         f |= N.FLAG_HW_SINCOS
-    if os.environ.get("CRIMP_MFMA", "").lower() == "f16":
-        f |= N.FLAG_MFMA_F16
+    mf = os.environ.get("CRIMP_MFMA", "").lower()
+    if mf == "f32":
+        f |= N.FLAG_MFMA_F32
+    elif mf == "t2":
+        f |= N.FLAG_MFMA_T2
     return f
 
 

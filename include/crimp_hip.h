@@ -38,7 +38,9 @@ extern "C" {
 #define CRIMP_FLAG_FORCE_DIRECT 4u /* periodicity search: never use the factorised MFMA kernel */
 #define CRIMP_FLAG_FORCE_MFMA 8u   /* periodicity search: fail unless the factorised kernel applies */
 #define CRIMP_FLAG_HW_SINCOS 16u   /* direct search: hardware v_sin/v_cos instead of the polynomial */
-#define CRIMP_FLAG_MFMA_F16 32u    /* factorised search: f16 hi/lo split operands on the f16 MFMA */
+#define CRIMP_FLAG_MFMA_F32 32u    /* factorised search: f32-input MFMA instead of the f16 hi/lo split */
+#define CRIMP_FLAG_MFMA_T2 64u     /* factorised f16 search: two tiles per wave sharing V (one wave/SIMD) */
+#define CRIMP_FLAG_TIME_KERNELS 128u /* search: time the harmonic-sum kernels with hipEvents (crimp_last_kernel_ms) */
 
 #define CRIMP_STAT_Z2 0 /* Z^2_m  (periodsearch.py:57-71, :73-106) */
 #define CRIMP_STAT_H 1  /* H-test (periodsearch.py:109-125)         */
@@ -77,6 +79,9 @@ typedef struct crimp_template {
 /* Library identification. */
 int crimp_version(void);
 const char* crimp_last_error(void);
+/* Duration (ms, hipEvents on the call's stream) of the harmonic-sum kernels of the last crimp_search
+ * made with CRIMP_FLAG_TIME_KERNELS; -1 if none. Measurement hook for bench.py, not in the reference. */
+double crimp_last_kernel_ms(void);
 int crimp_device_count(int32_t* count);
 
 /* calcphase(timeMJD, timMod) -> (total, folded)   [calcphase.py:152-176]

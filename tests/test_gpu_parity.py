@@ -65,12 +65,16 @@ def test_search_synthetic_golden_and_edges(gpu):
         PeriodSearch(t[:0], f, 2)
 
 
-@pytest.mark.parametrize("mode", ["direct", "auto"])
+@pytest.mark.parametrize("mode", ["direct", "auto", "f32", "t2"])
 def test_search_vs_oracle_larger(gpu, mode, monkeypatch):
+    """Every search kernel: direct VALU, factorised f16-split (default; two tiles per wave), f32-input MFMA."""
     from crimp_amd.periodsearch import PeriodSearch
     from crimp_amd.synth import pulsed_events
     if mode == "direct":
         monkeypatch.setenv("CRIMP_SEARCH", "direct")
+    elif mode in ("f32", "t2"):
+        monkeypatch.setenv("CRIMP_SEARCH", "mfma")
+        monkeypatch.setenv("CRIMP_MFMA", mode)
     t = pulsed_events(200000, 2.0e5, 7.123456789, pulsed_frac=0.05, seed=4)
     f = 7.123456789 + (np.arange(-1024, 1024) / (10 * 2.0e5))
     z = PeriodSearch(t, f, 2).ztest()

@@ -12,7 +12,7 @@ from crimp_amd.synth import pulsed_events  # noqa: E402
 from oracle import oracle as O  # noqa: E402
 
 dev = torch.device("cuda", 0)
-VARIANTS = {"f32": 0, "f16": N.FLAG_MFMA_F16}
+VARIANTS = {"f32": N.FLAG_MFMA_F32, "t1": 0, "t2": N.FLAG_MFMA_T2}
 
 
 def scaled(got, ref):
@@ -55,4 +55,5 @@ idx = np.unique(np.concatenate([[M // 2 - 1, M // 2, M // 2 + 1], np.random.defa
 zr = O.search(t_h, f_h[idx], 2)
 for name in VARIANTS:
     print("%s vs oracle on %d sampled trials: %.3g" % (name, idx.size, scaled(res[name][idx], zr)))
-print("f16 vs f32 over all trials: %.3g" % scaled(res["f16"], res["f32"]))
+for name in ("t1", "t2"):
+    print("%s vs f32 over all trials: %.3g" % (name, scaled(res[name], res["f32"])))
