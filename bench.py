@@ -28,7 +28,8 @@ PEAK_F16_DENSE_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16/F16 dense (no 2:1 sp
 SPLIT_PRODUCTS = 4              # f16 hi/lo split: one fp32-exact product = four f16 products
 # HBM bytes per harmonic-sum launch of this workload from rocprofv3 PMC passes (profiles/): (2 x FETCH_SIZE
 # + WRITE_SIZE) KB x 1024, FETCH_SIZE doubled per the gfx950 correction in MI355X_MICROARCH.md (HBM section).
-PMC_TRAFFIC_BYTES = {"f16": None, "f32": (2 * 588447.5625 + 153453.875) * 1024}
+PMC_TRAFFIC_BYTES = {"f16": (2 * 713800.0 + 651600.0) * 1024,   # profiles/r1_f16/pmc_traffic.txt
+                     "f32": (2 * 588447.5625 + 153453.875) * 1024}  # profiles/r1/search_mfma_pmc_summary.json
 FLOP_PER_EVAL_HARM = 8.0
 
 

@@ -50,7 +50,7 @@ class Template(ctypes.Structure):
 
 
 EXPORTS = ("crimp_version", "crimp_last_error", "crimp_last_kernel_ms", "crimp_device_count", "crimp_calcphase",
-           "crimp_search", "crimp_toa_points", "crimp_toa_grid", "crimp_binphases")
+           "crimp_search", "crimp_toa_points", "crimp_toa_grid", "crimp_toa_fit", "crimp_binphases")
 
 _lib = None
 _lock = threading.Lock()
@@ -78,6 +78,7 @@ def load(require_device=True):
             L.crimp_search.argtypes = [P, i64, ctypes.c_double, P, i64, P, i64, i32, i32, i64, i64, P, u32, P]
             L.crimp_toa_points.argtypes = [P, P, i64, ctypes.POINTER(Template), P, P, P, i64, P, u32, P]
             L.crimp_toa_grid.argtypes = [P, P, i64, ctypes.POINTER(Template), P, i64, P, i64, P, P, u32, P]
+            L.crimp_toa_fit.argtypes = [P, P, i64, ctypes.POINTER(Template), P, ctypes.c_double, i32, i32, P, u32, P]
             L.crimp_binphases.argtypes = [P, P, i64, P, i32, P, u32, P]
             for name in EXPORTS:
                 if name not in ("crimp_last_error", "crimp_last_kernel_ms"):

@@ -428,6 +428,74 @@ __device__ __forceinline__ double wave_min(double v) {
     return v;
 }
 
+// Point coefficients of component j at phShift phi:
+//   fourier   c0 = A cos(ph_j - j phi), c1 = -A sin(ph_j - j phi)
+//   cauchy/vm c0 = cos(cen_j + phi),    c1 = sin(cen_j + phi)
+__device__ __forceinline__ void tpl_coef(const TplDev* __restrict__ T, int j, double phi, double& c0, double& c1) {
+    if (T->model == CRIMP_MODEL_FOURIER) {
+        const double d = T->loc[j] - (double)(j + 1) * phi;
+        c0 = T->amp[j] * cos(d);
+        c1 = -T->amp[j] * sin(d);
+    } else {
+        const double d = T->loc[j] + phi;
+        c0 = cos(d);
+        c1 = sin(d);
+    }
+}
+
+// sin/cos of a photon's phase: x in cycles (fourier) or radians (cauchy, von Mises)
+__device__ __forceinline__ void photon_sincos(int model, double xv, double& s1, double& c1) {
+    if (model == CRIMP_MODEL_FOURIER)
+        sincospi(2.0 * xv, &s1, &c1);
+    else
+        sincos(xv, &s1, &c1);
+}
+
+// h = model - norm at one photon and its first two phShift derivatives h1, h2 (templatemodels.py:64-82,
+// :166-185, :271-290), from the photon's (s1, c1) and one point's coefficient rows c0[], cs[].
+__device__ __forceinline__ void tpl_terms(const TplDev* __restrict__ T, int model, int K, const double* c0,
+                                          const double* cs, double s1, double c1, double& h, double& h1,
+                                          double& h2) {
+    h = 0.0;
+    h1 = 0.0;
+    h2 = 0.0;
+    if (model == CRIMP_MODEL_FOURIER) {
+        double cj = c1, sj = s1;
+        for (int j = 0; j < K; ++j) {
+            const double al = c0[j], be = cs[j];
+            const double tj = al * cj + be * sj;
+            const double jj = (double)(j + 1);
+            h += tj;
+            h2 -= jj * jj * tj;
+            h1 += jj * (al * sj - be * cj);
+            const double cn = cj * c1 - sj * s1;
+            sj = sj * c1 + cj * s1;
+            cj = cn;
+        }
+    } else {
+        for (int j = 0; j < K; ++j) {
+            const double C = c0[j], S = cs[j];
+            const double cu = c1 * C + s1 * S;  // cos(x - cen - phi)
+            const double su = s1 * C - c1 * S;  // sin(x - cen - phi)
+            if (model == CRIMP_MODEL_CAUCHY) {
+                const double iD = 1.0 / (T->ch[j] - cu);
+                const double v = T->amp[j] * iD;  // amp' = a*sinh(w)
+                const double dvdu = -v * su * iD;
+                const double d2 = -v * iD * (cu - 2.0 * su * su * iD);
+                h += v;
+                h1 -= dvdu;
+                h2 += d2;
+            } else {
+                const double kp = T->kap[j];
+                const double v = T->amp[j] * exp(kp * cu);
+                h += v;
+                h1 += kp * su * v;
+                h2 += (-kp * cu + kp * kp * su * su) * v;
+            }
+        }
+    }
+}
+
 // One block per group of <= 4 points of one interval; lanes stride the photons. fp64.
 // Coefficient table per point (LDS): fourier  a_j = A cos(ph_j - j phi), b_j = -A sin(ph_j - j phi)
 //                                    cauchy/vm a_j = cos(cen_j + phi),   b_j = sin(cen_j + phi)
@@ -450,15 +518,7 @@ __global__ __launch_bounds__(kPtsBlock) void k_toa_points(const double* __restri
     if (tid < kPtsPerGroup * K) {
         const int p = tid / K, j = tid % K;
         const double phi = p < np ? pt_phi[p0 + p] : 0.0;
-        if (model == CRIMP_MODEL_FOURIER) {
-            const double d = T->loc[j] - (double)(j + 1) * phi;
-            coef[p][0][j] = T->amp[j] * cos(d);
-            coef[p][1][j] = -T->amp[j] * sin(d);
-        } else {
-            const double d = T->loc[j] + phi;
-            coef[p][0][j] = cos(d);
-            coef[p][1][j] = sin(d);
-        }
+        tpl_coef(T, j, phi, coef[p][0][j], coef[p][1][j]);
     }
     __syncthreads();
     double nrm[kPtsPerGroup];
@@ -473,51 +533,13 @@ __global__ __launch_bounds__(kPtsBlock) void k_toa_points(const double* __restri
     }
     const int64_t a = offsets[iv], b = offsets[iv + 1];
     for (int64_t i = a + tid; i < b; i += kPtsBlock) {
-        const double xv = x[i];
         double s1, c1;
-        if (model == CRIMP_MODEL_FOURIER)
-            sincospi(2.0 * xv, &s1, &c1);
-        else
-            sincos(xv, &s1, &c1);
+        photon_sincos(model, x[i], s1, c1);
 #pragma unroll
         for (int p = 0; p < kPtsPerGroup; ++p) {
             if (p >= np) break;
-            double h = 0.0, h1 = 0.0, h2 = 0.0;
-            if (model == CRIMP_MODEL_FOURIER) {
-                double cj = c1, sj = s1;
-                for (int j = 0; j < K; ++j) {
-                    const double al = coef[p][0][j], be = coef[p][1][j];
-                    const double tj = al * cj + be * sj;
-                    const double jj = (double)(j + 1);
-                    h += tj;
-                    h2 -= jj * jj * tj;
-                    h1 += jj * (al * sj - be * cj);
-                    const double cn = cj * c1 - sj * s1;
-                    sj = sj * c1 + cj * s1;
-                    cj = cn;
-                }
-            } else {
-                for (int j = 0; j < K; ++j) {
-                    const double C = coef[p][0][j], S = coef[p][1][j];
-                    const double cu = c1 * C + s1 * S;  // cos(x - cen - phi)
-                    const double su = s1 * C - c1 * S;  // sin(x - cen - phi)
-                    if (model == CRIMP_MODEL_CAUCHY) {
-                        const double iD = 1.0 / (T->ch[j] - cu);
-                        const double v = T->amp[j] * iD;           // amp' = a*sinh(w)
-                        const double dvdu = -v * su * iD;
-                        const double d2 = -v * iD * (cu - 2.0 * su * su * iD);
-                        h += v;
-                        h1 -= dvdu;
-                        h2 += d2;
-                    } else {
-                        const double kp = T->kap[j];
-                        const double v = T->amp[j] * exp(kp * cu);
-                        h += v;
-                        h1 += kp * su * v;
-                        h2 += (-kp * cu + kp * kp * su * su) * v;
-                    }
-                }
-            }
+            double h, h1, h2;
+            tpl_terms(T, model, K, coef[p][0], coef[p][1], s1, c1, h, h1, h2);
             const double mv = nrm[p] + h;
             const double q = 1.0 / mv;
             acc[p][0] += log(mv);
@@ -687,6 +709,8 @@ __global__ __launch_bounds__(256) void k_binphases(const double* __restrict__ x,
     __syncthreads();
     for (int b = threadIdx.x; b < nb; b += blockDim.x) counts[iv * nb + b] = cnt[b];
 }
+
+#include "toa_fit.h"
 
 // ============================================================== 6. C-ABI
 static hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
@@ -964,6 +988,123 @@ extern "C" int crimp_toa_points(const double* x, const int64_t* offsets, int64_t
     return finish(s, flags);
 }
 
+// Per-split brute-grid partial sums (k_toa_grid) for nint <= 65535 intervals of at most maxn photons:
+// pl[((split*nint + i)*nnorm + a)*nphi + b] (log2 sums), ph[(split*nint + i)*nphi + b] (min h).
+static int toa_grid_partials(Scratch& sc, hipStream_t s, const double* dx, const int64_t* doff, const TplDev* dT,
+                             const double* dnrm, int64_t nnorm, const double* dphi, int64_t nphi, int64_t nint,
+                             int64_t maxn, double** pl, double** ph, int64_t* splits_out) {
+    const int64_t pblocks = cdiv(nphi, kGridBlock);
+    int64_t splits = std::max<int64_t>(1, std::min<int64_t>(cdiv(2048, pblocks * nint), cdiv(std::max<int64_t>(maxn, 1), 1024)));
+    splits = std::min<int64_t>(splits, 65535);
+    int64_t chunk = cdiv(std::max<int64_t>(maxn, 1), splits);
+    chunk = cdiv(chunk, kGridBlock) * kGridBlock;
+    splits = cdiv(std::max<int64_t>(maxn, 1), chunk);
+    HIPCHK(sc.alloc(pl, (size_t)(splits * nint * nnorm * nphi)));
+    HIPCHK(sc.alloc(ph, (size_t)(splits * nint * nphi)));
+    dim3 grid((unsigned)pblocks, (unsigned)nint, (unsigned)splits);
+    for (int64_t a0 = 0; a0 < nnorm; a0 += kGridNN) {
+        const int na = (int)std::min<int64_t>(kGridNN, nnorm - a0);
+        k_toa_grid<kGridKMax><<<grid, kGridBlock, 0, s>>>(dx, doff, dT, dnrm, (int)nnorm, (int)a0, na, dphi, (int)nphi,
+                                                          chunk, (int)nint, *pl, *ph);
+        HIPCHK(hipGetLastError());
+    }
+    *splits_out = splits;
+    return CRIMP_OK;
+}
+
+extern "C" int crimp_toa_fit(const double* x, const int64_t* offsets, int64_t nint, const crimp_template* tpl,
+                             const double* exposure, double norm0, int32_t ph_shift_res, int32_t brutemin, double* out,
+                             uint32_t flags, void* stream) {
+    ARGCHK(nint >= 1, "bad sizes");
+    ARGCHK(ph_shift_res >= 1, "phShiftRes must be >= 1");
+    ARGCHK(norm0 > 0.0, "template norm must be positive");
+    ARGCHK(x != nullptr && offsets != nullptr && exposure != nullptr && out != nullptr, "null argument");
+    ARGCHK(nint <= 2147483647LL, "too many intervals");
+    TplDev T;
+    int rc = make_tpl(tpl, &T);
+    if (rc) return rc;
+    if (brutemin) ARGCHK(T.K <= kGridKMax, "brute grid supports at most 8 template components");
+    std::lock_guard<std::mutex> lk(g_mutex);
+    const bool dev = flags & CRIMP_FLAG_DEVICE_PTRS;
+    hipStream_t s = as_stream(stream);
+    std::vector<int64_t> hoff((size_t)nint + 1);
+    if (dev) {
+        HIPCHK(d2h(s, hoff.data(), offsets, (nint + 1) * sizeof(int64_t)));
+        HIPCHK(hipStreamSynchronize(s));
+    } else {
+        std::memcpy(hoff.data(), offsets, (nint + 1) * sizeof(int64_t));
+    }
+    for (int64_t i = 0; i < nint; ++i)
+        ARGCHK(hoff[i + 1] > hoff[i] && hoff[i] >= 0,
+               "every ToA interval needs photons (measureToAs.py:182 fails on an empty one)");
+    // measureToAs.py:715-725 / :757-771 (readvaryparam=False) and :320-376
+    FitCfg C;
+    C.lo = norm0 / 100.0;
+    C.hi = 500.0;
+    C.pb = T.model == CRIMP_MODEL_FOURIER ? M_PI : 1.5 * M_PI;
+    C.step = (2.0 * M_PI) / (double)ph_shift_res;
+    C.kcap = (double)ph_shift_res / 2.0;
+    C.sum_amp = 0.0;
+    for (int j = 0; j < tpl->ncomp; ++j) C.sum_amp += tpl->amp[j] * tpl->amp_shift;
+    {
+        Scratch sc(s);
+        const double *dx = nullptr, *de = nullptr;
+        const int64_t* doff = nullptr;
+        double* dout = nullptr;
+        HIPCHK(stage_in(sc, x, (size_t)hoff[nint], dev, &dx));
+        HIPCHK(stage_in(sc, offsets, (size_t)nint + 1, dev, &doff));
+        HIPCHK(stage_in(sc, exposure, (size_t)nint, dev, &de));
+        HIPCHK(stage_out(sc, out, (size_t)nint * 8, dev, &dout));
+        TplDev* dT = nullptr;
+        double* dstart = nullptr;
+        HIPCHK(sc.alloc(&dT, 1));
+        HIPCHK(h2d(dT, &T, sizeof(T)));
+        HIPCHK(sc.alloc(&dstart, (size_t)(2 * nint)));
+        std::vector<double> hphi, hnrm, hstart;
+        if (brutemin) {
+            // lmfit brute lattices (measureToAs.py:292-295): scipy mgrid phShift = k*0.05 - bound, 20 norms
+            const int64_t nphi = (int64_t)std::ceil((2.0 * C.pb) / (0.05 * 1.0));
+            const int64_t nn = 20;
+            hphi.resize((size_t)nphi);
+            for (int64_t k = 0; k < nphi; ++k) hphi[(size_t)k] = (double)k * 0.05 + (-C.pb);
+            hnrm.resize((size_t)(nint * nn));
+            for (int64_t a = 0; a < nn; ++a) hnrm[(size_t)a] = (double)a * ((C.hi - C.lo) / (double)(nn - 1)) + C.lo;
+            for (int64_t i = 1; i < nint; ++i) std::memcpy(&hnrm[(size_t)(i * nn)], &hnrm[0], nn * sizeof(double));
+            double *dphi = nullptr, *dnrm = nullptr;
+            HIPCHK(sc.alloc(&dphi, (size_t)nphi));
+            HIPCHK(sc.alloc(&dnrm, (size_t)(nint * nn)));
+            HIPCHK(h2d(dphi, hphi.data(), nphi * sizeof(double)));
+            HIPCHK(h2d(dnrm, hnrm.data(), nint * nn * sizeof(double)));
+            for (int64_t i0 = 0; i0 < nint; i0 += 65535) {
+                const int64_t nb = std::min<int64_t>(65535, nint - i0);
+                int64_t maxn = 0;
+                for (int64_t i = i0; i < i0 + nb; ++i) maxn = std::max(maxn, hoff[i + 1] - hoff[i]);
+                double *pl = nullptr, *ph = nullptr;
+                int64_t splits = 0;
+                rc = toa_grid_partials(sc, s, dx, doff + i0, dT, dnrm + i0 * nn, nn, dphi, nphi, nb, maxn, &pl, &ph,
+                                       &splits);
+                if (rc) return rc;
+                k_toa_grid_best<<<(unsigned)nb, 256, 0, s>>>(pl, ph, dnrm + i0 * nn, dphi, doff + i0, de + i0, (int)nn,
+                                                            (int)nphi, (int)nb, (int)splits, T.model, C.sum_amp,
+                                                            dstart + 2 * i0);
+                HIPCHK(hipGetLastError());
+            }
+        } else {  // Nelder-Mead starts from the template (norm0, phShift 0) (measureToAs.py:301)
+            hstart.resize((size_t)(2 * nint));
+            for (int64_t i = 0; i < nint; ++i) {
+                hstart[(size_t)(2 * i)] = norm0;
+                hstart[(size_t)(2 * i + 1)] = 0.0;
+            }
+            HIPCHK(h2d(dstart, hstart.data(), 2 * nint * sizeof(double)));
+        }
+        k_toa_fit<<<(unsigned)nint, kFitBlock, 0, s>>>(dx, doff, dT, de, dstart, C, dout);
+        HIPCHK(hipGetLastError());
+        HIPCHK(copy_back(s, out, dout, (size_t)nint * 8, dev));
+        HIPCHK(hipStreamSynchronize(s));
+    }
+    return finish(s, flags);
+}
+
 extern "C" int crimp_toa_grid(const double* x, const int64_t* offsets, int64_t nint, const crimp_template* tpl,
                               const double* norm, int64_t nnorm, const double* phi, int64_t nphi, double* lnsum,
                               double* hmin, uint32_t flags, void* stream) {
@@ -999,26 +1140,14 @@ extern "C" int crimp_toa_grid(const double* x, const int64_t* offsets, int64_t n
         HIPCHK(stage_in(sc, offsets, (size_t)nint + 1, dev, &doff));
         HIPCHK(stage_in(sc, norm, (size_t)(nint * nnorm), dev, &dnrm));
         HIPCHK(stage_in(sc, phi, (size_t)nphi, dev, &dphi));
-        const int64_t pblocks = cdiv(nphi, kGridBlock);
-        int64_t splits = std::max<int64_t>(1, std::min<int64_t>(cdiv(2048, pblocks * nint), cdiv(std::max<int64_t>(maxn, 1), 1024)));
-        splits = std::min<int64_t>(splits, 65535);
-        int64_t chunk = cdiv(std::max<int64_t>(maxn, 1), splits);
-        chunk = cdiv(chunk, kGridBlock) * kGridBlock;
-        splits = cdiv(std::max<int64_t>(maxn, 1), chunk);
-        double *pl = nullptr, *ph = nullptr;
-        HIPCHK(sc.alloc(&pl, (size_t)(splits * nint * nnorm * nphi)));
-        HIPCHK(sc.alloc(&ph, (size_t)(splits * nint * nphi)));
+        ARGCHK(nint <= 65535, "at most 65535 intervals per brute-grid call");
         TplDev* dT = nullptr;
         HIPCHK(sc.alloc(&dT, 1));
         HIPCHK(h2d(dT, &T, sizeof(T)));
-        ARGCHK(nint <= 65535, "at most 65535 intervals per brute-grid call");
-        dim3 grid((unsigned)pblocks, (unsigned)nint, (unsigned)splits);
-        for (int64_t a0 = 0; a0 < nnorm; a0 += kGridNN) {
-            const int na = (int)std::min<int64_t>(kGridNN, nnorm - a0);
-            k_toa_grid<kGridKMax><<<grid, kGridBlock, 0, s>>>(dx, doff, dT, dnrm, (int)nnorm, (int)a0, na, dphi,
-                                                              (int)nphi, chunk, (int)nint, pl, ph);
-            HIPCHK(hipGetLastError());
-        }
+        double *pl = nullptr, *ph = nullptr;
+        int64_t splits = 0;
+        rc = toa_grid_partials(sc, s, dx, doff, dT, dnrm, nnorm, dphi, nphi, nint, maxn, &pl, &ph, &splits);
+        if (rc) return rc;
         // combine splits on the host in a fixed order (deterministic)
         std::vector<double> hl((size_t)(splits * nint * nnorm * nphi)), hh((size_t)(splits * nint * nphi));
         HIPCHK(d2h(s, hl.data(), pl, hl.size() * sizeof(double)));

@@ -1,0 +1,289 @@
+// toa_fit.h -- measureToA_* fits on the device, one workgroup per ToA interval (included by crimp_hip.hip).
+//
+// crimp_amd/toafit.py drives the same iterations from the host, where every likelihood evaluation is a
+// k_toa_points launch and a host round trip. Here an interval's whole fit (measureToAs.py:285-376) runs
+// inside one 256-thread workgroup: an evaluation is one pass over the interval's photons and a workgroup
+// reduction that every thread reads back, so the workgroup iterates the reference driver itself, with
+// toafit.py's constants and stopping rules:
+//   start   the brute-grid maximum (k_toa_grid partial sums -> k_toa_grid_best) or (norm0, 0);
+//   ascent  damped 2-D Newton in (norm, phShift) with a backtracking line search (toafit.maximise);
+//   1 sigma phShift = best -/+ k*2pi/phShiftRes with lmfit's clip-to-bound semantics, the norm re-profiled by
+//           1-D Newton at every step (toafit.profile_norm); stop at the first LLmax - LL > 0.5*chi2.ppf(0.6827,1)
+//           or once k + 1 > phShiftRes/2 (measureToAs.py:331-376, toafit.error_scan).
+// The evaluation repeats k_toa_points' per-photon arithmetic (tpl_terms), thread striding and reduction
+// order, so its sums equal the host-driven path's.
+
+constexpr int kFitBlock = 256;
+constexpr double kHalfChi2OneSigma = 0.500021713558733;  // 0.5 * chi2.ppf(0.6827, 1)   (measureToAs.py:324)
+constexpr double kTwoPi = 6.283185307179586476925286766559;
+
+struct FitCfg {
+    double lo, hi;   // norm bounds [norm0/100, 500]                           (measureToAs.py:715-716, :757-758)
+    double pb;       // phShift bound: pi (fourier), 1.5 pi (cauchy, vonmises)   (:722, :767)
+    double step;     // 2 pi / phShiftRes                                       (:320)
+    double kcap;     // phShiftRes / 2                                          (:348, :373)
+    double sum_amp;  // sum_j amp_j: cauchy / von Mises normalisation F = 2 pi norm + sum_amp
+};
+
+struct FitEval {
+    double ll, gn, gp, hnn, hnp, hpp;
+};
+
+struct FitShared {
+    double red[kFitBlock / 64][8];
+    double coef[2][CRIMP_MAX_COMP];
+};
+
+// np.clip semantics (a NaN stays NaN)
+__device__ __forceinline__ double clipd(double v, double lo, double hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+// Reference extended LL (templatemodels.py:109-121, :213-226, :318-329) with its (norm, phShift) gradient and
+// Hessian at (n, phi), from one pass over photons x[a, b) (as toafit.ToAFitter.evaluate assembles them).
+__device__ FitEval fit_eval(const double* __restrict__ x, int64_t a, int64_t b, const TplDev* __restrict__ T, double n,
+                            double phi, double E, const FitCfg& C, FitShared& sh) {
+    const int tid = threadIdx.x;
+    const int model = T->model, K = T->K;
+    __syncthreads();  // the previous evaluation's readers are done with sh
+    if (tid < K) tpl_coef(T, tid, phi, sh.coef[0][tid], sh.coef[1][tid]);
+    __syncthreads();
+    double acc[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    double mn = INFINITY;
+    for (int64_t i = a + tid; i < b; i += kFitBlock) {
+        double s1, c1, h, h1, h2;
+        photon_sincos(model, x[i], s1, c1);
+        tpl_terms(T, model, K, sh.coef[0], sh.coef[1], s1, c1, h, h1, h2);
+        const double mv = n + h;
+        const double q = 1.0 / mv;
+        acc[0] += log(mv);
+        acc[1] += q;
+        acc[2] += h1 * q;
+        acc[3] -= q * q;
+        acc[4] -= h1 * q * q;
+        acc[5] += h2 * q - h1 * h1 * q * q;
+        mn = fmin(mn, mv);
+    }
+    const int w = tid >> 6, lane = tid & 63;
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+        const double v = wave_sum(acc[q]);
+        if (lane == 0) sh.red[w][q] = v;
+    }
+    const double vm = wave_min(mn);
+    if (lane == 0) sh.red[w][6] = vm;
+    __syncthreads();
+    double S[7];
+#pragma unroll
+    for (int q = 0; q < 7; ++q) {
+        double v = sh.red[0][q];
+        for (int ww = 1; ww < kFitBlock / 64; ++ww) v = (q == 6) ? fmin(v, sh.red[ww][q]) : v + sh.red[ww][q];
+        S[q] = v;
+    }
+    const double N = (double)(b - a);
+    FitEval r;
+    double F;
+    if (model == CRIMP_MODEL_FOURIER) {
+        F = n;
+        r.ll = -n * E + N * log(n * E) + (S[0] - N * log(n));
+    } else {
+        F = kTwoPi * n + C.sum_amp;
+        r.ll = -F * E / kTwoPi + N * log(F * E / kTwoPi) + (S[0] - N * log(F));
+    }
+    if (!(S[6] / F > 0)) r.ll = -INFINITY;  // min(model / normalisation) <= 0 (:113-115, :220-222, :324-326)
+    r.gn = -E + S[1];
+    r.gp = S[2];
+    r.hnn = S[3];
+    r.hnp = S[4];
+    r.hpp = S[5];
+    return r;
+}
+
+// toafit._newton_step: Levenberg-shifted Newton direction with a trust region (0.05 rad, half the norm)
+__device__ void fit_newton_dir(double n, const FitEval& e, double& dn, double& dp) {
+    const double hnn = e.hnn, hnp = e.hnp, hpp = e.hpp;
+    const double tr = hnn + hpp;
+    const double det = hnn * hpp - hnp * hnp;
+    const double disc = 0.25 * tr * tr - det;
+    const double lam_max = 0.5 * tr + sqrt(disc != disc ? disc : (disc > 0.0 ? disc : 0.0));
+    const double shift = lam_max < 0 ? 0.0 : lam_max * 1.5 + 1e-6 * (fabs(hnn) + fabs(hpp)) + 1e-12;
+    const double aa = hnn - shift, cc = hpp - shift;
+    const double det2 = aa * cc - hnp * hnp;
+    dn = -(cc * e.gn - hnp * e.gp) / det2;
+    dp = -(aa * e.gp - hnp * e.gn) / det2;
+    double sc = fmin(1.0, 0.05 / fmax(fabs(dp), 1e-300));
+    sc = fmin(sc, 0.5 * fabs(n) / fmax(fabs(dn), 1e-300));
+    dn *= sc;
+    dp *= sc;
+}
+
+// toafit.profile_norm: max over norm in [lo, hi] of LL(norm, phi) at fixed phi (1-D Newton, concave)
+__device__ double fit_profile(const double* __restrict__ x, int64_t a, int64_t b, const TplDev* __restrict__ T,
+                              double phi, double n_start, double E, const FitCfg& C, FitShared& sh, int& nev) {
+    double n = clipd(n_start, C.lo, C.hi);
+    FitEval e = fit_eval(x, a, b, T, n, phi, E, C, sh);
+    ++nev;
+    for (int it = 0; it < 30; ++it) {
+        const bool bad = !isfinite(e.ll);
+        double step = e.hnn < 0 ? -e.gn / e.hnn : 0.1 * n;
+        step = clipd(step, -0.5 * n, 0.5 * n);
+        if (bad) step = 0.5 * n;  // infeasible: model <= 0 somewhere, raise the norm
+        double nn = clipd(n + step, C.lo, C.hi);
+        FitEval e2 = fit_eval(x, a, b, T, nn, phi, E, C, sh);
+        ++nev;
+        const bool worse = isfinite(e.ll) && (!isfinite(e2.ll) || e2.ll < e.ll - 1e-12 * fabs(e.ll));
+        if (worse) {  // damp an overshoot
+            nn = clipd(n + 0.25 * step, C.lo, C.hi);
+            e2 = fit_eval(x, a, b, T, nn, phi, E, C, sh);
+            ++nev;
+        }
+        const bool conv = fabs(nn - n) <= 1e-13 * fmax(1.0, n);
+        n = nn;
+        e = e2;
+        if (conv) break;
+    }
+    return e.ll;
+}
+
+// One workgroup per interval: ascent from start[iv], then the 1-sigma scan on both sides.
+// out[iv*8 + 0..5] = norm, phShift, LLmax, phShift_LL, phShift_UL, likelihood evaluations.
+__global__ __launch_bounds__(kFitBlock) void k_toa_fit(const double* __restrict__ x, const int64_t* __restrict__ offsets,
+                                                       const TplDev* __restrict__ T, const double* __restrict__ expo,
+                                                       const double* __restrict__ start, FitCfg C,
+                                                       double* __restrict__ out) {
+    __shared__ FitShared sh;
+    const int64_t iv = blockIdx.x;
+    const int64_t a = offsets[iv], b = offsets[iv + 1];
+    const double E = expo[iv];
+    int nev = 0;
+    double n = start[2 * iv], p = start[2 * iv + 1];
+    FitEval e = fit_eval(x, a, b, T, n, p, E, C, sh);
+    ++nev;
+    for (int it = 0; it < 60; ++it) {  // toafit.maximise
+        double dn, dp;
+        fit_newton_dir(n, e, dn, dp);
+        double t = 1.0, tn = n, tp = p;
+        FitEval e2 = e;
+        bool ok = false;
+        for (int ls = 0; ls < 40; ++ls) {
+            tn = clipd(n + t * dn, C.lo, C.hi);
+            tp = clipd(p + t * dp, -C.pb, C.pb);
+            e2 = fit_eval(x, a, b, T, tn, tp, E, C, sh);
+            ++nev;
+            if (isfinite(e2.ll) && e2.ll >= e.ll - 1e-12 * fabs(e.ll)) {
+                ok = true;
+                break;
+            }
+            t *= 0.5;
+        }
+        if (!ok) break;  // line search exhausted: at the (numerical) optimum
+        const double mvn = fabs(tn - n), mvp = fabs(tp - p);
+        n = tn;
+        p = tp;
+        e = e2;
+        if (mvp < 1e-12 && mvn < 1e-12 * fmax(1.0, fabs(tn))) break;
+    }
+    const double nhat = n, phat = p, llmax = e.ll;
+    double sig[2];
+    for (int s = 0; s < 2; ++s) {  // toafit.error_scan, measureToAs.py:331-376
+        const int side = s == 0 ? -1 : 1;
+        bool past = false;
+        int kk = 0;
+        for (int k = 1;; ++k) {
+            const double target = phat + (double)(side * k) * C.step;
+            double ph;
+            if (T->model == CRIMP_MODEL_FOURIER) {
+                // the first step past +-pi is clipped to the bound; later ones move the bound (:332-334, :357-359)
+                const bool beyond = side < 0 ? (target <= -M_PI) : (target >= M_PI);
+                if (beyond && !past) {
+                    ph = side < 0 ? -M_PI : M_PI;
+                    past = true;
+                } else {
+                    ph = target;
+                }
+            } else {
+                ph = clipd(target, -C.pb, C.pb);
+            }
+            const double llk = fit_profile(x, a, b, T, ph, nhat, E, C, sh, nev);
+            const double diff = llmax - llk;
+            if (diff > kHalfChi2OneSigma || (double)(k + 1) > C.kcap) {
+                kk = k + 1;
+                break;
+            }
+        }
+        sig[s] = (double)kk * C.step + C.step / 2;
+    }
+    if (threadIdx.x == 0) {
+        double* o = out + iv * 8;
+        o[0] = nhat;
+        o[1] = phat;
+        o[2] = llmax;
+        o[3] = sig[0];
+        o[4] = sig[1];
+        o[5] = (double)nev;
+        o[6] = 0.0;
+        o[7] = 0.0;
+    }
+}
+
+// lmfit brute maximum per interval from k_toa_grid's per-split partial sums (toafit.brute): splits combined in
+// a fixed order, the reference LL formed for every (norm, phShift) lattice point, -inf where the model is not
+// positive, first maximum in norm-outer order (scipy.optimize.brute / np.argmax).
+__global__ __launch_bounds__(256) void k_toa_grid_best(const double* __restrict__ pl, const double* __restrict__ ph,
+                                                       const double* __restrict__ norm, const double* __restrict__ phi,
+                                                       const int64_t* __restrict__ offsets,
+                                                       const double* __restrict__ expo, int nnorm, int nphi, int nint,
+                                                       int splits, int model, double sum_amp,
+                                                       double* __restrict__ start) {
+    __shared__ double bv[4];
+    __shared__ int bi[4];
+    const int64_t iv = blockIdx.x;
+    const double N = (double)(offsets[iv + 1] - offsets[iv]);
+    const double E = expo[iv];
+    double best = -INFINITY;
+    int bidx = 0x7fffffff;
+    for (int idx = threadIdx.x; idx < nnorm * nphi; idx += 256) {
+        const int ai = idx / nphi, bj = idx - ai * nphi;
+        double v = 0.0;
+        for (int sp = 0; sp < splits; ++sp) v += pl[(((int64_t)sp * nint + iv) * nnorm + ai) * nphi + bj];
+        const double ln = v * 0.69314718055994530942;  // log2 sums -> ln
+        double hm = INFINITY;
+        for (int sp = 0; sp < splits; ++sp) hm = fmin(hm, ph[((int64_t)sp * nint + iv) * nphi + bj]);
+        const double nn = norm[iv * nnorm + ai];
+        double ll;
+        if (model == CRIMP_MODEL_FOURIER) {
+            ll = -nn * E + N * log(nn * E) + (ln - N * log(nn));
+        } else {
+            const double F = kTwoPi * nn + sum_amp;
+            ll = -F * E / kTwoPi + N * log(F * E / kTwoPi) + (ln - N * log(F));
+        }
+        if (!((hm + nn) > 0) || !isfinite(ll)) ll = -INFINITY;
+        if (ll > best || (ll == best && idx < bidx)) {
+            best = ll;
+            bidx = idx;
+        }
+    }
+    // (value, index) argmax, ties -> lowest index
+    for (int o = 32; o > 0; o >>= 1) {
+        const double ov = __shfl_xor(best, o);
+        const int oi = __shfl_xor(bidx, o);
+        if (ov > best || (ov == best && oi < bidx)) {
+            best = ov;
+            bidx = oi;
+        }
+    }
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        bv[w] = best;
+        bi[w] = bidx;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int ww = 1; ww < 4; ++ww)
+            if (bv[ww] > best || (bv[ww] == best && bi[ww] < bidx)) {
+                best = bv[ww];
+                bidx = bi[ww];
+            }
+        if (bidx == 0x7fffffff) bidx = 0;
+        start[2 * iv] = norm[iv * nnorm + bidx / nphi];
+        start[2 * iv + 1] = phi[bidx % nphi];
+    }
+}

@@ -164,6 +164,22 @@ def toa_grid(x, offsets, tpl, norms, phis):
     return ln.reshape(nint, nnorm, nphi), hm.reshape(nint, nphi)
 
 
+def toa_fit(x, offsets, tpl, exposure, norm0, ph_shift_res=1000, brutemin=False):
+    """Whole per-interval ToA fits on the device (crimp_toa_fit): [nint, 8] = norm, phShift, LLmax,
+    phShift_LL, phShift_UL, likelihood evaluations."""
+    L = N.load()
+    b = N.Buffers()
+    xp = b.arg(x, np.float64)
+    op = b.arg(offsets, np.int64)
+    ep = b.arg(exposure, np.float64)
+    nint = int((offsets.numel() if N._is_torch(offsets) else np.size(offsets)) - 1)
+    out = _empty_like_input(x, nint * 8, b)
+    outp = b.arg(out, np.float64, writable=True)
+    N.check(L.crimp_toa_fit(xp, op, nint, ctypes.byref(tpl), ep, float(norm0), int(ph_shift_res), int(bool(brutemin)),
+                            outp, b.flags(), b.stream()))
+    return out.reshape(nint, 8)
+
+
 def binphases_counts(x, offsets, edges):
     L = N.load()
     b = N.Buffers()

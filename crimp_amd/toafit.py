@@ -227,14 +227,17 @@ class ToAFitter:
         return n, ll
 
     # ------------------------------------------------------------------ step 3: error scan
-    def _scan_phases(self, phi_hat, side, ks):
-        """phShift values the lmfit loop evaluates at steps ks (clip-to-bound semantics)."""
+    def _scan_phases(self, phi_hat, side, ks, passed=None):
+        """phShift values the lmfit loop evaluates at steps ks (clip-to-bound semantics); ``passed`` marks
+        intervals whose scan already crossed the bound in an earlier batch of steps."""
         step = TWO_PI / self.res
         target = phi_hat[:, None] + side * ks[None, :] * step
         if self.model == "fourier":
             # the first step past +-pi is clipped to the bound; later steps move the bound (:332-334, :357-359)
             past = (target <= -math.pi) if side < 0 else (target >= math.pi)
             first = np.where(past.any(axis=1), past.argmax(axis=1), -1)
+            if passed is not None:
+                first = np.where(passed, -1, first)
             cur = target.copy()
             rows = np.nonzero(first >= 0)[0]
             cur[rows, first[rows]] = -math.pi if side < 0 else math.pi
@@ -247,6 +250,7 @@ class ToAFitter:
         out = {}
         for side in (-1, 1):
             kk_final = np.full(self.nint, -1, dtype=np.int64)
+            passed = np.zeros(self.nint, dtype=bool)
             k0 = 1
             batch = 12
             while True:
@@ -254,7 +258,9 @@ class ToAFitter:
                 if todo.size == 0:
                     break
                 ks = np.arange(k0, k0 + batch)
-                phis = self._scan_phases(phi_hat[todo], side, ks)
+                phis = self._scan_phases(phi_hat[todo], side, ks, passed[todo])
+                tg = phi_hat[todo][:, None] + side * ks[None, :] * step
+                passed[todo] |= ((tg <= -math.pi) if side < 0 else (tg >= math.pi)).any(axis=1)
                 iv = np.repeat(todo, ks.size)
                 nprof, llk = self.profile_norm(iv, phis.reshape(-1), np.repeat(n_hat[todo], ks.size))
                 diff = (ll_max[todo][:, None] - llk.reshape(todo.size, ks.size))
@@ -297,8 +303,21 @@ class ToAFitter:
                 y = y + (t.amp[j] / (2 * np.pi * t.i0[j])) * np.exp((1 / t.wid[j] ** 2) * np.cos(xx - t.loc[j] - phi))
         return y
 
-    # ------------------------------------------------------------------ driver
+    # ------------------------------------------------------------------ drivers
     def fit(self, brutemin=False):
+        """Every interval's fit in one device call (crimp_toa_fit: one workgroup per interval runs steps 1-3),
+        then the redChi2 of step 4."""
+        r = ops.toa_fit(self.x, self.offsets, self.tpl, self._arr(self.E, np.float64), self.norm0, self.res, brutemin)
+        if _is_torch(r):
+            r = r.cpu().numpy()
+        r = np.asarray(r)
+        n_hat, phi_hat = r[:, 0].copy(), r[:, 1].copy()
+        rchi2 = self.reduced_chi2(n_hat, phi_hat)
+        return {"phShi": phi_hat, "phShi_LL": r[:, 3].copy(), "phShi_UL": r[:, 4].copy(), "reducedChi2": rchi2,
+                "norm": n_hat, "LLmax": r[:, 2].copy(), "evaluations": r[:, 5].copy()}
+
+    def fit_host(self, brutemin=False):
+        """The same fit driven from the host, one batched likelihood launch per iteration (cross-check of fit)."""
         if brutemin:
             n0, p0 = self.brute()
         else:

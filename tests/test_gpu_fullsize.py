@@ -36,11 +36,13 @@ def test_config3_full_size(gpu):
     a = ops.search(t, t0, f, 2, 0, first=0, count=M // 2 + 123).cpu().numpy()
     b = ops.search(t, t0, f, 2, 0, first=M // 2 + 123, count=M - (M // 2 + 123)).cpu().numpy()
     np.testing.assert_array_equal(np.concatenate([a, b]), z)
-    # direct kernel over a window around the peak agrees with the factorised kernel
+    # direct kernel over a window around the peak agrees with the factorised kernel: each is within 1e-6 of
+    # the reference, so the two differ by at most 2e-6
     from crimp_amd import _native as N
     w = slice(M // 2 - 2048, M // 2 + 2048)
     zd = ops.search(t, t0, f[w].contiguous(), 2, 0, flags=N.FLAG_FORCE_DIRECT).cpu().numpy()
-    assert _scaled_err(zd, z[w], np.mean(z)).max() <= 1e-6
+    assert _scaled_err(zd, z[w], np.mean(z)).max() <= 2e-6
+    assert int(np.argmax(zd)) == 2048
     # noise statistic: Z^2_2 of unpulsed trials is chi^2 with 4 dof (mean 4) far from the signal
     far = z[: M // 4]
     assert abs(far.mean() - 4.0) < 0.05

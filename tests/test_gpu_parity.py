@@ -251,6 +251,35 @@ def test_toa_fits_match_reference_and_oracle(gpu):
         assert r["reducedChi2"][i] == pytest.approx(o["reducedChi2"], rel=1e-6)
 
 
+def test_device_toa_driver_equals_host_driver(gpu):
+    """crimp_toa_fit (one workgroup per interval runs the whole fit) against the host-driven iterations."""
+    from crimp_amd.toafit import ToAFitter
+    from crimp_amd.readPPtemplate import readPPtemplate
+    g, iv, ref = _golden_rows()
+    tm = readPPtemplate(gpath("1e2259_template.txt"))
+    E = iv["ToA_exposure"].to_numpy()[g["ids"]]
+    for bm in (True, False):
+        f = ToAFitter(g["folded"], g["offsets"], E, tm)
+        d, h = f.fit(brutemin=bm), f.fit_host(brutemin=bm)
+        np.testing.assert_allclose(d["phShi"], h["phShi"], rtol=0, atol=1e-9)
+        np.testing.assert_array_equal(d["phShi_LL"], h["phShi_LL"])
+        np.testing.assert_array_equal(d["phShi_UL"], h["phShi_UL"])
+        np.testing.assert_allclose(d["LLmax"], h["LLmax"], rtol=1e-12)
+        assert np.all(d["evaluations"] > 5)
+    tc = json.load(open(gpath("cauchy_vm_theta.json")))
+    gx = gold("templatemodels.npz")["x"]
+    for model in ("cauchy", "vonmises"):
+        t = {"model": model, "norm": {"value": 5.0, "vary": True}}
+        for j in (1, 2):
+            for nm in ("amp", "cen", "wid"):
+                t["%s_%d" % (nm, j)] = {"value": tc["%s_%d" % (nm, j)], "vary": True}
+        f = ToAFitter(gx, np.array([0, gx.size]), np.array([250.0]), t)
+        d, h = f.fit(brutemin=True), f.fit_host(brutemin=True)
+        np.testing.assert_allclose(d["phShi"], h["phShi"], rtol=0, atol=1e-9)
+        np.testing.assert_array_equal(d["phShi_LL"], h["phShi_LL"])
+        np.testing.assert_array_equal(d["phShi_UL"], h["phShi_UL"])
+
+
 def test_toa_fit_without_brute_and_other_templates(gpu):
     from crimp_amd.measureToAs import measureToA_fourier, measureToA_cauchy, measureToA_vonmises
     from crimp_amd.readPPtemplate import readPPtemplate
