@@ -85,6 +85,7 @@ def toa_leg(a, dev, world, rank):
             "toa_config": "config5: %d intervals/GPU x %d photons, Fourier K=6 (1e2259), brute+MLE+1-sigma scan"
                           % (a.toa_intervals, a.toa_photons),
             "toa_seconds": float(elt.item()),
+            "toa_mean_likelihood_evaluations": float(np.mean(res["evaluations"])),
             "toa_shift_recovery_rms_cycles": float(np.sqrt(np.mean(d ** 2)) / (2 * np.pi)),
             "toa_median_sigma_cycles": float(np.median(res["phShi_LL"]) / (2 * np.pi)),
             "toa_cpu_reference_fits_per_s": 0.42}

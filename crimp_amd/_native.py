@@ -12,7 +12,9 @@ import threading
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libcrimp_hip.so")
+# CRIMP_LIB_VARIANT=<name> loads lib/libcrimp_hip_<name>.so (kernel experiments built beside the default)
+LIB_PATH = os.path.join(_HERE, "lib", "libcrimp_hip%s.so" % (
+    ("_" + os.environ["CRIMP_LIB_VARIANT"]) if os.environ.get("CRIMP_LIB_VARIANT") else ""))
 
 FLAG_DEVICE_PTRS = 1
 FLAG_SYNC = 2

@@ -1013,7 +1013,7 @@ static int toa_grid_partials(Scratch& sc, hipStream_t s, const double* dx, const
 }
 
 extern "C" int crimp_toa_fit(const double* x, const int64_t* offsets, int64_t nint, const crimp_template* tpl,
-                             const double* exposure, double norm0, int32_t ph_shift_res, int32_t brutemin, double* out,
+                             const double* exposure, double norm0, int32_t ph_shift_res, int32_t options, double* out,
                              uint32_t flags, void* stream) {
     ARGCHK(nint >= 1, "bad sizes");
     ARGCHK(ph_shift_res >= 1, "phShiftRes must be >= 1");
@@ -1023,6 +1023,7 @@ extern "C" int crimp_toa_fit(const double* x, const int64_t* offsets, int64_t ni
     TplDev T;
     int rc = make_tpl(tpl, &T);
     if (rc) return rc;
+    const bool brutemin = options & CRIMP_TOA_BRUTE, vary_amps = options & CRIMP_TOA_VARY_AMPS;
     if (brutemin) ARGCHK(T.K <= kGridKMax, "brute grid supports at most 8 template components");
     std::lock_guard<std::mutex> lk(g_mutex);
     const bool dev = flags & CRIMP_FLAG_DEVICE_PTRS;
@@ -1097,7 +1098,10 @@ extern "C" int crimp_toa_fit(const double* x, const int64_t* offsets, int64_t ni
             }
             HIPCHK(h2d(dstart, hstart.data(), 2 * nint * sizeof(double)));
         }
-        k_toa_fit<<<(unsigned)nint, kFitBlock, 0, s>>>(dx, doff, dT, de, dstart, C, dout);
+        if (vary_amps)
+            k_toa_fit_amp<<<(unsigned)nint, kFitBlock, 0, s>>>(dx, doff, dT, de, dstart, C, dout);
+        else
+            k_toa_fit<<<(unsigned)nint, kFitBlock, 0, s>>>(dx, doff, dT, de, dstart, C, dout);
         HIPCHK(hipGetLastError());
         HIPCHK(copy_back(s, out, dout, (size_t)nint * 8, dev));
         HIPCHK(hipStreamSynchronize(s));

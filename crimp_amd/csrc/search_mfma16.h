@@ -90,18 +90,43 @@ __device__ __forceinline__ void mma(const AFrag& A, const BFrag& B, f32x16& re, 
 // One photon pair: V factors once, then every tile's U factors and MFMAs. FIRST groups take
 // harmonic 2 by squaring (unbiased: the sin/cos error is quarter-turn periodic); later groups evaluate
 // each harmonic from its own fp64 phase.
+// Table sin/cos (CRIMP_SINCOS_TABLE): r = k/1024 + y, |y| <= 1/2048 turn; (cos, sin)(2 pi k/1024) from a
+// 1024-entry LDS table held as fp32 hi + lo pairs (tab[k] = hi, tab[1024 + k] = lo), the residual rotation by
+// sin(2 pi y) ~ 2 pi y - (2 pi y)^3/6 and cos(2 pi y) - 1 ~ -(2 pi y)^2/2 (truncation < 4e-12), combined so
+// that only the final fp32 rounding remains (16 VALU + 2 LDS reads instead of 19 VALU).
+__device__ __forceinline__ void sincos_tab(const float2* __restrict__ tab, float r, float& s, float& c) {
+    const float kf = __builtin_rintf(1024.0f * r);
+    const float y = __builtin_fmaf(-1.0f / 1024.0f, kf, r);  // exact
+    const int k = ((int)kf) & 1023;
+    const float2 th = tab[k], tl = tab[1024 + k];
+    const float y2 = y * y;
+    const float sp = y * __builtin_fmaf(y2, -41.341702240399755f, 6.283185307179586f);
+    const float cm = y2 * -19.739208802178716f;
+    s = th.y + __builtin_fmaf(th.y, cm, __builtin_fmaf(th.x, sp, tl.y));
+    c = th.x + __builtin_fmaf(th.x, cm, __builtin_fmaf(-th.y, sp, tl.x));
+}
+
+__device__ __forceinline__ void sc_rev(const float2* __restrict__ tab, float r, float& s, float& c) {
+#ifdef CRIMP_SINCOS_TABLE
+    sincos_tab(tab, r, s, c);
+#else
+    (void)tab;
+    sincos_turn(r, s, c);
+#endif
+}
+
 template <int G, int TILES, bool FIRST>
-__device__ __forceinline__ void mfma16_pair(const double (&phu)[TILES], double phv, float live, int k0,
-                                            f32x16 (&re)[TILES][G], f32x16 (&im)[TILES][G]) {
+__device__ __forceinline__ void mfma16_pair(const float2* tab, const double (&phu)[TILES], double phv, float live,
+                                            int k0, f32x16 (&re)[TILES][G], f32x16 (&im)[TILES][G]) {
     if (FIRST) {
         float vs, vc;
-        sincos_turn(frac_turn(phv), vs, vc);
+        sc_rev(tab, frac_turn(phv), vs, vc);
         BFrag B1 = make_b(vc, vs), B2;
         if (G > 1) B2 = make_b(__builtin_fmaf(vc, vc, -(vs * vs)), (vc + vc) * vs);
 #pragma unroll
         for (int t = 0; t < TILES; ++t) {
             float us, uc;
-            sincos_turn(frac_turn(phu[t]), us, uc);
+            sc_rev(tab, frac_turn(phu[t]), us, uc);
             uc *= live;
             us *= live;
             mma(make_a(uc, us), B1, re[t][0], im[t][0]);
@@ -112,12 +137,12 @@ __device__ __forceinline__ void mfma16_pair(const double (&phu)[TILES], double p
         for (int g = 0; g < G; ++g) {
             const double kf = (double)(k0 + g);
             float vs, vc;
-            sincos_turn(frac_turn(phv * kf), vs, vc);
+            sc_rev(tab, frac_turn(phv * kf), vs, vc);
             const BFrag B = make_b(vc, vs);
 #pragma unroll
             for (int t = 0; t < TILES; ++t) {
                 float us, uc;
-                sincos_turn(frac_turn(phu[t] * kf), us, uc);
+                sc_rev(tab, frac_turn(phu[t] * kf), us, uc);
                 mma(make_a(uc * live, us * live), B, re[t][g], im[t][g]);
             }
         }
@@ -132,6 +157,20 @@ __global__ __launch_bounds__(256, TILES == 1 ? 2 : 1) void k_search_mfma16(
     double* __restrict__ part) {
     const int lane = threadIdx.x & 63;
     const int64_t T = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+#ifdef CRIMP_SINCOS_TABLE
+    __shared__ float2 s_tab[2048];
+    for (int i = threadIdx.x; i < 1024; i += 256) {
+        double sv, cv;
+        sincospi((double)i / 512.0, &sv, &cv);
+        const float ch = (float)cv, sh = (float)sv;
+        s_tab[i] = make_float2(ch, sh);
+        s_tab[1024 + i] = make_float2((float)(cv - (double)ch), (float)(sv - (double)sh));
+    }
+    __syncthreads();
+    const float2* tab = s_tab;
+#else
+    const float2* tab = nullptr;
+#endif
     if (T >= ntiles) return;  // wave-uniform
     const int64_t gt = tile_first + T;
     const int64_t frow = gt / tiles_per_row;
@@ -172,12 +211,17 @@ __global__ __launch_bounds__(256, TILES == 1 ? 2 : 1) void k_search_mfma16(
                 for (int r = 0; r < 16; ++r) re[t][g][r] = im[t][g][r] = 0.0f;
         auto pair = [&](int q, float live) {
             const int src = 2 * q + h;
+#ifdef CRIMP_D_GLOBAL  // experiment: each lane loads its photon (L1/L2 hit) instead of a bpermute
+            const double d = src < cnt ? dt[ib + src] : 0.0;
+            const double d2 = TWOD ? (src < cnt ? dt2[ib + src] : 0.0) : 0.0;
+#else
             const double d = bperm_d(dtv, src);
             const double d2 = TWOD ? bperm_d(d2v, src) : 0.0;
+#endif
             double phu[TILES];
 #pragma unroll
             for (int t = 0; t < TILES; ++t) phu[t] = TWOD ? fma(fa[t], d, c2 * d2) : fa[t] * d;
-            mfma16_pair<G, TILES, FIRST>(phu, gb * d, live, k0, re, im);
+            mfma16_pair<G, TILES, FIRST>(tab, phu, gb * d, live, k0, re, im);
         };
         if (cnt == kMfmaChunk) {
 #pragma unroll

@@ -143,8 +143,228 @@ __device__ double fit_profile(const double* __restrict__ x, int64_t a, int64_t b
     return e.ll;
 }
 
+// ---------------------------------------------------------------- varyAmps (measureToAs.py:305-312)
+// With ampShift A free the model is norm + A*h, and the extended LL, its gradient and Hessian in
+// (norm, phShift, A) follow from 11 photon sums; ampShift is bounded to [0.01, 100] (:308).
+constexpr double kAmpLo = 0.01, kAmpHi = 100.0;
+
+struct FitEval3 {
+    double ll, g[3], H[6];  // H = {nn, np, nA, pp, pA, AA}
+};
+
+struct FitShared3 {
+    double red[kFitBlock / 64][12];
+};
+
+__device__ FitEval3 fit_eval3(const double* __restrict__ x, int64_t a, int64_t b, const TplDev* __restrict__ T,
+                              double n, double phi, double A, double E, const FitCfg& C, FitShared& sh,
+                              FitShared3& s3) {
+    const int tid = threadIdx.x;
+    const int model = T->model, K = T->K;
+    __syncthreads();
+    if (tid < K) tpl_coef(T, tid, phi, sh.coef[0][tid], sh.coef[1][tid]);
+    __syncthreads();
+    // sums: ln mv, q, h q, h1 q, h2 q, q^2, h q^2, h1 q^2, h^2 q^2, h h1 q^2, h1^2 q^2 ; min mv
+    double acc[11];
+#pragma unroll
+    for (int q = 0; q < 11; ++q) acc[q] = 0.0;
+    double mn = INFINITY;
+    for (int64_t i = a + tid; i < b; i += kFitBlock) {
+        double s1, c1, h, h1, h2;
+        photon_sincos(model, x[i], s1, c1);
+        tpl_terms(T, model, K, sh.coef[0], sh.coef[1], s1, c1, h, h1, h2);
+        const double mv = n + A * h;
+        const double q = 1.0 / mv;
+        const double q2 = q * q;
+        acc[0] += log(mv);
+        acc[1] += q;
+        acc[2] += h * q;
+        acc[3] += h1 * q;
+        acc[4] += h2 * q;
+        acc[5] += q2;
+        acc[6] += h * q2;
+        acc[7] += h1 * q2;
+        acc[8] += h * h * q2;
+        acc[9] += h * h1 * q2;
+        acc[10] += h1 * h1 * q2;
+        mn = fmin(mn, mv);
+    }
+    const int w = tid >> 6, lane = tid & 63;
+#pragma unroll
+    for (int q = 0; q < 11; ++q) {
+        const double v = wave_sum(acc[q]);
+        if (lane == 0) s3.red[w][q] = v;
+    }
+    const double vm = wave_min(mn);
+    if (lane == 0) s3.red[w][11] = vm;
+    __syncthreads();
+    double S[12];
+#pragma unroll
+    for (int q = 0; q < 12; ++q) {
+        double v = s3.red[0][q];
+        for (int ww = 1; ww < kFitBlock / 64; ++ww) v = (q == 11) ? fmin(v, s3.red[ww][q]) : v + s3.red[ww][q];
+        S[q] = v;
+    }
+    const double N = (double)(b - a);
+    FitEval3 r;
+    double F;
+    if (model == CRIMP_MODEL_FOURIER) {
+        F = n;
+        r.ll = -n * E + N * log(n * E) + (S[0] - N * log(n));
+        r.g[2] = S[2];
+    } else {
+        F = kTwoPi * n + A * C.sum_amp;
+        r.ll = -F * E / kTwoPi + N * log(F * E / kTwoPi) + (S[0] - N * log(F));
+        r.g[2] = S[2] - C.sum_amp * E / kTwoPi;
+    }
+    if (!(S[11] / F > 0)) r.ll = -INFINITY;
+    r.g[0] = -E + S[1];
+    r.g[1] = A * S[3];
+    r.H[0] = -S[5];
+    r.H[1] = -A * S[7];
+    r.H[2] = -S[6];
+    r.H[3] = A * S[4] - A * A * S[10];
+    r.H[4] = S[3] - A * S[9];
+    r.H[5] = -S[8];
+    return r;
+}
+
+// Newton direction for the free coordinates (mask bits: 1 norm, 2 phShift, 4 ampShift) of a 3-parameter
+// ascent: Levenberg shift by a Gershgorin bound of the largest eigenvalue, then a trust region (0.05 rad
+// in phShift, half the current norm and ampShift).
+__device__ void fit_newton_dir3(const double* v, const FitEval3& e, int mask, double* d) {
+    double H[3][3] = {{e.H[0], e.H[1], e.H[2]}, {e.H[1], e.H[3], e.H[4]}, {e.H[2], e.H[4], e.H[5]}};
+    double g[3] = {e.g[0], e.g[1], e.g[2]};
+    for (int i = 0; i < 3; ++i)
+        if (!(mask & (1 << i))) {
+            for (int j = 0; j < 3; ++j) H[i][j] = H[j][i] = 0.0;
+            H[i][i] = -1.0;
+            g[i] = 0.0;
+        }
+    double lam = -INFINITY, diag = 0.0;
+    for (int i = 0; i < 3; ++i) {
+        double r = H[i][i];
+        for (int j = 0; j < 3; ++j)
+            if (j != i) r += fabs(H[i][j]);
+        lam = fmax(lam, r);
+        diag += fabs(H[i][i]);
+    }
+    const double shift = lam < 0 ? 0.0 : lam * 1.5 + 1e-6 * diag + 1e-12;
+    for (int i = 0; i < 3; ++i) H[i][i] -= shift;
+    // solve H d = -g (symmetric 3x3, Cramer)
+    const double c00 = H[1][1] * H[2][2] - H[1][2] * H[2][1];
+    const double c01 = H[1][2] * H[2][0] - H[1][0] * H[2][2];
+    const double c02 = H[1][0] * H[2][1] - H[1][1] * H[2][0];
+    const double det = H[0][0] * c00 + H[0][1] * c01 + H[0][2] * c02;
+    const double inv[3][3] = {
+        {c00 / det, (H[0][2] * H[2][1] - H[0][1] * H[2][2]) / det, (H[0][1] * H[1][2] - H[0][2] * H[1][1]) / det},
+        {c01 / det, (H[0][0] * H[2][2] - H[0][2] * H[2][0]) / det, (H[0][2] * H[1][0] - H[0][0] * H[1][2]) / det},
+        {c02 / det, (H[0][1] * H[2][0] - H[0][0] * H[2][1]) / det, (H[0][0] * H[1][1] - H[0][1] * H[1][0]) / det}};
+    for (int i = 0; i < 3; ++i) d[i] = -(inv[i][0] * g[0] + inv[i][1] * g[1] + inv[i][2] * g[2]);
+    double sc = 1.0;
+    sc = fmin(sc, 0.5 * fabs(v[0]) / fmax(fabs(d[0]), 1e-300));
+    sc = fmin(sc, 0.05 / fmax(fabs(d[1]), 1e-300));
+    sc = fmin(sc, 0.5 * fabs(v[2]) / fmax(fabs(d[2]), 1e-300));
+    for (int i = 0; i < 3; ++i) d[i] *= sc;
+}
+
+// Damped Newton ascent over the free coordinates of v = (norm, phShift, ampShift) within the bounds.
+__device__ FitEval3 fit_ascent3(const double* __restrict__ x, int64_t a, int64_t b, const TplDev* __restrict__ T,
+                                double* v, int mask, int max_iter, double E, const FitCfg& C, FitShared& sh,
+                                FitShared3& s3, int& nev) {
+    const double lo[3] = {C.lo, -C.pb, kAmpLo}, hi[3] = {C.hi, C.pb, kAmpHi};
+    FitEval3 e = fit_eval3(x, a, b, T, v[0], v[1], v[2], E, C, sh, s3);
+    ++nev;
+    for (int it = 0; it < max_iter; ++it) {
+        double d[3];
+        fit_newton_dir3(v, e, mask, d);
+        double t = 1.0, tv[3] = {v[0], v[1], v[2]};
+        FitEval3 e2 = e;
+        bool ok = false;
+        for (int ls = 0; ls < 40; ++ls) {
+            for (int i = 0; i < 3; ++i) tv[i] = clipd(v[i] + t * d[i], lo[i], hi[i]);
+            e2 = fit_eval3(x, a, b, T, tv[0], tv[1], tv[2], E, C, sh, s3);
+            ++nev;
+            if (isfinite(e2.ll) && e2.ll >= e.ll - 1e-12 * fabs(e.ll)) {
+                ok = true;
+                break;
+            }
+            t *= 0.5;
+        }
+        if (!ok) break;
+        bool moved = false;
+        for (int i = 0; i < 3; ++i) {
+            const double tol = (i == 1) ? 1e-12 : 1e-12 * fmax(1.0, fabs(tv[i]));
+            moved |= fabs(tv[i] - v[i]) >= tol;
+            v[i] = tv[i];
+        }
+        e = e2;
+        if (!moved) break;
+    }
+    return e;
+}
+
+// varyAmps fit of one interval: the (norm, phShift) ascent with ampShift = 1, then all three free from there
+// (:306-312), then the 1-sigma scan with norm and ampShift re-profiled at each phShift step.
+__global__ __launch_bounds__(kFitBlock) void k_toa_fit_amp(const double* __restrict__ x,
+                                                           const int64_t* __restrict__ offsets,
+                                                           const TplDev* __restrict__ T, const double* __restrict__ expo,
+                                                           const double* __restrict__ start, FitCfg C,
+                                                           double* __restrict__ out) {
+    __shared__ FitShared sh;
+    __shared__ FitShared3 s3;
+    const int64_t iv = blockIdx.x;
+    const int64_t a = offsets[iv], b = offsets[iv + 1];
+    const double E = expo[iv];
+    int nev = 0;
+    double v[3] = {start[2 * iv], start[2 * iv + 1], 1.0};
+    fit_ascent3(x, a, b, T, v, 1 | 2, 60, E, C, sh, s3, nev);
+    const FitEval3 em = fit_ascent3(x, a, b, T, v, 1 | 2 | 4, 100, E, C, sh, s3, nev);
+    const double nhat = v[0], phat = v[1], ahat = v[2], llmax = em.ll;
+    double sig[2];
+    for (int s = 0; s < 2; ++s) {
+        const int side = s == 0 ? -1 : 1;
+        bool past = false;
+        int kk = 0;
+        for (int k = 1;; ++k) {
+            const double target = phat + (double)(side * k) * C.step;
+            double ph;
+            if (T->model == CRIMP_MODEL_FOURIER) {
+                const bool beyond = side < 0 ? (target <= -M_PI) : (target >= M_PI);
+                if (beyond && !past) {
+                    ph = side < 0 ? -M_PI : M_PI;
+                    past = true;
+                } else {
+                    ph = target;
+                }
+            } else {
+                ph = clipd(target, -C.pb, C.pb);
+            }
+            double w[3] = {nhat, ph, ahat};
+            const FitEval3 ek = fit_ascent3(x, a, b, T, w, 1 | 4, 30, E, C, sh, s3, nev);
+            const double diff = llmax - ek.ll;
+            if (diff > kHalfChi2OneSigma || (double)(k + 1) > C.kcap) {
+                kk = k + 1;
+                break;
+            }
+        }
+        sig[s] = (double)kk * C.step + C.step / 2;
+    }
+    if (threadIdx.x == 0) {
+        double* o = out + iv * 8;
+        o[0] = nhat;
+        o[1] = phat;
+        o[2] = llmax;
+        o[3] = sig[0];
+        o[4] = sig[1];
+        o[5] = (double)nev;
+        o[6] = ahat;
+        o[7] = 0.0;
+    }
+}
+
 // One workgroup per interval: ascent from start[iv], then the 1-sigma scan on both sides.
-// out[iv*8 + 0..5] = norm, phShift, LLmax, phShift_LL, phShift_UL, likelihood evaluations.
+// out[iv*8 + 0..6] = norm, phShift, LLmax, phShift_LL, phShift_UL, likelihood evaluations, ampShift (1).
 __global__ __launch_bounds__(kFitBlock) void k_toa_fit(const double* __restrict__ x, const int64_t* __restrict__ offsets,
                                                        const TplDev* __restrict__ T, const double* __restrict__ expo,
                                                        const double* __restrict__ start, FitCfg C,
@@ -219,7 +439,7 @@ __global__ __launch_bounds__(kFitBlock) void k_toa_fit(const double* __restrict_
         o[3] = sig[0];
         o[4] = sig[1];
         o[5] = (double)nev;
-        o[6] = 0.0;
+        o[6] = 1.0;
         o[7] = 0.0;
     }
 }

@@ -7,8 +7,8 @@ batches on the device (crimp_amd/toafit.py); the loop body keeps the
 reference's order of operations and its text formatting (``str()`` of each value,
 tab-separated, 13 columns, :161-162, :222-226).
 
-Not implemented in this build (raise ``NotImplementedError``): ``varyAmps`` and
-``readvaryparam``.
+Not implemented in this build (raises ``NotImplementedError``):
+``readvaryparam``. ``varyAmps`` runs on the device (crimp_toa_fit).
 """
 import argparse
 import math
@@ -68,8 +68,6 @@ def defineinitialfitparam(tempModPP, readvaryparam=False):
 
 
 def _check_opts(varyAmps, readvaryparam):
-    if varyAmps:
-        raise NotImplementedError("varyAmps=True is not implemented in this build")
     if readvaryparam:
         raise NotImplementedError("readvaryparam=True is not implemented in this build")
 
@@ -81,7 +79,7 @@ def _single(model, tempModPP, phases, exposureInt, phShiftRes, nbrBins, varyAmps
         raise ValueError("template model %s used with measureToA_%s" % (tempModPP["model"], model))
     x = np.ascontiguousarray(np.ravel(phases), dtype=np.float64)
     fit = ToAFitter(x, np.array([0, x.size]), np.array([float(exposureInt)]), tempModPP, phShiftRes, nbrBins)
-    r = fit.fit(brutemin=brutemin)
+    r = fit.fit(brutemin=brutemin, vary_amps=bool(varyAmps))
     if plotLLs or plotPPs:
         logger.warning("plotPPs/plotLLs are diagnostic plots and are not produced by this build")
     return {"phShi": float(r["phShi"][0]), "phShi_LL": float(r["phShi_LL"][0]), "phShi_UL": float(r["phShi_UL"][0]),
@@ -113,7 +111,7 @@ HEADER = ('ToA \t ToA_mid \t ToA_start \t ToA_end \t ToA_lenInt \t ToA_exp \t nb
           ' \t phShift_LL \t phShift_UL \t Hpower \t redChi2\n')
 
 
-def measure_intervals(TIMEMJD, timMod, tempModPP, starts, ends, exposures, phShiftRes=1000, nbrBins=15,
+def measure_intervals(TIMEMJD, timMod, tempModPP, starts, ends, exposures, phShiftRes=1000, nbrBins=15, varyAmps=False,
                       brutemin=False):
     """Batched core of measureToAs on in-memory arrays: per interval ToA_mid, fit dict entries, H power."""
     tmpl = readPPtemplate(tempModPP) if isinstance(tempModPP, str) else tempModPP
@@ -129,7 +127,7 @@ def measure_intervals(TIMEMJD, timMod, tempModPP, starts, ends, exposures, phShi
     if model in ("cauchy", "vonmises"):
         folded = folded * (2 * np.pi)                  # :195, :200
     fit = ToAFitter(folded, np.array(offs), np.asarray(exposures, dtype=np.float64), tmpl, phShiftRes, nbrBins)
-    res = fit.fit(brutemin=brutemin)
+    res = fit.fit(brutemin=brutemin, vary_amps=bool(varyAmps))
     hp = []
     for t, mid in zip(sel, mids):
         eph = ephemTmjd(mid, timMod)
@@ -161,7 +159,8 @@ def measureToAs(evtFile, timMod, tempModPP, toagtifile, eneLow=0.5, eneHigh=10.,
     logger.info('\n Using best fit model of template {} to measure ToAs'.format(tmpl["model"]))
     for ii in rng:
         print('ToA {}'.format(ii))
-    res = measure_intervals(TIMEMJD, timMod, tmpl, st[rng], en[rng], expo[rng], phShiftRes, nbrBins, brutemin)
+    res = measure_intervals(TIMEMJD, timMod, tmpl, st[rng], en[rng], expo[rng], phShiftRes, nbrBins, varyAmps,
+                            brutemin)
     with open(toaFile + '.txt', "w+") as f:
         f.write(HEADER)
         for k, ii in enumerate(rng):

@@ -164,9 +164,13 @@ def toa_grid(x, offsets, tpl, norms, phis):
     return ln.reshape(nint, nnorm, nphi), hm.reshape(nint, nphi)
 
 
-def toa_fit(x, offsets, tpl, exposure, norm0, ph_shift_res=1000, brutemin=False):
+TOA_BRUTE, TOA_VARY_AMPS = 1, 2
+
+
+def toa_fit(x, offsets, tpl, exposure, norm0, ph_shift_res=1000, brutemin=False, vary_amps=False):
     """Whole per-interval ToA fits on the device (crimp_toa_fit): [nint, 8] = norm, phShift, LLmax,
-    phShift_LL, phShift_UL, likelihood evaluations."""
+    phShift_LL, phShift_UL, likelihood evaluations, ampShift."""
+    options = (TOA_BRUTE if brutemin else 0) | (TOA_VARY_AMPS if vary_amps else 0)
     L = N.load()
     b = N.Buffers()
     xp = b.arg(x, np.float64)
@@ -175,8 +179,8 @@ def toa_fit(x, offsets, tpl, exposure, norm0, ph_shift_res=1000, brutemin=False)
     nint = int((offsets.numel() if N._is_torch(offsets) else np.size(offsets)) - 1)
     out = _empty_like_input(x, nint * 8, b)
     outp = b.arg(out, np.float64, writable=True)
-    N.check(L.crimp_toa_fit(xp, op, nint, ctypes.byref(tpl), ep, float(norm0), int(ph_shift_res), int(bool(brutemin)),
-                            outp, b.flags(), b.stream()))
+    N.check(L.crimp_toa_fit(xp, op, nint, ctypes.byref(tpl), ep, float(norm0), int(ph_shift_res), options, outp,
+                            b.flags(), b.stream()))
     return out.reshape(nint, 8)
 
 

@@ -276,7 +276,7 @@ class ToAFitter:
         return out[-1], out[1]
 
     # ------------------------------------------------------------------ step 4: redChi2
-    def reduced_chi2(self, n_hat, phi_hat, nfree=2):
+    def reduced_chi2(self, n_hat, phi_hat, nfree=2, amp_shift=None):
         upper = 1.0 if self.model == "fourier" else TWO_PI
         edges = np.linspace(0, upper, self.nbins + 1, endpoint=True)
         cts = ops.binphases_counts(self.x, self.offsets, self._arr(edges, np.float64))
@@ -286,35 +286,40 @@ class ToAFitter:
         pp = np.linspace(0, upper, self.nbins, endpoint=False) + (upper / self.nbins) / 2
         rate = cts / (self.E[:, None] / self.nbins)
         err = np.sqrt(cts) / (self.E[:, None] / self.nbins)
-        model = self.curve(n_hat[:, None], phi_hat[:, None], pp[None, :])
+        amp = np.ones_like(n_hat) if amp_shift is None else np.asarray(amp_shift, dtype=np.float64)
+        model = self.curve(n_hat[:, None], phi_hat[:, None], pp[None, :], amp[:, None])
         with np.errstate(divide="ignore", invalid="ignore"):
             chi2 = np.sum(np.divide((model - rate) ** 2, err ** 2), axis=1)
         return np.divide(chi2, self.nbins - nfree)
 
-    def curve(self, n, phi, xx):
+    def curve(self, n, phi, xx, amp_shift=1.0):
+        """fourseries / wrapcauchy / vonmises at xx (templatemodels.py:64-82, :166-185, :271-290)."""
         y = np.zeros(np.broadcast(n, xx).shape) + n
         t = self.tpl
+        a = amp_shift
         for j in range(self.K):
             if self.model == "fourier":
-                y = y + t.amp[j] * np.cos((j + 1) * 2 * np.pi * xx + t.loc[j] - (j + 1) * phi)
+                y = y + t.amp[j] * a * np.cos((j + 1) * 2 * np.pi * xx + t.loc[j] - (j + 1) * phi)
             elif self.model == "cauchy":
-                y = y + (t.amp[j] / (2 * np.pi)) * (np.sinh(t.wid[j]) / (np.cosh(t.wid[j]) - np.cos(xx - t.loc[j] - phi)))
+                y = y + ((t.amp[j] * a) / (2 * np.pi)) * (np.sinh(t.wid[j]) / (np.cosh(t.wid[j]) - np.cos(xx - t.loc[j] - phi)))
             else:
-                y = y + (t.amp[j] / (2 * np.pi * t.i0[j])) * np.exp((1 / t.wid[j] ** 2) * np.cos(xx - t.loc[j] - phi))
+                y = y + ((t.amp[j] * a) / (2 * np.pi * t.i0[j])) * np.exp((1 / t.wid[j] ** 2) * np.cos(xx - t.loc[j] - phi))
         return y
 
     # ------------------------------------------------------------------ drivers
-    def fit(self, brutemin=False):
+    def fit(self, brutemin=False, vary_amps=False):
         """Every interval's fit in one device call (crimp_toa_fit: one workgroup per interval runs steps 1-3),
-        then the redChi2 of step 4."""
-        r = ops.toa_fit(self.x, self.offsets, self.tpl, self._arr(self.E, np.float64), self.norm0, self.res, brutemin)
+        then the redChi2 of step 4. ``vary_amps``: ampShift free in [0.01, 100] after the (norm, phShift) fit,
+        re-profiled with the norm in the 1-sigma scan, one more free parameter in redChi2 (:305-312)."""
+        r = ops.toa_fit(self.x, self.offsets, self.tpl, self._arr(self.E, np.float64), self.norm0, self.res, brutemin,
+                        vary_amps)
         if _is_torch(r):
             r = r.cpu().numpy()
         r = np.asarray(r)
-        n_hat, phi_hat = r[:, 0].copy(), r[:, 1].copy()
-        rchi2 = self.reduced_chi2(n_hat, phi_hat)
+        n_hat, phi_hat, amp = r[:, 0].copy(), r[:, 1].copy(), r[:, 6].copy()
+        rchi2 = self.reduced_chi2(n_hat, phi_hat, nfree=3 if vary_amps else 2, amp_shift=amp)
         return {"phShi": phi_hat, "phShi_LL": r[:, 3].copy(), "phShi_UL": r[:, 4].copy(), "reducedChi2": rchi2,
-                "norm": n_hat, "LLmax": r[:, 2].copy(), "evaluations": r[:, 5].copy()}
+                "norm": n_hat, "LLmax": r[:, 2].copy(), "evaluations": r[:, 5].copy(), "ampShift": amp}
 
     def fit_host(self, brutemin=False):
         """The same fit driven from the host, one batched likelihood launch per iteration (cross-check of fit)."""

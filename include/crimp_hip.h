@@ -121,15 +121,19 @@ int crimp_toa_grid(const double* x, const int64_t* offsets, int64_t nint, const 
                    const double* norm, int64_t nnorm, const double* phi, int64_t nphi, double* lnsum,
                    double* hmin, uint32_t flags, void* stream);
 
-/* measureToA_fourier / _cauchy / _vonmises(tempModPP, phases, exposure, phShiftRes=res, brutemin=...) for
- * every interval at once, with readvaryparam=False, varyAmps=False   [measureToAs.py:254-693, :698-806]:
+#define CRIMP_TOA_BRUTE 1      /* crimp_toa_fit options: lmfit brute start (measureToAs.py:292-295, -bm) */
+#define CRIMP_TOA_VARY_AMPS 2  /* ampShift free in [0.01, 100] after the first fit (measureToAs.py:305-312, -va) */
+
+/* measureToA_fourier / _cauchy / _vonmises(tempModPP, phases, exposure, phShiftRes=res, brutemin=...,
+ * varyAmps=...) for every interval at once, readvaryparam=False   [measureToAs.py:254-693, :698-806]:
  * optional lmfit brute start (20 norms in [norm0/100, 500] x phShift = k*0.05 - bound), the extended-LL
- * maximum in (norm, phShift), and the 1-sigma scan in steps of 2pi/res with the norm re-profiled at each
- * step. One workgroup per interval runs the whole fit on the device (csrc/toa_fit.h).
- * out[i*8 + 0..5] = { norm, phShift, LLmax, phShift_LL, phShift_UL, likelihood evaluations }.
+ * maximum in (norm, phShift) -- and ampShift with CRIMP_TOA_VARY_AMPS --, and the 1-sigma scan in steps of
+ * 2pi/res with the other free parameters re-profiled at each step. One workgroup per interval runs the
+ * whole fit on the device (csrc/toa_fit.h).
+ * out[i*8 + 0..6] = { norm, phShift, LLmax, phShift_LL, phShift_UL, likelihood evaluations, ampShift }.
  * The reduced chi2 (:385-393) is left to the caller (crimp_binphases + the template curve). */
 int crimp_toa_fit(const double* x, const int64_t* offsets, int64_t nint, const crimp_template* tpl,
-                  const double* exposure, double norm0, int32_t ph_shift_res, int32_t brutemin, double* out,
+                  const double* exposure, double norm0, int32_t ph_shift_res, int32_t options, double* out,
                   uint32_t flags, void* stream);
 
 /* binphases(phases, nbrBins) counts per interval   [binphases.py:9-39]:

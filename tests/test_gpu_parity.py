@@ -280,6 +280,28 @@ def test_device_toa_driver_equals_host_driver(gpu):
         np.testing.assert_array_equal(d["phShi_UL"], h["phShi_UL"])
 
 
+def test_toa_fit_vary_amps_vs_oracle(gpu):
+    """varyAmps (measureToAs.py:305-312): ampShift free in [0.01, 100]. No reference output exercises it
+    (parity unpinned); checked against the oracle's optimum restatement."""
+    from crimp_amd.measureToAs import measureToA_fourier
+    from crimp_amd.toafit import ToAFitter
+    from crimp_amd.readPPtemplate import readPPtemplate
+    g, iv, ref = _golden_rows()
+    tm = readPPtemplate(gpath("1e2259_template.txt"))
+    E = iv["ToA_exposure"].to_numpy()[g["ids"]]
+    r = ToAFitter(g["folded"], g["offsets"], E, tm).fit(brutemin=True, vary_amps=True)
+    for i in (2,):  # the oracle's nested optimisation takes ~15 s per ToA on the host
+        x = g["folded"][g["offsets"][i]:g["offsets"][i + 1]]
+        o = O.fit_toa_vary_amps(x, E[i], tm, brutemin=True)
+        assert abs(r["phShi"][i] - o["phShi"]) / (2 * math.pi) < 1e-6
+        assert r["ampShift"][i] == pytest.approx(o["ampShift"], rel=1e-5)
+        assert r["LLmax"][i] == pytest.approx(o["LLmax"], abs=1e-6)
+        assert r["phShi_LL"][i] == o["phShi_LL"] and r["phShi_UL"][i] == o["phShi_UL"]
+        assert r["reducedChi2"][i] == pytest.approx(o["reducedChi2"], rel=1e-5)
+    s = measureToA_fourier(tm, g["folded"][g["offsets"][2]:g["offsets"][3]], E[2], brutemin=True, varyAmps=True)
+    assert s["phShi"] == pytest.approx(r["phShi"][2], abs=1e-12)
+
+
 def test_toa_fit_without_brute_and_other_templates(gpu):
     from crimp_amd.measureToAs import measureToA_fourier, measureToA_cauchy, measureToA_vonmises
     from crimp_amd.readPPtemplate import readPPtemplate

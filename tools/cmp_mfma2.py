@@ -21,7 +21,7 @@ for n in (32, 64, 2048, 65536, 300000):
     for m in (1, 2, 3):
         ref = O.search(t, f, m)
         line = "n=%6d m=%d:" % (n, m)
-        for name, fl in (("f32", 0), ("f16", N.FLAG_MFMA_F16)):
+        for name, fl in (("f32", N.FLAG_MFMA_F32), ("f16", 0)):
             got = ops.search(t, t0, f, m, 0, flags=fl | N.FLAG_FORCE_MFMA)
             e = np.abs(got - ref) / np.maximum(np.abs(ref), np.mean(np.abs(ref)))
             line += "  %s max %.3g (at %d) median %.3g" % (name, e.max(), int(e.argmax()), np.median(e))

@@ -24,5 +24,5 @@ t1 = time.perf_counter()
 z = ops.search(t, t0, f, m, 0)
 torch.cuda.synchronize()
 el = time.perf_counter() - t1
-print("variant %s: %.1f ms %.3e evals/s argmax %d" % (os.environ.get("CRIMP_MFMA", "t1"), el * 1e3, n * M / el,
+print("variant %s lib %s: %.1f ms %.3e evals/s argmax %d" % (os.environ.get("CRIMP_MFMA", "t1"), os.environ.get("CRIMP_LIB_VARIANT", "default"), el * 1e3, n * M / el,
                                                        int(torch.argmax(z))), flush=True)
