@@ -233,6 +233,32 @@ static void launch_mfma(int G, bool firstk, dim3 grid, hipStream_t s, const doub
 #undef CRIMP_LM
 }
 
+// Harmonic groups of the f16 kernel: pairs (k, 2k) share one sin/cos evaluation (the second by
+// squaring), taken greedily from k = 1 up; the harmonics left over go in pairs (each from its own
+// phase) and a final single. m = 2: {(1,2)}; m = 20: six squared pairs + (11,12) (13,15) (16,17) (19,20),
+// 14 sin/cos evaluations per photon and trial instead of 20.
+struct HarmGroup {
+    int g, ka, kb;
+    bool square;
+};
+
+static std::vector<HarmGroup> harmonic_groups(int m) {
+    std::vector<HarmGroup> out;
+    std::vector<char> used((size_t)m + 1, 0);
+    for (int k = 1; 2 * k <= m; ++k)
+        if (!used[k] && !used[2 * k]) {
+            out.push_back({2, k, 2 * k, true});
+            used[k] = used[2 * k] = 1;
+        }
+    std::vector<int> rest;
+    for (int k = 1; k <= m; ++k)
+        if (!used[k]) rest.push_back(k);
+    for (size_t i = 0; i < rest.size(); i += 2)
+        out.push_back(i + 1 < rest.size() ? HarmGroup{2, rest[i], rest[i + 1], false}
+                                          : HarmGroup{1, rest[i], rest[i], false});
+    return out;
+}
+
 // Returns 1 when the factorised kernel produced `out`, 0 when it declines, <0 on error.
 static int mfma_search(Scratch& sc, hipStream_t s, const double* dt, const double* dt2, int64_t n,
                        const double* freq, int64_t nf, const double* c2, bool twod, int nharm, int stat,
@@ -266,21 +292,33 @@ static int mfma_search(Scratch& sc, hipStream_t s, const double* dt, const doubl
     dim3 grid((unsigned)cdiv(nt, 4), (unsigned)splits);
     KernelTimer kt(s, flags & CRIMP_FLAG_TIME_KERNELS);
     kt.start();
-    for (int k0 = 1; k0 <= nharm;) {
-        // groups {1,2}, {3,4}, {5,6}, ...: harmonic 2 by squaring, later ones from exact phases
-        const int G = (nharm - k0 + 1) >= 2 ? 2 : 1;
-#define CRIMP_ARGS G, k0 == 1, grid, s, dt, dt2, n, chunk, freq, nf, c2, delta, tf, nt, tpr, first, count, k0, ncomp, part
-        if (variant == 0) {
-            if (twod) launch_mfma<true>(CRIMP_ARGS); else launch_mfma<false>(CRIMP_ARGS);
-        } else if (variant == 1) {
-            if (twod) launch_mfma16<true, 1>(CRIMP_ARGS); else launch_mfma16<false, 1>(CRIMP_ARGS);
-        } else {
-            if (twod) launch_mfma16<true, 2>(CRIMP_ARGS); else launch_mfma16<false, 2>(CRIMP_ARGS);
+    if (variant == 0) {
+        for (int k0 = 1; k0 <= nharm;) {
+            // groups {1,2}, {3,4}, {5,6}, ...: harmonic 2 by squaring, later ones from exact phases
+            const int G = (nharm - k0 + 1) >= 2 ? 2 : 1;
+            if (twod)
+                launch_mfma<true>(G, k0 == 1, grid, s, dt, dt2, n, chunk, freq, nf, c2, delta, tf, nt, tpr, first,
+                                  count, k0, ncomp, part);
+            else
+                launch_mfma<false>(G, k0 == 1, grid, s, dt, dt2, n, chunk, freq, nf, c2, delta, tf, nt, tpr, first,
+                                   count, k0, ncomp, part);
+            e = hipGetLastError();
+            if (e != hipSuccess) return set_err(CRIMP_ERR_HIP, std::string("k_search_mfma: ") + hipGetErrorString(e));
+            k0 += G;
         }
+    } else {
+        for (const HarmGroup& hg : harmonic_groups(nharm)) {
+#define CRIMP_ARGS hg.g, hg.square, grid, s, dt, dt2, n, chunk, freq, nf, c2, delta, tf, nt, tpr, first, count, hg.ka, \
+                   hg.kb, ncomp, part
+            if (variant == 1) {
+                if (twod) launch_mfma16<true, 1>(CRIMP_ARGS); else launch_mfma16<false, 1>(CRIMP_ARGS);
+            } else {
+                if (twod) launch_mfma16<true, 2>(CRIMP_ARGS); else launch_mfma16<false, 2>(CRIMP_ARGS);
+            }
 #undef CRIMP_ARGS
-        e = hipGetLastError();
-        if (e != hipSuccess) return set_err(CRIMP_ERR_HIP, std::string("k_search_mfma: ") + hipGetErrorString(e));
-        k0 += G;
+            e = hipGetLastError();
+            if (e != hipSuccess) return set_err(CRIMP_ERR_HIP, std::string("k_search_mfma16: ") + hipGetErrorString(e));
+        }
     }
     kt.stop();
     k_search_finalize<<<(unsigned)cdiv(count, 256), 256, 0, s>>>(part, count, (int)splits, nharm, stat, (double)n,

@@ -87,9 +87,9 @@ __device__ __forceinline__ void mma(const AFrag& A, const BFrag& B, f32x16& re, 
     im = __builtin_amdgcn_mfma_f32_32x32x16_f16(A.v, B.im, im, 0, 0, 0);
 }
 
-// One photon pair: V factors once, then every tile's U factors and MFMAs. FIRST groups take
-// harmonic 2 by squaring (unbiased: the sin/cos error is quarter-turn periodic); later groups evaluate
-// each harmonic from its own fp64 phase.
+// One photon pair: V factors once, then every tile's U factors and MFMAs. SQUARE groups are harmonic
+// pairs (ka, 2 ka), the second by squaring the first (unbiased: the sin/cos error is quarter-turn
+// periodic); other groups evaluate each of their harmonics (ka, kb) from its own fp64 phase.
 // Table sin/cos (CRIMP_SINCOS_TABLE): r = k/1024 + y, |y| <= 1/2048 turn; (cos, sin)(2 pi k/1024) from a
 // 1024-entry LDS table held as fp32 hi + lo pairs (tab[k] = hi, tab[1024 + k] = lo), the residual rotation by
 // sin(2 pi y) ~ 2 pi y - (2 pi y)^3/6 and cos(2 pi y) - 1 ~ -(2 pi y)^2/2 (truncation < 4e-12), combined so
@@ -115,10 +115,10 @@ __device__ __forceinline__ void sc_rev(const float2* __restrict__ tab, float r, 
 #endif
 }
 
-template <int G, int TILES, bool FIRST>
+template <int G, int TILES, bool SQUARE>
 __device__ __forceinline__ void mfma16_pair(const float2* tab, const double (&phu)[TILES], double phv, float live,
-                                            int k0, f32x16 (&re)[TILES][G], f32x16 (&im)[TILES][G]) {
-    if (FIRST) {
+                                            int ka, int kb, f32x16 (&re)[TILES][G], f32x16 (&im)[TILES][G]) {
+    if (SQUARE) {  // harmonics (ka, 2 ka): phases arrive pre-scaled by ka
         float vs, vc;
         sc_rev(tab, frac_turn(phv), vs, vc);
         BFrag B1 = make_b(vc, vs), B2;
@@ -135,7 +135,7 @@ __device__ __forceinline__ void mfma16_pair(const float2* tab, const double (&ph
     } else {
 #pragma unroll
         for (int g = 0; g < G; ++g) {
-            const double kf = (double)(k0 + g);
+            const double kf = (double)(g == 0 ? ka : kb);
             float vs, vc;
             sc_rev(tab, frac_turn(phv * kf), vs, vc);
             const BFrag B = make_b(vc, vs);
@@ -149,12 +149,12 @@ __device__ __forceinline__ void mfma16_pair(const float2* tab, const double (&ph
     }
 }
 
-template <int G, bool TWOD, bool FIRST, int TILES>
+template <int G, bool TWOD, bool SQUARE, int TILES>
 __global__ __launch_bounds__(256, TILES == 1 ? 2 : 1) void k_search_mfma16(
     const double* __restrict__ dt, const double* __restrict__ dt2, int64_t n, int64_t chunk,
     const double* __restrict__ freq, int64_t nf, const double* __restrict__ c2row, double delta,
-    int64_t tile_first, int64_t ntiles, int64_t tiles_per_row, int64_t first, int64_t count, int k0, int ncomp,
-    double* __restrict__ part) {
+    int64_t tile_first, int64_t ntiles, int64_t tiles_per_row, int64_t first, int64_t count, int ka, int kb,
+    int ncomp, double* __restrict__ part) {
     const int lane = threadIdx.x & 63;
     const int64_t T = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
 #ifdef CRIMP_SINCOS_TABLE
@@ -177,14 +177,16 @@ __global__ __launch_bounds__(256, TILES == 1 ? 2 : 1) void k_search_mfma16(
     const int64_t c0 = (gt - frow * tiles_per_row) * (kTile * TILES);
     const int a = lane & 31;
     const int h = lane >> 5;
+    // SQUARE groups evaluate harmonic ka directly: scale the phase coefficients once (exact for ka = 1)
+    const double ks = SQUARE ? (double)ka : 1.0;
     double fa[TILES];
 #pragma unroll
     for (int t = 0; t < TILES; ++t) {
         const int64_t ca = c0 + t * kTile + a;
-        fa[t] = freq[ca < nf ? ca : nf - 1];
+        fa[t] = freq[ca < nf ? ca : nf - 1] * ks;
     }
-    const double gb = (double)(32 * a) * delta;
-    const double c2 = TWOD ? c2row[frow] : 0.0;
+    const double gb = (double)(32 * a) * delta * ks;
+    const double c2 = TWOD ? c2row[frow] * ks : 0.0;
     const int64_t split = blockIdx.y;
     const int64_t i0 = split * chunk;
     const int64_t i1 = i0 + chunk < n ? i0 + chunk : n;
@@ -221,7 +223,7 @@ __global__ __launch_bounds__(256, TILES == 1 ? 2 : 1) void k_search_mfma16(
             double phu[TILES];
 #pragma unroll
             for (int t = 0; t < TILES; ++t) phu[t] = TWOD ? fma(fa[t], d, c2 * d2) : fa[t] * d;
-            mfma16_pair<G, TILES, FIRST>(tab, phu, gb * d, live, k0, re, im);
+            mfma16_pair<G, TILES, SQUARE>(tab, phu, gb * d, live, ka, kb, re, im);
         };
         if (cnt == kMfmaChunk) {
 #pragma unroll
@@ -250,7 +252,7 @@ __global__ __launch_bounds__(256, TILES == 1 ? 2 : 1) void k_search_mfma16(
             if (c < nf && o >= 0 && o < count) {
 #pragma unroll
                 for (int g = 0; g < G; ++g) {
-                    const int comp = 2 * (k0 - 1 + g);
+                    const int comp = 2 * ((g == 0 ? ka : kb) - 1);
                     part[(split * ncomp + comp) * count + o] = Cr[t][g][r];
                     part[(split * ncomp + comp + 1) * count + o] = Ci[t][g][r];
                 }
@@ -259,17 +261,17 @@ __global__ __launch_bounds__(256, TILES == 1 ? 2 : 1) void k_search_mfma16(
 }
 
 template <bool TWOD, int TILES>
-static void launch_mfma16(int G, bool firstk, dim3 grid, hipStream_t s, const double* dt, const double* dt2,
+static void launch_mfma16(int G, bool square, dim3 grid, hipStream_t s, const double* dt, const double* dt2,
                           int64_t n, int64_t chunk, const double* fr, int64_t nf, const double* c2, double delta,
-                          int64_t tf, int64_t nt, int64_t tpr, int64_t first, int64_t count, int k0, int ncomp,
+                          int64_t tf, int64_t nt, int64_t tpr, int64_t first, int64_t count, int ka, int kb, int ncomp,
                           double* part) {
 #define CRIMP_LM16(GG, FF)                                                                                      \
     k_search_mfma16<GG, TWOD, FF, TILES><<<grid, 256, 0, s>>>(dt, dt2, n, chunk, fr, nf, c2, delta, tf, nt, tpr, \
-                                                              first, count, k0, ncomp, part)
+                                                              first, count, ka, kb, ncomp, part)
     if (G == 2) {
-        if (firstk) CRIMP_LM16(2, true); else CRIMP_LM16(2, false);
+        if (square) CRIMP_LM16(2, true); else CRIMP_LM16(2, false);
     } else {
-        if (firstk) CRIMP_LM16(1, true); else CRIMP_LM16(1, false);
+        CRIMP_LM16(1, false);
     }
 #undef CRIMP_LM16
 }

@@ -59,3 +59,10 @@ if [[ $STEPS == *repeat* ]]; then
   stop_on_fault $? repeat_ser
   cat "$OUT/repeat_ser.log"
 fi
+if [[ $STEPS == *h20* ]]; then  # H-test (m = 20) timing, this library vs CRIMP_OLD_LIB (if built)
+  for v in "" ${CRIMP_OLD_LIB:-}; do
+    NHARM=20 NPH=2000000 NTR=1000000 CRIMP_LIB_VARIANT=$v timeout -k 10 200 python3 tools/run_search.py >> "$OUT/h20.log" 2>&1
+    stop_on_fault $? h20
+  done
+  cat "$OUT/h20.log"
+fi
