@@ -45,6 +45,9 @@ class TimingModel(ctypes.Structure):
                 ("wave_ab", (ctypes.c_double * 2) * MAX_WAVE)]
 
 
+SHAPE_SUMS = 4 + 3 * MAX_COMP  # CRIMP_SHAPE_SUMS
+
+
 class Template(ctypes.Structure):
     _fields_ = [("model", ctypes.c_int32), ("ncomp", ctypes.c_int32), ("amp", ctypes.c_double * MAX_COMP),
                 ("loc", ctypes.c_double * MAX_COMP), ("wid", ctypes.c_double * MAX_COMP),
@@ -52,7 +55,7 @@ class Template(ctypes.Structure):
 
 
 EXPORTS = ("crimp_version", "crimp_last_error", "crimp_last_kernel_ms", "crimp_device_count", "crimp_calcphase",
-           "crimp_search", "crimp_toa_points", "crimp_toa_grid", "crimp_toa_fit", "crimp_binphases")
+           "crimp_search", "crimp_toa_points", "crimp_toa_grid", "crimp_toa_fit", "crimp_toa_shape_points", "crimp_binphases")
 
 _lib = None
 _lock = threading.Lock()
@@ -81,6 +84,7 @@ def load(require_device=True):
             L.crimp_toa_points.argtypes = [P, P, i64, ctypes.POINTER(Template), P, P, P, i64, P, u32, P]
             L.crimp_toa_grid.argtypes = [P, P, i64, ctypes.POINTER(Template), P, i64, P, i64, P, P, u32, P]
             L.crimp_toa_fit.argtypes = [P, P, i64, ctypes.POINTER(Template), P, ctypes.c_double, i32, i32, P, u32, P]
+            L.crimp_toa_shape_points.argtypes = [P, P, i64, ctypes.POINTER(Template), P, P, P, P, i64, P, u32, P]
             L.crimp_binphases.argtypes = [P, P, i64, P, i32, P, u32, P]
             for name in EXPORTS:
                 if name not in ("crimp_last_error", "crimp_last_kernel_ms"):

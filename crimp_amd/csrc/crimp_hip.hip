@@ -711,6 +711,7 @@ __global__ __launch_bounds__(256) void k_binphases(const double* __restrict__ x,
 }
 
 #include "toa_fit.h"
+#include "toa_shape.h"
 
 // ============================================================== 6. C-ABI
 static hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
@@ -1177,6 +1178,77 @@ extern "C" int crimp_toa_grid(const double* x, const int64_t* offsets, int64_t n
             std::memcpy(lnsum, rl.data(), L * sizeof(double));
             std::memcpy(hmin, rh.data(), H * sizeof(double));
         }
+    }
+    return finish(s, flags);
+}
+
+extern "C" int crimp_toa_shape_points(const double* x, const int64_t* offsets, int64_t nint, const crimp_template* tpls,
+                                      const double* aux, const int64_t* pt_interval, const double* pt_norm,
+                                      const double* pt_phi, int64_t npts, double* out, uint32_t flags, void* stream) {
+    ARGCHK(nint >= 1 && npts >= 0, "bad sizes");
+    ARGCHK(x != nullptr && offsets != nullptr && tpls != nullptr && pt_interval != nullptr && pt_norm != nullptr &&
+               pt_phi != nullptr && out != nullptr,
+           "null argument");
+    ARGCHK(npts <= 2147483647LL, "too many points");
+    if (npts == 0) return CRIMP_OK;
+    // templates and point intervals are host arrays (checked here); photons, norms, phases and out may be device
+    for (int64_t p = 0; p < npts; ++p) {
+        ARGCHK(tpls[p].ncomp >= 1 && tpls[p].ncomp <= CRIMP_MAX_COMP, "ncomp out of range");
+        ARGCHK(tpls[p].model >= 0 && tpls[p].model <= 2, "unknown template model");
+        ARGCHK(pt_interval[p] >= 0 && pt_interval[p] < nint, "point interval out of range");
+    }
+    std::lock_guard<std::mutex> lk(g_mutex);
+    const bool dev = flags & CRIMP_FLAG_DEVICE_PTRS;
+    hipStream_t s = as_stream(stream);
+    std::vector<int64_t> hoff((size_t)nint + 1);
+    if (dev) {
+        HIPCHK(d2h(s, hoff.data(), offsets, (nint + 1) * sizeof(int64_t)));
+        HIPCHK(hipStreamSynchronize(s));
+    } else {
+        std::memcpy(hoff.data(), offsets, (nint + 1) * sizeof(int64_t));
+    }
+    for (int64_t i = 0; i < nint; ++i) ARGCHK(hoff[i + 1] >= hoff[i] && hoff[i] >= 0, "offsets must be non-decreasing");
+    {
+        Scratch sc(s);
+        const double *dx = nullptr, *dn = nullptr, *dp = nullptr;
+        const int64_t* doff = nullptr;
+        double* dout = nullptr;
+        HIPCHK(stage_in(sc, x, (size_t)hoff[nint], dev, &dx));
+        HIPCHK(stage_in(sc, offsets, (size_t)nint + 1, dev, &doff));
+        HIPCHK(stage_in(sc, pt_norm, (size_t)npts, dev, &dn));
+        HIPCHK(stage_in(sc, pt_phi, (size_t)npts, dev, &dp));
+        HIPCHK(stage_out(sc, out, (size_t)npts * kShapeSums, dev, &dout));
+        crimp_template* dT = nullptr;
+        int64_t* dpi = nullptr;
+        double* daux = nullptr;
+        HIPCHK(sc.alloc(&dT, (size_t)npts));
+        HIPCHK(sc.alloc(&dpi, (size_t)npts));
+        HIPCHK(h2d(dT, tpls, npts * sizeof(crimp_template)));
+        HIPCHK(h2d(dpi, pt_interval, npts * sizeof(int64_t)));
+        if (aux != nullptr) {
+            HIPCHK(sc.alloc(&daux, (size_t)npts * CRIMP_MAX_COMP));
+            HIPCHK(h2d(daux, aux, npts * CRIMP_MAX_COMP * sizeof(double)));
+        }
+        // one launch per run of points sharing a model (the kernel is specialised per model)
+        for (int64_t p0 = 0; p0 < npts;) {
+            int64_t p1 = p0 + 1;
+            while (p1 < npts && tpls[p1].model == tpls[p0].model) ++p1;
+            const unsigned nb = (unsigned)(p1 - p0);
+            const double* da = daux != nullptr ? daux + p0 * CRIMP_MAX_COMP : nullptr;
+            if (tpls[p0].model == CRIMP_MODEL_FOURIER)
+                k_toa_shape<CRIMP_MODEL_FOURIER><<<nb, kShapeBlock, 0, s>>>(dx, doff, dT + p0, da, dpi + p0, dn + p0,
+                                                                            dp + p0, dout + p0 * kShapeSums);
+            else if (tpls[p0].model == CRIMP_MODEL_CAUCHY)
+                k_toa_shape<CRIMP_MODEL_CAUCHY><<<nb, kShapeBlock, 0, s>>>(dx, doff, dT + p0, da, dpi + p0, dn + p0,
+                                                                           dp + p0, dout + p0 * kShapeSums);
+            else
+                k_toa_shape<CRIMP_MODEL_VONMISES><<<nb, kShapeBlock, 0, s>>>(dx, doff, dT + p0, da, dpi + p0, dn + p0,
+                                                                             dp + p0, dout + p0 * kShapeSums);
+            p0 = p1;
+        }
+        HIPCHK(hipGetLastError());
+        HIPCHK(copy_back(s, out, dout, (size_t)npts * kShapeSums, dev));
+        HIPCHK(hipStreamSynchronize(s));
     }
     return finish(s, flags);
 }

@@ -7,8 +7,9 @@ batches on the device (crimp_amd/toafit.py); the loop body keeps the
 reference's order of operations and its text formatting (``str()`` of each value,
 tab-separated, 13 columns, :161-162, :222-226).
 
-Not implemented in this build (raises ``NotImplementedError``):
-``readvaryparam``. ``varyAmps`` runs on the device (crimp_toa_fit).
+``varyAmps`` runs on the device (crimp_toa_fit); ``readvaryparam`` frees the template parameters
+flagged ``vary True`` (crimp_amd/toafit_vary.py, photon sums on the device through
+crimp_toa_shape_points). Not implemented (raises ``NotImplementedError``): the two together.
 """
 import argparse
 import math
@@ -24,6 +25,7 @@ from .periodsearch import PeriodSearch
 from .readPPtemplate import readPPtemplate
 from .timfile import phshiftTotimfile
 from .toafit import ToAFitter
+from .toafit_vary import VaryParamFitter
 
 logger = get_logger(__name__)
 
@@ -43,9 +45,30 @@ class Param:
 
 def defineinitialfitparam(tempModPP, readvaryparam=False):
     """Initial parameters and number of free parameters (measureToAs.py:698-806)."""
-    if readvaryparam:
-        raise NotImplementedError("readvaryparam=True is not implemented in this build")
     model = tempModPP["model"]
+    if readvaryparam:
+        if model not in ("fourier", "vonmises", "cauchy"):
+            raise ValueError("Unknown template model. Only fourier, cauchy, or vonmises are supported")
+        K = len([k for k in tempModPP if k.startswith("amp_")])
+        n0 = tempModPP["norm"]["value"]
+        p = {"norm": Param("norm", n0, tempModPP["norm"]["vary"], n0 / 5, n0 * 5)}
+        nfree = 1 if tempModPP["norm"]["vary"] else 0
+        for k in range(1, K + 1):
+            if model == "fourier":
+                a, ph = tempModPP["amp_%d" % k], tempModPP["ph_%d" % k]
+                p["amp_%d" % k] = Param("amp_%d" % k, a["value"], a["vary"], 0, 1000)
+                p["ph_%d" % k] = Param("ph_%d" % k, ph["value"], ph["vary"], -np.pi, np.pi)
+                nfree += int(bool(a["vary"])) + int(bool(ph["vary"]))
+            else:
+                a, c, w = (tempModPP["%s_%d" % (nm, k)] for nm in ("amp", "cen", "wid"))
+                p["amp_%d" % k] = Param("amp_%d" % k, a["value"], a["vary"], 0, 5 * a["value"])
+                p["cen_%d" % k] = Param("cen_%d" % k, c["value"], c["vary"], -0.6 + c["value"], 0.6 + c["value"], 0.05)
+                p["wid_%d" % k] = Param("wid_%d" % k, w["value"], w["vary"], 0, 30 * np.pi)
+                nfree += int(bool(a["vary"])) + int(bool(c["vary"])) + int(bool(w["vary"]))
+        pb = np.pi if model == "fourier" else 1.5 * np.pi
+        p["phShift"] = Param("phShift", 0, True, -pb, pb, 0.05)
+        p["ampShift"] = Param("ampShift", 1, False, *((0, 100) if model == "fourier" else (-np.inf, np.inf)))
+        return p, nfree
     K = len([k for k in tempModPP if k.startswith("amp_")])
     n0 = tempModPP["norm"]["value"]
     p = {"norm": Param("norm", n0, True, n0 / 100, 500)}
@@ -68,8 +91,8 @@ def defineinitialfitparam(tempModPP, readvaryparam=False):
 
 
 def _check_opts(varyAmps, readvaryparam):
-    if readvaryparam:
-        raise NotImplementedError("readvaryparam=True is not implemented in this build")
+    if readvaryparam and varyAmps:
+        raise NotImplementedError("readvaryparam together with varyAmps is not implemented in this build")
 
 
 def _single(model, tempModPP, phases, exposureInt, phShiftRes, nbrBins, varyAmps, brutemin, readvaryparam,
@@ -78,8 +101,12 @@ def _single(model, tempModPP, phases, exposureInt, phShiftRes, nbrBins, varyAmps
     if str(tempModPP["model"]).lower() != model:
         raise ValueError("template model %s used with measureToA_%s" % (tempModPP["model"], model))
     x = np.ascontiguousarray(np.ravel(phases), dtype=np.float64)
-    fit = ToAFitter(x, np.array([0, x.size]), np.array([float(exposureInt)]), tempModPP, phShiftRes, nbrBins)
-    r = fit.fit(brutemin=brutemin, vary_amps=bool(varyAmps))
+    if readvaryparam:
+        r = VaryParamFitter(x, np.array([0, x.size]), np.array([float(exposureInt)]), tempModPP, phShiftRes,
+                            nbrBins).fit(brutemin=brutemin)
+    else:
+        fit = ToAFitter(x, np.array([0, x.size]), np.array([float(exposureInt)]), tempModPP, phShiftRes, nbrBins)
+        r = fit.fit(brutemin=brutemin, vary_amps=bool(varyAmps))
     if plotLLs or plotPPs:
         logger.warning("plotPPs/plotLLs are diagnostic plots and are not produced by this build")
     return {"phShi": float(r["phShi"][0]), "phShi_LL": float(r["phShi_LL"][0]), "phShi_UL": float(r["phShi_UL"][0]),
@@ -112,7 +139,7 @@ HEADER = ('ToA \t ToA_mid \t ToA_start \t ToA_end \t ToA_lenInt \t ToA_exp \t nb
 
 
 def measure_intervals(TIMEMJD, timMod, tempModPP, starts, ends, exposures, phShiftRes=1000, nbrBins=15, varyAmps=False,
-                      brutemin=False):
+                      brutemin=False, readvaryparam=False):
     """Batched core of measureToAs on in-memory arrays: per interval ToA_mid, fit dict entries, H power."""
     tmpl = readPPtemplate(tempModPP) if isinstance(tempModPP, str) else tempModPP
     model = str(tmpl["model"]).lower()
@@ -126,8 +153,12 @@ def measure_intervals(TIMEMJD, timMod, tempModPP, starts, ends, exposures, phShi
     _, folded = calcphase(allt, timMod)
     if model in ("cauchy", "vonmises"):
         folded = folded * (2 * np.pi)                  # :195, :200
-    fit = ToAFitter(folded, np.array(offs), np.asarray(exposures, dtype=np.float64), tmpl, phShiftRes, nbrBins)
-    res = fit.fit(brutemin=brutemin, vary_amps=bool(varyAmps))
+    if readvaryparam:
+        res = VaryParamFitter(folded, np.array(offs), np.asarray(exposures, dtype=np.float64), tmpl, phShiftRes,
+                              nbrBins).fit(brutemin=brutemin)
+    else:
+        fit = ToAFitter(folded, np.array(offs), np.asarray(exposures, dtype=np.float64), tmpl, phShiftRes, nbrBins)
+        res = fit.fit(brutemin=brutemin, vary_amps=bool(varyAmps))
     hp = []
     for t, mid in zip(sel, mids):
         eph = ephemTmjd(mid, timMod)
@@ -160,7 +191,7 @@ def measureToAs(evtFile, timMod, tempModPP, toagtifile, eneLow=0.5, eneHigh=10.,
     for ii in rng:
         print('ToA {}'.format(ii))
     res = measure_intervals(TIMEMJD, timMod, tmpl, st[rng], en[rng], expo[rng], phShiftRes, nbrBins, varyAmps,
-                            brutemin)
+                            brutemin, readvaryparam)
     with open(toaFile + '.txt', "w+") as f:
         f.write(HEADER)
         for k, ii in enumerate(rng):

@@ -144,6 +144,35 @@ def toa_points(x, offsets, tpl, pt_interval, pt_norm, pt_phi):
     return out.reshape(npts, 8)
 
 
+def toa_shape_points(x, offsets, tpls, pt_interval, pt_norm, pt_phi, aux=None):
+    """[npts, CRIMP_SHAPE_SUMS] extended-LL sums with template-shape gradients (crimp_toa_shape_points):
+    point p = interval pt_interval[p] with its own template tpls[p]; aux[p, j] = I1/I0(1/wid_j^2) for
+    von Mises templates. Templates, intervals and aux are host data; pt_norm/pt_phi follow x."""
+    L = N.load()
+    b = N.Buffers()
+    xp = b.arg(x, np.float64)
+    op = b.arg(offsets, np.int64)
+    npts = len(tpls)
+    arr = (N.Template * max(npts, 1))(*tpls)
+    pint = np.ascontiguousarray(pt_interval, dtype=np.int64)
+    if pint.size != npts:
+        raise ValueError("one interval per point")
+    if b.device:
+        import torch
+        pt_norm = torch.as_tensor(np.asarray(pt_norm, np.float64), device=x.device)
+        pt_phi = torch.as_tensor(np.asarray(pt_phi, np.float64), device=x.device)
+    npp = b.arg(pt_norm, np.float64)
+    pp = b.arg(pt_phi, np.float64)
+    auxa = None if aux is None else np.ascontiguousarray(aux, dtype=np.float64).reshape(npts, N.MAX_COMP)
+    nint = int((offsets.numel() if N._is_torch(offsets) else np.size(offsets)) - 1)
+    out = _empty_like_input(x, npts * N.SHAPE_SUMS, b)
+    outp = b.arg(out, np.float64, writable=True)
+    N.check(L.crimp_toa_shape_points(xp, op, nint, arr, None if auxa is None else auxa.ctypes.data,
+                                     pint.ctypes.data, npp, pp, npts, outp, b.flags(), b.stream()))
+    out = out.cpu().numpy() if N._is_torch(out) else out
+    return out.reshape(npts, N.SHAPE_SUMS)
+
+
 def toa_grid(x, offsets, tpl, norms, phis):
     """lnsum [nint, nnorm, nphi], hmin [nint, nphi] of the brute grid (fp64 accumulation)."""
     L = N.load()

@@ -136,6 +136,19 @@ int crimp_toa_fit(const double* x, const int64_t* offsets, int64_t nint, const c
                   const double* exposure, double norm0, int32_t ph_shift_res, int32_t options, double* out,
                   uint32_t flags, void* stream);
 
+/* Extended-LL sums with template-shape gradients, for fits that free template parameters
+ * (readvaryparam, measureToAs.py:727-801 with the likelihoods of templatemodels.py:98-121, 201-226,
+ * 306-329). Point p is interval pt_interval[p] with its own template tpls[p] (ampShift applied),
+ * norm pt_norm[p] and phShift pt_phi[p]; aux[p*CRIMP_MAX_COMP + j] = I1(k)/I0(k), k = 1/wid_j^2
+ * (vonmises; may be NULL otherwise). With m = norm + h the model at a photon:
+ * out[p*CRIMP_SHAPE_SUMS + ...] = { sum ln m, min m, sum 1/m, sum (dh/dphShift)/m,
+ *     then for j < CRIMP_MAX_COMP: sum (dh/damp_j)/m, sum (dh/dloc_j)/m, sum (dh/dwid_j)/m }
+ * (loc = ph_j or cen_j; unused components and the Fourier wid terms are 0). fp64. */
+#define CRIMP_SHAPE_SUMS (4 + 3 * CRIMP_MAX_COMP)
+int crimp_toa_shape_points(const double* x, const int64_t* offsets, int64_t nint, const crimp_template* tpls,
+                           const double* aux, const int64_t* pt_interval, const double* pt_norm,
+                           const double* pt_phi, int64_t npts, double* out, uint32_t flags, void* stream);
+
 /* binphases(phases, nbrBins) counts per interval   [binphases.py:9-39]:
  * np.histogram(x, bins=edges) semantics with edges[nbins+1] (numpy.linspace). counts[i*nbins+b]. */
 int crimp_binphases(const double* x, const int64_t* offsets, int64_t nint, const double* edges, int32_t nbins,

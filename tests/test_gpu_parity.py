@@ -347,3 +347,114 @@ def test_measuretoas_end_to_end(gpu, tmp_path):
     np.testing.assert_allclose(tab["Hpower"].to_numpy(), g["h5"], rtol=1e-6)
     lines = open(out + ".txt").read().splitlines()
     assert lines[0] == open(gpath("ToAs_2259.txt")).read().splitlines()[0]
+
+
+def _vary_template(base, free):
+    t = {k: (dict(v) if isinstance(v, dict) else v) for k, v in base.items()}
+    for k, v in t.items():
+        if isinstance(v, dict):
+            v["vary"] = k in free
+    return t
+
+
+# two-component peaked templates of the bundled 1-5 keV profile (Cauchy: the 70-bin fit of
+# crimp_amd.pulseprofile, rates in counts/s; von Mises: the same peaks with wid 0.25)
+PEAKED = {"cauchy": {"norm": 15.864028670406764, "amp_1": 2.729162017889153, "cen_1": 3.9150528740296684,
+                     "wid_1": 0.15062796589359873, "amp_2": 1.3486800419057134, "cen_2": 3.418941216972105,
+                     "wid_2": 0.13877334840312794},
+          "vonmises": {"norm": 15.86, "amp_1": 2.73, "cen_1": 3.915, "wid_1": 0.25, "amp_2": 1.35, "cen_2": 3.419,
+                       "wid_2": 0.25}}
+
+
+def _cauchy_vm_template(model, th=None):
+    th = th or PEAKED[model]
+    t = {"model": model, "nbrComp": 2}
+    for k, v in th.items():
+        if k not in ("phShift", "ampShift"):
+            t[k] = {"value": np.float64(v), "vary": False}
+    return t
+
+
+@pytest.mark.parametrize("model", ["fourier", "cauchy", "vonmises"])
+def test_shape_gradient_sums_vs_oracle(gpu, model):
+    """crimp_toa_shape_points: the extended LL and its gradient in every template parameter against the
+    oracle's NumPy LL and central differences of it."""
+    from crimp_amd.readPPtemplate import readPPtemplate
+    from crimp_amd.toafit_vary import VaryParamFitter
+    g, iv, _ = _golden_rows()
+    x = g["folded"][g["offsets"][2]:g["offsets"][3]]
+    E = float(iv["ToA_exposure"].to_numpy()[g["ids"]][2])
+    if model == "fourier":
+        tm = readPPtemplate(gpath("1e2259_template.txt"))
+    else:
+        tm = _cauchy_vm_template(model, json.load(open(gpath("cauchy_vm_theta.json"))))
+        x = x * 2 * np.pi
+    f = VaryParamFitter(x, np.array([0, x.size]), np.array([E]), tm)
+    rng = np.random.default_rng(3)
+    th = f.theta0.copy()
+    th[-1] = 0.07
+    th[1:-1] *= 1 + 0.05 * rng.standard_normal(th.size - 2)
+    ll, gr = f.evaluate_theta([0], th[None, :])
+    _, K, _, _, _, _, _, _ = O._readvary_setup(tm)
+    ref = O.readvary_ll(x, E, model, K, th)
+    assert ll[0] == pytest.approx(ref, rel=1e-12)
+    for j in range(th.size):
+        h = 1e-5 * max(1.0, abs(th[j]))
+        tp, tm_ = th.copy(), th.copy()
+        tp[j] += h
+        tm_[j] -= h
+        fd = (O.readvary_ll(x, E, model, K, tp) - O.readvary_ll(x, E, model, K, tm_)) / (2 * h)
+        assert gr[0, j] == pytest.approx(fd, rel=2e-5, abs=1e-3), (model, f.names[j])
+
+
+def test_readvaryparam_vs_oracle(gpu):
+    """readvaryparam (measureToAs.py:727-801): template amplitudes 1-2 freed with the norm. No reference
+    output exercises it (parity unpinned beyond the oracle's optimum restatement); with only the norm
+    free it must reproduce the default fit."""
+    from crimp_amd.measureToAs import measureToA_fourier, defineinitialfitparam
+    from crimp_amd.readPPtemplate import readPPtemplate
+    from crimp_amd.toafit import ToAFitter
+    from crimp_amd.toafit_vary import VaryParamFitter
+    g, iv, _ = _golden_rows()
+    base = readPPtemplate(gpath("1e2259_template.txt"))
+    E = iv["ToA_exposure"].to_numpy()[g["ids"]]
+    tm = _vary_template(base, {"norm", "amp_1", "amp_2"})
+    assert defineinitialfitparam(tm, readvaryparam=True)[1] == 3
+    r = VaryParamFitter(g["folded"], g["offsets"], E, tm).fit()
+    for i in (2, 5):
+        x = g["folded"][g["offsets"][i]:g["offsets"][i + 1]]
+        o = O.fit_toa_readvary(x, E[i], tm)
+        assert abs(r["phShi"][i] - o["phShi"]) / (2 * math.pi) < 1e-6
+        assert r["LLmax"][i] == pytest.approx(o["LLmax"], abs=1e-5)
+        assert r["phShi_LL"][i] == o["phShi_LL"] and r["phShi_UL"][i] == o["phShi_UL"]
+        assert r["LLmax"][i] >= o["LLmax"] - 1e-6
+        # the LL is flat to 1e-7 along the freed amplitudes within 1e-3 sigma: two optimisers agree to ~1e-5
+        assert r["reducedChi2"][i] == pytest.approx(o["reducedChi2"], rel=1e-4)
+        np.testing.assert_allclose(r["theta"][i], o["theta"], rtol=1e-4, atol=1e-6)
+    s = measureToA_fourier(tm, g["folded"][g["offsets"][2]:g["offsets"][3]], E[2], readvaryparam=True)
+    assert s["phShi"] == pytest.approx(r["phShi"][2], abs=1e-9)
+    # only the norm free: the default fit's optimum (its norm bounds are not active here)
+    tn = _vary_template(base, {"norm"})
+    rn = VaryParamFitter(g["folded"], g["offsets"], E, tn).fit()
+    rd = ToAFitter(g["folded"], g["offsets"], E, base).fit()
+    np.testing.assert_allclose(rn["phShi"], rd["phShi"], rtol=0, atol=2 * math.pi * 1e-7)
+    np.testing.assert_array_equal(rn["phShi_LL"], rd["phShi_LL"])
+    np.testing.assert_array_equal(rn["phShi_UL"], rd["phShi_UL"])
+    np.testing.assert_allclose(rn["LLmax"], rd["LLmax"], rtol=0, atol=1e-6)
+
+
+@pytest.mark.parametrize("model", ["cauchy", "vonmises"])
+def test_readvaryparam_peaked_vs_oracle(gpu, model):
+    from crimp_amd.toafit_vary import VaryParamFitter
+    g, iv, _ = _golden_rows()
+    i = 2
+    x = g["folded"][g["offsets"][i]:g["offsets"][i + 1]] * 2 * np.pi
+    E = float(iv["ToA_exposure"].to_numpy()[g["ids"]][i])
+    tm = _vary_template(_cauchy_vm_template(model), {"norm", "cen_1", "wid_2" if model == "cauchy" else "amp_2"})
+    r = VaryParamFitter(x, np.array([0, x.size]), np.array([E]), tm).fit()
+    o = O.fit_toa_readvary(x, E, tm)
+    assert abs(r["phShi"][0] - o["phShi"]) / (2 * math.pi) < 1e-6
+    assert r["LLmax"][0] == pytest.approx(o["LLmax"], abs=1e-5)
+    assert r["phShi_LL"][0] == o["phShi_LL"] and r["phShi_UL"][0] == o["phShi_UL"]
+    assert r["LLmax"][0] >= o["LLmax"] - 1e-6
+    np.testing.assert_allclose(r["theta"][0], o["theta"], rtol=1e-4, atol=1e-6)

@@ -1,0 +1,61 @@
+"""readvaryparam host logic and its oracle (measureToAs.py:727-801). The oracle's readvaryparam fit is
+pinned through the default fit: with only the norm free it must land on fit_toa's optimum, which
+tests/test_oracle_golden.py pins to data/ToAs_2259.txt."""
+import math
+
+import numpy as np
+import pandas as pd
+import pytest
+
+from conftest import gold, gpath
+from crimp_amd.measureToAs import defineinitialfitparam, measureToA_fourier
+from crimp_amd.readPPtemplate import readPPtemplate
+from oracle import oracle as O
+
+
+def _with_vary(t, free):
+    t = {k: (dict(v) if isinstance(v, dict) else v) for k, v in t.items()}
+    for k, v in t.items():
+        if isinstance(v, dict):
+            v["vary"] = k in free
+    return t
+
+
+def test_defineinitialfitparam_readvaryparam():
+    t = _with_vary(readPPtemplate(gpath("1e2259_template.txt")), {"norm", "amp_1", "ph_3"})
+    p, nfree = defineinitialfitparam(t, readvaryparam=True)
+    assert nfree == 3                                   # norm + amp_1 + ph_3; phShift not counted (:733-748)
+    n0 = float(t["norm"]["value"])
+    assert (p["norm"].min, p["norm"].max, p["norm"].vary) == (n0 / 5, n0 * 5, True)
+    assert (p["amp_1"].min, p["amp_1"].max, p["amp_1"].vary) == (0, 1000, True)
+    assert (p["amp_2"].vary, p["ph_3"].vary, p["ph_3"].min, p["ph_3"].max) == (False, True, -np.pi, np.pi)
+    assert (p["phShift"].min, p["phShift"].max, p["phShift"].vary) == (-np.pi, np.pi, True)
+    c = {"model": "cauchy", "norm": {"value": 2.0, "vary": False}, "amp_1": {"value": 3.0, "vary": True},
+         "cen_1": {"value": 1.0, "vary": True}, "wid_1": {"value": 0.2, "vary": False}}
+    p, nfree = defineinitialfitparam(c, readvaryparam=True)
+    assert nfree == 2 and not p["norm"].vary
+    assert (p["amp_1"].min, p["amp_1"].max) == (0, 15.0)
+    assert p["cen_1"].min == pytest.approx(0.4) and p["cen_1"].max == pytest.approx(1.6)
+    assert (p["wid_1"].min, p["wid_1"].max) == (0, 30 * np.pi)
+    assert (p["phShift"].min, p["phShift"].max) == (-1.5 * np.pi, 1.5 * np.pi)
+
+
+def test_readvary_with_varyamps_is_rejected():
+    t = readPPtemplate(gpath("1e2259_template.txt"))
+    with pytest.raises(NotImplementedError):
+        measureToA_fourier(t, np.array([0.1, 0.2]), 10.0, varyAmps=True, readvaryparam=True)
+
+
+def test_oracle_readvary_norm_only_is_the_default_fit():
+    g = gold("toa_1e2259.npz")
+    iv = pd.read_csv(gpath("timIntToAs_1e2259.txt"), sep=r"\s+", comment="#")
+    E = iv["ToA_exposure"].to_numpy()[g["ids"]]
+    base = readPPtemplate(gpath("1e2259_template.txt"))
+    i = 2
+    x = g["folded"][g["offsets"][i]:g["offsets"][i + 1]]
+    o = O.fit_toa_readvary(x, E[i], _with_vary(base, {"norm"}))
+    d = O.fit_toa(x, E[i], base)
+    assert abs(o["phShi"] - d["phShi"]) / (2 * math.pi) < 1e-7
+    assert o["LLmax"] == pytest.approx(d["LLmax"], abs=1e-6)
+    assert (o["phShi_LL"], o["phShi_UL"]) == (d["phShi_LL"], d["phShi_UL"])
+    assert o["reducedChi2"] * 14 == pytest.approx(d["reducedChi2"] * 13, rel=1e-6)  # dof 15-1 vs 15-2

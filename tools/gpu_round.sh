@@ -13,7 +13,7 @@ stop_on_fault() {  # rc 0 ok, 1 = test failures (not a fault); anything else: st
 }
 STEPS=${STEPS:-tests,smoke,bench,prof}
 if [[ $STEPS == *tests* ]]; then
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -rs --timeout 120 --timeout-method thread ${PYTEST_ARGS:-} > "$OUT/pytest_gpu.log" 2>&1
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -rs --timeout 120 --timeout-method thread ${PYTEST_ARGS:-} ${PYTEST_K:+-k "$PYTEST_K"} > "$OUT/pytest_gpu.log" 2>&1
   stop_on_fault $? pytest
   tail -5 "$OUT/pytest_gpu.log"
 fi
