@@ -24,6 +24,7 @@ FLAG_HW_SINCOS = 16
 FLAG_MFMA_F32 = 32
 FLAG_MFMA_T2 = 64
 FLAG_TIME_KERNELS = 128
+FLAG_F64 = 256
 
 STAT_Z2 = 0
 STAT_H = 1

@@ -375,6 +375,66 @@ __global__ __launch_bounds__(kSearchBlock) void k_search_direct(
     }
 }
 
+// fp64 kernel (CRIMP_FLAG_F64): the reference's arithmetic precision end to end. One lane per trial,
+// photons broadcast as in k_search_direct; fp64 phase reduced to a centred fractional cycle r, fp64
+// sincospi(2r) for harmonic k0 of the group, harmonics k0+1 .. k0+G-1 by fp64 angle addition, fp64 sums.
+// Every term differs from np.cos(2*k*pi*f*(t-t0)) (periodsearch.py:64-65) by the fp64 rounding of the
+// phase argument only (~1e-9 rad at 1e7 cycles), so powers agree with the reference to ~1e-9 relative
+// on every trial, including near-zero noise bins that the fp32 sin/cos paths resolve only to 1e-6 of the
+// grid's mean power.
+template <int G, bool TWOD>
+__global__ __launch_bounds__(kSearchBlock) void k_search_f64(
+    const double* __restrict__ dt, const double* __restrict__ dt2, int64_t n, int64_t chunk,
+    const double* __restrict__ freq, int64_t nf, const double* __restrict__ c2row, int64_t first, int64_t count,
+    int k0, int ncomp, double* __restrict__ part) {
+    const int64_t t = (int64_t)blockIdx.x * kSearchBlock + threadIdx.x;
+    const int64_t split = blockIdx.y;
+    const int64_t tt = t < count ? t : count - 1;
+    const int64_t g = first + tt;
+    const int64_t row = TWOD ? g / nf : 0;
+    const double f = freq[g - row * nf];
+    const double c2 = TWOD ? c2row[row] : 0.0;
+    const double kf = (double)k0;
+    const int64_t i0 = split * chunk;
+    const int64_t i1 = i0 + chunk < n ? i0 + chunk : n;
+    double C[G], S[G];
+#pragma unroll
+    for (int k = 0; k < G; ++k) C[k] = S[k] = 0.0;
+#pragma unroll 2
+    for (int64_t i = i0; i < i1; ++i) {
+        const double d = dt[i];
+        const double ph = TWOD ? fma(f, d, c2 * dt2[i]) : f * d;
+        double s1 = 0.0, c1 = 1.0, s, c;
+        if (G > 1) sincospi(2.0 * (ph - rint(ph)), &s1, &c1);
+        if (k0 == 1 && G > 1) {
+            s = s1;
+            c = c1;
+        } else {
+            const double pk = ph * kf;
+            sincospi(2.0 * (pk - rint(pk)), &s, &c);
+        }
+        C[0] += c;
+        S[0] += s;
+#pragma unroll
+        for (int k = 1; k < G; ++k) {
+            const double cn = fma(c, c1, -s * s1);
+            const double sn = fma(s, c1, c * s1);
+            c = cn;
+            s = sn;
+            C[k] += c;
+            S[k] += s;
+        }
+    }
+    if (t < count) {
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+            const int comp = 2 * (k0 - 1 + k);
+            part[(split * ncomp + comp) * count + t] = C[k];
+            part[(split * ncomp + comp + 1) * count + t] = S[k];
+        }
+    }
+}
+
 // Z^2 = (2/n) sum_k (C_k^2 + S_k^2)            (periodsearch.py:66-69)
 // H   = max_k (cumsum_k[(C^2+S^2)(2/n)] - 4(k-1)) (periodsearch.py:118-123)
 __global__ __launch_bounds__(256) void k_search_finalize(const double* __restrict__ part, int64_t count, int splits,
@@ -804,6 +864,16 @@ static void launch_direct(int G, bool firstk, dim3 grid, hipStream_t s, const do
 #undef CRIMP_LD
 }
 
+template <bool TWOD>
+static void launch_f64(int G, dim3 grid, hipStream_t s, const double* dt, const double* dt2, int64_t n, int64_t chunk,
+                       const double* fr, int64_t nf, const double* c2, int64_t first, int64_t count, int k0, int ncomp,
+                       double* part) {
+#define CRIMP_LF(GG) \
+    k_search_f64<GG, TWOD><<<grid, kSearchBlock, 0, s>>>(dt, dt2, n, chunk, fr, nf, c2, first, count, k0, ncomp, part)
+    if (G == 8) CRIMP_LF(8); else if (G == 4) CRIMP_LF(4); else if (G == 2) CRIMP_LF(2); else CRIMP_LF(1);
+#undef CRIMP_LF
+}
+
 // Harmonic groups of the direct kernel. Inside a group harmonics come from the group's first
 // harmonic (exact fp64 phase) by angle addition with the fundamental. The fp32 sin/cos error is
 // periodic in the quarter turn, so a harmonic k = 0 (mod 4) reached by angle addition from the
@@ -859,12 +929,14 @@ extern "C" int crimp_search(const double* t, int64_t n, double t0, const double*
         HIPCHK(hipGetLastError());
 
         int rc = -1;
-        if (!(flags & CRIMP_FLAG_FORCE_DIRECT)) {
+        const bool f64 = flags & CRIMP_FLAG_F64;
+        if (!(flags & CRIMP_FLAG_FORCE_DIRECT) && !f64) {
             rc = mfma_search(sc, s, ddt, ddt2, n, dfr, nf, dc2, twod, nharm, stat, first, count, dout, flags);
             if (rc < 0) return rc;  // error already recorded
         }
         if (rc != 1) {  // factorised path declined (grid not an arithmetic progression, too small, ...)
-            if (flags & CRIMP_FLAG_FORCE_MFMA) return set_err(CRIMP_ERR_ARG, "factorised search not applicable");
+            if ((flags & CRIMP_FLAG_FORCE_MFMA) && !f64)
+                return set_err(CRIMP_ERR_ARG, "factorised search not applicable");
             const int64_t tblocks = cdiv(count, kSearchBlock);
             int64_t splits = std::max<int64_t>(1, std::min<int64_t>(cdiv(2048, tblocks), cdiv(n, 2048)));
             int64_t chunk = cdiv(cdiv(n, splits), kSearchFold) * kSearchFold;
@@ -877,6 +949,14 @@ extern "C" int crimp_search(const double* t, int64_t n, double t0, const double*
             int k0 = 1;
             KernelTimer kt(s, flags & CRIMP_FLAG_TIME_KERNELS);
             kt.start();
+            while (k0 <= nharm && f64) {  // groups of 8, 4, 2, 1 harmonics, each started from its exact phase
+                const int rem = nharm - k0 + 1;
+                const int G = rem >= 8 ? 8 : rem >= 4 ? 4 : rem >= 2 ? 2 : 1;
+                if (twod) launch_f64<true>(G, grid, s, ddt, ddt2, n, chunk, dfr, nf, dc2, first, count, k0, ncomp, part);
+                else launch_f64<false>(G, grid, s, ddt, ddt2, n, chunk, dfr, nf, dc2, first, count, k0, ncomp, part);
+                HIPCHK(hipGetLastError());
+                k0 += G;
+            }
             while (k0 <= nharm) {
                 const int G = direct_group(k0, nharm);
                 if (twod) {

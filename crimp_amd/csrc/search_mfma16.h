@@ -7,9 +7,11 @@
 // exact products hi.hi + hi.lo + lo.hi + lo.lo of each real product fill the K = 16 of one
 // v_mfma_f32_32x32x16_f16 together with the complex structure:
 //   lane (a, h) holds the 8 K-values of photon 2q+h;
-//   A (U side, shared by both MFMAs) = [uc_h uc_h | uc_l uc_l | us_h us_h | us_l us_l]
-//   B_im = [vs_h vs_l | vs_h vs_l | vc_h vc_l | vc_h vc_l]      -> Im += uc.vs + us.vc
-//   B_re = [vc_h vc_l | vc_h vc_l | -vs_h -vs_l | -vs_h -vs_l]  -> Re += uc.vc - us.vs
+//   A (U side, shared by both MFMAs) = [uc_h us_h | uc_l us_l | uc_l us_l | uc_h us_h]
+//   B_re = [vc_h -vs_h | vc_l -vs_l | vc_h -vs_h | vc_l -vs_l]  -> Re += uc.vc - us.vs
+//   B_im = [vs_h  vc_h | vs_l  vc_l | vs_h  vc_h | vs_l  vc_l]  -> Im += uc.vs + us.vc
+//   (every K pair is one dword, so A costs one conversion and two fma_mix; CRIMP_SPLIT_DUP builds the
+//   earlier [uc_h uc_h | uc_l uc_l | ...] layout)
 // so one photon pair and harmonic costs two 32-cycle MFMAs (the f32-input form needs four 64-cycle
 // ones), the products are exact in the fp32 accumulator, and the result matches the f32 path.
 //
@@ -64,6 +66,26 @@ __device__ __forceinline__ uint32_t split_b(float x) {
     return d;
 }
 
+// Two values at once: hi = (RN(x), RN(y)) in one conversion, lo = (RN(x - hi.x), RN(y - hi.y)); NEGY splits -y
+// (the sign rides on the instructions' source modifiers, no extra negation).
+template <bool NEGY>
+__device__ __forceinline__ void split_xy(float x, float y, uint32_t& dh, uint32_t& dl) {
+    if (NEGY)
+        asm volatile(
+            "v_cvt_pk_f16_f32 %0, %2, -%3\n\t"
+            "v_fma_mixlo_f16 %1, %2, 1.0, -%0 op_sel_hi:[0,0,1]\n\t"
+            "v_fma_mixhi_f16 %1, -%3, 1.0, -%0 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+            : "=&v"(dh), "=&v"(dl)
+            : "v"(x), "v"(y));
+    else
+        asm volatile(
+            "v_cvt_pk_f16_f32 %0, %2, %3\n\t"
+            "v_fma_mixlo_f16 %1, %2, 1.0, -%0 op_sel_hi:[0,0,1]\n\t"
+            "v_fma_mixhi_f16 %1, %3, 1.0, -%0 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+            : "=&v"(dh), "=&v"(dl)
+            : "v"(x), "v"(y));
+}
+
 struct AFrag {
     f16x8 v;
 };
@@ -71,6 +93,8 @@ struct BFrag {
     f16x8 re, im;
 };
 
+#ifdef CRIMP_SPLIT_DUP
+// previous layout: A = [uc_h uc_h | uc_l uc_l | us_h us_h | us_l us_l] (6 instructions for A, 5 for B)
 __device__ __forceinline__ AFrag make_a(float uc, float us) {
     uint32_t ch, cl, sh, sl;
     split_aa(uc, ch, cl);
@@ -81,6 +105,30 @@ __device__ __forceinline__ BFrag make_b(float vc, float vs) {
     const uint32_t bc = split_b(vc), bs = split_b(vs), bn = bs ^ 0x80008000u;
     return BFrag{__builtin_bit_cast(f16x8, u32x4{bc, bc, bn, bn}), __builtin_bit_cast(f16x8, u32x4{bs, bs, bc, bc})};
 }
+#else
+// Interleaved layout (3 instructions for A, 5 for B; A is built once per tile and harmonic, B once per photon pair).
+// Dwords h = (uc_h, us_h), l = (uc_l, us_l), e_h = (vc_h, -vs_h), e_l = (vc_l, -vs_l), f_h = (vs_h, vc_h), f_l = (vs_l, vc_l):
+//   A    = [h | l | l | h]
+//   B_re = [e_h | e_l | e_h | e_l]   -> Re += uc.vc - us.vs (the four hi/lo products h.e_h, l.e_l, l.e_h, h.e_l)
+//   B_im = [f_h | f_l | f_h | f_l]   -> Im += uc.vs + us.vc
+__device__ __forceinline__ AFrag make_a(float uc, float us) {
+    uint32_t h, l;
+    split_xy<false>(uc, us, h, l);
+    return AFrag{__builtin_bit_cast(f16x8, u32x4{h, l, l, h})};
+}
+// (a, -b) -> (b, a) in one packed multiply by (1, 1): halves swapped by op_sel, the sign by neg_lo (exact)
+__device__ __forceinline__ uint32_t swap_neg_lo(uint32_t e) {
+    uint32_t d;
+    asm volatile("v_pk_mul_f16 %0, %1, %2 op_sel:[1,0] op_sel_hi:[0,1] neg_lo:[1,0]" : "=v"(d) : "v"(e), "v"(0x3C003C00u));
+    return d;
+}
+__device__ __forceinline__ BFrag make_b(float vc, float vs) {
+    uint32_t eh, el;
+    split_xy<true>(vc, vs, eh, el);
+    const uint32_t fh = swap_neg_lo(eh), fl = swap_neg_lo(el);
+    return BFrag{__builtin_bit_cast(f16x8, u32x4{eh, el, eh, el}), __builtin_bit_cast(f16x8, u32x4{fh, fl, fh, fl})};
+}
+#endif
 
 __device__ __forceinline__ void mma(const AFrag& A, const BFrag& B, f32x16& re, f32x16& im) {
     re = __builtin_amdgcn_mfma_f32_32x32x16_f16(A.v, B.re, re, 0, 0, 0);

@@ -69,8 +69,11 @@ def _empty_like_input(a, n, b, dtype=np.float64):
 
 
 def search_flags():
-    """Extra search flags from the environment (CRIMP_SEARCH=direct|mfma, CRIMP_SINCOS=hw, CRIMP_MFMA=f32|t2)."""
+    """Extra search flags from the environment (CRIMP_SEARCH=direct|mfma, CRIMP_SINCOS=hw, CRIMP_MFMA=f32|t2,
+    CRIMP_PRECISION=f64)."""
     f = 0
+    if os.environ.get("CRIMP_PRECISION", "").lower() == "f64":
+        f |= N.FLAG_F64
     mode = os.environ.get("CRIMP_SEARCH", "").lower()
     if mode == "direct":
         f |= N.FLAG_FORCE_DIRECT
@@ -86,8 +89,14 @@ def search_flags():
     return f
 
 
-def search(t, t0, freq, nharm, stat, log10_negfdot=None, first=0, count=None, out=None, flags=0):
-    """Z^2 / H over the fd-outer grid; computes flat trials [first, first+count)."""
+def search(t, t0, freq, nharm, stat, log10_negfdot=None, first=0, count=None, out=None, flags=0, precision=None):
+    """Z^2 / H over the fd-outer grid; computes flat trials [first, first+count).
+    ``precision``: None/"fast" (fp32 sin/cos, fp32-exact MFMA products, fp64 phases and sums) or "f64"
+    (fp64 throughout, k_search_f64: the reference's precision on every trial, several times slower)."""
+    if precision not in (None, "fast", "f64"):
+        raise ValueError("precision must be None, 'fast' or 'f64'")
+    if precision == "f64":
+        flags |= N.FLAG_F64
     L = N.load()
     b = N.Buffers()
     tp = b.arg(t, np.float64)

@@ -19,10 +19,15 @@ from ._native import STAT_H, STAT_Z2, _is_torch
 
 
 class PeriodSearch:
-    def __init__(self, time, freq, nbrHarm: int = 2):
+    """``precision`` (keyword, not in the reference): None/"fast" is the default MFMA/fp32-sin-cos path
+    (within 1e-6 of the grid's power scale); "f64" evaluates every term in fp64 like the reference
+    (within ~1e-9 relative on every trial, including near-zero bins)."""
+
+    def __init__(self, time, freq, nbrHarm: int = 2, *, precision=None):
         self.time = time
         self.freq = freq
         self.nbrHarm = nbrHarm
+        self.precision = precision
         if _is_torch(time):
             self.t0 = float((time[0] + time[-1]).item()) / 2
         else:
@@ -52,7 +57,7 @@ class PeriodSearch:
         if fd is not None and _is_torch(t):
             import torch
             fd = torch.as_tensor(fd, device=t.device)
-        return ops.search(t, self.t0, f, m, stat, log10_negfdot=fd)
+        return ops.search(t, self.t0, f, m, stat, log10_negfdot=fd, precision=self.precision)
 
     def ztest(self):
         """Z^2_m power at each frequency (periodsearch.py:57-71)."""

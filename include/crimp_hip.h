@@ -41,6 +41,7 @@ extern "C" {
 #define CRIMP_FLAG_MFMA_F32 32u    /* factorised search: f32-input MFMA instead of the f16 hi/lo split */
 #define CRIMP_FLAG_MFMA_T2 64u     /* factorised f16 search: two tiles per wave sharing V (one wave/SIMD) */
 #define CRIMP_FLAG_TIME_KERNELS 128u /* search: time the harmonic-sum kernels with hipEvents (crimp_last_kernel_ms) */
+#define CRIMP_FLAG_F64 256u         /* search: fp64 sin/cos and sums (reference precision on every trial; slower) */
 
 #define CRIMP_STAT_Z2 0 /* Z^2_m  (periodsearch.py:57-71, :73-106) */
 #define CRIMP_STAT_H 1  /* H-test (periodsearch.py:109-125)         */

@@ -36,6 +36,27 @@ def test_hot_path_fails_loudly_without_gpu():
         PeriodSearch(np.arange(10.0), np.array([0.1]), 2).ztest()
 
 
+def test_header_flags_match_python_bindings():
+    from crimp_amd import _native
+    src = open(os.path.join(ROOT, "include", "crimp_hip.h")).read()
+    flags = dict(re.findall(r"#define CRIMP_(FLAG_\w+)\s+(\d+)u", src))
+    assert "FLAG_F64" in flags
+    for name, val in flags.items():
+        assert getattr(_native, name) == int(val), name
+
+
+def test_search_precision_option_validated_and_no_fallback():
+    import torch
+    from crimp_amd import _native
+    from crimp_amd.periodsearch import PeriodSearch
+    with pytest.raises(ValueError):
+        PeriodSearch(np.arange(10.0), np.array([0.1]), 2, precision="f16").ztest()
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(_native.CrimpNativeError):
+        PeriodSearch(np.arange(10.0), np.array([0.1]), 2, precision="f64").ztest()
+
+
 def test_readtimingmodel_matches_reference():
     from crimp_amd.readtimingmodel import ReadTimingModel
     ref = json.load(open(gpath("parsed.json")))["par"]

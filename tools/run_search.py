@@ -19,10 +19,12 @@ dev = torch.device("cuda", 0)
 t = torch.as_tensor(t_h, device=dev)
 f = torch.as_tensor(f0 + (np.arange(M) - M // 2) / (10 * span), device=dev)
 t0 = (t_h[0] + t_h[-1]) / 2
-torch.cuda.synchronize()
-t1 = time.perf_counter()
-z = ops.search(t, t0, f, m, 0)
-torch.cuda.synchronize()
-el = time.perf_counter() - t1
-print("variant %s lib %s: %.1f ms %.3e evals/s argmax %d" % (os.environ.get("CRIMP_MFMA", "t1"), os.environ.get("CRIMP_LIB_VARIANT", "default"), el * 1e3, n * M / el,
-                                                       int(torch.argmax(z))), flush=True)
+for rep in range(int(os.environ.get("REPS", 1))):
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    z = ops.search(t, t0, f, m, 0)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t1
+    print("variant %s precision %s lib %s: %.1f ms %.3e evals/s argmax %d" % (
+        os.environ.get("CRIMP_MFMA", "t1"), os.environ.get("CRIMP_PRECISION", "fast"),
+        os.environ.get("CRIMP_LIB_VARIANT", "default"), el * 1e3, n * M / el, int(torch.argmax(z))), flush=True)
