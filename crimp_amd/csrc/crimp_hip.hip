@@ -639,6 +639,11 @@ __global__ __launch_bounds__(kPtsBlock) void k_toa_points(const double* __restri
 constexpr int kGridBlock = 128;
 constexpr int kGridNN = 20;
 constexpr int kGridKMax = 8;
+#ifdef CRIMP_GRID_PROD1
+constexpr int kGridProd = 1;
+#else
+constexpr int kGridProd = 4;
+#endif
 
 template <int KMAX>
 __global__ __launch_bounds__(kGridBlock) void k_toa_grid(const double* __restrict__ x,
@@ -707,30 +712,53 @@ __global__ __launch_bounds__(kGridBlock) void k_toa_grid(const double* __restric
             }
         }
         __syncthreads();
+        auto hval = [&](int i) {
+            float h = 0.0f;
+            if (model == CRIMP_MODEL_FOURIER) {
+#pragma unroll
+                for (int j = 0; j < KMAX; ++j)
+                    if (j < K) h = __builtin_fmaf(ca[j], basis[i][2 * j], __builtin_fmaf(cb[j], basis[i][2 * j + 1], h));
+            } else {
+                const float cx = basis[i][0], sx = basis[i][1];
+#pragma unroll
+                for (int j = 0; j < KMAX; ++j) {
+                    if (j < K) {
+                        const float cu = __builtin_fmaf(cx, ca[j], sx * cb[j]);
+                        if (model == CRIMP_MODEL_CAUCHY)
+                            h += amp[j] * __builtin_amdgcn_rcpf(chj[j] - cu);
+                        else
+                            h += amp[j] * __builtin_amdgcn_exp2f(kpj[j] * cu);
+                    }
+                }
+            }
+            return h;
+        };
         for (int i0 = 0; i0 < cnt; i0 += 32) {
             float pa[kGridNN];
 #pragma unroll
             for (int a = 0; a < kGridNN; ++a) pa[a] = 0.0f;
             const int i1 = std::min(cnt, i0 + 32);
-            for (int i = i0; i < i1; ++i) {
-                float h = 0.0f;
-                if (model == CRIMP_MODEL_FOURIER) {
+            int i = i0;
+            // log2 of a product of kGridProd model values instead of kGridProd logs (v_log issues at quarter
+            // rate): one photon costs an add and a multiply per norm plus 1/kGridProd of a log and an add.
+            // Four factors of (norm + h) <= 2^31 cannot overflow fp32; the product adds <= 3 roundings.
+            for (; i + kGridProd <= i1; i += kGridProd) {
+                float hv[kGridProd];
 #pragma unroll
-                    for (int j = 0; j < KMAX; ++j)
-                        if (j < K) h = __builtin_fmaf(ca[j], basis[i][2 * j], __builtin_fmaf(cb[j], basis[i][2 * j + 1], h));
-                } else {
-                    const float cx = basis[i][0], sx = basis[i][1];
-#pragma unroll
-                    for (int j = 0; j < KMAX; ++j) {
-                        if (j < K) {
-                            const float cu = __builtin_fmaf(cx, ca[j], sx * cb[j]);
-                            if (model == CRIMP_MODEL_CAUCHY)
-                                h += amp[j] * __builtin_amdgcn_rcpf(chj[j] - cu);
-                            else
-                                h += amp[j] * __builtin_amdgcn_exp2f(kpj[j] * cu);
-                        }
-                    }
+                for (int j = 0; j < kGridProd; ++j) {
+                    hv[j] = hval(i + j);
+                    hmn = fminf(hmn, hv[j]);
                 }
+#pragma unroll
+                for (int a = 0; a < kGridNN; ++a) {
+                    float pr = nr[a] + hv[0];
+#pragma unroll
+                    for (int j = 1; j < kGridProd; ++j) pr *= nr[a] + hv[j];
+                    pa[a] += __builtin_amdgcn_logf(pr);
+                }
+            }
+            for (; i < i1; ++i) {
+                const float h = hval(i);
                 hmn = fminf(hmn, h);
 #pragma unroll
                 for (int a = 0; a < kGridNN; ++a) pa[a] += __builtin_amdgcn_logf(nr[a] + h);
