@@ -1207,10 +1207,15 @@ extern "C" int crimp_toa_fit(const double* x, const int64_t* offsets, int64_t ni
             }
             HIPCHK(h2d(dstart, hstart.data(), 2 * nint * sizeof(double)));
         }
-        if (vary_amps)
+        if (vary_amps) {
             k_toa_fit_amp<<<(unsigned)nint, kFitBlock, 0, s>>>(dx, doff, dT, de, dstart, C, dout);
-        else
-            k_toa_fit<<<(unsigned)nint, kFitBlock, 0, s>>>(dx, doff, dT, de, dstart, C, dout);
+        } else {
+            double* hcache = nullptr;  // per-photon template part for the norm profiles of the 1-sigma scan
+#ifndef CRIMP_NO_HCACHE
+            HIPCHK(sc.alloc(&hcache, (size_t)hoff[nint]));
+#endif
+            k_toa_fit<<<(unsigned)nint, kFitBlock, 0, s>>>(dx, doff, dT, de, dstart, C, dout, hcache);
+        }
         HIPCHK(hipGetLastError());
         HIPCHK(copy_back(s, out, dout, (size_t)nint * 8, dev));
         HIPCHK(hipStreamSynchronize(s));

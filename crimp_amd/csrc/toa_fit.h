@@ -37,10 +37,19 @@ struct FitShared {
 // np.clip semantics (a NaN stays NaN)
 __device__ __forceinline__ double clipd(double v, double lo, double hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
+// Template-part cache modes of fit_eval: the norm profile of the 1-sigma scan evaluates one phShift at several
+// norms, and the template part h(x_i; phShift) of the model norm + h does not depend on the norm. The profile's
+// first pass stores each photon's h (the thread that computes it is the one that reads it back: same striding),
+// later passes read it instead of recomputing sin/cos and the template terms. The stored value is the
+// recomputed one bit for bit, so the sums are unchanged.
+enum : int { kHNone = 0, kHStore = 1, kHLoad = 2 };
+
 // Reference extended LL (templatemodels.py:109-121, :213-226, :318-329) with its (norm, phShift) gradient and
 // Hessian at (n, phi), from one pass over photons x[a, b) (as toafit.ToAFitter.evaluate assembles them).
+// kHLoad passes return the LL and the norm derivatives only (gp, hnp, hpp are 0).
 __device__ FitEval fit_eval(const double* __restrict__ x, int64_t a, int64_t b, const TplDev* __restrict__ T, double n,
-                            double phi, double E, const FitCfg& C, FitShared& sh) {
+                            double phi, double E, const FitCfg& C, FitShared& sh, double* __restrict__ hc = nullptr,
+                            int hmode = kHNone) {
     const int tid = threadIdx.x;
     const int model = T->model, K = T->K;
     __syncthreads();  // the previous evaluation's readers are done with sh
@@ -48,10 +57,20 @@ __device__ FitEval fit_eval(const double* __restrict__ x, int64_t a, int64_t b, 
     __syncthreads();
     double acc[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
     double mn = INFINITY;
-    for (int64_t i = a + tid; i < b; i += kFitBlock) {
+    if (hmode == kHLoad) {
+        for (int64_t i = a + tid; i < b; i += kFitBlock) {
+            const double mv = n + hc[i];
+            const double q = 1.0 / mv;
+            acc[0] += log(mv);
+            acc[1] += q;
+            acc[3] -= q * q;
+            mn = fmin(mn, mv);
+        }
+    } else for (int64_t i = a + tid; i < b; i += kFitBlock) {
         double s1, c1, h, h1, h2;
         photon_sincos(model, x[i], s1, c1);
         tpl_terms(T, model, K, sh.coef[0], sh.coef[1], s1, c1, h, h1, h2);
+        if (hmode == kHStore) hc[i] = h;
         const double mv = n + h;
         const double q = 1.0 / mv;
         acc[0] += log(mv);
@@ -116,10 +135,13 @@ __device__ void fit_newton_dir(double n, const FitEval& e, double& dn, double& d
 }
 
 // toafit.profile_norm: max over norm in [lo, hi] of LL(norm, phi) at fixed phi (1-D Newton, concave)
+// hc: per-photon template-part cache (nullptr: recompute every pass).
 __device__ double fit_profile(const double* __restrict__ x, int64_t a, int64_t b, const TplDev* __restrict__ T,
-                              double phi, double n_start, double E, const FitCfg& C, FitShared& sh, int& nev) {
+                              double phi, double n_start, double E, const FitCfg& C, FitShared& sh, int& nev,
+                              double* __restrict__ hc = nullptr) {
     double n = clipd(n_start, C.lo, C.hi);
-    FitEval e = fit_eval(x, a, b, T, n, phi, E, C, sh);
+    const int hm = hc ? kHLoad : kHNone;
+    FitEval e = fit_eval(x, a, b, T, n, phi, E, C, sh, hc, hc ? kHStore : kHNone);
     ++nev;
     for (int it = 0; it < 30; ++it) {
         const bool bad = !isfinite(e.ll);
@@ -127,12 +149,12 @@ __device__ double fit_profile(const double* __restrict__ x, int64_t a, int64_t b
         step = clipd(step, -0.5 * n, 0.5 * n);
         if (bad) step = 0.5 * n;  // infeasible: model <= 0 somewhere, raise the norm
         double nn = clipd(n + step, C.lo, C.hi);
-        FitEval e2 = fit_eval(x, a, b, T, nn, phi, E, C, sh);
+        FitEval e2 = fit_eval(x, a, b, T, nn, phi, E, C, sh, hc, hm);
         ++nev;
         const bool worse = isfinite(e.ll) && (!isfinite(e2.ll) || e2.ll < e.ll - 1e-12 * fabs(e.ll));
         if (worse) {  // damp an overshoot
             nn = clipd(n + 0.25 * step, C.lo, C.hi);
-            e2 = fit_eval(x, a, b, T, nn, phi, E, C, sh);
+            e2 = fit_eval(x, a, b, T, nn, phi, E, C, sh, hc, hm);
             ++nev;
         }
         const bool conv = fabs(nn - n) <= 1e-13 * fmax(1.0, n);
@@ -368,7 +390,7 @@ __global__ __launch_bounds__(kFitBlock) void k_toa_fit_amp(const double* __restr
 __global__ __launch_bounds__(kFitBlock) void k_toa_fit(const double* __restrict__ x, const int64_t* __restrict__ offsets,
                                                        const TplDev* __restrict__ T, const double* __restrict__ expo,
                                                        const double* __restrict__ start, FitCfg C,
-                                                       double* __restrict__ out) {
+                                                       double* __restrict__ out, double* __restrict__ hcache) {
     __shared__ FitShared sh;
     const int64_t iv = blockIdx.x;
     const int64_t a = offsets[iv], b = offsets[iv + 1];
@@ -422,7 +444,7 @@ __global__ __launch_bounds__(kFitBlock) void k_toa_fit(const double* __restrict_
             } else {
                 ph = clipd(target, -C.pb, C.pb);
             }
-            const double llk = fit_profile(x, a, b, T, ph, nhat, E, C, sh, nev);
+            const double llk = fit_profile(x, a, b, T, ph, nhat, E, C, sh, nev, hcache);
             const double diff = llmax - llk;
             if (diff > kHalfChi2OneSigma || (double)(k + 1) > C.kcap) {
                 kk = k + 1;
