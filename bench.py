@@ -28,9 +28,10 @@ PEAK_F16_DENSE_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16/F16 dense (no 2:1 sp
 SPLIT_PRODUCTS = 4              # f16 hi/lo split: one fp32-exact product = four f16 products
 # HBM bytes per harmonic-sum launch of this workload from rocprofv3 PMC passes (profiles/): (2 x FETCH_SIZE
 # + WRITE_SIZE) KB x 1024, FETCH_SIZE doubled per the gfx950 correction in MI355X_MICROARCH.md (HBM section).
-PMC_TRAFFIC_BYTES = {"f16": (2 * 713800.0 + 651600.0) * 1024,   # profiles/r1_f16/pmc_traffic.txt
+PMC_TRAFFIC_BYTES = {"f16": (2 * 685800.0 + 640100.0) * 1024,   # profiles/r1_s4/pmc/pmc_summary.txt
                      "f32": (2 * 588447.5625 + 153453.875) * 1024}  # profiles/r1/search_mfma_pmc_summary.json
 FLOP_PER_EVAL_HARM = 8.0
+PEAK_HBM_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E ~8 TB/s
 
 
 def parse():
@@ -46,6 +47,8 @@ def parse():
     p.add_argument("--toa-intervals", type=int, default=1250, help="ToA intervals per GPU (config 5: 1e4 over 8)")
     p.add_argument("--toa-photons", type=int, default=100_000)
     p.add_argument("--no-toa", action="store_true", help="skip the ToA-fit throughput leg")
+    p.add_argument("--calcphase-photons", type=int, default=100_000_000)
+    p.add_argument("--no-calcphase", action="store_true", help="skip the calcphase (HBM-bound) leg")
     return p.parse_args()
 
 
@@ -94,6 +97,36 @@ def toa_leg(a, dev, world, rank):
             "toa_shift_recovery_rms_cycles": float(np.sqrt(np.mean(d ** 2)) / (2 * np.pi)),
             "toa_median_sigma_cycles": float(np.median(res["phShi_LL"]) / (2 * np.pi)),
             "toa_cpu_reference_fits_per_s": 0.42}
+
+
+def calcphase_leg(a, dev):
+    """calcphase (calcphase.py:152-176) over 1e8 photons resident in HBM: 8 B read + 16 B written per photon
+    (SURVEY.md §8d), HBM-bound; hipEvents on the stream the library launches on (torch's current stream)."""
+    import torch
+    from crimp_amd import ops
+    n = a.calcphase_photons
+    tm = {"PEPOCH": 58000.0, "F0": 7.123456789, "F1": -1.0e-12, "F2": 1.0e-22}
+    t = torch.rand(n, dtype=torch.float64, device=dev) * 120.0 + 57940.0   # +-60 d around PEPOCH (MJD)
+    tot = torch.empty_like(t)
+    fol = torch.empty_like(t)
+    for _ in range(2):
+        ops.calcphase(t, tm, total=tot, folded=fol)
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    reps = 5
+    ev[0].record(stream)
+    for _ in range(reps):
+        ops.calcphase(t, tm, total=tot, folded=fol)
+    ev[1].record(stream)
+    torch.cuda.synchronize()
+    ms = ev[0].elapsed_time(ev[1]) / reps
+    gbs = 24.0 * n / (ms * 1e-3) / 1e9
+    del t, tot, fol
+    torch.cuda.empty_cache()
+    return {"photons": n, "ms": ms, "photons_per_s": n / (ms * 1e-3),
+            "roofline": {"bound": "hbm", "achieved": gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS,
+                         "note": "24 algorithmic bytes per photon (8 in, 16 out) / call time incl. the model upload"}}
 
 
 def cpu_baseline(t, f0, df, nharm, budget_s):
@@ -227,9 +260,11 @@ def main():
         }
         if not a.no_cpu:
             rec["cpu_baseline"] = cpu_baseline(t_h, f0, df, a.nharm, a.cpu_seconds)
+    del t, f, out
+    torch.cuda.empty_cache()
+    if not a.no_calcphase and rank == 0:
+        rec["calcphase"] = calcphase_leg(a, dev)
     if not a.no_toa:
-        del t, f, out
-        torch.cuda.empty_cache()
         toa = toa_leg(a, dev, world, rank)
         if rank == 0:
             rec.update(toa)
