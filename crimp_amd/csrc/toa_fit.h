@@ -43,6 +43,9 @@ __device__ __forceinline__ double clipd(double v, double lo, double hi) { return
 // later passes read it instead of recomputing sin/cos and the template terms. The stored value is the
 // recomputed one bit for bit, so the sums are unchanged.
 enum : int { kHNone = 0, kHStore = 1, kHLoad = 2 };
+#ifndef CRIMP_FIT_PROD
+#define CRIMP_FIT_PROD 4
+#endif
 
 // Reference extended LL (templatemodels.py:109-121, :213-226, :318-329) with its (norm, phShift) gradient and
 // Hessian at (n, phi), from one pass over photons x[a, b) (as toafit.ToAFitter.evaluate assembles them).
@@ -57,11 +60,28 @@ __device__ FitEval fit_eval(const double* __restrict__ x, int64_t a, int64_t b, 
     __syncthreads();
     double acc[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
     double mn = INFINITY;
+    // sum of ln(model) as ln of products of CRIMP_FIT_PROD consecutive (per thread) model values: one fp64 log per
+    // CRIMP_FIT_PROD photons; a product of <= 4 model values in (1e-75, 1e75) stays in the fp64 range and adds <= 3
+    // roundings (~3e-16 relative). A non-positive model makes the LL -inf through min(model) below.
+    double pr = 1.0;
+    int np = 0;
+    auto lnacc = [&](double mv) {
+#if CRIMP_FIT_PROD > 1
+        pr *= mv;
+        if (++np == CRIMP_FIT_PROD) {
+            acc[0] += log(pr);
+            pr = 1.0;
+            np = 0;
+        }
+#else
+        acc[0] += log(mv);
+#endif
+    };
     if (hmode == kHLoad) {
         for (int64_t i = a + tid; i < b; i += kFitBlock) {
             const double mv = n + hc[i];
             const double q = 1.0 / mv;
-            acc[0] += log(mv);
+            lnacc(mv);
             acc[1] += q;
             acc[3] -= q * q;
             mn = fmin(mn, mv);
@@ -73,7 +93,7 @@ __device__ FitEval fit_eval(const double* __restrict__ x, int64_t a, int64_t b, 
         if (hmode == kHStore) hc[i] = h;
         const double mv = n + h;
         const double q = 1.0 / mv;
-        acc[0] += log(mv);
+        lnacc(mv);
         acc[1] += q;
         acc[2] += h1 * q;
         acc[3] -= q * q;
@@ -81,6 +101,7 @@ __device__ FitEval fit_eval(const double* __restrict__ x, int64_t a, int64_t b, 
         acc[5] += h2 * q - h1 * h1 * q * q;
         mn = fmin(mn, mv);
     }
+    if (np) acc[0] += log(pr);
     const int w = tid >> 6, lane = tid & 63;
 #pragma unroll
     for (int q = 0; q < 6; ++q) {
