@@ -247,11 +247,25 @@ __global__ __launch_bounds__(256, TILES == 1 ? 2 : 1) void k_search_mfma16(
 #pragma unroll
             for (int r = 0; r < 16; ++r) Cr[t][g][r] = Ci[t][g][r] = 0.0;
 
+#ifndef CRIMP_NO_PREFETCH
+    // the next chunk's photon times are loaded one chunk ahead (the global-load latency hides behind a chunk)
+    double dtn = (i0 + a < i1) ? dt[i0 + a] : 0.0;
+    double d2n = TWOD ? ((i0 + a < i1) ? dt2[i0 + a] : 0.0) : 0.0;
+#endif
     for (int64_t ib = i0; ib < i1; ib += kMfmaChunk) {
         const int cnt = (int)(i1 - ib < kMfmaChunk ? i1 - ib : kMfmaChunk);
         // the chunk's photon times: one coalesced load; lane (a, h) then fetches photon 2q+h's
+#ifndef CRIMP_NO_PREFETCH
+        const double dtv = dtn, d2v = d2n;
+        {
+            const int64_t nb = ib + kMfmaChunk;
+            dtn = (nb + a < i1) ? dt[nb + a] : 0.0;
+            if (TWOD) d2n = (nb + a < i1) ? dt2[nb + a] : 0.0;
+        }
+#else
         const double dtv = a < cnt ? dt[ib + a] : 0.0;
         const double d2v = TWOD ? (a < cnt ? dt2[ib + a] : 0.0) : 0.0;
+#endif
         f32x16 re[TILES][G], im[TILES][G];
 #pragma unroll
         for (int t = 0; t < TILES; ++t)
@@ -274,8 +288,26 @@ __global__ __launch_bounds__(256, TILES == 1 ? 2 : 1) void k_search_mfma16(
             mfma16_pair<G, TILES, SQUARE>(tab, phu, gb * d, live, ka, kb, re, im);
         };
         if (cnt == kMfmaChunk) {
+#if !defined(CRIMP_NO_PREFETCH) && !defined(CRIMP_D_GLOBAL)
+            // photon pair q+1's times are fetched (ds_bpermute) while pair q computes
+            double dn = bperm_d(dtv, h), d2nn = TWOD ? bperm_d(d2v, h) : 0.0;
+#pragma unroll
+            for (int q = 0; q < kMfmaChunk / 2; ++q) {
+                const double d = dn, d2 = d2nn;
+                if (q + 1 < kMfmaChunk / 2) {
+                    dn = bperm_d(dtv, 2 * (q + 1) + h);
+                    if (TWOD) d2nn = bperm_d(d2v, 2 * (q + 1) + h);
+                }
+                __builtin_amdgcn_sched_barrier(0);  // keep the fetch ahead of this pair's arithmetic
+                double phu[TILES];
+#pragma unroll
+                for (int t = 0; t < TILES; ++t) phu[t] = TWOD ? fma(fa[t], d, c2 * d2) : fa[t] * d;
+                mfma16_pair<G, TILES, SQUARE>(tab, phu, gb * d, 1.0f, ka, kb, re, im);
+            }
+#else
 #pragma unroll
             for (int q = 0; q < kMfmaChunk / 2; ++q) pair(q, 1.0f);
+#endif
         } else {
             for (int q = 0; 2 * q < cnt; ++q) pair(q, 2 * q + h < cnt ? 1.0f : 0.0f);
         }

@@ -5,7 +5,8 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out
 mkdir -p "$OUT"
 chk() { local rc=$1; echo "[$2] rc=$rc" | tee -a "$OUT/cmp_steps.log"; if [ "$rc" -ne 0 ]; then exit "$rc"; fi; }
-for v in ${VARIANTS:-"" dup "" dup}; do
+for v in ${VARIANTS:-default dup default dup}; do
+  [ "$v" = default ] && v=""
   REPS=3 CRIMP_LIB_VARIANT=$v timeout -k 10 120 python3 tools/run_search.py >> "$OUT/cmp.log" 2>&1
   chk $? "z2 $v"
 done
