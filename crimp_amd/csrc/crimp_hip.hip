@@ -30,7 +30,7 @@
 static thread_local std::string g_err;
 static std::mutex g_mutex;
 
-// CRIMP_FLAG_TIME_KERNELS: hipEvents around the harmonic-sum kernels of the last search (ms)
+// CRIMP_FLAG_TIME_KERNELS: hipEvents around the harmonic-sum kernels of the last search, or the calcphase kernel (ms)
 static double g_last_kernel_ms = -1.0;
 struct KernelTimer {
     hipEvent_t a = nullptr, b = nullptr;
@@ -223,6 +223,7 @@ struct CPModel {
     double wave_epoch, wave_om, f0;
     double wave_ab[CRIMP_MAX_WAVE][2];
 };
+static_assert(sizeof(CPModel) + 64 <= 4096, "CPModel is passed by value in the kernel arguments (4 KB limit)");
 
 __device__ __forceinline__ double cp_one(const CPModel* __restrict__ M, double t) {
     double te = 0.0;
@@ -261,12 +262,14 @@ __device__ __forceinline__ double cp_one(const CPModel* __restrict__ M, double t
     return te + gl + wv;
 }
 
-// Two photons per thread, 16-byte loads and stores (24 B of HBM traffic per photon). One pair per thread over a
+// Two photons per thread, 16-byte loads and stores (24 B of HBM traffic per photon; non-temporal loads and
+// stores measured the same, profiles/r1_final/ab_cos6_nt.log). One pair per thread over a
 // grid that covers the array (up to 2^28 pairs per sweep): 5.5-5.6 TB/s at 1e8 photons, against 4.6-5.1 TB/s
 // for a 4096-block grid-stride loop with 1, 2 or 4 loads in flight per thread (profiles/r1_s4/calcphase_ab.log).
 __global__ __launch_bounds__(256) void k_calcphase_vec(const double2* __restrict__ t, int64_t npair,
-                                                       const CPModel* __restrict__ M, double2* __restrict__ total,
+                                                       const CPModel Mv, double2* __restrict__ total,
                                                        double2* __restrict__ folded) {
+    const CPModel* M = &Mv;  // the model rides in the kernel arguments (no upload, no copy to the stack)
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < npair; i += (int64_t)gridDim.x * blockDim.x) {
         const double2 tv = t[i];
         double2 tot;
@@ -283,8 +286,9 @@ __global__ __launch_bounds__(256) void k_calcphase_vec(const double2* __restrict
 }
 
 __global__ __launch_bounds__(256) void k_calcphase_scalar(const double* __restrict__ t, int64_t n,
-                                                          const CPModel* __restrict__ M, double* __restrict__ total,
+                                                          const CPModel Mv, double* __restrict__ total,
                                                           double* __restrict__ folded) {
+    const CPModel* M = &Mv;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const double tot = cp_one(M, t[i]);
         total[i] = tot;
@@ -856,9 +860,6 @@ extern "C" int crimp_calcphase(const double* t_mjd, int64_t n, const crimp_timin
     std::memcpy(hm.wave_ab, model->wave_ab, sizeof(hm.wave_ab));
     {
         Scratch sc(s);
-        CPModel* dm = nullptr;
-        HIPCHK(sc.alloc(&dm, 1));
-        HIPCHK(h2d(dm, &hm, sizeof(CPModel)));
         const double* dt = nullptr;
         double *dtot = nullptr, *dfol = nullptr;
         HIPCHK(stage_in(sc, t_mjd, (size_t)n, dev, &dt));
@@ -867,12 +868,15 @@ extern "C" int crimp_calcphase(const double* t_mjd, int64_t n, const crimp_timin
         const bool vec = ((reinterpret_cast<uintptr_t>(dt) | reinterpret_cast<uintptr_t>(dtot) |
                            reinterpret_cast<uintptr_t>(dfol)) & 15u) == 0 && (n % 2 == 0);
         const int blocks = (int)std::min<int64_t>(cdiv(vec ? n / 2 : n, 256), int64_t(1) << 20);
+        KernelTimer kt(s, flags & CRIMP_FLAG_TIME_KERNELS);
+        kt.start();
         if (vec)
-            k_calcphase_vec<<<blocks, 256, 0, s>>>(reinterpret_cast<const double2*>(dt), n / 2, dm,
+            k_calcphase_vec<<<blocks, 256, 0, s>>>(reinterpret_cast<const double2*>(dt), n / 2, hm,
                                                      reinterpret_cast<double2*>(dtot), reinterpret_cast<double2*>(dfol));
         else
-            k_calcphase_scalar<<<blocks, 256, 0, s>>>(dt, n, dm, dtot, dfol);
+            k_calcphase_scalar<<<blocks, 256, 0, s>>>(dt, n, hm, dtot, dfol);
         HIPCHK(hipGetLastError());
+        kt.stop();
         HIPCHK(copy_back(s, total, dtot, (size_t)n, dev));
         HIPCHK(copy_back(s, folded, dfol, (size_t)n, dev));
     }

@@ -45,7 +45,7 @@ def _modeltm(tm):
     return m
 
 
-def calcphase(t_mjd, timing_model_dict, parts=7, total=None, folded=None, want_folded=True):
+def calcphase(t_mjd, timing_model_dict, parts=7, total=None, folded=None, want_folded=True, flags=0):
     L = N.load()
     b = N.Buffers()
     tp = b.arg(t_mjd, np.float64)
@@ -57,7 +57,7 @@ def calcphase(t_mjd, timing_model_dict, parts=7, total=None, folded=None, want_f
     op = b.arg(total, np.float64, writable=True)
     fp = b.arg(folded, np.float64, writable=True) if folded is not None else None
     m = _modeltm(timing_model_dict)
-    N.check(L.crimp_calcphase(tp, n, ctypes.byref(m), int(parts), op, fp, b.flags(), b.stream()))
+    N.check(L.crimp_calcphase(tp, n, ctypes.byref(m), int(parts), op, fp, b.flags(flags), b.stream()))
     return total, folded
 
 

@@ -40,7 +40,7 @@ extern "C" {
 #define CRIMP_FLAG_HW_SINCOS 16u   /* direct search: hardware v_sin/v_cos instead of the polynomial */
 #define CRIMP_FLAG_MFMA_F32 32u    /* factorised search: f32-input MFMA instead of the f16 hi/lo split */
 #define CRIMP_FLAG_MFMA_T2 64u     /* factorised f16 search: two tiles per wave sharing V (one wave/SIMD) */
-#define CRIMP_FLAG_TIME_KERNELS 128u /* search: time the harmonic-sum kernels with hipEvents (crimp_last_kernel_ms) */
+#define CRIMP_FLAG_TIME_KERNELS 128u /* search / calcphase: time the kernels with hipEvents (crimp_last_kernel_ms) */
 #define CRIMP_FLAG_F64 256u         /* search: fp64 sin/cos and sums (reference precision on every trial; slower) */
 
 #define CRIMP_STAT_Z2 0 /* Z^2_m  (periodsearch.py:57-71, :73-106) */
@@ -80,8 +80,9 @@ typedef struct crimp_template {
 /* Library identification. */
 int crimp_version(void);
 const char* crimp_last_error(void);
-/* Duration (ms, hipEvents on the call's stream) of the harmonic-sum kernels of the last crimp_search
- * made with CRIMP_FLAG_TIME_KERNELS; -1 if none. Measurement hook for bench.py, not in the reference. */
+/* Duration (ms, hipEvents on the call's stream) of the harmonic-sum kernels of the last crimp_search, or of
+ * the kernel of the last crimp_calcphase, made with CRIMP_FLAG_TIME_KERNELS; -1 if none. Measurement hook for
+ * bench.py, not in the reference. */
 double crimp_last_kernel_ms(void);
 int crimp_device_count(int32_t* count);
 
