@@ -110,78 +110,108 @@ class VaryParamFitter(ToAFitter):
 
     # ------------------------------------------------------------------ maximisation
     def _maximise(self, i, theta_start, free, max_iter=200):
-        """Bounded maximum over the ``free`` mask for interval i: projected Newton ascent with the exact
-        gradient and a forward-difference Hessian of it (all n+1 points in one device launch),
-        eigenvalue-shifted when not negative definite, backtracking line search on the LL."""
-        th = theta_start.copy()
-        idx = np.nonzero(free)[0]
-        lo, hi = self.blo[idx], self.bhi[idx]
-        z = np.clip(th[idx], lo, hi)
-        nz = idx.size
+        """Bounded maximum over the ``free`` mask for interval i (one-interval form of _maximise_batch)."""
+        th, ll = self._maximise_batch(np.array([i]), theta_start[None, :], free, max_iter)
+        return th[0], float(ll[0])
 
-        def at(zz):
-            t = th.copy()
-            t[idx] = zz
+    def _maximise_batch(self, ivs, starts, free, max_iter=200):
+        """Bounded maxima over the ``free`` mask, one per (interval, start) row: projected Newton ascent with
+        the exact gradient and a forward-difference Hessian of it, eigenvalue-shifted when not negative
+        definite, backtracking line search on the LL. The intervals iterate in lockstep so that every
+        Hessian stage and every line-search trial of all still-active intervals is one device launch; each
+        interval's own sequence of evaluation points (hence its result) is the one-interval iteration's."""
+        ivs = np.asarray(ivs, dtype=np.int64).reshape(-1)
+        th = np.array(starts, dtype=np.float64).reshape(ivs.size, -1)
+        B = ivs.size
+        idx = np.nonzero(free)[0]
+        nz = idx.size
+        if nz == 0:
+            ll, _ = self.evaluate_theta(ivs, th)
+            return th, ll
+        lo, hi = self.blo[idx], self.bhi[idx]
+        Z = np.clip(th[:, idx], lo, hi)
+
+        def at(rows, zz):
+            t = th[rows].copy()
+            t[:, idx] = zz
             return t
 
-        if nz == 0:
-            ll, _ = self.evaluate_theta([i], th[None, :])
-            return th, float(ll[0])
-        ll0, g0 = self.evaluate_theta([i], at(z)[None, :])
-        f, g = float(ll0[0]), g0[0, idx]
-        if not np.isfinite(f):
+        ll0, g0 = self.evaluate_theta(ivs, at(np.arange(B), Z))
+        F, G = ll0.astype(np.float64), g0[:, idx]
+        if not np.all(np.isfinite(F)):
             raise FloatingPointError("readvaryparam: the starting template gives a non-positive model")
-        small = 0
+        small = np.zeros(B, dtype=np.int64)
+        active = np.ones(B, dtype=bool)
         for _ in range(max_iter):
-            h = 1e-6 * np.maximum(1.0, np.abs(z))
-            # step inward at an upper bound so that the difference stays inside the box
-            h = np.where(z + h > hi, -h, h)
-            pts = np.repeat(at(z)[None, :], nz, axis=0)
-            pts[np.arange(nz), idx] += h
-            _, gp = self.evaluate_theta(np.full(nz, i), pts)
-            H = (gp[:, idx] - g[None, :]) / h[:, None]
-            H = 0.5 * (H + H.T)
-            # active bounds (maximisation): at lo with g < 0, or at hi with g > 0
-            act = ((z <= lo) & (g < 0)) | ((z >= hi) & (g > 0))
-            fr = ~act
-            d = np.zeros(nz)
-            if fr.any():
-                Hf = H[np.ix_(fr, fr)]
-                w = np.linalg.eigvalsh(Hf)
-                if w.max() >= 0:
-                    Hf = Hf - (w.max() + 1e-8 * max(1.0, abs(w.min()))) * np.eye(fr.sum())
-                d[fr] = -np.linalg.solve(Hf, g[fr])
-            slope = float(g @ d)
-            t, accepted = 1.0, False
+            A = np.nonzero(active)[0]
+            if A.size == 0:
+                break
+            # forward-difference Hessian points of every active interval, one launch
+            hs = np.empty((A.size, nz))
+            pts = np.empty((A.size * nz, th.shape[1]))
+            for p, b in enumerate(A):
+                h = 1e-6 * np.maximum(1.0, np.abs(Z[b]))
+                h = np.where(Z[b] + h > hi, -h, h)   # step inward at an upper bound
+                P = np.repeat(at([b], Z[b][None, :]), nz, axis=0)
+                P[np.arange(nz), idx] += h
+                pts[p * nz:(p + 1) * nz] = P
+                hs[p] = h
+            _, gp = self.evaluate_theta(np.repeat(ivs[A], nz), pts)
+            Dm = np.zeros((A.size, nz))
+            slope = np.zeros(A.size)
+            for p, b in enumerate(A):
+                z, g = Z[b], G[b]
+                H = (gp[p * nz:(p + 1) * nz][:, idx] - g[None, :]) / hs[p][:, None]
+                H = 0.5 * (H + H.T)
+                # active bounds (maximisation): at lo with g < 0, or at hi with g > 0
+                act = ((z <= lo) & (g < 0)) | ((z >= hi) & (g > 0))
+                fr = ~act
+                if fr.any():
+                    Hf = H[np.ix_(fr, fr)]
+                    w = np.linalg.eigvalsh(Hf)
+                    if w.max() >= 0:
+                        Hf = Hf - (w.max() + 1e-8 * max(1.0, abs(w.min()))) * np.eye(fr.sum())
+                    Dm[p, fr] = -np.linalg.solve(Hf, g[fr])
+                slope[p] = float(g @ Dm[p])
+            # backtracking line search, all pending intervals' trial points in one launch
+            t = np.ones(A.size)
+            accepted = np.zeros(A.size, dtype=bool)
+            ZN, LLN, GN = np.empty((A.size, nz)), np.empty(A.size), np.empty((A.size, nz))
             for _ls in range(60):
-                zn = np.clip(z + t * d, lo, hi)
-                lln, gn = self.evaluate_theta([i], at(zn)[None, :])
-                if np.isfinite(lln[0]) and lln[0] >= f + 1e-4 * t * max(slope, 0.0):
-                    accepted = True
+                Pn = np.nonzero(~accepted)[0]
+                if Pn.size == 0:
                     break
-                t *= 0.5
-            if not accepted:
-                break
-            df = float(lln[0]) - f
-            z, f, g = zn, float(lln[0]), gn[0, idx]
-            step = np.max(np.abs(t * d) / np.maximum(1.0, np.abs(z)))
-            small = small + 1 if (df <= 1e-11 * max(1.0, abs(f)) and step < 1e-9) else 0
-            if small >= 2 or step < 1e-14:
-                break
-        th[idx] = z
-        return th, f
+                zn = np.clip(Z[A[Pn]] + t[Pn, None] * Dm[Pn], lo, hi)
+                lln, gn = self.evaluate_theta(ivs[A[Pn]], at(A[Pn], zn))
+                ok = np.isfinite(lln) & (lln >= F[A[Pn]] + 1e-4 * t[Pn] * np.maximum(slope[Pn], 0.0))
+                for k, p in enumerate(Pn):
+                    if ok[k]:
+                        accepted[p] = True
+                        ZN[p], LLN[p], GN[p] = zn[k], lln[k], gn[k, idx]
+                    else:
+                        t[p] *= 0.5
+            for p, b in enumerate(A):
+                if not accepted[p]:
+                    active[b] = False
+                    continue
+                df = float(LLN[p]) - F[b]
+                Z[b], F[b], G[b] = ZN[p], LLN[p], GN[p]
+                step = np.max(np.abs(t[p] * Dm[p]) / np.maximum(1.0, np.abs(Z[b])))
+                small[b] = small[b] + 1 if (df <= 1e-11 * max(1.0, abs(F[b])) and step < 1e-9) else 0
+                if small[b] >= 2 or step < 1e-14:
+                    active[b] = False
+        th[:, idx] = Z
+        return th, F
 
     def fit(self, brutemin=False):
         if brutemin:
             n0, p0 = self.brute()
         else:
             n0, p0 = np.full(self.nint, self.norm0), np.zeros(self.nint)
-        theta_hat = np.tile(self.theta0, (self.nint, 1))
-        ll_max = np.zeros(self.nint)
-        for i in range(self.nint):
-            start = self.theta0.copy()
-            start[0], start[-1] = np.clip(n0[i], self.blo[0], self.bhi[0]), p0[i]
-            theta_hat[i], ll_max[i] = self._maximise(i, start, self.vary)
+        starts = np.tile(self.theta0, (self.nint, 1))
+        starts[:, 0] = np.clip(n0, self.blo[0], self.bhi[0])
+        starts[:, -1] = p0
+        theta_hat, ll_max = self._maximise_batch(np.arange(self.nint), starts, self.vary)
         lo_err, up_err = self._scan(theta_hat, ll_max)
         rchi2 = self._reduced_chi2_theta(theta_hat)
         return {"phShi": theta_hat[:, -1].copy(), "phShi_LL": lo_err, "phShi_UL": up_err, "reducedChi2": rchi2,
@@ -196,22 +226,25 @@ class VaryParamFitter(ToAFitter):
         free[-1] = False
         out = {}
         for side in (-1, 1):
+            # every interval steps k = 1, 2, ... in lockstep; each step's re-maximisations are one batch
             res = np.zeros(self.nint)
-            for i in range(self.nint):
-                passed = np.zeros(1, dtype=bool)
-                k = 1
-                while True:
-                    ks = np.array([k])
-                    phi = self._scan_phases(theta_hat[i:i + 1, -1], side, ks, passed)[0, 0]
-                    tg = theta_hat[i, -1] + side * k * step
-                    passed |= (tg <= -math.pi) if side < 0 else (tg >= math.pi)
-                    start = theta_hat[i].copy()
-                    start[-1] = phi          # fixed (phShift is not among the re-maximised parameters)
-                    _, llk = self._maximise(i, start, free)
-                    k += 1
-                    if ll_max[i] - llk > CHI2_1SIG_1DOF or k > kcap:
-                        break
-                res[i] = k * step + step / 2
+            k = np.ones(self.nint, dtype=np.int64)
+            passed = np.zeros(self.nint, dtype=bool)
+            going = np.ones(self.nint, dtype=bool)
+            while going.any():
+                A = np.nonzero(going)[0]
+                starts = theta_hat[A].copy()
+                for p, i in enumerate(A):
+                    pa = passed[i:i + 1].copy()
+                    starts[p, -1] = self._scan_phases(theta_hat[i:i + 1, -1], side, k[i:i + 1], pa)[0, 0]
+                    tg = theta_hat[i, -1] + side * k[i] * step
+                    passed[i] |= (tg <= -math.pi) if side < 0 else (tg >= math.pi)
+                # phShift fixed (not among the re-maximised parameters)
+                _, llk = self._maximise_batch(A, starts, free)
+                k[A] += 1
+                stop = (ll_max[A] - llk > CHI2_1SIG_1DOF) | (k[A] > kcap)
+                going[A[stop]] = False
+            res[:] = k * step + step / 2
             out[side] = res
         return out[-1], out[1]
 
