@@ -28,7 +28,7 @@ PEAK_F16_DENSE_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16/F16 dense (no 2:1 sp
 SPLIT_PRODUCTS = 4              # f16 hi/lo split: one fp32-exact product = four f16 products
 # HBM bytes per harmonic-sum launch of this workload from rocprofv3 PMC passes (profiles/): (2 x FETCH_SIZE
 # + WRITE_SIZE) KB x 1024, FETCH_SIZE doubled per the gfx950 correction in MI355X_MICROARCH.md (HBM section).
-PMC_TRAFFIC_BYTES = {"f16": (2 * 685800.0 + 640100.0) * 1024,   # profiles/r1_s4/pmc/pmc_summary.txt
+PMC_TRAFFIC_BYTES = {"f16": (2 * 659900.0 + 2019000.0) * 1024,  # profiles/r1_final2/pmc_s64/pmc_summary.txt (64 splits)
                      "f32": (2 * 588447.5625 + 153453.875) * 1024}  # profiles/r1/search_mfma_pmc_summary.json
 FLOP_PER_EVAL_HARM = 8.0
 PEAK_HBM_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E ~8 TB/s

@@ -274,56 +274,67 @@ static int mfma_search(Scratch& sc, hipStream_t s, const double* dt, const doubl
     const int variant = (flags & CRIMP_FLAG_MFMA_F32) ? 0 : ((flags & CRIMP_FLAG_MFMA_T2) ? 2 : 1);
     const int64_t wtile = kTile * (variant == 2 ? 2 : 1);
     const int64_t tpr = cdiv(nf, wtile);
-    const int64_t last = first + count - 1;
-    const int64_t tf = (first / nf) * tpr + (first % nf) / wtile;
-    const int64_t tl = (last / nf) * tpr + (last % nf) / wtile;
-    const int64_t nt = tl - tf + 1;
     // photon splits depend on the photon count alone, so that every trial's value is bit-identical
     // however the grid is partitioned (tiles are already aligned to absolute trial indices): a
-    // sharded search returns exactly what one unsharded call returns. 16 splits of >= 64k photons
-    // fill the 2048 resident wave slots from ~128 tiles up at a tail cost <= 1/16 of a round.
-    const int64_t best_s = std::min<int64_t>(16, std::max<int64_t>(1, n / 65536));
+    // sharded search returns exactly what one unsharded call returns. Up to 64 splits of >= 64k photons:
+    // the last round of resident waves is then a small part of the launch (config 3: 977 tiles x 64 splits
+    // = 30.5 rounds of the 2048 wave slots, 98.5 % filled, against 7.6 of 8 rounds = 95.4 % with 16).
+#ifndef CRIMP_MAX_SPLITS
+#define CRIMP_MAX_SPLITS 64
+#endif
+    const int64_t best_s = std::min<int64_t>(CRIMP_MAX_SPLITS, std::max<int64_t>(1, n / 65536));
     int64_t chunk = cdiv(cdiv(n, best_s), kMfmaChunk) * kMfmaChunk;
     const int64_t splits = cdiv(n, chunk);
     const int ncomp = 2 * nharm;
+    // per-split partial sums are fp64 [splits][ncomp][trials]; a trial range whose partials would pass
+    // kPartBudget bytes is searched in blocks of trials (tiles straddling a block edge run twice)
+    const int64_t kPartBudget = int64_t(4) << 30;
+    const int64_t cb = std::max<int64_t>(wtile, std::min<int64_t>(count, kPartBudget / (8 * splits * ncomp)));
     double* part = nullptr;
-    e = sc.alloc(&part, (size_t)(splits * ncomp * count));
+    e = sc.alloc(&part, (size_t)(splits * ncomp * cb));
     if (e != hipSuccess) return set_err(CRIMP_ERR_HIP, std::string("mfma_search alloc: ") + hipGetErrorString(e));
-    dim3 grid((unsigned)cdiv(nt, 4), (unsigned)splits);
     KernelTimer kt(s, flags & CRIMP_FLAG_TIME_KERNELS);
     kt.start();
-    if (variant == 0) {
-        for (int k0 = 1; k0 <= nharm;) {
-            // groups {1,2}, {3,4}, {5,6}, ...: harmonic 2 by squaring, later ones from exact phases
-            const int G = (nharm - k0 + 1) >= 2 ? 2 : 1;
-            if (twod)
-                launch_mfma<true>(G, k0 == 1, grid, s, dt, dt2, n, chunk, freq, nf, c2, delta, tf, nt, tpr, first,
-                                  count, k0, ncomp, part);
-            else
-                launch_mfma<false>(G, k0 == 1, grid, s, dt, dt2, n, chunk, freq, nf, c2, delta, tf, nt, tpr, first,
-                                   count, k0, ncomp, part);
-            e = hipGetLastError();
-            if (e != hipSuccess) return set_err(CRIMP_ERR_HIP, std::string("k_search_mfma: ") + hipGetErrorString(e));
-            k0 += G;
-        }
-    } else {
-        for (const HarmGroup& hg : harmonic_groups(nharm)) {
-#define CRIMP_ARGS hg.g, hg.square, grid, s, dt, dt2, n, chunk, freq, nf, c2, delta, tf, nt, tpr, first, count, hg.ka, \
-                   hg.kb, ncomp, part
-            if (variant == 1) {
-                if (twod) launch_mfma16<true, 1>(CRIMP_ARGS); else launch_mfma16<false, 1>(CRIMP_ARGS);
-            } else {
-                if (twod) launch_mfma16<true, 2>(CRIMP_ARGS); else launch_mfma16<false, 2>(CRIMP_ARGS);
+    for (int64_t b0 = 0; b0 < count; b0 += cb) {
+        const int64_t bfirst = first + b0, bcount = std::min<int64_t>(cb, count - b0);
+        const int64_t last = bfirst + bcount - 1;
+        const int64_t tf = (bfirst / nf) * tpr + (bfirst % nf) / wtile;
+        const int64_t tl = (last / nf) * tpr + (last % nf) / wtile;
+        const int64_t nt = tl - tf + 1;
+        dim3 grid((unsigned)cdiv(nt, 4), (unsigned)splits);
+        if (variant == 0) {
+            for (int k0 = 1; k0 <= nharm;) {
+                // groups {1,2}, {3,4}, {5,6}, ...: harmonic 2 by squaring, later ones from exact phases
+                const int G = (nharm - k0 + 1) >= 2 ? 2 : 1;
+                if (twod)
+                    launch_mfma<true>(G, k0 == 1, grid, s, dt, dt2, n, chunk, freq, nf, c2, delta, tf, nt, tpr, bfirst,
+                                      bcount, k0, ncomp, part);
+                else
+                    launch_mfma<false>(G, k0 == 1, grid, s, dt, dt2, n, chunk, freq, nf, c2, delta, tf, nt, tpr, bfirst,
+                                       bcount, k0, ncomp, part);
+                e = hipGetLastError();
+                if (e != hipSuccess) return set_err(CRIMP_ERR_HIP, std::string("k_search_mfma: ") + hipGetErrorString(e));
+                k0 += G;
             }
+        } else {
+            for (const HarmGroup& hg : harmonic_groups(nharm)) {
+#define CRIMP_ARGS hg.g, hg.square, grid, s, dt, dt2, n, chunk, freq, nf, c2, delta, tf, nt, tpr, bfirst, bcount, hg.ka, \
+                       hg.kb, ncomp, part
+                if (variant == 1) {
+                    if (twod) launch_mfma16<true, 1>(CRIMP_ARGS); else launch_mfma16<false, 1>(CRIMP_ARGS);
+                } else {
+                    if (twod) launch_mfma16<true, 2>(CRIMP_ARGS); else launch_mfma16<false, 2>(CRIMP_ARGS);
+                }
 #undef CRIMP_ARGS
-            e = hipGetLastError();
-            if (e != hipSuccess) return set_err(CRIMP_ERR_HIP, std::string("k_search_mfma16: ") + hipGetErrorString(e));
+                e = hipGetLastError();
+                if (e != hipSuccess) return set_err(CRIMP_ERR_HIP, std::string("k_search_mfma16: ") + hipGetErrorString(e));
+            }
         }
+        if (b0 + cb >= count) kt.stop();  // the last block's harmonic-sum kernels end the timed span
+        k_search_finalize<<<(unsigned)cdiv(bcount, 256), 256, 0, s>>>(part, bcount, (int)splits, nharm, stat, (double)n,
+                                                                    out + b0);
+        e = hipGetLastError();
+        if (e != hipSuccess) return set_err(CRIMP_ERR_HIP, std::string("finalize: ") + hipGetErrorString(e));
     }
-    kt.stop();
-    k_search_finalize<<<(unsigned)cdiv(count, 256), 256, 0, s>>>(part, count, (int)splits, nharm, stat, (double)n,
-                                                               out);
-    e = hipGetLastError();
-    if (e != hipSuccess) return set_err(CRIMP_ERR_HIP, std::string("finalize: ") + hipGetErrorString(e));
     return 1;
 }
