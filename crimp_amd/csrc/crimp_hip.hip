@@ -1109,7 +1109,14 @@ static int toa_grid_partials(Scratch& sc, hipStream_t s, const double* dx, const
                              const double* dnrm, int64_t nnorm, const double* dphi, int64_t nphi, int64_t nint,
                              int64_t maxn, double** pl, double** ph, int64_t* splits_out) {
     const int64_t pblocks = cdiv(nphi, kGridBlock);
-    int64_t splits = std::max<int64_t>(1, std::min<int64_t>(cdiv(2048, pblocks * nint), cdiv(std::max<int64_t>(maxn, 1), 1024)));
+    // photon splits: aim at CRIMP_GRID_TARGET blocks (2 waves each; 3 waves/SIMD fit, 3072 resident slots), so
+    // that the last round of waves is a small part of the launch (config 5: 1250 intervals x 14 splits = 11.4
+    // rounds, against 1.6 of 2 rounds with the earlier 2048-block target), splits of >= 1024 photons
+#ifndef CRIMP_GRID_TARGET
+#define CRIMP_GRID_TARGET 16384
+#endif
+    int64_t splits = std::max<int64_t>(1, std::min<int64_t>(cdiv(CRIMP_GRID_TARGET, pblocks * nint),
+                                                            cdiv(std::max<int64_t>(maxn, 1), 1024)));
     splits = std::min<int64_t>(splits, 65535);
     int64_t chunk = cdiv(std::max<int64_t>(maxn, 1), splits);
     chunk = cdiv(chunk, kGridBlock) * kGridBlock;
