@@ -481,7 +481,10 @@ struct TplDev {
 };
 
 constexpr int kPtsPerGroup = 4;
-constexpr int kPtsBlock = 256;
+#ifndef CRIMP_FIT_BLOCK
+#define CRIMP_FIT_BLOCK 512
+#endif
+constexpr int kPtsBlock = CRIMP_FIT_BLOCK;  // = kFitBlock: the device fit driver strides and reduces as k_toa_points
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll

@@ -2,7 +2,7 @@
 //
 // crimp_amd/toafit.py drives the same iterations from the host, where every likelihood evaluation is a
 // k_toa_points launch and a host round trip. Here an interval's whole fit (measureToAs.py:285-376) runs
-// inside one 256-thread workgroup: an evaluation is one pass over the interval's photons and a workgroup
+// inside one 512-thread workgroup: an evaluation is one pass over the interval's photons and a workgroup
 // reduction that every thread reads back, so the workgroup iterates the reference driver itself, with
 // toafit.py's constants and stopping rules:
 //   start   the brute-grid maximum (k_toa_grid partial sums -> k_toa_grid_best) or (norm0, 0);
@@ -13,7 +13,10 @@
 // The evaluation repeats k_toa_points' per-photon arithmetic (tpl_terms), thread striding and reduction
 // order, so its sums equal the host-driven path's.
 
-constexpr int kFitBlock = 256;
+#ifndef CRIMP_FIT_BLOCK
+#define CRIMP_FIT_BLOCK 512
+#endif
+constexpr int kFitBlock = CRIMP_FIT_BLOCK;
 constexpr double kHalfChi2OneSigma = 0.500021713558733;  // 0.5 * chi2.ppf(0.6827, 1)   (measureToAs.py:324)
 constexpr double kTwoPi = 6.283185307179586476925286766559;
 
