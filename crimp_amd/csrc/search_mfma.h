@@ -287,9 +287,12 @@ static int mfma_search(Scratch& sc, hipStream_t s, const double* dt, const doubl
     const int64_t splits = cdiv(n, chunk);
     const int ncomp = 2 * nharm;
     // per-split partial sums are fp64 [splits][ncomp][trials]; a trial range whose partials would pass
-    // kPartBudget bytes is searched in blocks of trials (tiles straddling a block edge run twice)
-    const int64_t kPartBudget = int64_t(4) << 30;
-    const int64_t cb = std::max<int64_t>(wtile, std::min<int64_t>(count, kPartBudget / (8 * splits * ncomp)));
+    // kPartBudget bytes (of the 288 GB HBM) is searched in equal blocks of trials, so that no block is a
+    // sliver that leaves most wave slots idle (tiles straddling a block edge run twice)
+    const int64_t kPartBudget = int64_t(16) << 30;
+    const int64_t cbmax = std::max<int64_t>(wtile, kPartBudget / (8 * splits * ncomp));
+    const int64_t nblk = cdiv(count, cbmax);
+    const int64_t cb = std::min<int64_t>(count, cdiv(cdiv(count, nblk), wtile) * wtile);
     double* part = nullptr;
     e = sc.alloc(&part, (size_t)(splits * ncomp * cb));
     if (e != hipSuccess) return set_err(CRIMP_ERR_HIP, std::string("mfma_search alloc: ") + hipGetErrorString(e));

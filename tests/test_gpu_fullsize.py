@@ -72,13 +72,14 @@ def test_config4_full_photon_count_h20(gpu):
 
 
 def test_partial_budget_trial_blocks(gpu):
-    """A search whose per-split partial sums exceed the 4 GiB budget (64 photon splits x 40 components
-    x 300k trials x 8 B = 6.1 GB) runs in trial blocks (search_mfma.h); it equals, bit for bit, the
-    same trials searched as two shards that each fit in one block, and the oracle on sampled trials."""
+    """A search whose per-split partial sums exceed the 16 GiB budget (64 photon splits x 40 components
+    x 900k trials x 8 B = 18.4 GB) runs in two equal trial blocks (search_mfma.h); it equals, bit for bit,
+    the same trials searched as two shards that each fit in one block, and the oracle on sampled trials
+    (block edge at 450560)."""
     import torch
     from crimp_amd import ops
     from crimp_amd.synth import pulsed_events
-    n, M, span, f0 = 4_200_000, 300_000, 1.0e6, 7.123456789
+    n, M, span, f0 = 4_200_000, 900_000, 1.0e6, 7.123456789
     t_h = pulsed_events(n, span, f0, pulsed_frac=0.1, seed=4)
     f_h = f0 + (np.arange(M) - M // 2) / (10.0 * span)
     t = torch.as_tensor(t_h, device=gpu)
@@ -90,6 +91,6 @@ def test_partial_budget_trial_blocks(gpu):
     b = ops.search(t, t0, f, 20, 1, first=cut, count=M - cut).cpu().numpy()
     np.testing.assert_array_equal(np.concatenate([a, b]), h)
     assert int(np.argmax(h)) == M // 2
-    idx = np.array([0, 104_856, 104_857, 209_714, 209_715, M // 2, M - 1])   # around the block edges
+    idx = np.array([0, 450_000, 450_559, 450_560, 450_561, M - 1])   # around the block edge
     hr = O.search(t_h, f_h[idx], 20, stat="h")
     assert _scaled_err(h[idx], hr, np.mean(h)).max() <= 1e-6
