@@ -17,7 +17,7 @@ from crimp_amd import _native as N  # noqa: E402
 from crimp_amd.synth import pulsed_events  # noqa: E402
 
 n = int(os.environ.get("NPH", 100_000_000))
-chunks = int(os.environ.get("CHUNKS", 10))
+chunks = int(os.environ.get("CHUNKS", 2))
 nf, nfd, ngpu = 100_000, 100, 8
 span, f0 = 1.0e7, 7.123456789
 t1 = time.perf_counter()
