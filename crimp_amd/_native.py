@@ -5,6 +5,7 @@ loaded, or no HIP device is visible, every hot-path call raises
 ``CrimpNativeError``. Buffers may be NumPy arrays (host; the library stages them)
 or torch CUDA tensors (device; passed by pointer on torch's current stream).
 """
+import contextlib
 import ctypes
 import os
 import threading
@@ -12,19 +13,16 @@ import threading
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# CRIMP_LIB_VARIANT=<name> loads lib/libcrimp_hip_<name>.so (kernel experiments built beside the default)
-LIB_PATH = os.path.join(_HERE, "lib", "libcrimp_hip%s.so" % (
-    ("_" + os.environ["CRIMP_LIB_VARIANT"]) if os.environ.get("CRIMP_LIB_VARIANT") else ""))
+LIB_PATH = os.path.join(_HERE, "lib", "libcrimp_hip.so")
 
 FLAG_DEVICE_PTRS = 1
 FLAG_SYNC = 2
 FLAG_FORCE_DIRECT = 4
 FLAG_FORCE_MFMA = 8
 FLAG_HW_SINCOS = 16
-FLAG_MFMA_F32 = 32
-FLAG_MFMA_T2 = 64
 FLAG_TIME_KERNELS = 128
 FLAG_F64 = 256
+FLAG_FAST = 512
 
 STAT_Z2 = 0
 STAT_H = 1
@@ -55,8 +53,9 @@ class Template(ctypes.Structure):
                 ("i0", ctypes.c_double * MAX_COMP), ("amp_shift", ctypes.c_double)]
 
 
-EXPORTS = ("crimp_version", "crimp_last_error", "crimp_last_kernel_ms", "crimp_device_count", "crimp_calcphase",
-           "crimp_search", "crimp_toa_points", "crimp_toa_grid", "crimp_toa_fit", "crimp_toa_shape_points", "crimp_binphases")
+EXPORTS = ("crimp_version", "crimp_last_error", "crimp_last_kernel_ms", "crimp_last_fixups", "crimp_release_scratch",
+           "crimp_device_count", "crimp_calcphase", "crimp_search", "crimp_toa_points", "crimp_toa_grid", "crimp_toa_fit",
+           "crimp_toa_shape_points", "crimp_binphases")
 
 _lib = None
 _lock = threading.Lock()
@@ -79,6 +78,7 @@ def load(require_device=True):
             L.crimp_version.restype = ctypes.c_int
             L.crimp_last_error.restype = ctypes.c_char_p
             L.crimp_last_kernel_ms.restype = ctypes.c_double
+            L.crimp_last_fixups.restype = ctypes.c_int64
             L.crimp_device_count.argtypes = [ctypes.POINTER(i32)]
             L.crimp_calcphase.argtypes = [P, i64, ctypes.POINTER(TimingModel), i32, P, P, u32, P]
             L.crimp_search.argtypes = [P, i64, ctypes.c_double, P, i64, P, i64, i32, i32, i64, i64, P, u32, P]
@@ -88,7 +88,7 @@ def load(require_device=True):
             L.crimp_toa_shape_points.argtypes = [P, P, i64, ctypes.POINTER(Template), P, P, P, P, i64, P, u32, P]
             L.crimp_binphases.argtypes = [P, P, i64, P, i32, P, u32, P]
             for name in EXPORTS:
-                if name not in ("crimp_last_error", "crimp_last_kernel_ms"):
+                if name not in ("crimp_last_error", "crimp_last_kernel_ms", "crimp_last_fixups"):
                     getattr(L, name).restype = ctypes.c_int
             _lib = L
         if require_device and not _dev_ok:
@@ -113,11 +113,13 @@ def _is_torch(a):
 
 
 class Buffers:
-    """Collects the pointers for one call; all-host or all-device (torch CUDA) arrays."""
+    """Collects the pointers for one call; all-host or all-device (torch CUDA) arrays. Device tensors must all
+    live on one GPU: the call runs with that GPU current (``device_guard``) on its current torch stream."""
 
     def __init__(self):
         self.keep = []
         self.device = None
+        self.tdev = None
 
     def arg(self, a, dtype, writable=False, allow_none=False):
         if a is None:
@@ -135,6 +137,10 @@ class Buffers:
                         raise ValueError("output tensors must be contiguous %s" % tdt)
                     a = a.to(tdt).contiguous()
                 self._mode(True)
+                if self.tdev is None:
+                    self.tdev = a.device
+                elif a.device != self.tdev:
+                    raise ValueError("device tensors of one call must be on one GPU (%s and %s)" % (self.tdev, a.device))
                 self.keep.append(a)
                 return ctypes.c_void_p(a.data_ptr())
         arr = np.asarray(a)
@@ -159,5 +165,13 @@ class Buffers:
     def stream(self):
         if self.device:
             import torch
-            return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+            return ctypes.c_void_p(torch.cuda.current_stream(self.tdev).cuda_stream)
         return None
+
+    def device_guard(self):
+        """Context making the tensors' GPU the current HIP device for the native call (the library allocates its
+        scratch and launches on the current device)."""
+        if self.device and self.tdev is not None:
+            import torch
+            return torch.cuda.device(self.tdev)
+        return contextlib.nullcontext()

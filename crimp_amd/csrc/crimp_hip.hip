@@ -5,11 +5,10 @@
 //   1. runtime helpers (errors, stream-ordered scratch, staging of host buffers)
 //   2. fp32 sin/cos in revolutions (polynomial and hardware v_sin/v_cos)
 //   3. calcphase            -- HBM-bound fp64 phase folding
-//   4. periodicity search   -- direct VALU kernel (any trial grid) + finalize
+//   4. periodicity search   -- exact i8-MFMA kernel (search_exact.h, default), fp64 kernel, fast f16-MFMA /
+//                              fp32 kernels (search_fast.h, opt-in), finalize
 //   5. ToA likelihood scan  -- fp64 point evaluator, fp32 brute grid, binning
 //   6. C-ABI
-// The factorised MFMA search kernel for arithmetic-progression grids lives in
-// search_mfma.h and is included below.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -24,7 +23,7 @@
 
 #include "../../include/crimp_hip.h"
 
-#define CRIMP_VERSION 1
+#define CRIMP_VERSION 2
 
 // ============================================================== 1. runtime helpers
 static thread_local std::string g_err;
@@ -32,6 +31,8 @@ static std::mutex g_mutex;
 
 // CRIMP_FLAG_TIME_KERNELS: hipEvents around the harmonic-sum kernels of the last search, or the calcphase kernel (ms)
 static double g_last_kernel_ms = -1.0;
+// trials of the last crimp_search recomputed by the fp64 fix-up (exact path)
+static int64_t g_last_fixups = 0;
 struct KernelTimer {
     hipEvent_t a = nullptr, b = nullptr;
     hipStream_t s;
@@ -84,7 +85,9 @@ static int debug_level() {
 
 // Device scratch: a small caching allocator (hipMalloc'd blocks reused across calls). Every
 // entry point synchronises its stream before returning and calls are serialised by g_mutex, so
-// a block handed back at the end of a call is idle when the next call takes it.
+// a block handed back at the end of a call is idle when the next call takes it. The idle blocks
+// of a device are freed when hipMalloc fails (then the allocation is retried once) or when the
+// cached bytes would pass CRIMP_SCRATCH_CAP_MB (default 8192), and by crimp_release_scratch().
 struct Block {
     void* p;
     size_t bytes;
@@ -93,33 +96,68 @@ struct Block {
 };
 static std::vector<Block> g_blocks;
 
+static size_t scratch_cap_bytes() {
+    static size_t cap = 0;
+    if (cap == 0) {
+        const char* e = getenv("CRIMP_SCRATCH_CAP_MB");
+        const long long mb = e ? atoll(e) : 8192;
+        cap = (size_t)(mb > 0 ? mb : 8192) << 20;
+    }
+    return cap;
+}
+
+// frees the idle blocks of device `dev` (all devices for dev < 0)
+static void release_idle_blocks(int dev) {
+    std::vector<Block> keep;
+    for (const Block& b : g_blocks) {
+        if (!b.busy && (dev < 0 || b.dev == dev)) {
+            (void)hipFree(b.p);
+        } else {
+            keep.push_back(b);
+        }
+    }
+    g_blocks.swap(keep);
+}
+
 struct Scratch {
     hipStream_t s;
     int dev = 0;
-    std::vector<size_t> held;
+    std::vector<void*> held;
     explicit Scratch(hipStream_t st) : s(st) { (void)hipGetDevice(&dev); }
     ~Scratch() {
-        for (size_t i : held) g_blocks[i].busy = false;
+        // an error return may leave kernels of this call queued on the stream: drain it before the blocks
+        // they may still write become reusable (a no-op on the normal path, which returns drained)
+        if (!held.empty()) (void)hipStreamSynchronize(s);
+        for (void* p : held)
+            for (Block& b : g_blocks)
+                if (b.p == p) b.busy = false;
     }
     template <typename T>
     hipError_t alloc(T** out, size_t count) {
         const size_t bytes = (std::max<size_t>(count * sizeof(T), 16) + 255) & ~size_t(255);
-        size_t pick = (size_t)-1;
+        size_t pick = (size_t)-1, cached = 0;
         for (size_t i = 0; i < g_blocks.size(); ++i) {
             const Block& b = g_blocks[i];
+            cached += b.bytes;
             if (!b.busy && b.dev == dev && b.bytes >= bytes && b.bytes <= 2 * bytes + (1u << 20) &&
                 (pick == (size_t)-1 || b.bytes < g_blocks[pick].bytes))
                 pick = i;
         }
         if (pick == (size_t)-1) {
+            if (cached + bytes > scratch_cap_bytes()) release_idle_blocks(dev);
             void* p = nullptr;
             hipError_t e = hipMalloc(&p, bytes);
-            if (e != hipSuccess) return e;
+            if (e != hipSuccess) {
+                (void)hipGetLastError();
+                release_idle_blocks(dev);
+                e = hipMalloc(&p, bytes);
+                if (e != hipSuccess) return e;
+            }
             g_blocks.push_back(Block{p, bytes, dev, false});
             pick = g_blocks.size() - 1;
         }
         g_blocks[pick].busy = true;
-        held.push_back(pick);
+        held.push_back(g_blocks[pick].p);
         *out = static_cast<T*>(g_blocks[pick].p);
         if (debug_level() > 0) return hipMemset(g_blocks[pick].p, 0xFF, g_blocks[pick].bytes);
         return hipSuccess;
@@ -297,6 +335,11 @@ __global__ __launch_bounds__(256) void k_calcphase_scalar(const double* __restri
 }
 
 // ============================================================== 4. periodicity search
+// Three kernels compute the per-trial harmonic sums C_k, S_k (periodsearch.py:67-69, :93-99, :120-121):
+//   k_search_exact (search_exact.h, the default for arithmetic-progression grids): i8 MFMA, exact integer sums;
+//   k_search_f64   (any grid; the default when the grid is not a progression or has < 256 trials, and the
+//                   fix-up of trials the exact kernel cannot certify): fp64 throughout;
+//   k_search_fast / k_search_direct (opt-in CRIMP_FLAG_FAST): fp32 sin/cos, f16 MFMA / VALU.
 // dt[i] = t[i] - t0 (periodsearch.py: self.time - self.t0); dt2 = dt*dt for the 2-D grid.
 __global__ __launch_bounds__(256) void k_search_prep(const double* __restrict__ t, int64_t n, double t0,
                                                      double* __restrict__ dt, double* __restrict__ dt2) {
@@ -307,22 +350,27 @@ __global__ __launch_bounds__(256) void k_search_prep(const double* __restrict__ 
     }
 }
 
-// Direct kernel: one lane per trial, every photon of its split broadcast to the wave through
-// the scalar data path. Harmonics k0 .. k0+G-1 of one pass: fp64 phase, centred fractional
-// cycle, fp32 sin/cos in revolutions, angle-addition for k>k0, fp32 sums over 32-photon blocks
-// folded into fp64. part layout: [split][2*m][count] (C_k at 2(k-1), S_k at 2(k-1)+1).
+// Direct kernels: one lane per trial, every photon of its split broadcast to the wave through the scalar
+// path. Trial t of the launch is flat grid index first + (tidx ? tidx[t] : t). part layout: [split][2m][count]
+// (C_k at 2(k-1), S_k at 2(k-1)+1).
 constexpr int kSearchBlock = 256;
 constexpr int kSearchFold = 32;
 
+__device__ __forceinline__ int64_t trial_index(const int64_t* __restrict__ tidx, int64_t first, int64_t t) {
+    return first + (tidx ? tidx[t] : t);
+}
+
+// fp32 direct kernel (fast path, any grid): harmonics k0 .. k0+G-1 of one pass, centred fractional cycle,
+// fp32 sin/cos in revolutions (polynomial, or v_sin/v_cos with CRIMP_FLAG_HW_SINCOS), angle addition for k>k0,
+// fp32 sums over 32-photon blocks folded into fp64.
 template <int G, bool TWOD, bool FIRST, bool HW>
 __global__ __launch_bounds__(kSearchBlock) void k_search_direct(
     const double* __restrict__ dt, const double* __restrict__ dt2, int64_t n, int64_t chunk,
-    const double* __restrict__ freq, int64_t nf, const double* __restrict__ c2row, int64_t first, int64_t count,
-    int k0, int ncomp, double* __restrict__ part) {
+    const double* __restrict__ freq, int64_t nf, const double* __restrict__ c2row, int64_t first,
+    const int64_t* __restrict__ tidx, int64_t count, int k0, int ncomp, double* __restrict__ part) {
     const int64_t t = (int64_t)blockIdx.x * kSearchBlock + threadIdx.x;
     const int64_t split = blockIdx.y;
-    const int64_t tt = t < count ? t : count - 1;
-    const int64_t g = first + tt;
+    const int64_t g = trial_index(tidx, first, t < count ? t : count - 1);
     const int64_t row = TWOD ? g / nf : 0;
     const double f = freq[g - row * nf];
     const double c2 = TWOD ? c2row[row] : 0.0;
@@ -381,22 +429,18 @@ __global__ __launch_bounds__(kSearchBlock) void k_search_direct(
     }
 }
 
-// fp64 kernel (CRIMP_FLAG_F64): the reference's arithmetic precision end to end. One lane per trial,
-// photons broadcast as in k_search_direct; fp64 phase reduced to a centred fractional cycle r, fp64
-// sincospi(2r) for harmonic k0 of the group, harmonics k0+1 .. k0+G-1 by fp64 angle addition, fp64 sums.
-// Every term differs from np.cos(2*k*pi*f*(t-t0)) (periodsearch.py:64-65) by the fp64 rounding of the
-// phase argument only (~1e-9 rad at 1e7 cycles), so powers agree with the reference to ~1e-9 relative
-// on every trial, including near-zero noise bins that the fp32 sin/cos paths resolve only to 1e-6 of the
-// grid's mean power.
+// fp64 kernel: the reference's arithmetic precision end to end. fp64 phase reduced to a centred fractional
+// cycle r, fp64 sincospi(2r) for harmonic k0 of the group, harmonics k0+1 .. k0+G-1 by fp64 angle addition,
+// fp64 sums. Every term differs from np.cos(2*k*pi*f*(t-t0)) (periodsearch.py:67) by the fp64 rounding of the
+// phase argument only.
 template <int G, bool TWOD>
 __global__ __launch_bounds__(kSearchBlock) void k_search_f64(
     const double* __restrict__ dt, const double* __restrict__ dt2, int64_t n, int64_t chunk,
-    const double* __restrict__ freq, int64_t nf, const double* __restrict__ c2row, int64_t first, int64_t count,
-    int k0, int ncomp, double* __restrict__ part) {
+    const double* __restrict__ freq, int64_t nf, const double* __restrict__ c2row, int64_t first,
+    const int64_t* __restrict__ tidx, int64_t count, int k0, int ncomp, double* __restrict__ part) {
     const int64_t t = (int64_t)blockIdx.x * kSearchBlock + threadIdx.x;
     const int64_t split = blockIdx.y;
-    const int64_t tt = t < count ? t : count - 1;
-    const int64_t g = first + tt;
+    const int64_t g = trial_index(tidx, first, t < count ? t : count - 1);
     const int64_t row = TWOD ? g / nf : 0;
     const double f = freq[g - row * nf];
     const double c2 = TWOD ? c2row[row] : 0.0;
@@ -441,10 +485,12 @@ __global__ __launch_bounds__(kSearchBlock) void k_search_f64(
     }
 }
 
-// Z^2 = (2/n) sum_k (C_k^2 + S_k^2)            (periodsearch.py:66-69)
-// H   = max_k (cumsum_k[(C^2+S^2)(2/n)] - 4(k-1)) (periodsearch.py:118-123)
+// Z^2 = sum_k (C_k^2 + S_k^2) * (2/n)            (periodsearch.py:67-69)
+// H   = max_k (cumsum_k[(C^2+S^2)(2/n)] - 4(k-1)) (periodsearch.py:120-123)
+// from fp64 per-split partial sums; out[map ? map[t] : t].
 __global__ __launch_bounds__(256) void k_search_finalize(const double* __restrict__ part, int64_t count, int splits,
-                                                         int m, int stat, double n, double* __restrict__ out) {
+                                                         int m, int stat, double n, const int64_t* __restrict__ map,
+                                                         double* __restrict__ out) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= count) return;
     const int ncomp = 2 * m;
@@ -465,10 +511,11 @@ __global__ __launch_bounds__(256) void k_search_finalize(const double* __restric
             best = v > best ? v : best;
         }
     }
-    out[t] = (stat == CRIMP_STAT_Z2) ? zsum * w : best;
+    out[map ? map[t] : t] = (stat == CRIMP_STAT_Z2) ? zsum * w : best;
 }
 
-#include "search_mfma.h"
+#include "search_fast.h"
+#include "search_exact.h"
 
 // ============================================================== 5. ToA likelihood scan
 struct TplDev {
@@ -481,10 +528,7 @@ struct TplDev {
 };
 
 constexpr int kPtsPerGroup = 4;
-#ifndef CRIMP_FIT_BLOCK
-#define CRIMP_FIT_BLOCK 512
-#endif
-constexpr int kPtsBlock = CRIMP_FIT_BLOCK;  // = kFitBlock: the device fit driver strides and reduces as k_toa_points
+constexpr int kPtsBlock = 512;  // = kFitBlock: the device fit driver strides and reduces as k_toa_points
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -648,11 +692,8 @@ __global__ __launch_bounds__(kPtsBlock) void k_toa_points(const double* __restri
 constexpr int kGridBlock = 128;
 constexpr int kGridNN = 20;
 constexpr int kGridKMax = 8;
-#ifdef CRIMP_GRID_PROD1
-constexpr int kGridProd = 1;
-#else
 constexpr int kGridProd = 4;
-#endif
+constexpr int64_t kGridTarget = 16384;  // brute-grid blocks per launch (toa_grid_partials)
 
 template <int KMAX>
 __global__ __launch_bounds__(kGridBlock) void k_toa_grid(const double* __restrict__ x,
@@ -817,6 +858,14 @@ extern "C" double crimp_last_kernel_ms(void) { return g_last_kernel_ms; }
 
 extern "C" int crimp_version(void) { return CRIMP_VERSION; }
 
+extern "C" int64_t crimp_last_fixups(void) { return g_last_fixups; }
+
+extern "C" int crimp_release_scratch(void) {
+    std::lock_guard<std::mutex> lk(g_mutex);
+    release_idle_blocks(-1);
+    return CRIMP_OK;
+}
+
 extern "C" const char* crimp_last_error(void) { return g_err.c_str(); }
 
 extern "C" int crimp_device_count(int32_t* count) {
@@ -886,13 +935,13 @@ extern "C" int crimp_calcphase(const double* t_mjd, int64_t n, const crimp_timin
     return finish(s, flags);
 }
 
-// Launch the direct kernel for one harmonic group.
 template <bool TWOD, bool HW>
 static void launch_direct(int G, bool firstk, dim3 grid, hipStream_t s, const double* dt, const double* dt2,
                           int64_t n, int64_t chunk, const double* fr, int64_t nf, const double* c2, int64_t first,
-                          int64_t count, int k0, int ncomp, double* part) {
-#define CRIMP_LD(GG, FF) \
-    k_search_direct<GG, TWOD, FF, HW><<<grid, kSearchBlock, 0, s>>>(dt, dt2, n, chunk, fr, nf, c2, first, count, k0, ncomp, part)
+                          const int64_t* tidx, int64_t count, int k0, int ncomp, double* part) {
+#define CRIMP_LD(GG, FF)                                                                                          \
+    k_search_direct<GG, TWOD, FF, HW><<<grid, kSearchBlock, 0, s>>>(dt, dt2, n, chunk, fr, nf, c2, first, tidx, \
+                                                                     count, k0, ncomp, part)
     if (firstk) {
         if (G == 4) CRIMP_LD(4, true); else if (G == 3) CRIMP_LD(3, true); else if (G == 2) CRIMP_LD(2, true); else CRIMP_LD(1, true);
     } else {
@@ -903,22 +952,206 @@ static void launch_direct(int G, bool firstk, dim3 grid, hipStream_t s, const do
 
 template <bool TWOD>
 static void launch_f64(int G, dim3 grid, hipStream_t s, const double* dt, const double* dt2, int64_t n, int64_t chunk,
-                       const double* fr, int64_t nf, const double* c2, int64_t first, int64_t count, int k0, int ncomp,
-                       double* part) {
-#define CRIMP_LF(GG) \
-    k_search_f64<GG, TWOD><<<grid, kSearchBlock, 0, s>>>(dt, dt2, n, chunk, fr, nf, c2, first, count, k0, ncomp, part)
+                       const double* fr, int64_t nf, const double* c2, int64_t first, const int64_t* tidx,
+                       int64_t count, int k0, int ncomp, double* part) {
+#define CRIMP_LF(GG)                                                                                             \
+    k_search_f64<GG, TWOD><<<grid, kSearchBlock, 0, s>>>(dt, dt2, n, chunk, fr, nf, c2, first, tidx, count, k0, \
+                                                         ncomp, part)
     if (G == 8) CRIMP_LF(8); else if (G == 4) CRIMP_LF(4); else if (G == 2) CRIMP_LF(2); else CRIMP_LF(1);
 #undef CRIMP_LF
 }
 
-// Harmonic groups of the direct kernel. Inside a group harmonics come from the group's first
-// harmonic (exact fp64 phase) by angle addition with the fundamental. The fp32 sin/cos error is
-// periodic in the quarter turn, so a harmonic k = 0 (mod 4) reached by angle addition from the
-// fundamental inherits a coherent bias (its e^{-ik theta} error component sums over photons);
-// groups therefore start at k = 1 and at every multiple of 4: {1,2,3}, {4..7}, {8..11}, ...
+// Harmonic groups of the fp32 direct kernel. Inside a group harmonics come from the group's first harmonic
+// (exact fp64 phase) by angle addition with the fundamental. The fp32 sin/cos error is periodic in the quarter
+// turn, so a harmonic k = 0 (mod 4) reached by angle addition from the fundamental inherits a coherent bias
+// (its e^{-ik theta} error component sums over photons); groups therefore start at k = 1 and at every multiple
+// of 4: {1,2,3}, {4..7}, {8..11}, ...
 static int direct_group(int k0, int m) {
     const int rem = m - k0 + 1;
     return k0 == 1 ? (rem < 3 ? rem : 3) : (rem < 4 ? rem : 4);
+}
+
+// Per-trial device buffers of a search (fp64 per-split partial sums of the direct / fast kernels, int64 totals of
+// the exact kernel) are bounded by this many bytes (CRIMP_SEARCH_BUDGET_MB, default 2048): a larger trial range
+// is computed in blocks of trials.
+static int64_t part_budget() {
+    static int64_t b = -1;
+    if (b < 0) {
+        const char* e = getenv("CRIMP_SEARCH_BUDGET_MB");
+        const long long mb = e ? atoll(e) : 2048;
+        b = (int64_t)(mb > 0 ? mb : 2048) << 20;
+    }
+    return b;
+}
+
+// Relative error the exact path certifies per trial before the fp64 fix-up (CRIMP_FIXUP_REL, default 1e-6; a
+// larger value is a test hook that sends more trials through the fix-up).
+static double fixup_rel() {
+    static double r = -1.0;
+    if (r < 0.0) {
+        const char* e = getenv("CRIMP_FIXUP_REL");
+        r = e ? atof(e) : 1e-6;
+        if (!(r > 0.0)) r = 1e-6;
+    }
+    return r;
+}
+
+// Direct (one lane per trial) search over trials first + (tidx ? tidx[t] : t), t < count, of any grid, into
+// out[t] (or out[tidx[t]] with scatter): fp64 kernel (f64) or the fp32 one (fast path). The photon split count
+// is a function of the photon count only.
+static int direct_search(Scratch& sc, hipStream_t s, const double* dt, const double* dt2, int64_t n,
+                         const double* freq, int64_t nf, const double* c2, bool twod, int nharm, int stat,
+                         int64_t first, const int64_t* tidx, int64_t count, double* out, bool scatter, bool f64,
+                         bool hw, KernelTimer* kt) {
+    const int64_t splits0 = std::max<int64_t>(1, std::min<int64_t>(64, n / 16384));
+    const int64_t chunk = cdiv(cdiv(n, splits0), kSearchFold) * kSearchFold;
+    const int64_t splits = cdiv(n, chunk);
+    const int ncomp = 2 * nharm;
+    const int64_t cbmax = std::max<int64_t>(kSearchBlock, part_budget() / (8 * splits * ncomp));
+    const int64_t cb = std::min<int64_t>(count, cdiv(cdiv(count, cdiv(count, cbmax)), kSearchBlock) * kSearchBlock);
+    double* part = nullptr;
+    HIPCHK(sc.alloc(&part, (size_t)(splits * ncomp * cb)));
+    if (kt) kt->start();
+    for (int64_t b0 = 0; b0 < count; b0 += cb) {
+        const int64_t bc = std::min<int64_t>(cb, count - b0);
+        const int64_t* bt = tidx ? tidx + b0 : nullptr;
+        const int64_t bfirst = tidx ? first : first + b0;
+        dim3 grid((unsigned)cdiv(bc, kSearchBlock), (unsigned)splits);
+        int k0 = 1;
+        while (k0 <= nharm && f64) {  // groups of 8, 4, 2, 1 harmonics, each started from its exact phase
+            const int rem = nharm - k0 + 1;
+            const int G = rem >= 8 ? 8 : rem >= 4 ? 4 : rem >= 2 ? 2 : 1;
+            if (twod) launch_f64<true>(G, grid, s, dt, dt2, n, chunk, freq, nf, c2, bfirst, bt, bc, k0, ncomp, part);
+            else launch_f64<false>(G, grid, s, dt, dt2, n, chunk, freq, nf, c2, bfirst, bt, bc, k0, ncomp, part);
+            HIPCHK(hipGetLastError());
+            k0 += G;
+        }
+        while (k0 <= nharm) {
+            const int G = direct_group(k0, nharm);
+            if (twod) {
+                if (hw) launch_direct<true, true>(G, k0 == 1, grid, s, dt, dt2, n, chunk, freq, nf, c2, bfirst, bt, bc, k0, ncomp, part);
+                else launch_direct<true, false>(G, k0 == 1, grid, s, dt, dt2, n, chunk, freq, nf, c2, bfirst, bt, bc, k0, ncomp, part);
+            } else {
+                if (hw) launch_direct<false, true>(G, k0 == 1, grid, s, dt, dt2, n, chunk, freq, nf, c2, bfirst, bt, bc, k0, ncomp, part);
+                else launch_direct<false, false>(G, k0 == 1, grid, s, dt, dt2, n, chunk, freq, nf, c2, bfirst, bt, bc, k0, ncomp, part);
+            }
+            HIPCHK(hipGetLastError());
+            k0 += G;
+        }
+        if (kt && b0 + cb >= count) kt->stop();
+        k_search_finalize<<<(unsigned)cdiv(bc, 256), 256, 0, s>>>(part, bc, (int)splits, nharm, stat, (double)n,
+                                                                 scatter ? bt : nullptr, scatter ? out : out + b0);
+        HIPCHK(hipGetLastError());
+    }
+    return CRIMP_OK;
+}
+
+// Arithmetic-progression check of the (device) frequency grid: 16 ulp of max|f| (k_ap_check). Writes delta
+// into ap[0] on the device (read by the factorised kernels) and returns whether the grid qualifies.
+static int grid_is_progression(Scratch& sc, hipStream_t s, const double* freq, int64_t nf, double** ap, bool* ok) {
+    *ok = false;
+    unsigned long long* info = nullptr;
+    HIPCHK(sc.alloc(&info, 3));
+    *ap = reinterpret_cast<double*>(info);
+    if (nf < 2) return CRIMP_OK;
+    HIPCHK(hipMemsetAsync(info, 0, 3 * sizeof(unsigned long long), s));
+    k_ap_check<<<(unsigned)std::min<int64_t>(cdiv(nf, 256), 1024), 256, 0, s>>>(freq, nf, info);
+    HIPCHK(hipGetLastError());
+    double h[3];
+    HIPCHK(d2h(s, h, info, sizeof(h)));
+    *ok = std::isfinite(h[0]) && h[0] != 0.0 && h[1] <= 16.0 * 2.220446049250313e-16 * h[2];
+    return CRIMP_OK;
+}
+
+// Fast path (CRIMP_FLAG_FAST): the f16-split kernel over an arithmetic-progression grid.
+static int fast_search(Scratch& sc, hipStream_t s, const double* dt, const double* dt2, int64_t n, const double* freq,
+                       int64_t nf, const double* c2, const double* ap, bool twod, int nharm, int stat, int64_t first,
+                       int64_t count, double* out, KernelTimer* kt) {
+    const int64_t tpr = cdiv(nf, kTile);
+    // up to 64 photon splits of >= 64k photons (a function of the photon count only)
+    const int64_t best_s = std::min<int64_t>(64, std::max<int64_t>(1, n / 65536));
+    const int64_t chunk = cdiv(cdiv(n, best_s), kMfmaChunk) * kMfmaChunk;
+    const int64_t splits = cdiv(n, chunk);
+    const int ncomp = 2 * nharm;
+    const int64_t cbmax = std::max<int64_t>(kTile, part_budget() / (8 * splits * ncomp));
+    const int64_t cb = std::min<int64_t>(count, cdiv(cdiv(count, cdiv(count, cbmax)), kTile) * kTile);
+    double* part = nullptr;
+    HIPCHK(sc.alloc(&part, (size_t)(splits * ncomp * cb)));
+    if (kt) kt->start();
+    for (int64_t b0 = 0; b0 < count; b0 += cb) {
+        const int64_t bfirst = first + b0, bcount = std::min<int64_t>(cb, count - b0);
+        const int64_t last = bfirst + bcount - 1;
+        const int64_t tf = (bfirst / nf) * tpr + (bfirst % nf) / kTile;
+        const int64_t tl = (last / nf) * tpr + (last % nf) / kTile;
+        const int64_t nt = tl - tf + 1;
+        dim3 grid((unsigned)cdiv(nt, 4), (unsigned)splits);
+        for (const HarmGroup& hg : harmonic_groups(nharm)) {
+            if (twod) launch_fast<true>(hg, grid, s, dt, dt2, n, chunk, freq, nf, c2, ap, tf, nt, tpr, bfirst, bcount, ncomp, part);
+            else launch_fast<false>(hg, grid, s, dt, dt2, n, chunk, freq, nf, c2, ap, tf, nt, tpr, bfirst, bcount, ncomp, part);
+            HIPCHK(hipGetLastError());
+        }
+        if (kt && b0 + cb >= count) kt->stop();
+        k_search_finalize<<<(unsigned)cdiv(bcount, 256), 256, 0, s>>>(part, bcount, (int)splits, nharm, stat,
+                                                                     (double)n, nullptr, out + b0);
+        HIPCHK(hipGetLastError());
+    }
+    return CRIMP_OK;
+}
+
+// Default path: the exact integer-MFMA kernel (search_exact.h) over an arithmetic-progression grid, then the
+// fp64 fix-up of the trials whose power is too small for the kernel's error bound (k_search_finalize_exact).
+// int64 totals in units of 2^-36 hold |C_k| <= n exactly for n < 2^27 photons.
+static const int64_t kExactMaxPhotons = int64_t(1) << 27;
+static int exact_search(Scratch& sc, hipStream_t s, const double* dt, const double* dt2, int64_t n, const double* freq,
+                        int64_t nf, const double* c2, const double* ap, bool twod, int nharm, int stat, int64_t first,
+                        int64_t count, double* out, KernelTimer* kt, int64_t* nfixed) {
+    const int64_t tpr = cdiv(nf, kTile);
+    const int ncomp = 2 * nharm;
+    // trial blocks bounded by the int64 totals buffer (2 GiB), whole 8-tile block groups
+    const int64_t cbmax = std::max<int64_t>(kTile * kExWaves, part_budget() / (8 * ncomp));
+    const int64_t cb = std::min<int64_t>(count, cdiv(cdiv(count, cdiv(count, cbmax)), kTile) * kTile);
+    unsigned long long* tot = nullptr;
+    int64_t* flagged = nullptr;
+    int* nflag = nullptr;
+    HIPCHK(sc.alloc(&tot, (size_t)(ncomp * cb)));
+    HIPCHK(sc.alloc(&flagged, (size_t)count));
+    HIPCHK(sc.alloc(&nflag, 1));
+    HIPCHK(hipMemsetAsync(nflag, 0, sizeof(int), s));
+    const double dc = 10.0 * std::sqrt((double)n) * 1e-9;  // 10-sigma bound on |error of C_k| (search_exact.h)
+    if (kt) kt->start();
+    for (int64_t b0 = 0; b0 < count; b0 += cb) {
+        const int64_t bfirst = first + b0, bcount = std::min<int64_t>(cb, count - b0);
+        const int64_t last = bfirst + bcount - 1;
+        const int64_t tf = (bfirst / nf) * tpr + (bfirst % nf) / kTile;
+        const int64_t tl = (last / nf) * tpr + (last % nf) / kTile;
+        const int64_t nt = tl - tf + 1;
+        const int64_t bpg = cdiv(nt, kExWaves);
+        // photon splits: >= 8 rounds of the 256 CUs' block slots (one 512-thread block per CU), >= 4096 photons each
+        const int64_t want = std::max<int64_t>(1, std::min<int64_t>(cdiv(8 * 256, bpg), cdiv(n, 4096)));
+        const int64_t chunk = cdiv(cdiv(n, std::min<int64_t>(want, 65535)), kExChunk) * kExChunk;
+        const int64_t splits = cdiv(n, chunk);
+        HIPCHK(hipMemsetAsync(tot, 0, (size_t)(ncomp * bcount) * sizeof(unsigned long long), s));
+        dim3 grid((unsigned)bpg, (unsigned)splits);
+        for (int k = 1; k <= nharm; ++k) {
+            if (twod)
+                k_search_exact<true><<<grid, kExBlock, 0, s>>>(dt, dt2, n, chunk, freq, nf, c2, ap, tf, nt, tpr, bfirst,
+                                                               bcount, k, tot);
+            else
+                k_search_exact<false><<<grid, kExBlock, 0, s>>>(dt, dt2, n, chunk, freq, nf, c2, ap, tf, nt, tpr,
+                                                                bfirst, bcount, k, tot);
+            HIPCHK(hipGetLastError());
+        }
+        if (kt && b0 + cb >= count) kt->stop();
+        k_search_finalize_exact<<<(unsigned)cdiv(bcount, 256), 256, 0, s>>>(
+            reinterpret_cast<const long long*>(tot), bcount, nharm, stat, (double)n, dc, fixup_rel(), b0, out + b0, nflag, flagged);
+        HIPCHK(hipGetLastError());
+    }
+    int nf_h = 0;
+    HIPCHK(d2h(s, &nf_h, nflag, sizeof(int)));
+    *nfixed = nf_h;
+    if (nf_h == 0) return CRIMP_OK;
+    return direct_search(sc, s, dt, dt2, n, freq, nf, c2, twod, nharm, stat, first, flagged, nf_h, out, true, true,
+                         false, nullptr);
 }
 
 extern "C" int crimp_search(const double* t, int64_t n, double t0, const double* freq, int64_t nf,
@@ -932,10 +1165,14 @@ extern "C" int crimp_search(const double* t, int64_t n, double t0, const double*
     const bool twod = log10_negfdot != nullptr && nfd > 0;
     const int64_t total = (twod ? nfd : 1) * nf;
     ARGCHK(first >= 0 && count >= 0 && first + count <= total, "trial range outside the grid");
+    const bool f64 = flags & CRIMP_FLAG_F64;
+    const bool fast = flags & (CRIMP_FLAG_FAST | CRIMP_FLAG_FORCE_DIRECT | CRIMP_FLAG_FORCE_MFMA | CRIMP_FLAG_HW_SINCOS);
+    ARGCHK(!(f64 && fast), "CRIMP_FLAG_F64 excludes the fast-path flags");
     if (count == 0) return CRIMP_OK;
     std::lock_guard<std::mutex> lk(g_mutex);
     const bool dev = flags & CRIMP_FLAG_DEVICE_PTRS;
     hipStream_t s = as_stream(stream);
+    g_last_fixups = 0;
     {
         Scratch sc(s);
         const double *dtm = nullptr, *dfr = nullptr;
@@ -943,21 +1180,18 @@ extern "C" int crimp_search(const double* t, int64_t n, double t0, const double*
         HIPCHK(stage_in(sc, t, (size_t)n, dev, &dtm));
         HIPCHK(stage_in(sc, freq, (size_t)nf, dev, &dfr));
         HIPCHK(stage_out(sc, out, (size_t)count, dev, &dout));
-        // fdot term per row, formed on the host exactly as periodsearch.py:271: 0.5*(-1*10**fd)
+        // fdot term per row, formed on the host exactly as periodsearch.py:95: 0.5*(-1*10**fd)
         double* dc2 = nullptr;
         if (twod) {
             std::vector<double> fdh((size_t)nfd), c2h((size_t)nfd);
             if (dev) {
                 HIPCHK(d2h(s, fdh.data(), log10_negfdot, nfd * sizeof(double)));
-                HIPCHK(hipStreamSynchronize(s));
             } else {
                 std::memcpy(fdh.data(), log10_negfdot, nfd * sizeof(double));
             }
             for (int64_t r = 0; r < nfd; ++r) c2h[r] = 0.5 * (-1.0 * std::pow(10.0, fdh[r]));
             HIPCHK(sc.alloc(&dc2, (size_t)nfd));
             HIPCHK(h2d(dc2, c2h.data(), nfd * sizeof(double)));
-            // c2h must stay alive until the copy has been consumed
-            HIPCHK(hipStreamSynchronize(s));
         }
         double *ddt = nullptr, *ddt2 = nullptr;
         HIPCHK(sc.alloc(&ddt, (size_t)n));
@@ -965,52 +1199,35 @@ extern "C" int crimp_search(const double* t, int64_t n, double t0, const double*
         k_search_prep<<<(int)std::min<int64_t>(cdiv(n, 256), 4096), 256, 0, s>>>(dtm, n, t0, ddt, ddt2);
         HIPCHK(hipGetLastError());
 
-        int rc = -1;
-        const bool f64 = flags & CRIMP_FLAG_F64;
-        if (!(flags & CRIMP_FLAG_FORCE_DIRECT) && !f64) {
-            rc = mfma_search(sc, s, ddt, ddt2, n, dfr, nf, dc2, twod, nharm, stat, first, count, dout, flags);
-            if (rc < 0) return rc;  // error already recorded
+        // Routing by properties of the whole grid (not of this call's trial range), so that every shard of a
+        // sharded search takes the kernel an unsharded search takes:
+        //   default: exact i8 kernel for progressions of >= 256 trials and < 2^27 photons, fp64 kernel otherwise;
+        //   fast:    f16-split MFMA kernel for progressions of >= 256 trials, fp32 direct kernel otherwise;
+        //   f64:     fp64 kernel.
+        KernelTimer kt(s, flags & CRIMP_FLAG_TIME_KERNELS);
+        bool factorised = !f64 && !(flags & CRIMP_FLAG_FORCE_DIRECT) &&
+                          (total >= 256 || (flags & CRIMP_FLAG_FORCE_MFMA)) && (fast || n < kExactMaxPhotons);
+        double* ap = nullptr;
+        if (factorised) {
+            bool ok = false;
+            int rc = grid_is_progression(sc, s, dfr, nf, &ap, &ok);
+            if (rc) return rc;
+            factorised = ok;
         }
-        if (rc != 1) {  // factorised path declined (grid not an arithmetic progression, too small, ...)
-            if ((flags & CRIMP_FLAG_FORCE_MFMA) && !f64)
-                return set_err(CRIMP_ERR_ARG, "factorised search not applicable");
-            const int64_t tblocks = cdiv(count, kSearchBlock);
-            int64_t splits = std::max<int64_t>(1, std::min<int64_t>(cdiv(2048, tblocks), cdiv(n, 2048)));
-            int64_t chunk = cdiv(cdiv(n, splits), kSearchFold) * kSearchFold;
-            splits = cdiv(n, chunk);
-            const int ncomp = 2 * nharm;
-            double* part = nullptr;
-            HIPCHK(sc.alloc(&part, (size_t)(splits * ncomp * count)));
-            dim3 grid((unsigned)tblocks, (unsigned)splits);
-            const bool hw = flags & CRIMP_FLAG_HW_SINCOS;
-            int k0 = 1;
-            KernelTimer kt(s, flags & CRIMP_FLAG_TIME_KERNELS);
-            kt.start();
-            while (k0 <= nharm && f64) {  // groups of 8, 4, 2, 1 harmonics, each started from its exact phase
-                const int rem = nharm - k0 + 1;
-                const int G = rem >= 8 ? 8 : rem >= 4 ? 4 : rem >= 2 ? 2 : 1;
-                if (twod) launch_f64<true>(G, grid, s, ddt, ddt2, n, chunk, dfr, nf, dc2, first, count, k0, ncomp, part);
-                else launch_f64<false>(G, grid, s, ddt, ddt2, n, chunk, dfr, nf, dc2, first, count, k0, ncomp, part);
-                HIPCHK(hipGetLastError());
-                k0 += G;
-            }
-            while (k0 <= nharm) {
-                const int G = direct_group(k0, nharm);
-                if (twod) {
-                    if (hw) launch_direct<true, true>(G, k0 == 1, grid, s, ddt, ddt2, n, chunk, dfr, nf, dc2, first, count, k0, ncomp, part);
-                    else launch_direct<true, false>(G, k0 == 1, grid, s, ddt, ddt2, n, chunk, dfr, nf, dc2, first, count, k0, ncomp, part);
-                } else {
-                    if (hw) launch_direct<false, true>(G, k0 == 1, grid, s, ddt, ddt2, n, chunk, dfr, nf, dc2, first, count, k0, ncomp, part);
-                    else launch_direct<false, false>(G, k0 == 1, grid, s, ddt, ddt2, n, chunk, dfr, nf, dc2, first, count, k0, ncomp, part);
-                }
-                HIPCHK(hipGetLastError());
-                k0 += G;
-            }
-            kt.stop();
-            k_search_finalize<<<(unsigned)cdiv(count, 256), 256, 0, s>>>(part, count, (int)splits, nharm, stat,
-                                                                       (double)n, dout);
-            HIPCHK(hipGetLastError());
+        if ((flags & CRIMP_FLAG_FORCE_MFMA) && !factorised)
+            return set_err(CRIMP_ERR_ARG, "factorised search not applicable (grid is not an arithmetic progression)");
+        int rc;
+        if (factorised && fast) {
+            rc = fast_search(sc, s, ddt, ddt2, n, dfr, nf, dc2, ap, twod, nharm, stat, first, count, dout, &kt);
+        } else if (factorised) {
+            int64_t nfix = 0;
+            rc = exact_search(sc, s, ddt, ddt2, n, dfr, nf, dc2, ap, twod, nharm, stat, first, count, dout, &kt, &nfix);
+            g_last_fixups = nfix;
+        } else {
+            rc = direct_search(sc, s, ddt, ddt2, n, dfr, nf, dc2, twod, nharm, stat, first, nullptr, count, dout,
+                               false, !fast, flags & CRIMP_FLAG_HW_SINCOS, &kt);
         }
+        if (rc) return rc;
         HIPCHK(copy_back(s, out, dout, (size_t)count, dev));
     }
     return finish(s, flags);
@@ -1112,13 +1329,10 @@ static int toa_grid_partials(Scratch& sc, hipStream_t s, const double* dx, const
                              const double* dnrm, int64_t nnorm, const double* dphi, int64_t nphi, int64_t nint,
                              int64_t maxn, double** pl, double** ph, int64_t* splits_out) {
     const int64_t pblocks = cdiv(nphi, kGridBlock);
-    // photon splits: aim at CRIMP_GRID_TARGET blocks (2 waves each; 3 waves/SIMD fit, 3072 resident slots), so
+    // photon splits: aim at kGridTarget blocks (2 waves each; 3 waves/SIMD fit, 3072 resident slots), so
     // that the last round of waves is a small part of the launch (config 5: 1250 intervals x 14 splits = 11.4
     // rounds, against 1.6 of 2 rounds with the earlier 2048-block target), splits of >= 1024 photons
-#ifndef CRIMP_GRID_TARGET
-#define CRIMP_GRID_TARGET 16384
-#endif
-    int64_t splits = std::max<int64_t>(1, std::min<int64_t>(cdiv(CRIMP_GRID_TARGET, pblocks * nint),
+    int64_t splits = std::max<int64_t>(1, std::min<int64_t>(cdiv(kGridTarget, pblocks * nint),
                                                             cdiv(std::max<int64_t>(maxn, 1), 1024)));
     splits = std::min<int64_t>(splits, 65535);
     int64_t chunk = cdiv(std::max<int64_t>(maxn, 1), splits);
@@ -1227,9 +1441,7 @@ extern "C" int crimp_toa_fit(const double* x, const int64_t* offsets, int64_t ni
             k_toa_fit_amp<<<(unsigned)nint, kFitBlock, 0, s>>>(dx, doff, dT, de, dstart, C, dout);
         } else {
             double* hcache = nullptr;  // per-photon template part for the norm profiles of the 1-sigma scan
-#ifndef CRIMP_NO_HCACHE
             HIPCHK(sc.alloc(&hcache, (size_t)hoff[nint]));
-#endif
             k_toa_fit<<<(unsigned)nint, kFitBlock, 0, s>>>(dx, doff, dT, de, dstart, C, dout, hcache);
         }
         HIPCHK(hipGetLastError());

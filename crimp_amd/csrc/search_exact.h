@@ -1,0 +1,262 @@
+// search_exact.h -- the default periodicity-search kernel: factorised harmonic sums on the i8 matrix cores
+// with EXACT integer accumulation (MI355X / gfx950).
+//
+// Trial grid: an arithmetic progression f_j = f_0 + j*delta (fd-outer rows for the 2-D grid). A tile of
+// 1024 trials j = c0 + 32a + b (a, b in 0..31) factorises (periodsearch.py:67, :93-98, :120):
+//     exp(2 pi i k (f_j dt + c2 dt^2)) = U_a * V_b,   U_a = exp(2 pi i k (f_{c0+32a} dt + c2 dt^2)),
+//                                                   V_b = exp(2 pi i k (b delta) dt),
+// so C_k + i S_k of the tile is the complex matrix product sum_photons U_a V_b.
+//
+// Numerics (why this is the default): the phase is fp64 (as the reference's argument), reduced to table
+// units t = phase * kExTab turns; cos/sin come from a 4096-entry LDS table of fp64 values plus a short
+// fp32 rotation by the residual angle (|theta| <= pi/4096), and are emitted directly as 2^30 fixed-point
+// integers (error <= ~1.3 units = 1.2e-9). Each integer is split into four balanced base-256 digits
+// (d3 2^24 + d2 2^16 + d1 2^8 + d0, d_i in [-128, 127], |d3| <= 64) packed in one dword by two
+// integer ops: digits(y) = (y + 0x808080) ^ 0x808080. A product U.V = sum_{i,j} d_i e_j 2^{8(i+j)} is
+// accumulated per digit LEVEL L = i+j on v_mfma_i32_32x32x32_i8 in int32 (exact), levels 3..6
+// kept (the dropped levels 0..2 contribute < 5e-14 per photon): the A operand holds U's digits in natural
+// order, the B operand V's digits byte-reversed, so one dword pair dots to level 3, and A >> 8, >> 16,
+// >> 24 give levels 4, 5, 6 against the same B. The level sums are folded into int64 registers in units
+// of 2^-36 (acc3 + acc4 << 8 + acc5 << 16 + acc6 << 24, exact) every kExFold chunks, and each block adds
+// its int64 totals to the global per-trial totals with 64-bit integer atomics: integer sums are exact and
+// order-independent, so the result does not depend on photon splits, trial blocking or sharding, and the
+// only errors are the 2^30 roundings of U and V (per-term ~1e-9, against ~1e-7 for fp32 sin/cos).
+//
+// Layout: one 512-thread block (8 waves, one 1024-trial tile per wave) per group of 8 consecutive tiles
+// and photon split. Per chunk of 32 photons the block stages dt in LDS, all 512 threads compute the
+// tile-independent V digits once for the 8 tiles (32 photons x 32 b, stored [photon][b] as
+// {rev Vr, rev -Vi, rev Vi, rev Vr}), and every wave computes its own U digits in registers; lane
+// (a, h) holds photons 4q+2h, 4q+2h+1 of quad q ({Ur, Ui} of each: 16 bytes = the K slice of one
+// i8 MFMA), so one quad costs 8 MFMAs (4 levels x Re/Im). V and dt are double/triple buffered so
+// that the producers of chunk c+1 run beside the MFMAs of chunk c with one barrier per chunk.
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kExTab = 4096;    // sin/cos table entries per turn
+constexpr int kExChunk = 32;    // photons per LDS chunk
+constexpr int kExWaves = 8;     // waves (tiles) per block
+constexpr int kExBlock = 64 * kExWaves;
+constexpr int kExFold = 128;    // chunks between int32 -> int64 folds (4096 photons; overflow bound 2^31 at 16384)
+constexpr double kExUnit = 1.4551915228366852e-11;  // 2^-36: value of one unit of the int64 totals
+
+struct ExEntry {
+    int32_t sk, ck;  // rint(sin, cos * 2^30) - 0x4B400000 (the bias of the fp32 rounding trick below)
+    float s, c;      // fp32 sin, cos
+};
+
+// t in table units (turns * kExTab) -> (cos, sin) * 2^30 rounded to int32
+__device__ __forceinline__ void ex_sincos(const ExEntry* __restrict__ tab, double t, int32_t& yc, int32_t& ys) {
+    const double M = 6755399441055744.0;  // 1.5 * 2^52: low mantissa bits of t + M = rint(t) (|t| < 2^51)
+    const double tm = t + M;
+    const double kf = tm - M;
+    const float y = (float)(t - kf);      // exact residual, |y| <= 1/2 table step
+    const ExEntry e = tab[(uint32_t)__double2loint(tm) & (kExTab - 1)];
+    const float th = y * (6.2831853071795864769f / (float)kExTab);
+    const float th2 = th * th;
+    const float st = th * __builtin_fmaf(th2, -0.16666666666666666f, 1.0f);  // sin(th), error th^5/120
+    const float cm = th2 * -0.5f;                                           // cos(th) - 1, error th^4/24
+    const float dsn = __builtin_fmaf(e.c, st, e.s * cm);                    // sin(x) - s_k
+    const float dcs = __builtin_fmaf(-e.s, st, e.c * cm);                   // cos(x) - c_k
+    // |d * 2^30| < 2^22: the low mantissa bits of fma(d, 2^30, 1.5 * 2^23) are rint(d * 2^30) + 0x400000
+    ys = (int32_t)((uint32_t)e.sk + __float_as_uint(__builtin_fmaf(dsn, 1073741824.0f, 12582912.0f)));
+    yc = (int32_t)((uint32_t)e.ck + __float_as_uint(__builtin_fmaf(dcs, 1073741824.0f, 12582912.0f)));
+}
+
+__device__ __forceinline__ uint32_t ex_digits(int32_t y) { return ((uint32_t)y + 0x00808080u) ^ 0x00808080u; }
+__device__ __forceinline__ uint32_t ex_digits_neg(int32_t y) { return (0x00808080u - (uint32_t)y) ^ 0x00808080u; }
+
+__device__ __forceinline__ int64_t ex_level_sum(int a3, int a4, int a5, int a6) {
+    return (int64_t)a3 + ((int64_t)a4 << 8) + ((int64_t)a5 << 16) + ((int64_t)a6 << 24);
+}
+
+template <bool TWOD>
+__global__ __launch_bounds__(kExBlock, 2) void k_search_exact(
+    const double* __restrict__ dt, const double* __restrict__ dt2, int64_t n, int64_t chunk,
+    const double* __restrict__ freq, int64_t nf, const double* __restrict__ c2row, const double* __restrict__ apinfo,
+    int64_t tile_first, int64_t ntiles, int64_t tiles_per_row, int64_t first, int64_t count, int kh,
+    unsigned long long* __restrict__ tot) {
+    __shared__ ExEntry tab[kExTab];                        // 64 KB
+    __shared__ uint4 vbuf[2][kExChunk][32];                // 32 KB
+    __shared__ double sdt[3][kExChunk];
+    __shared__ double sdt2[TWOD ? 3 : 1][kExChunk];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wv = tid >> 6;
+    for (int i = tid; i < kExTab; i += kExBlock) {
+        double s, c;
+        sincospi((double)i * (2.0 / kExTab), &s, &c);
+        ExEntry e;
+        e.s = (float)s;
+        e.c = (float)c;
+        e.sk = (int32_t)((uint32_t)(int32_t)rint(s * 1073741824.0) - 0x4B400000u);
+        e.ck = (int32_t)((uint32_t)(int32_t)rint(c * 1073741824.0) - 0x4B400000u);
+        tab[i] = e;
+    }
+    const double kT = (double)kh * (double)kExTab;
+    const int64_t T = (int64_t)blockIdx.x * kExWaves + wv;  // this wave's tile; waves past the end only produce V
+    const bool active = T < ntiles;                          // wave-uniform
+    const int64_t gt = tile_first + (active ? T : 0);
+    const int64_t frow = gt / tiles_per_row;
+    const int64_t c0 = (gt - frow * tiles_per_row) * 1024;
+    const int ar = lane & 31, h = lane >> 5;
+    const int64_t ca = c0 + 32 * ar;
+    const double fa = freq[ca < nf ? ca : nf - 1] * kT;
+    const double c2 = TWOD ? c2row[frow] * kT : 0.0;
+    const int pb = tid & 31;                                  // producer: V_b for b = pb, photons (tid >> 5) + 16 s
+    const double gbv = (double)pb * apinfo[0] * kT;
+    const int64_t split = blockIdx.y;
+    const int64_t i0 = split * chunk;
+    const int64_t i1 = i0 + chunk < n ? i0 + chunk : n;
+    const int nch = (int)((i1 - i0 + kExChunk - 1) / kExChunk);
+
+    auto load_dt = [&](int c, int slot) {
+        if (tid < kExChunk) {
+            const int64_t i = i0 + (int64_t)c * kExChunk + tid;
+            const bool ok = c < nch && i < i1;
+            sdt[slot][tid] = ok ? dt[i] : 0.0;
+            if (TWOD) sdt2[TWOD ? slot : 0][tid] = ok ? dt2[i] : 0.0;
+        }
+    };
+    auto produce = [&](int slot, int vb) {
+#pragma unroll
+        for (int s = 0; s < kExChunk * 32 / kExBlock; ++s) {
+            const int p = (tid >> 5) + (kExBlock / 32) * s;
+            int32_t yc, ys;
+            ex_sincos(tab, gbv * sdt[slot][p], yc, ys);
+            uint4 v;
+            v.x = __builtin_bswap32(ex_digits(yc));
+            v.y = __builtin_bswap32(ex_digits_neg(ys));
+            v.z = __builtin_bswap32(ex_digits(ys));
+            v.w = v.x;
+            vbuf[vb][p][pb] = v;
+        }
+    };
+
+    i32x16 acc[4][2];
+#pragma unroll
+    for (int L = 0; L < 4; ++L)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[L][0][r] = acc[L][1][r] = 0;
+    int64_t sre[16], sim[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sre[r] = sim[r] = 0;
+
+    load_dt(0, 0);
+    load_dt(1, 1);
+    __syncthreads();  // table + first two dt chunks
+    produce(0, 0);
+    __syncthreads();
+    for (int c = 0; c < nch; ++c) {
+        const int ds = c % 3, vb = c & 1;
+        load_dt(c + 2, (c + 2) % 3);
+        if (c + 1 < nch) produce((c + 1) % 3, vb ^ 1);
+        if (active) {
+            const int64_t pbase = i0 + (int64_t)c * kExChunk;
+#pragma unroll 2
+            for (int q = 0; q < kExChunk / 4; ++q) {
+                const int p0 = 4 * q + 2 * h;
+                const double d0 = sdt[ds][p0], d1 = sdt[ds][p0 + 1];
+                double t0v, t1v;
+                if (TWOD) {
+                    t0v = fma(fa, d0, c2 * sdt2[TWOD ? ds : 0][p0]);
+                    t1v = fma(fa, d1, c2 * sdt2[TWOD ? ds : 0][p0 + 1]);
+                } else {
+                    t0v = fa * d0;
+                    t1v = fa * d1;
+                }
+                int32_t uc0, us0, uc1, us1;
+                ex_sincos(tab, t0v, uc0, us0);
+                ex_sincos(tab, t1v, uc1, us1);
+                uint32_t a0 = ex_digits(uc0), a1 = ex_digits(us0), a2 = ex_digits(uc1), a3 = ex_digits(us1);
+                if (pbase + p0 >= i1) a0 = a1 = 0u;      // photons past the split: zero U
+                if (pbase + p0 + 1 >= i1) a2 = a3 = 0u;
+                const uint4 v0 = vbuf[vb][p0][ar], v1 = vbuf[vb][p0 + 1][ar];
+                const i32x4 bre = {(int)v0.x, (int)v0.y, (int)v1.x, (int)v1.y};
+                const i32x4 bim = {(int)v0.z, (int)v0.w, (int)v1.z, (int)v1.w};
+#pragma unroll
+                for (int L = 0; L < 4; ++L) {
+                    const int sh = 8 * L;
+                    const i32x4 A = {(int)(a0 >> sh), (int)(a1 >> sh), (int)(a2 >> sh), (int)(a3 >> sh)};
+                    acc[L][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A, bre, acc[L][0], 0, 0, 0);
+                    acc[L][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A, bim, acc[L][1], 0, 0, 0);
+                }
+            }
+            if ((c + 1) % kExFold == 0 || c + 1 == nch) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    sre[r] += ex_level_sum(acc[0][0][r], acc[1][0][r], acc[2][0][r], acc[3][0][r]);
+                    sim[r] += ex_level_sum(acc[0][1][r], acc[1][1][r], acc[2][1][r], acc[3][1][r]);
+                }
+#pragma unroll
+                for (int L = 0; L < 4; ++L)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) acc[L][0][r] = acc[L][1][r] = 0;
+            }
+        }
+        __syncthreads();
+    }
+    if (!active) return;
+    // D[row a][col b] of the 32x32 tile: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 h; trial c0 + 32 a + b
+    const int comp = 2 * (kh - 1);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int ra = (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int64_t c = c0 + 32 * ra + ar;
+        const int64_t o = frow * nf + c - first;
+        if (c < nf && o >= 0 && o < count) {
+            atomicAdd(&tot[(int64_t)comp * count + o], (unsigned long long)sre[r]);
+            atomicAdd(&tot[(int64_t)(comp + 1) * count + o], (unsigned long long)sim[r]);
+        }
+    }
+}
+
+// Statistic from the exact totals (periodsearch.py:67-69 and :120-123 in the reference's formula order), and
+// the fix-up list: trials whose power is too small for the kernel's error bound to guarantee 1e-6 relative.
+// Per-term error of U.V (2^30 roundings of both factors, fp32 residual rotation): |e| <= 3e-9, rms <= 1e-9;
+// the error of C_k is a sum of N such terms with random signs, so with kappa = 10 standard deviations
+// dC = 10 sqrt(N) 1e-9 (and the same for S_k), and |Z2_k error| <= (2/N)(2(|C| + |S|) dC + 2 dC^2).
+__global__ __launch_bounds__(256) void k_search_finalize_exact(const long long* __restrict__ tot, int64_t count, int m,
+                                                               int stat, double n, double dc, double rel, int64_t tbase,
+                                                               double* __restrict__ out, int* __restrict__ nflag,
+                                                               int64_t* __restrict__ flagged) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= count) return;
+    const double w = 2.0 / n;
+    double zsum = 0.0, cum = 0.0, best = -INFINITY, err = 0.0;
+    for (int k = 0; k < m; ++k) {
+        const double c = (double)tot[(int64_t)(2 * k) * count + t] * kExUnit;
+        const double s = (double)tot[(int64_t)(2 * k + 1) * count + t] * kExUnit;
+        const double z = c * c + s * s;
+        err += w * (2.0 * (fabs(c) + fabs(s)) * dc + 2.0 * dc * dc);
+        if (stat == CRIMP_STAT_Z2) {
+            zsum += z;
+        } else {
+            cum += z * w;
+            const double v = cum - 4.0 * (double)k;
+            best = v > best ? v : best;
+        }
+    }
+    const double p = (stat == CRIMP_STAT_Z2) ? zsum * w : best;
+    out[t] = p;
+    if (!(err <= rel * fabs(p))) flagged[atomicAdd(nflag, 1)] = tbase + t;
+}
+
+// arithmetic-progression check on the device: |f_j - (f_0 + j delta)| <= 16 ulp(max|f|), delta from the ends.
+// info[0] = delta, info[1] = max deviation (as bits: non-negative doubles order as integers), info[2] = max |f|.
+__global__ __launch_bounds__(256) void k_ap_check(const double* __restrict__ f, int64_t nf,
+                                                  unsigned long long* __restrict__ info) {
+    const double d = (f[nf - 1] - f[0]) / (double)(nf - 1);
+    double dev = 0.0, fm = 0.0;
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nf; j += (int64_t)gridDim.x * blockDim.x) {
+        dev = fmax(dev, fabs(f[j] - (f[0] + (double)j * d)));
+        fm = fmax(fm, fabs(f[j]));
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        dev = fmax(dev, __shfl_xor(dev, o));
+        fm = fmax(fm, __shfl_xor(fm, o));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMax(&info[1], (unsigned long long)__double_as_longlong(dev));
+        atomicMax(&info[2], (unsigned long long)__double_as_longlong(fm));
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) info[0] = (unsigned long long)__double_as_longlong(d);
+}

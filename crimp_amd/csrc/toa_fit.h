@@ -13,10 +13,7 @@
 // The evaluation repeats k_toa_points' per-photon arithmetic (tpl_terms), thread striding and reduction
 // order, so its sums equal the host-driven path's.
 
-#ifndef CRIMP_FIT_BLOCK
-#define CRIMP_FIT_BLOCK 512
-#endif
-constexpr int kFitBlock = CRIMP_FIT_BLOCK;
+constexpr int kFitBlock = kPtsBlock;
 constexpr double kHalfChi2OneSigma = 0.500021713558733;  // 0.5 * chi2.ppf(0.6827, 1)   (measureToAs.py:324)
 constexpr double kTwoPi = 6.283185307179586476925286766559;
 
@@ -46,9 +43,7 @@ __device__ __forceinline__ double clipd(double v, double lo, double hi) { return
 // later passes read it instead of recomputing sin/cos and the template terms. The stored value is the
 // recomputed one bit for bit, so the sums are unchanged.
 enum : int { kHNone = 0, kHStore = 1, kHLoad = 2 };
-#ifndef CRIMP_FIT_PROD
-#define CRIMP_FIT_PROD 4
-#endif
+constexpr int kFitProd = 4;  // model values per fp64 log in fit_eval
 
 // Reference extended LL (templatemodels.py:109-121, :213-226, :318-329) with its (norm, phShift) gradient and
 // Hessian at (n, phi), from one pass over photons x[a, b) (as toafit.ToAFitter.evaluate assembles them).
@@ -63,22 +58,18 @@ __device__ FitEval fit_eval(const double* __restrict__ x, int64_t a, int64_t b, 
     __syncthreads();
     double acc[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
     double mn = INFINITY;
-    // sum of ln(model) as ln of products of CRIMP_FIT_PROD consecutive (per thread) model values: one fp64 log per
-    // CRIMP_FIT_PROD photons; a product of <= 4 model values in (1e-75, 1e75) stays in the fp64 range and adds <= 3
+    // sum of ln(model) as ln of products of kFitProd consecutive (per thread) model values: one fp64 log per
+    // kFitProd photons; a product of <= 4 model values in (1e-75, 1e75) stays in the fp64 range and adds <= 3
     // roundings (~3e-16 relative). A non-positive model makes the LL -inf through min(model) below.
     double pr = 1.0;
     int np = 0;
     auto lnacc = [&](double mv) {
-#if CRIMP_FIT_PROD > 1
         pr *= mv;
-        if (++np == CRIMP_FIT_PROD) {
+        if (++np == kFitProd) {
             acc[0] += log(pr);
             pr = 1.0;
             np = 0;
         }
-#else
-        acc[0] += log(mv);
-#endif
     };
     if (hmode == kHLoad) {
         for (int64_t i = a + tid; i < b; i += kFitBlock) {

@@ -57,7 +57,8 @@ def calcphase(t_mjd, timing_model_dict, parts=7, total=None, folded=None, want_f
     op = b.arg(total, np.float64, writable=True)
     fp = b.arg(folded, np.float64, writable=True) if folded is not None else None
     m = _modeltm(timing_model_dict)
-    N.check(L.crimp_calcphase(tp, n, ctypes.byref(m), int(parts), op, fp, b.flags(flags), b.stream()))
+    with b.device_guard():
+        N.check(L.crimp_calcphase(tp, n, ctypes.byref(m), int(parts), op, fp, b.flags(flags), b.stream()))
     return total, folded
 
 
@@ -69,11 +70,14 @@ def _empty_like_input(a, n, b, dtype=np.float64):
 
 
 def search_flags():
-    """Extra search flags from the environment (CRIMP_SEARCH=direct|mfma, CRIMP_SINCOS=hw, CRIMP_MFMA=f32|t2,
-    CRIMP_PRECISION=f64)."""
+    """Extra search flags from the environment: CRIMP_PRECISION=f64|fast, and for the fast path
+    CRIMP_SEARCH=direct|mfma and CRIMP_SINCOS=hw."""
     f = 0
-    if os.environ.get("CRIMP_PRECISION", "").lower() == "f64":
+    prec = os.environ.get("CRIMP_PRECISION", "").lower()
+    if prec == "f64":
         f |= N.FLAG_F64
+    elif prec == "fast":
+        f |= N.FLAG_FAST
     mode = os.environ.get("CRIMP_SEARCH", "").lower()
     if mode == "direct":
         f |= N.FLAG_FORCE_DIRECT
@@ -81,22 +85,23 @@ def search_flags():
         f |= N.FLAG_FORCE_MFMA
     if os.environ.get("CRIMP_SINCOS", "").lower() == "hw":
         f |= N.FLAG_HW_SINCOS
-    mf = os.environ.get("CRIMP_MFMA", "").lower()
-    if mf == "f32":
-        f |= N.FLAG_MFMA_F32
-    elif mf == "t2":
-        f |= N.FLAG_MFMA_T2
     return f
+
+
+PRECISIONS = (None, "exact", "fast", "f64")
 
 
 def search(t, t0, freq, nharm, stat, log10_negfdot=None, first=0, count=None, out=None, flags=0, precision=None):
     """Z^2 / H over the fd-outer grid; computes flat trials [first, first+count).
-    ``precision``: None/"fast" (fp32 sin/cos, fp32-exact MFMA products, fp64 phases and sums) or "f64"
-    (fp64 throughout, k_search_f64: the reference's precision on every trial, several times slower)."""
-    if precision not in (None, "fast", "f64"):
-        raise ValueError("precision must be None, 'fast' or 'f64'")
+    ``precision``: None/"exact" (default: exact-integer i8 MFMA kernel on progressions, fp64 otherwise, every
+    trial within 1e-6 relative of the reference), "fast" (fp32 sin/cos kernels, ~1e-6 of the grid's mean
+    power) or "f64" (fp64 kernel everywhere)."""
+    if precision not in PRECISIONS:
+        raise ValueError("precision must be one of %s" % (PRECISIONS,))
     if precision == "f64":
         flags |= N.FLAG_F64
+    elif precision == "fast":
+        flags |= N.FLAG_FAST
     L = N.load()
     b = N.Buffers()
     tp = b.arg(t, np.float64)
@@ -112,8 +117,9 @@ def search(t, t0, freq, nharm, stat, log10_negfdot=None, first=0, count=None, ou
     if out is None:
         out = _empty_like_input(t, count, b)
     op = b.arg(out, np.float64, writable=True)
-    N.check(L.crimp_search(tp, n, float(t0), fp, nf, dp, nfd, int(nharm), int(stat), int(first), int(count), op,
-                           b.flags(flags | search_flags()), b.stream()))
+    with b.device_guard():
+        N.check(L.crimp_search(tp, n, float(t0), fp, nf, dp, nfd, int(nharm), int(stat), int(first), int(count), op,
+                               b.flags(flags | search_flags()), b.stream()))
     return out
 
 
@@ -149,7 +155,8 @@ def toa_points(x, offsets, tpl, pt_interval, pt_norm, pt_phi):
     nint = int((offsets.numel() if N._is_torch(offsets) else np.size(offsets)) - 1)
     out = _empty_like_input(x, npts * 8, b)
     outp = b.arg(out, np.float64, writable=True)
-    N.check(L.crimp_toa_points(xp, op, nint, ctypes.byref(tpl), ip, npp, pp, npts, outp, b.flags(), b.stream()))
+    with b.device_guard():
+        N.check(L.crimp_toa_points(xp, op, nint, ctypes.byref(tpl), ip, npp, pp, npts, outp, b.flags(), b.stream()))
     return out.reshape(npts, 8)
 
 
@@ -176,8 +183,9 @@ def toa_shape_points(x, offsets, tpls, pt_interval, pt_norm, pt_phi, aux=None):
     nint = int((offsets.numel() if N._is_torch(offsets) else np.size(offsets)) - 1)
     out = _empty_like_input(x, npts * N.SHAPE_SUMS, b)
     outp = b.arg(out, np.float64, writable=True)
-    N.check(L.crimp_toa_shape_points(xp, op, nint, arr, None if auxa is None else auxa.ctypes.data,
-                                     pint.ctypes.data, npp, pp, npts, outp, b.flags(), b.stream()))
+    with b.device_guard():
+        N.check(L.crimp_toa_shape_points(xp, op, nint, arr, None if auxa is None else auxa.ctypes.data,
+                                         pint.ctypes.data, npp, pp, npts, outp, b.flags(), b.stream()))
     out = out.cpu().numpy() if N._is_torch(out) else out
     return out.reshape(npts, N.SHAPE_SUMS)
 
@@ -198,7 +206,8 @@ def toa_grid(x, offsets, tpl, norms, phis):
     hm = _empty_like_input(x, nint * nphi, b)
     lp = b.arg(ln, np.float64, writable=True)
     hp = b.arg(hm, np.float64, writable=True)
-    N.check(L.crimp_toa_grid(xp, op, nint, ctypes.byref(tpl), np_, nnorm, pp, nphi, lp, hp, b.flags(), b.stream()))
+    with b.device_guard():
+        N.check(L.crimp_toa_grid(xp, op, nint, ctypes.byref(tpl), np_, nnorm, pp, nphi, lp, hp, b.flags(), b.stream()))
     return ln.reshape(nint, nnorm, nphi), hm.reshape(nint, nphi)
 
 
@@ -217,8 +226,9 @@ def toa_fit(x, offsets, tpl, exposure, norm0, ph_shift_res=1000, brutemin=False,
     nint = int((offsets.numel() if N._is_torch(offsets) else np.size(offsets)) - 1)
     out = _empty_like_input(x, nint * 8, b)
     outp = b.arg(out, np.float64, writable=True)
-    N.check(L.crimp_toa_fit(xp, op, nint, ctypes.byref(tpl), ep, float(norm0), int(ph_shift_res), options, outp,
-                            b.flags(), b.stream()))
+    with b.device_guard():
+        N.check(L.crimp_toa_fit(xp, op, nint, ctypes.byref(tpl), ep, float(norm0), int(ph_shift_res), options, outp,
+                                b.flags(), b.stream()))
     return out.reshape(nint, 8)
 
 
@@ -232,5 +242,6 @@ def binphases_counts(x, offsets, edges):
     nb = int((edges.numel() if N._is_torch(edges) else np.size(edges)) - 1)
     out = _empty_like_input(x, nint * nb, b, dtype=np.int64)
     cp = b.arg(out, np.int64, writable=True)
-    N.check(L.crimp_binphases(xp, op, nint, ep, nb, cp, b.flags(), b.stream()))
+    with b.device_guard():
+        N.check(L.crimp_binphases(xp, op, nint, ep, nb, cp, b.flags(), b.stream()))
     return out.reshape(nint, nb)

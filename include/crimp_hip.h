@@ -35,13 +35,16 @@ extern "C" {
 
 #define CRIMP_FLAG_DEVICE_PTRS 1u  /* array arguments are device pointers */
 #define CRIMP_FLAG_SYNC 2u         /* synchronise the stream before returning */
-#define CRIMP_FLAG_FORCE_DIRECT 4u /* periodicity search: never use the factorised MFMA kernel */
-#define CRIMP_FLAG_FORCE_MFMA 8u   /* periodicity search: fail unless the factorised kernel applies */
-#define CRIMP_FLAG_HW_SINCOS 16u   /* direct search: hardware v_sin/v_cos instead of the polynomial */
-#define CRIMP_FLAG_MFMA_F32 32u    /* factorised search: f32-input MFMA instead of the f16 hi/lo split */
-#define CRIMP_FLAG_MFMA_T2 64u     /* factorised f16 search: two tiles per wave sharing V (one wave/SIMD) */
+/* Periodicity-search precision. Default: the exact i8-MFMA kernel on arithmetic-progression grids of >= 256
+ * trials (per-term error ~1e-9, integer sums; every trial within 1e-6 relative of the reference, trials it
+ * cannot certify recomputed in fp64 -- crimp_last_fixups()), the fp64 kernel otherwise. */
+#define CRIMP_FLAG_FORCE_DIRECT 4u /* fast search: the fp32 direct kernel even on a progression (implies FAST) */
+#define CRIMP_FLAG_FORCE_MFMA 8u   /* search: fail unless a factorised kernel applies (with FAST: the f16 one) */
+#define CRIMP_FLAG_HW_SINCOS 16u   /* fast direct search: hardware v_sin/v_cos (implies FAST) */
 #define CRIMP_FLAG_TIME_KERNELS 128u /* search / calcphase: time the kernels with hipEvents (crimp_last_kernel_ms) */
-#define CRIMP_FLAG_F64 256u         /* search: fp64 sin/cos and sums (reference precision on every trial; slower) */
+#define CRIMP_FLAG_F64 256u         /* search: fp64 kernel on every grid */
+#define CRIMP_FLAG_FAST 512u        /* search: fp32 sin/cos kernels (f16-split MFMA / direct): ~1e-6 of the grid's
+                                       mean power, not per trial; faster */
 
 #define CRIMP_STAT_Z2 0 /* Z^2_m  (periodsearch.py:57-71, :73-106) */
 #define CRIMP_STAT_H 1  /* H-test (periodsearch.py:109-125)         */
@@ -84,6 +87,10 @@ const char* crimp_last_error(void);
  * the kernel of the last crimp_calcphase, made with CRIMP_FLAG_TIME_KERNELS; -1 if none. Measurement hook for
  * bench.py, not in the reference. */
 double crimp_last_kernel_ms(void);
+/* Trials of the last crimp_search (default precision) whose power was recomputed by the fp64 fix-up. */
+int64_t crimp_last_fixups(void);
+/* Frees the library's idle cached device scratch on every device (not in the reference). */
+int crimp_release_scratch(void);
 int crimp_device_count(int32_t* count);
 
 /* calcphase(timeMJD, timMod) -> (total, folded)   [calcphase.py:152-176]
@@ -98,7 +105,9 @@ int crimp_calcphase(const double* t_mjd, int64_t n, const crimp_timing_model* mo
  * shards of one search share it); freq [nf] (Hz); log10_negfdot [nfd] or NULL (1-D); the trial
  * grid is fd-outer/f-inner (periodsearch.py:264-278) and this call computes flat trials
  * [first, first+count) of it into out[count]. stat = CRIMP_STAT_Z2 or CRIMP_STAT_H (the latter
- * over the 2-D grid is this library's extension). */
+ * over the 2-D grid is this library's extension). Precision: the CRIMP_FLAG_F64 / _FAST notes
+ * above; the kernel is chosen from the whole grid (nf, nfd, progression), not from [first, count), so a sharded
+ * search computes every trial exactly as an unsharded one. */
 int crimp_search(const double* t, int64_t n, double t0, const double* freq, int64_t nf,
                  const double* log10_negfdot, int64_t nfd, int32_t nharm, int32_t stat, int64_t first,
                  int64_t count, double* out, uint32_t flags, void* stream);

@@ -13,7 +13,7 @@ from conftest import ROOT, gold, gpath
 
 def _declared():
     src = open(os.path.join(ROOT, "include", "crimp_hip.h")).read()
-    return sorted(set(re.findall(r"^\s*(?:int|double|const char\*)\s+(crimp_\w+)\s*\(", src, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|int64_t|double|const char\*)\s+(crimp_\w+)\s*\(", src, re.M)))
 
 
 def test_library_exports_every_declared_symbol():

@@ -33,36 +33,8 @@ if [[ $STEPS == *prof* ]]; then
   stop_on_fault $? rocprof
   find "$OUT/prof" -name "*stats*" | head
 fi
-if [[ $STEPS == *k4* ]]; then
-  timeout -k 10 300 python tools/diag_k4.py > "$OUT/k4.log" 2>&1
-  stop_on_fault $? k4
-  cat "$OUT/k4.log"
-fi
-if [[ $STEPS == *harm* ]]; then
-  timeout -k 10 600 python tools/diag_harm.py > "$OUT/harm.log" 2>&1
-  stop_on_fault $? harm
-  cat "$OUT/harm.log"
-fi
-if [[ $STEPS == *diag* ]]; then
-  timeout -k 10 600 python tools/diag_search.py > "$OUT/diag.log" 2>&1
-  stop_on_fault $? diag
-  cat "$OUT/diag.log"
-fi
-if [[ $STEPS == *repeat* ]]; then
-  timeout -k 10 300 python tools/diag_repeat.py > "$OUT/repeat.log" 2>&1
-  stop_on_fault $? repeat
-  cat "$OUT/repeat.log"
-  CRIMP_DEBUG=1 timeout -k 10 300 python tools/diag_repeat.py > "$OUT/repeat_dbg.log" 2>&1
-  stop_on_fault $? repeat_dbg
-  cat "$OUT/repeat_dbg.log"
-  AMD_SERIALIZE_KERNEL=3 AMD_SERIALIZE_COPY=3 timeout -k 10 300 python tools/diag_repeat.py > "$OUT/repeat_ser.log" 2>&1
-  stop_on_fault $? repeat_ser
-  cat "$OUT/repeat_ser.log"
-fi
-if [[ $STEPS == *h20* ]]; then  # H-test (m = 20) timing, this library vs CRIMP_OLD_LIB (if built)
-  for v in "" ${CRIMP_OLD_LIB:-}; do
-    NHARM=20 NPH=2000000 NTR=1000000 CRIMP_LIB_VARIANT=$v timeout -k 10 200 python3 tools/run_search.py >> "$OUT/h20.log" 2>&1
-    stop_on_fault $? h20
-  done
+if [[ $STEPS == *h20* ]]; then  # H-test (m = 20) timing
+  NHARM=20 NPH=2000000 NTR=1000000 timeout -k 10 200 python3 tools/run_search.py >> "$OUT/h20.log" 2>&1
+  stop_on_fault $? h20
   cat "$OUT/h20.log"
 fi

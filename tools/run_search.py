@@ -1,4 +1,4 @@
-"""One config-3 Z^2_2 search (1e7 photons x 1e6 trials) for profiling; variant from CRIMP_MFMA."""
+"""One config-3 Z^2_2 search (1e7 photons x 1e6 trials) for profiling; precision from CRIMP_PRECISION."""
 import os
 import sys
 import time
@@ -25,6 +25,5 @@ for rep in range(int(os.environ.get("REPS", 1))):
     z = ops.search(t, t0, f, m, 0)
     torch.cuda.synchronize()
     el = time.perf_counter() - t1
-    print("variant %s precision %s lib %s: %.1f ms %.3e evals/s argmax %d" % (
-        os.environ.get("CRIMP_MFMA", "t1"), os.environ.get("CRIMP_PRECISION", "fast"),
-        os.environ.get("CRIMP_LIB_VARIANT", "default"), el * 1e3, n * M / el, int(torch.argmax(z))), flush=True)
+    print("precision %s: %.1f ms %.3e evals/s argmax %d" % (
+        os.environ.get("CRIMP_PRECISION", "exact"), el * 1e3, n * M / el, int(torch.argmax(z))), flush=True)

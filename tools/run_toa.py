@@ -1,4 +1,4 @@
-"""Config-5 ToA fits on one GPU (brute + MLE + 1-sigma scan), timed after a warm-up; CRIMP_LIB_VARIANT selects
+"""Config-5 ToA fits on one GPU (brute + MLE + 1-sigma scan), timed after a warm-up; 
 a kernel experiment. NINT / NPH override the interval count and photons per interval."""
 import os
 import sys
@@ -26,4 +26,4 @@ for rep in range(3):
     torch.cuda.synchronize()
     el = time.perf_counter() - t1
     print("lib %s: %d x %d photons: %.1f ms, %.4g fits/s, phShi[0:3] %s" % (
-        os.environ.get("CRIMP_LIB_VARIANT", "default"), nint, nph, el * 1e3, nint / el, r["phShi"][:3]), flush=True)
+        "libcrimp_hip", nint, nph, el * 1e3, nint / el, r["phShi"][:3]), flush=True)
