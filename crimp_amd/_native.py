@@ -13,7 +13,8 @@ import threading
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libcrimp_hip.so")
+# CRIMP_LIB=<path> loads another build of the library (A/B measurements of kernel builds)
+LIB_PATH = os.environ.get("CRIMP_LIB") or os.path.join(_HERE, "lib", "libcrimp_hip.so")
 
 FLAG_DEVICE_PTRS = 1
 FLAG_SYNC = 2
@@ -54,8 +55,8 @@ class Template(ctypes.Structure):
 
 
 EXPORTS = ("crimp_version", "crimp_last_error", "crimp_last_kernel_ms", "crimp_last_fixups", "crimp_release_scratch",
-           "crimp_device_count", "crimp_calcphase", "crimp_search", "crimp_toa_points", "crimp_toa_grid", "crimp_toa_fit",
-           "crimp_toa_shape_points", "crimp_binphases")
+           "crimp_device_count", "crimp_calcphase", "crimp_search", "crimp_search_sets", "crimp_toa_points",
+           "crimp_toa_grid", "crimp_toa_fit", "crimp_toa_shape_points", "crimp_binphases")
 
 _lib = None
 _lock = threading.Lock()
@@ -82,6 +83,7 @@ def load(require_device=True):
             L.crimp_device_count.argtypes = [ctypes.POINTER(i32)]
             L.crimp_calcphase.argtypes = [P, i64, ctypes.POINTER(TimingModel), i32, P, P, u32, P]
             L.crimp_search.argtypes = [P, i64, ctypes.c_double, P, i64, P, i64, i32, i32, i64, i64, P, u32, P]
+            L.crimp_search_sets.argtypes = [P, P, i64, P, i32, i32, P, u32, P]
             L.crimp_toa_points.argtypes = [P, P, i64, ctypes.POINTER(Template), P, P, P, i64, P, u32, P]
             L.crimp_toa_grid.argtypes = [P, P, i64, ctypes.POINTER(Template), P, i64, P, i64, P, P, u32, P]
             L.crimp_toa_fit.argtypes = [P, P, i64, ctypes.POINTER(Template), P, ctypes.c_double, i32, i32, P, u32, P]

@@ -848,6 +848,80 @@ __global__ __launch_bounds__(256) void k_binphases(const double* __restrict__ x,
     for (int b = threadIdx.x; b < nb; b += blockDim.x) counts[iv * nb + b] = cnt[b];
 }
 
+// Many independent one-trial searches (measureToAs.py:210-212: PeriodSearch(TIME_toa*86400, [f(ToA_mid)], 5).htest()
+// per interval): set i is t[offsets[i] : offsets[i+1]] with its own t0 = (t[first] + t[last])/2 (periodsearch.py:54)
+// and trial frequency freq[i]. One block per set; fp64 as k_search_f64 (harmonic groups of 8 from exact phases,
+// fp64 angle addition inside a group), block-reduced fp64 sums, statistic in the reference's formula order.
+constexpr int kSetBlock = 256;
+__global__ __launch_bounds__(kSetBlock) void k_search_sets(const double* __restrict__ t,
+                                                           const int64_t* __restrict__ offsets,
+                                                           const double* __restrict__ freq, int m, int stat,
+                                                           double* __restrict__ out) {
+    __shared__ double red[kSetBlock / 64][16];
+    const int64_t set = blockIdx.x;
+    const int64_t a = offsets[set], b = offsets[set + 1];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const double t0 = (t[a] + t[b - 1]) / 2;
+    const double f = freq[set];
+    const double w = 2.0 / (double)(b - a);
+    double zsum = 0.0, cum = 0.0, best = -INFINITY;
+    for (int k0 = 1; k0 <= m; k0 += 8) {
+        const int G = m - k0 + 1 < 8 ? m - k0 + 1 : 8;
+        double C[8], S[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) C[k] = S[k] = 0.0;
+        for (int64_t i = a + tid; i < b; i += kSetBlock) {
+            const double ph = f * (t[i] - t0);
+            double s1, c1, s, c;
+            sincospi(2.0 * (ph - rint(ph)), &s1, &c1);
+            if (k0 == 1) {
+                s = s1;
+                c = c1;
+            } else {
+                const double pk = ph * (double)k0;
+                sincospi(2.0 * (pk - rint(pk)), &s, &c);
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                if (k < G) {
+                    C[k] += c;
+                    S[k] += s;
+                    const double cn = fma(c, c1, -s * s1);
+                    s = fma(s, c1, c * s1);
+                    c = cn;
+                }
+            }
+        }
+        for (int k = 0; k < G; ++k) {
+            const double cw = wave_sum(C[k]), sw = wave_sum(S[k]);
+            if (lane == 0) {
+                red[wid][2 * k] = cw;
+                red[wid][2 * k + 1] = sw;
+            }
+        }
+        __syncthreads();
+        if (tid == 0) {
+            for (int k = 0; k < G; ++k) {
+                double c = 0.0, s = 0.0;
+                for (int q = 0; q < kSetBlock / 64; ++q) {
+                    c += red[q][2 * k];
+                    s += red[q][2 * k + 1];
+                }
+                const double z = c * c + s * s;
+                if (stat == CRIMP_STAT_Z2) {
+                    zsum += z;
+                } else {
+                    cum += z * w;
+                    const double v = cum - 4.0 * (double)(k0 - 1 + k);
+                    best = v > best ? v : best;
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (tid == 0) out[set] = (stat == CRIMP_STAT_Z2) ? zsum * w : best;
+}
+
 #include "toa_fit.h"
 #include "toa_shape.h"
 
@@ -1229,6 +1303,41 @@ extern "C" int crimp_search(const double* t, int64_t n, double t0, const double*
         }
         if (rc) return rc;
         HIPCHK(copy_back(s, out, dout, (size_t)count, dev));
+    }
+    return finish(s, flags);
+}
+
+extern "C" int crimp_search_sets(const double* t, const int64_t* offsets, int64_t nset, const double* freq,
+                                 int32_t nharm, int32_t stat, double* out, uint32_t flags, void* stream) {
+    ARGCHK(nset >= 0, "nset < 0");
+    ARGCHK(nharm >= 1 && nharm <= 256, "nbrHarm must be in 1..256");
+    ARGCHK(stat == CRIMP_STAT_Z2 || stat == CRIMP_STAT_H, "unknown statistic");
+    ARGCHK(t != nullptr && offsets != nullptr && freq != nullptr && out != nullptr, "null argument");
+    ARGCHK(nset <= 2147483647LL, "too many sets");
+    if (nset == 0) return CRIMP_OK;
+    std::lock_guard<std::mutex> lk(g_mutex);
+    const bool dev = flags & CRIMP_FLAG_DEVICE_PTRS;
+    hipStream_t s = as_stream(stream);
+    std::vector<int64_t> hoff((size_t)nset + 1);
+    if (dev) {
+        HIPCHK(d2h(s, hoff.data(), offsets, (nset + 1) * sizeof(int64_t)));
+    } else {
+        std::memcpy(hoff.data(), offsets, (nset + 1) * sizeof(int64_t));
+    }
+    for (int64_t i = 0; i < nset; ++i)
+        ARGCHK(hoff[i + 1] > hoff[i] && hoff[i] >= 0, "every set needs photons (periodsearch.py:54 reads time[0])");
+    {
+        Scratch sc(s);
+        const double *dt = nullptr, *df = nullptr;
+        const int64_t* doff = nullptr;
+        double* dout = nullptr;
+        HIPCHK(stage_in(sc, t, (size_t)hoff[nset], dev, &dt));
+        HIPCHK(stage_in(sc, offsets, (size_t)nset + 1, dev, &doff));
+        HIPCHK(stage_in(sc, freq, (size_t)nset, dev, &df));
+        HIPCHK(stage_out(sc, out, (size_t)nset, dev, &dout));
+        k_search_sets<<<(unsigned)nset, kSetBlock, 0, s>>>(dt, doff, df, nharm, stat, dout);
+        HIPCHK(hipGetLastError());
+        HIPCHK(copy_back(s, out, dout, (size_t)nset, dev));
     }
     return finish(s, flags);
 }

@@ -33,10 +33,13 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kExTab = 4096;    // sin/cos table entries per turn
-constexpr int kExChunk = 32;    // photons per LDS chunk
+#ifndef EX_CHUNK
+#define EX_CHUNK 32
+#endif
+constexpr int kExChunk = EX_CHUNK;  // photons per LDS chunk
 constexpr int kExWaves = 8;     // waves (tiles) per block
 constexpr int kExBlock = 64 * kExWaves;
-constexpr int kExFold = 128;    // chunks between int32 -> int64 folds (4096 photons; overflow bound 2^31 at 16384)
+constexpr int kExFold = 4096 / kExChunk;  // chunks between int32 -> int64 folds (4096 photons; overflow bound 2^31 at 16384)
 constexpr double kExUnit = 1.4551915228366852e-11;  // 2^-36: value of one unit of the int64 totals
 
 struct ExEntry {
@@ -44,13 +47,19 @@ struct ExEntry {
     float s, c;      // fp32 sin, cos
 };
 
-// t in table units (turns * kExTab) -> (cos, sin) * 2^30 rounded to int32
-__device__ __forceinline__ void ex_sincos(const ExEntry* __restrict__ tab, double t, int32_t& yc, int32_t& ys) {
+// t in table units (turns * kExTab) -> (cos, sin) * 2^30 rounded to int32, in two halves so that the table
+// read of one photon can be issued ahead of the arithmetic of another (ex_begin / ex_end).
+struct ExArg {
+    uint32_t idx;  // table index
+    float y;       // residual in table steps, |y| <= 1/2
+};
+__device__ __forceinline__ ExArg ex_begin(double t) {
     const double M = 6755399441055744.0;  // 1.5 * 2^52: low mantissa bits of t + M = rint(t) (|t| < 2^51)
     const double tm = t + M;
     const double kf = tm - M;
-    const float y = (float)(t - kf);      // exact residual, |y| <= 1/2 table step
-    const ExEntry e = tab[(uint32_t)__double2loint(tm) & (kExTab - 1)];
+    return ExArg{(uint32_t)__double2loint(tm) & (kExTab - 1), (float)(t - kf)};  // t - kf is exact
+}
+__device__ __forceinline__ void ex_end(const ExEntry& e, float y, int32_t& yc, int32_t& ys) {
     const float th = y * (6.2831853071795864769f / (float)kExTab);
     const float th2 = th * th;
     const float st = th * __builtin_fmaf(th2, -0.16666666666666666f, 1.0f);  // sin(th), error th^5/120
@@ -60,6 +69,10 @@ __device__ __forceinline__ void ex_sincos(const ExEntry* __restrict__ tab, doubl
     // |d * 2^30| < 2^22: the low mantissa bits of fma(d, 2^30, 1.5 * 2^23) are rint(d * 2^30) + 0x400000
     ys = (int32_t)((uint32_t)e.sk + __float_as_uint(__builtin_fmaf(dsn, 1073741824.0f, 12582912.0f)));
     yc = (int32_t)((uint32_t)e.ck + __float_as_uint(__builtin_fmaf(dcs, 1073741824.0f, 12582912.0f)));
+}
+__device__ __forceinline__ void ex_sincos(const ExEntry* __restrict__ tab, double t, int32_t& yc, int32_t& ys) {
+    const ExArg g = ex_begin(t);
+    ex_end(tab[g.idx], g.y, yc, ys);
 }
 
 __device__ __forceinline__ uint32_t ex_digits(int32_t y) { return ((uint32_t)y + 0x00808080u) ^ 0x00808080u; }
@@ -76,11 +89,15 @@ __global__ __launch_bounds__(kExBlock, 2) void k_search_exact(
     int64_t tile_first, int64_t ntiles, int64_t tiles_per_row, int64_t first, int64_t count, int kh,
     unsigned long long* __restrict__ tot) {
     __shared__ ExEntry tab[kExTab];                        // 64 KB
-    __shared__ uint4 vbuf[2][kExChunk][32];                // 32 KB
+    __shared__ uint4 vre[2][kExChunk / 2][32];             // B fragments (Re) per photon pair and column b
+    __shared__ uint4 vim[2][kExChunk / 2][32];             // B fragments (Im)
     __shared__ double sdt[3][kExChunk];
     __shared__ double sdt2[TWOD ? 3 : 1][kExChunk];
     const int tid = threadIdx.x;
     const int lane = tid & 63, wv = tid >> 6;
+#ifdef EX_PRIO
+    if (wv >= kExWaves / 2) __builtin_amdgcn_s_setprio(1);  // the second-dispatched half wins issue arbitration
+#endif
     for (int i = tid; i < kExTab; i += kExBlock) {
         double s, c;
         sincospi((double)i * (2.0 / kExTab), &s, &c);
@@ -116,19 +133,23 @@ __global__ __launch_bounds__(kExBlock, 2) void k_search_exact(
             if (TWOD) sdt2[TWOD ? slot : 0][tid] = ok ? dt2[i] : 0.0;
         }
     };
-    auto produce = [&](int slot, int vb) {
+    // V digits of chunk c as B fragments; photons past the split get V = 0, so that their products vanish
+    auto produce = [&](int c, int slot, int vb) {
 #pragma unroll
         for (int s = 0; s < kExChunk * 32 / kExBlock; ++s) {
             const int p = (tid >> 5) + (kExBlock / 32) * s;
             int32_t yc, ys;
             ex_sincos(tab, gbv * sdt[slot][p], yc, ys);
-            uint4 v;
-            v.x = __builtin_bswap32(ex_digits(yc));
-            v.y = __builtin_bswap32(ex_digits_neg(ys));
-            v.z = __builtin_bswap32(ex_digits(ys));
-            v.w = v.x;
-            vbuf[vb][p][pb] = v;
+            const bool live = i0 + (int64_t)c * kExChunk + p < i1;
+            const uint32_t rc = live ? __builtin_bswap32(ex_digits(yc)) : 0u;
+            const uint32_t rs = live ? __builtin_bswap32(ex_digits(ys)) : 0u;
+            const uint32_t rn = live ? __builtin_bswap32(ex_digits_neg(ys)) : 0u;
+            *(reinterpret_cast<uint2*>(&vre[vb][p >> 1][pb]) + (p & 1)) = make_uint2(rc, rn);
+            *(reinterpret_cast<uint2*>(&vim[vb][p >> 1][pb]) + (p & 1)) = make_uint2(rs, rc);
         }
+    };
+    auto uphase = [&](int ds, int p) -> double {
+        return TWOD ? fma(fa, sdt[ds][p], c2 * sdt2[TWOD ? ds : 0][p]) : fa * sdt[ds][p];
     };
 
     i32x16 acc[4][2];
@@ -143,35 +164,17 @@ __global__ __launch_bounds__(kExBlock, 2) void k_search_exact(
     load_dt(0, 0);
     load_dt(1, 1);
     __syncthreads();  // table + first two dt chunks
-    produce(0, 0);
+    produce(0, 0, 0);
     __syncthreads();
     for (int c = 0; c < nch; ++c) {
         const int ds = c % 3, vb = c & 1;
         load_dt(c + 2, (c + 2) % 3);
-        if (c + 1 < nch) produce((c + 1) % 3, vb ^ 1);
+        if (c + 1 < nch) produce(c + 1, (c + 1) % 3, vb ^ 1);
         if (active) {
-            const int64_t pbase = i0 + (int64_t)c * kExChunk;
-#pragma unroll 2
-            for (int q = 0; q < kExChunk / 4; ++q) {
-                const int p0 = 4 * q + 2 * h;
-                const double d0 = sdt[ds][p0], d1 = sdt[ds][p0 + 1];
-                double t0v, t1v;
-                if (TWOD) {
-                    t0v = fma(fa, d0, c2 * sdt2[TWOD ? ds : 0][p0]);
-                    t1v = fma(fa, d1, c2 * sdt2[TWOD ? ds : 0][p0 + 1]);
-                } else {
-                    t0v = fa * d0;
-                    t1v = fa * d1;
-                }
-                int32_t uc0, us0, uc1, us1;
-                ex_sincos(tab, t0v, uc0, us0);
-                ex_sincos(tab, t1v, uc1, us1);
-                uint32_t a0 = ex_digits(uc0), a1 = ex_digits(us0), a2 = ex_digits(uc1), a3 = ex_digits(us1);
-                if (pbase + p0 >= i1) a0 = a1 = 0u;      // photons past the split: zero U
-                if (pbase + p0 + 1 >= i1) a2 = a3 = 0u;
-                const uint4 v0 = vbuf[vb][p0][ar], v1 = vbuf[vb][p0 + 1][ar];
-                const i32x4 bre = {(int)v0.x, (int)v0.y, (int)v1.x, (int)v1.y};
-                const i32x4 bim = {(int)v0.z, (int)v0.w, (int)v1.z, (int)v1.w};
+            auto mfmas = [&](int q, uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3) {
+                const uint4 br = vre[vb][2 * q + h][ar], bi = vim[vb][2 * q + h][ar];
+                const i32x4 bre = {(int)br.x, (int)br.y, (int)br.z, (int)br.w};
+                const i32x4 bim = {(int)bi.x, (int)bi.y, (int)bi.z, (int)bi.w};
 #pragma unroll
                 for (int L = 0; L < 4; ++L) {
                     const int sh = 8 * L;
@@ -179,7 +182,36 @@ __global__ __launch_bounds__(kExBlock, 2) void k_search_exact(
                     acc[L][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A, bre, acc[L][0], 0, 0, 0);
                     acc[L][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A, bim, acc[L][1], 0, 0, 0);
                 }
+            };
+#ifdef EX_PIPE
+            // quad q+1's table reads are issued before quad q's MFMAs (their LDS latency hides behind them)
+            ExArg g0 = ex_begin(uphase(ds, 2 * h)), g1 = ex_begin(uphase(ds, 2 * h + 1));
+            ExEntry e0 = tab[g0.idx], e1 = tab[g1.idx];
+#pragma unroll
+            for (int q = 0; q < kExChunk / 4; ++q) {
+                int32_t uc0, us0, uc1, us1;
+                ex_end(e0, g0.y, uc0, us0);
+                ex_end(e1, g1.y, uc1, us1);
+                if (q + 1 < kExChunk / 4) {
+                    const int p0 = 4 * (q + 1) + 2 * h;
+                    g0 = ex_begin(uphase(ds, p0));
+                    g1 = ex_begin(uphase(ds, p0 + 1));
+                    e0 = tab[g0.idx];
+                    e1 = tab[g1.idx];
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                mfmas(q, ex_digits(uc0), ex_digits(us0), ex_digits(uc1), ex_digits(us1));
             }
+#else
+#pragma unroll 2
+            for (int q = 0; q < kExChunk / 4; ++q) {
+                const int p0 = 4 * q + 2 * h;
+                int32_t uc0, us0, uc1, us1;
+                ex_sincos(tab, uphase(ds, p0), uc0, us0);
+                ex_sincos(tab, uphase(ds, p0 + 1), uc1, us1);
+                mfmas(q, ex_digits(uc0), ex_digits(us0), ex_digits(uc1), ex_digits(us1));
+            }
+#endif
             if ((c + 1) % kExFold == 0 || c + 1 == nch) {
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {

@@ -1,15 +1,26 @@
-"""Spin frequency and its derivative at an MJD (host scalar; sets the H-test trial frequency
-of measureToAs, measureToAs.py:210). Same result dict as CRIMP v2.3.0 ``ephemTmjd.py:19-77``:
-Taylor terms F0..F12 plus every glitch with Tmjd >= GLEP (GLF0, GLF1, GLF2 and a GLF0D/GLTD decay)."""
+"""Spin frequency and its derivative at an MJD (host; sets the H-test trial frequency of measureToAs,
+measureToAs.py:210). Same result dict as CRIMP v2.3.0 ``ephemTmjd.py:19-77``: Taylor terms F0..F12 plus every
+glitch with Tmjd >= GLEP (GLF0, GLF1, GLF2 and a GLF0D/GLTD decay). ``Tmjd`` may be an array (element-wise, as
+the reference's expressions are) and ``timMod`` an already parsed model dict (values or {value, flag}) as well
+as a .par path, so that a ToA loop parses the model once."""
 from math import factorial
 
 import numpy as np
 
-from .readtimingmodel import ReadTimingModel
+from .readtimingmodel import ReadTimingModel, get_parameter_value
+
+
+def _model(timMod):
+    if isinstance(timMod, dict):
+        p = {k: get_parameter_value(v) for k, v in timMod.items()}
+        for k in range(13):
+            p.setdefault("F%d" % k, 0.0)  # absent Taylor terms are 0 (readtimingmodel.py:64-65)
+        return p
+    return ReadTimingModel(timMod).readfulltimingmodel()[0]
 
 
 def ephemTmjd(Tmjd, timMod):
-    p = ReadTimingModel(timMod).readfulltimingmodel()[0]
+    p = _model(timMod)
     dts = (Tmjd - p["PEPOCH"]) * 86400
     f = p["F0"]
     for k in range(1, 13):

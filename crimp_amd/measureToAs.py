@@ -21,8 +21,10 @@ from .calcphase import calcphase
 from .ephemTmjd import ephemTmjd
 from .eventfile import EvtFileOps
 from .logging_utils import configure_logging, get_logger
-from .periodsearch import PeriodSearch
+from . import ops
+from ._native import STAT_H
 from .readPPtemplate import readPPtemplate
+from .readtimingmodel import ReadTimingModel
 from .timfile import phshiftTotimfile
 from .toafit import ToAFitter
 from .toafit_vary import VaryParamFitter
@@ -138,33 +140,49 @@ HEADER = ('ToA \t ToA_mid \t ToA_start \t ToA_end \t ToA_lenInt \t ToA_exp \t nb
           ' \t phShift_LL \t phShift_UL \t Hpower \t redChi2\n')
 
 
+def select_intervals(TIMEMJD, starts, ends):
+    """Concatenated photons of every interval [start, end] (inclusive, measureToAs.py:173-174) and the offsets.
+    Time-sorted input (event files are): two binary searches per interval; otherwise the reference's mask."""
+    T = np.asarray(TIMEMJD, dtype=np.float64)
+    starts, ends = np.asarray(starts, dtype=np.float64), np.asarray(ends, dtype=np.float64)
+    if T.size < 2 or np.all(T[1:] >= T[:-1]):
+        lo = np.searchsorted(T, starts, side="left")
+        hi = np.maximum(np.searchsorted(T, ends, side="right"), lo)
+        offs = np.concatenate([[0], np.cumsum(hi - lo)]).astype(np.int64)
+        idx = np.concatenate([np.arange(a, b) for a, b in zip(lo, hi)]) if len(lo) else np.zeros(0, np.int64)
+        return T[idx.astype(np.int64)], offs
+    sel = [T[(T >= a) & (T <= b)] for a, b in zip(starts, ends)]
+    return (np.concatenate(sel) if sel else np.zeros(0)), np.concatenate([[0], np.cumsum([x.size for x in sel])]).astype(
+        np.int64)
+
+
 def measure_intervals(TIMEMJD, timMod, tempModPP, starts, ends, exposures, phShiftRes=1000, nbrBins=15, varyAmps=False,
                       brutemin=False, readvaryparam=False):
-    """Batched core of measureToAs on in-memory arrays: per interval ToA_mid, fit dict entries, H power."""
+    """Batched core of measureToAs on in-memory arrays: per interval ToA_mid, fit dict entries, H power.
+    The timing model is parsed once; photons of all intervals are folded in one calcphase call, fitted in one
+    device fit, and H-tested (measureToAs.py:210-212) in one crimp_search_sets launch."""
     tmpl = readPPtemplate(tempModPP) if isinstance(tempModPP, str) else tempModPP
     model = str(tmpl["model"]).lower()
-    sel, mids, offs = [], [], [0]
-    for a, b in zip(starts, ends):
-        t = TIMEMJD[(TIMEMJD >= a) & (TIMEMJD <= b)]  # measureToAs.py:173-174
-        mids.append(((t[-1] - t[0]) / 2) + t[0])       # :182 (IndexError on an empty interval, as the reference)
-        sel.append(t)
-        offs.append(offs[-1] + t.size)
-    allt = np.concatenate(sel)
-    _, folded = calcphase(allt, timMod)
+    tm = timMod if isinstance(timMod, dict) else ReadTimingModel(str(timMod)).readfulltimingmodel()[0]
+    allt, offs = select_intervals(TIMEMJD, starts, ends)
+    n = np.diff(offs)
+    if np.any(n <= 0):  # measureToAs.py:182 reads TIME_toa[-1] of every interval
+        raise IndexError("index -1 is out of bounds for axis 0 with size 0 (a ToA interval holds no photons)")
+    first, last = allt[offs[:-1]], allt[offs[1:] - 1]
+    mids = ((last - first) / 2) + first                 # measureToAs.py:182
+    _, folded = calcphase(allt, tm)
     if model in ("cauchy", "vonmises"):
         folded = folded * (2 * np.pi)                  # :195, :200
     if readvaryparam:
-        res = VaryParamFitter(folded, np.array(offs), np.asarray(exposures, dtype=np.float64), tmpl, phShiftRes,
+        res = VaryParamFitter(folded, offs, np.asarray(exposures, dtype=np.float64), tmpl, phShiftRes,
                               nbrBins).fit(brutemin=brutemin)
     else:
-        fit = ToAFitter(folded, np.array(offs), np.asarray(exposures, dtype=np.float64), tmpl, phShiftRes, nbrBins)
+        fit = ToAFitter(folded, offs, np.asarray(exposures, dtype=np.float64), tmpl, phShiftRes, nbrBins)
         res = fit.fit(brutemin=brutemin, vary_amps=bool(varyAmps))
-    hp = []
-    for t, mid in zip(sel, mids):
-        eph = ephemTmjd(mid, timMod)
-        hp.append(PeriodSearch(t * 86400, np.atleast_1d(eph["freqAtTmjd"]), nbrHarm=5).htest()[0])  # :210-212
-    res["ToA_mid"] = np.array(mids)
-    res["htestPow"] = np.array(hp)
+    freqs = np.atleast_1d(ephemTmjd(mids, tm)["freqAtTmjd"])          # :210
+    hp = ops.search_sets(allt * 86400, offs, freqs, 5, STAT_H)      # :211-212, one trial per interval
+    res["ToA_mid"] = mids
+    res["htestPow"] = np.asarray(hp)
     return res
 
 

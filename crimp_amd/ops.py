@@ -123,6 +123,22 @@ def search(t, t0, freq, nharm, stat, log10_negfdot=None, first=0, count=None, ou
     return out
 
 
+def search_sets(t, offsets, freq, nharm, stat):
+    """One-trial Z^2 / H of many photon sets (crimp_search_sets): set i = t[offsets[i]:offsets[i+1]] (seconds) at
+    freq[i], each with its own t0 = (first + last)/2. fp64."""
+    L = N.load()
+    b = N.Buffers()
+    tp = b.arg(t, np.float64)
+    op = b.arg(offsets, np.int64)
+    fp = b.arg(freq, np.float64)
+    nset = int((offsets.numel() if N._is_torch(offsets) else np.size(offsets)) - 1)
+    out = _empty_like_input(t, nset, b)
+    outp = b.arg(out, np.float64, writable=True)
+    with b.device_guard():
+        N.check(L.crimp_search_sets(tp, op, nset, fp, int(nharm), int(stat), outp, b.flags(), b.stream()))
+    return out
+
+
 def make_template(model, amps, locs, wids=None, amp_shift=1.0):
     """crimp_template from arrays (model in {'fourier','cauchy','vonmises'})."""
     from scipy.special import i0

@@ -112,6 +112,12 @@ int crimp_search(const double* t, int64_t n, double t0, const double* freq, int6
                  const double* log10_negfdot, int64_t nfd, int32_t nharm, int32_t stat, int64_t first,
                  int64_t count, double* out, uint32_t flags, void* stream);
 
+/* Many one-trial searches at once: for every set i, PeriodSearch(t[offsets[i]:offsets[i+1]], [freq[i]],
+ * nbrHarm).htest() / .ztest()   [periodsearch.py:40-125 as measureToAs.py:210-212 calls it per ToA interval;
+ * t0 = (first + last)/2 of each set, :54]. t in seconds; out[nset]. fp64 (the reference's precision). */
+int crimp_search_sets(const double* t, const int64_t* offsets, int64_t nset, const double* freq, int32_t nharm,
+                      int32_t stat, double* out, uint32_t flags, void* stream);
+
 /* Fourier|WrappedCauchy|VonMises(theta, x).loglikelihood{FS,CA,VM}normalized(exposure) and its
  * (norm, phShift) derivatives at arbitrary points   [templatemodels.py:98-121, 201-226, 306-329].
  * x: folded phases of all intervals concatenated, interval i = x[offsets[i] : offsets[i+1]]

@@ -124,6 +124,34 @@ def test_ephemtmjd_matches_reference():
         assert e["freqAtTmjd"] == f and e["freqdotAtTmjd"] == fd
 
 
+def test_ephemtmjd_vectorised_and_parsed_model():
+    """measure_intervals evaluates ephemTmjd once over all ToA mids with the model parsed once: the frequencies
+    (the H-test trials) equal the reference's per-ToA values to the last bit or within 1 ulp."""
+    from crimp_amd.ephemTmjd import ephemTmjd
+    from crimp_amd.readtimingmodel import ReadTimingModel
+    g = gold("toa_1e2259.npz")
+    tm = ReadTimingModel(gpath("1e2259.par")).readfulltimingmodel()[0]
+    e = ephemTmjd(np.asarray(g["mid"]), tm)
+    np.testing.assert_array_max_ulp(e["freqAtTmjd"], g["freq"], maxulp=1)
+    np.testing.assert_array_max_ulp(e["freqdotAtTmjd"], g["fdot"], maxulp=1)
+
+
+def test_select_intervals_equals_reference_mask():
+    """Interval selection by binary search on time-sorted photons (and the reference's mask otherwise,
+    measureToAs.py:173-174) returns the reference's photons, inclusive bounds, in order."""
+    from crimp_amd.measureToAs import select_intervals
+    rng = np.random.default_rng(7)
+    t = np.sort(rng.uniform(0.0, 100.0, 5000))
+    starts = np.array([1.0, t[10], 50.0, 99.9])
+    ends = np.array([2.0, t[20], 50.0 + 1e-9, 120.0])
+    for tt in (t, rng.permutation(t)):
+        x, off = select_intervals(tt, starts, ends)
+        ref = [tt[(tt >= a) & (tt <= b)] for a, b in zip(starts, ends)]
+        assert off.tolist() == np.concatenate([[0], np.cumsum([r.size for r in ref])]).tolist()
+        np.testing.assert_array_equal(x, np.concatenate(ref))
+    assert select_intervals(t, starts, ends)[1][2] - select_intervals(t, starts, ends)[1][1] == 11  # t[10]..t[20]
+
+
 def test_error_scan_phase_sequence_clip_semantics():
     """lmfit clips a stepped phShift to [-pi, pi] once, then the loop moves the bound (measureToAs.py:332-334)."""
     from crimp_amd.toafit import ToAFitter
