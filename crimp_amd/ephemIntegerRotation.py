@@ -3,6 +3,7 @@
 ``ephemIntegerRotation.py:25-86``. A per-ToA scalar used only by the .tim writer; the
 phase is evaluated on the host with the reference's own NumPy expression
 (calcphase.py:80-126) so the written ToAs match CRIMP's digits."""
+import argparse
 from math import factorial
 
 import numpy as np
@@ -57,3 +58,19 @@ def ephemIntegerRotation(Tmjd, timMod, printOutput=False, tol_phase=1e-10, max_i
               f"rotation = {t}. Corresponding frequency = {eph['freqAtTmjd']}. Corresponding phase = {ph}\n "
               f"Phase residual from integer = {out['phase_residual_from_integer']}")
     return out
+
+
+def main(argv=None):
+    """ephemintegerrotation CLI (ephemIntegerRotation.py:89-99)."""
+    parser = argparse.ArgumentParser(description="Calculate earliest MJD (and corresponding spin frequency and "
+                                                 "rotational phase) that results in an integer number of rotations")
+    parser.add_argument("tMJD", help="Time in MJD at which to derive frequency and rotational phase", type=float)
+    parser.add_argument("timMod", help="Timing model in text format. A tempo2 .par file should work", type=str)
+    parser.add_argument("-po", "--printOutput", help="Print output", default=False,
+                        action=argparse.BooleanOptionalAction)
+    args = parser.parse_args(argv)
+    ephemIntegerRotation(args.tMJD, args.timMod, args.printOutput)
+
+
+if __name__ == "__main__":
+    main()

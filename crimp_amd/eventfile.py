@@ -7,9 +7,14 @@ consumes, restating the parts of CRIMP v2.3.0 ``eventfile.py`` on the ToA path:
   * ``build_time_energy_df`` TIME/86400 + MJDREF and PI -> keV per telescope (:238-280)
   * ``filtenergy``          inclusive energy cut (pandas ``between``)         (:282-298)
   * ``filttime``            inclusive time cut                                (:300-316)
+  * ``addphasecolEF``       PHASE column from calcphase on the device, the EVENTS table rewritten in place
+                            (and optionally a non-barycentred file's) (:319-375); ``main`` = ``addphasecolumn`` (:378)
 The conversions keep the reference's operation order (``TIME / 86400 + MJDREF``,
 ``PI * 0.01`` for NICER/SWIFT) so the MJDs are bit-identical to the astropy path.
 """
+import argparse
+import os
+
 import numpy as np
 
 _CODES = {"L": ("u1", 1), "B": ("u1", 1), "I": (">i2", 2), "J": (">i4", 4), "K": (">i8", 8), "E": (">f4", 4),
@@ -194,6 +199,21 @@ class EvtFileOps:
         self.time_energy_df = self.time_energy_df.loc[mask].copy()
         return self
 
+    def addphasecolEF(self, timMod, nonBaryEvtFile=None):
+        """PHASE column (cycle-folded phase of TIME / 86400 + MJDREF under ``timMod``, calcphase.py:152-176 on the
+        device) appended to the EVENTS table of this file, and to that of ``nonBaryEvtFile`` when given
+        (eventfile.py:319-375). Returns the header keywords (readEF)."""
+        from .calcphase import calcphase
+        kw = self.readEF()
+        hdr, start = self._hdu("EVENTS")
+        cols = read_table(self._raw, hdr, start)
+        timeMJD = cols["TIME"] / 86400 + kw["MJDREF"]
+        _, folded = calcphase(timeMJD, timMod)
+        add_column(self.evtFile, "EVENTS", "PHASE", np.asarray(folded, dtype=np.float64))
+        if nonBaryEvtFile is not None:
+            add_column(nonBaryEvtFile, "EVENTS", "PHASE", np.asarray(folded, dtype=np.float64))
+        self._raw, self._hdus = read_fits(self.evtFile)
+        return kw
 
     def read_fpmsel(self):
         """NICER FPM_SEL extension condensed to selected / on detector counts per time stamp
@@ -279,3 +299,80 @@ def write_events_fits(path, time, pi, mjdrefi, mjdreff, telescope="NICER"):
     data += b"\0" * (((len(data) + 2879) // 2880) * 2880 - len(data))
     with open(path, "wb") as fh:
         fh.write(prim + ext + data)
+
+
+def _header_cards(raw, hstart, dstart):
+    """The 80-character cards of the header in raw[hstart:dstart] (END card and padding excluded)."""
+    text = raw[hstart:dstart].decode("ascii", errors="replace")
+    cards = [text[i:i + 80] for i in range(0, len(text), 80)]
+    return cards[:next(i for i, c in enumerate(cards) if c[:8].strip() == "END")]
+
+
+def add_column(path, extname, name, values):
+    """Append a double-precision column to a BINTABLE extension of a FITS file in place (the astropy
+    Table.add_column + fits.update of eventfile.py:345-353): each row gets 8 big-endian bytes, the header gets
+    NAXIS1 += 8, TFIELDS += 1, TTYPEn / TFORMn = 'D'; every other HDU is copied byte for byte. A table with a
+    heap keeps it (THEAP moved with the main table). Like astropy, refuses a name the table already has."""
+    raw, hdus = read_fits(path)
+    out, found = [], False
+    pos = 0  # each header starts where the previous HDU's (padded) data ends
+    for hdr, dstart, dsize in hdus:
+        hstart = pos
+        cards = _header_cards(raw, hstart, dstart)
+        dend = dstart + ((dsize + 2879) // 2880) * 2880
+        if str(hdr.get("EXTNAME", "")).strip() != extname or found:
+            out.append(raw[hstart:dend])
+            pos = dend
+            continue
+        found = True
+        width, nrow, nf = int(hdr["NAXIS1"]), int(hdr["NAXIS2"]), int(hdr["TFIELDS"])
+        names = [str(hdr.get("TTYPE%d" % c, "")).strip() for c in range(1, nf + 1)]
+        if name in names:
+            raise ValueError("Duplicate column names: %s" % name)
+        vals = np.asarray(values, dtype=">f8").reshape(-1)
+        if vals.size != nrow:
+            raise ValueError("Inconsistent data column lengths: %d rows, %d values" % (nrow, vals.size))
+        rows = np.frombuffer(raw, dtype=np.uint8, count=width * nrow, offset=dstart).reshape(nrow, width)
+        newrows = np.concatenate([rows, vals.view(np.uint8).reshape(nrow, 8)], axis=1)
+        pcount = int(hdr.get("PCOUNT", 0))
+        heap = raw[dstart + width * nrow:dstart + width * nrow + pcount] if pcount else b""
+        new = []
+        for c in cards:
+            k = c[:8].strip()
+            if k == "NAXIS1":
+                c = _card("NAXIS1", width + 8)
+            elif k == "TFIELDS":
+                c = _card("TFIELDS", nf + 1)
+            elif k == "THEAP":
+                c = _card("THEAP", int(hdr["THEAP"]) + 8 * nrow)
+            new.append(c)
+        # the new column's keywords go after the last existing column keyword
+        last = max(i for i, c in enumerate(new) if c[:5] in ("TTYPE", "TFORM", "TUNIT", "TZERO", "TSCAL", "TDISP",
+                                                              "TNULL", "TDIM"))
+        new[last + 1:last + 1] = [_card("TTYPE%d" % (nf + 1), name), _card("TFORM%d" % (nf + 1), "D")]
+        data = newrows.tobytes() + heap
+        out.append(_block(new))
+        out.append(data + b"\0" * (((len(data) + 2879) // 2880) * 2880 - len(data)))
+        pos = dend
+    if not found:
+        raise KeyError("no %s extension in %s" % (extname, path))
+    out.append(raw[pos:])
+    tmp = path + ".tmp%d" % os.getpid()
+    with open(tmp, "wb") as fh:
+        fh.write(b"".join(out))
+    os.replace(tmp, path)
+
+
+def main(argv=None):
+    """addphasecolumn CLI (eventfile.py:378-390)."""
+    parser = argparse.ArgumentParser(description="Create and append event file with Phase column")
+    parser.add_argument("evtFile", help="Name of (X-ray) fits event file", type=str)
+    parser.add_argument("timMod", help="Timing model for phase folding, e.g., a .par file", type=str)
+    parser.add_argument("-ne", "--nonBaryEvtFile", help="Name of non-barycentered event file", type=str,
+                        default=None)
+    args = parser.parse_args(argv)
+    EvtFileOps(args.evtFile).addphasecolEF(args.timMod, args.nonBaryEvtFile)
+
+
+if __name__ == "__main__":
+    main()

@@ -194,3 +194,53 @@ def test_ephem_integer_rotation_lands_on_integer_phase():
     from crimp_amd.ephemIntegerRotation import ephemIntegerRotation
     e = ephemIntegerRotation(58144.25468778948, gpath("1e2259.par"))
     assert abs(e["phase_residual_from_integer"]) < 1e-6 and e["Tmjd_intRotation"] <= 58144.25468778948
+
+
+def test_crimp_import_name_and_entry_points():
+    """``import crimp.<module>`` resolves to the drop-in modules; the reference's console scripts for the provided
+    modules (pyproject.toml:36-48) are declared in pyproject.toml and setup.cfg and their targets exist."""
+    import importlib
+    import crimp.periodsearch
+    import crimp_amd.periodsearch
+    assert crimp.periodsearch is crimp_amd.periodsearch
+    from crimp.measureToAs import measureToAs  # noqa: F401
+    with pytest.raises(ImportError):
+        importlib.import_module("crimp.plot_pps")  # out of scope (SURVEY.md section 2)
+    want = {"timeintervalsfortoas": "buildtimeintervalsToAs", "templatepulseprofile": "pulseprofile",
+            "measuretoas": "measureToAs", "addphasecolumn": "eventfile", "ephemintegerrotation": "ephemIntegerRotation",
+            "phshifttotimfile": "timfile"}
+    py = open(os.path.join(ROOT, "pyproject.toml")).read()
+    cfg = open(os.path.join(ROOT, "setup.cfg")).read()
+    for script, mod in want.items():
+        line = '%s = "crimp_amd.%s:main"' % (script, mod)
+        assert line in py, line
+        assert "%s = crimp_amd.%s:main" % (script, mod) in cfg
+        assert callable(getattr(importlib.import_module("crimp_amd." + mod), "main"))
+
+
+def test_add_column_rewrites_events_table(tmp_path):
+    """The FITS rewrite of addphasecolEF (eventfile.py:345-353): every original column, the other HDUs and the
+    header keywords survive; the new double column reads back exactly; a duplicate name is refused."""
+    from crimp_amd.eventfile import EvtFileOps, add_column, read_fits, read_table, write_fits
+    p = str(tmp_path / "e.fits")
+    t = np.linspace(0.0, 1.0e4, 777)
+    flags = np.zeros((777, 8), bool)
+    flags[::3, 2] = True
+    write_fits(p, [("EVENTS", [("TIME", "D", t), ("PI", "J", np.arange(777) % 600), ("EVENT_FLAGS", "8L", flags)],
+                    {"TELESCOP": "NICER", "MJDREFI": 56658, "MJDREFF": 0.000777592592592593}),
+                   ("GTI", [("START", "D", np.array([0.0, 20.0])), ("STOP", "D", np.array([10.0, 30.0]))], {})])
+    before = EvtFileOps(p).readEF()
+    ph = np.random.default_rng(1).uniform(0, 1, 777)
+    add_column(p, "EVENTS", "PHASE", ph)
+    raw, hdus = read_fits(p)
+    ev = read_table(raw, hdus[1][0], hdus[1][1])
+    np.testing.assert_array_equal(ev["TIME"], t)
+    np.testing.assert_array_equal(ev["PI"], np.arange(777) % 600)
+    np.testing.assert_array_equal(ev["EVENT_FLAGS"], flags)
+    np.testing.assert_array_equal(ev["PHASE"], ph)
+    assert EvtFileOps(p).readEF() == before
+    np.testing.assert_array_equal(EvtFileOps(p).readGTI()[1][:, 0], np.array([0.0, 20.0]) / 86400 + before["MJDREF"])
+    with pytest.raises(ValueError):
+        add_column(p, "EVENTS", "PHASE", ph)
+    with pytest.raises(ValueError):
+        add_column(p, "EVENTS", "PHASE2", ph[:5])

@@ -513,3 +513,56 @@ def test_readvaryparam_peaked_vs_oracle(gpu, model):
     assert r["phShi_LL"][0] == o["phShi_LL"] and r["phShi_UL"][0] == o["phShi_UL"]
     assert r["LLmax"][0] >= o["LLmax"] - 1e-6
     np.testing.assert_allclose(r["theta"][0], o["theta"], rtol=1e-4, atol=1e-6)
+
+
+def test_addphasecolumn_cli_phases(gpu, tmp_path):
+    """addphasecolumn (eventfile.py:319-390) on a FITS file written from the bundled events: the PHASE column
+    equals the oracle's calcphase of TIME/86400 + MJDREF (calcphase.py:152-176) within 1e-9 cycles, in both the
+    barycentred file and the -ne file; the original columns are untouched."""
+    from crimp_amd.eventfile import main, write_events_fits, read_fits, read_table
+    ev = gold("events_1e2259.npz")
+    paths = []
+    for name in ("bary.fits", "nonbary.fits"):
+        p = str(tmp_path / name)
+        write_events_fits(p, ev["TIME"], ev["PI"], int(ev["MJDREFI"]), float(ev["MJDREFF"]))
+        paths.append(p)
+    main([paths[0], gpath("1e2259.par"), "-ne", paths[1]])
+    mjd = ev["TIME"] / 86400 + (int(ev["MJDREFI"]) + float(ev["MJDREFF"]))
+    from crimp_amd.readtimingmodel import ReadTimingModel
+    _, ref = O.calcphase(mjd, ReadTimingModel(gpath("1e2259.par")).readfulltimingmodel()[0])
+    for p in paths:
+        raw, hdus = read_fits(p)
+        cols = read_table(raw, hdus[1][0], hdus[1][1])
+        np.testing.assert_array_equal(cols["TIME"], ev["TIME"])
+        d = np.abs(cols["PHASE"] - ref)
+        assert np.max(np.minimum(d, 1 - d)) <= 1e-9
+
+
+def test_search_sets_equals_per_interval_search(gpu):
+    """crimp_search_sets (one launch for every ToA interval's H_5 at f(ToA_mid), measureToAs.py:210-212) equals
+    PeriodSearch(...).htest() interval by interval: the reference's H5 of ToAs 35-41 within 1e-9 relative, and
+    the fp64 path on synthetic sets of 1..5000 photons within 1e-9 relative."""
+    from crimp_amd import ops
+    from crimp_amd.periodsearch import PeriodSearch
+    from crimp_amd._native import STAT_H, STAT_Z2
+    from crimp_amd.measureToAs import select_intervals
+    g = gold("toa_1e2259.npz")
+    ev = gold("events_1e2259.npz")
+    keep = (ev["PI"] * 0.01 >= 1.0) & (ev["PI"] * 0.01 <= 5.0)
+    mjd = ev["TIME"][keep] / 86400 + (int(ev["MJDREFI"]) + float(ev["MJDREFF"]))
+    iv = pd.read_csv(gpath("timIntToAs_1e2259.txt"), sep=r"\s+", comment="#")
+    t, off = select_intervals(mjd, iv["ToA_tstart"].to_numpy()[g["ids"]], iv["ToA_tend"].to_numpy()[g["ids"]])
+    np.testing.assert_array_equal(np.diff(off), g["n"])
+    h = ops.search_sets(t * 86400, off, g["freq"], 5, STAT_H)
+    close_rel(h, g["h5"], 1e-9)
+    rng = np.random.default_rng(5)
+    sizes = np.array([1, 2, 3, 64, 1000, 5000])
+    x = np.sort(rng.uniform(0, 1e4, sizes.sum())) + 5.0e9
+    o = np.concatenate([[0], np.cumsum(sizes)])
+    fr = rng.uniform(0.1, 3.0, sizes.size)
+    for stat, m in ((STAT_Z2, 2), (STAT_H, 7), (STAT_H, 20)):
+        got = ops.search_sets(x, o, fr, m, stat)
+        for i in range(sizes.size):
+            ps = PeriodSearch(x[o[i]:o[i + 1]], np.array([fr[i]]), m, precision="f64")
+            ref = ps.ztest() if stat == STAT_Z2 else ps.htest()
+            close_rel(got[i:i + 1], ref, 1e-9)
