@@ -9,7 +9,7 @@ tab-separated, 13 columns, :161-162, :222-226).
 
 ``varyAmps`` runs on the device (crimp_toa_fit); ``readvaryparam`` frees the template parameters
 flagged ``vary True`` (crimp_amd/toafit_vary.py, photon sums on the device through
-crimp_toa_shape_points). Not implemented (raises ``NotImplementedError``): the two together.
+crimp_toa_shape_points); with both, ampShift is freed after the readvaryparam fit (:306-312).
 """
 import argparse
 import math
@@ -92,20 +92,14 @@ def defineinitialfitparam(tempModPP, readvaryparam=False):
     return p, 2
 
 
-def _check_opts(varyAmps, readvaryparam):
-    if readvaryparam and varyAmps:
-        raise NotImplementedError("readvaryparam together with varyAmps is not implemented in this build")
-
-
 def _single(model, tempModPP, phases, exposureInt, phShiftRes, nbrBins, varyAmps, brutemin, readvaryparam,
             plotLLs, plotPPs):
-    _check_opts(varyAmps, readvaryparam)
     if str(tempModPP["model"]).lower() != model:
         raise ValueError("template model %s used with measureToA_%s" % (tempModPP["model"], model))
     x = np.ascontiguousarray(np.ravel(phases), dtype=np.float64)
     if readvaryparam:
         r = VaryParamFitter(x, np.array([0, x.size]), np.array([float(exposureInt)]), tempModPP, phShiftRes,
-                            nbrBins).fit(brutemin=brutemin)
+                            nbrBins, vary_amps=bool(varyAmps)).fit(brutemin=brutemin)
     else:
         fit = ToAFitter(x, np.array([0, x.size]), np.array([float(exposureInt)]), tempModPP, phShiftRes, nbrBins)
         r = fit.fit(brutemin=brutemin, vary_amps=bool(varyAmps))
@@ -175,7 +169,7 @@ def measure_intervals(TIMEMJD, timMod, tempModPP, starts, ends, exposures, phShi
         folded = folded * (2 * np.pi)                  # :195, :200
     if readvaryparam:
         res = VaryParamFitter(folded, offs, np.asarray(exposures, dtype=np.float64), tmpl, phShiftRes,
-                              nbrBins).fit(brutemin=brutemin)
+                              nbrBins, vary_amps=bool(varyAmps)).fit(brutemin=brutemin)
     else:
         fit = ToAFitter(folded, offs, np.asarray(exposures, dtype=np.float64), tmpl, phShiftRes, nbrBins)
         res = fit.fit(brutemin=brutemin, vary_amps=bool(varyAmps))
@@ -191,7 +185,6 @@ def measureToAs(evtFile, timMod, tempModPP, toagtifile, eneLow=0.5, eneHigh=10.,
                 plotLLs=False, toaFile='ToAs', timFile=None):
     """ToAs of every interval of ``toagtifile`` (measureToAs.py:64-251)."""
     import pandas as pd
-    _check_opts(varyAmps, readvaryparam)
     logger.info("\n Running measureToAs with input parameters: evtFile: %s timMod: %s tempModPP: %s toagtifile: %s"
                 " eneLow: %s eneHigh: %s toaStart: %s toaEnd: %s phShiftRes: %s brutemin: %s toaFile: %s",
                 evtFile, timMod, tempModPP, toagtifile, eneLow, eneHigh, toaStart, toaEnd, phShiftRes, brutemin,

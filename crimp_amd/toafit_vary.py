@@ -12,6 +12,11 @@ at each phShift step, starting from the best fit as the reference does (``initPa
 is a copy of the best-fit parameters, :319), and redChi2 counts the free parameters the way
 :733-748 does (norm and the freed template parameters -- not phShift).
 
+``varyAmps`` together with ``readvaryparam`` (:306-312 after :727-801): once the freed parameters are fitted,
+ampShift (a common factor on every template amplitude) is freed in [0.01, 100] from 1 and everything free is
+maximised again; the 1-sigma scan then re-maximises ampShift too, and redChi2 counts one more free parameter.
+The parameter vector is then [norm, template..., ampShift, phShift].
+
 Deviation: with ``brutemin`` the reference hands every free parameter to lmfit's brute grid (20
 points per bounded parameter without a ``brute_step``: 20^k x 126 evaluations). Here the brute start
 is the (norm, phShift) grid of the default path with the template's shape, then the full local
@@ -29,8 +34,9 @@ from .toafit import CHI2_1SIG_1DOF, TWO_PI, ToAFitter
 class VaryParamFitter(ToAFitter):
     """readvaryparam fits of every interval of one concatenated folded-phase array."""
 
-    def __init__(self, x, offsets, exposure, tmpl, ph_shift_res=1000, nbr_bins=15, device=None):
+    def __init__(self, x, offsets, exposure, tmpl, ph_shift_res=1000, nbr_bins=15, device=None, vary_amps=False):
         super().__init__(x, offsets, exposure, tmpl, ph_shift_res, nbr_bins, device)
+        self.vary_amps = bool(vary_amps)
         K, m = self.K, self.model
         names, val, lo, hi, vary = ["norm"], [self.norm0], [self.norm0 / 5], [self.norm0 * 5], [bool(tmpl["norm"]["vary"])]
         for k in range(1, K + 1):
@@ -47,6 +53,12 @@ class VaryParamFitter(ToAFitter):
                 lo.append(l)
                 hi.append(h)
                 vary.append(bool(tmpl[nm]["vary"]))
+        if self.vary_amps:  # measureToAs.py:308: ampShift 1 in [0.01, 100], freed after the first fit
+            names.append("ampShift")
+            val.append(1.0)
+            lo.append(0.01)
+            hi.append(100.0)
+            vary.append(False)
         names.append("phShift")
         val.append(0.0)
         lo.append(-self.pb)
@@ -61,13 +73,18 @@ class VaryParamFitter(ToAFitter):
         self.evals = np.zeros(self.nint, dtype=np.int64)
 
     # ------------------------------------------------------------------ one batch of evaluations
+    def _amp_shift(self, th):
+        return float(th[-2]) if self.vary_amps else 1.0
+
     def _template(self, th):
+        """Device template of a parameter vector (amplitudes times ampShift), its amplitudes and widths."""
         K = self.K
         if self.model == "fourier":
             amps, locs, wids = th[1:1 + 2 * K:2], th[2:2 + 2 * K:2], None
         else:
             amps, locs, wids = th[1:1 + 3 * K:3], th[2:2 + 3 * K:3], th[3:3 + 3 * K:3]
-        return ops.make_template(self.model, amps, locs, wids, 1.0), amps, wids
+        A = self._amp_shift(th)
+        return ops.make_template(self.model, np.asarray(amps) * A, locs, wids, 1.0), amps, wids
 
     def evaluate_theta(self, iv, thetas):
         """LL and its gradient over the full parameter vector at (interval, theta) points."""
@@ -78,10 +95,11 @@ class VaryParamFitter(ToAFitter):
         if self.model == "vonmises":
             from scipy.special import i0e, i1e
             aux = np.zeros((iv.size, N.MAX_COMP))
+        A = np.array([self._amp_shift(th) for th in thetas])
         for p, th in enumerate(thetas):
             t, amps, wids = self._template(th)
             tpls.append(t)
-            amp_sum[p] = np.sum(amps)
+            amp_sum[p] = np.sum(amps) * A[p]
             if aux is not None:
                 kap = 1.0 / np.asarray(wids) ** 2
                 aux[p, :K] = i1e(kap) / i0e(kap)
@@ -96,6 +114,10 @@ class VaryParamFitter(ToAFitter):
         for j in range(K):
             for c in range(step):
                 g[:, 1 + step * j + c] = s[:, 4 + 3 * j + c]
+        # the device sums are gradients in the effective amplitudes amp_j * ampShift
+        ga = g[:, 1:1 + step * K:step].copy()
+        if self.model != "fourier":
+            ga -= (E / TWO_PI)[:, None]                     # dF/d(amp_j ampShift) = 1
         with np.errstate(divide="ignore", invalid="ignore"):
             if self.model == "fourier":
                 ll = -n * E + Np * np.log(n * E) + (s[:, 0] - Np * np.log(n))
@@ -104,7 +126,9 @@ class VaryParamFitter(ToAFitter):
                 F = TWO_PI * n + amp_sum
                 ll = -F * E / TWO_PI + Np * np.log(F * E / TWO_PI) + (s[:, 0] - Np * np.log(F))
                 ok = s[:, 1] / F > 0
-                g[:, 1:1 + 3 * K:3] -= (E / TWO_PI)[:, None]   # dF/damp_j = 1 (ampShift 1)
+        g[:, 1:1 + step * K:step] = ga * A[:, None]
+        if self.vary_amps:
+            g[:, -2] = np.sum(ga * thetas[:, 1:1 + step * K:step], axis=1)
         ll = np.where(ok, ll, -np.inf)
         return ll, g
 
@@ -204,6 +228,9 @@ class VaryParamFitter(ToAFitter):
         return th, F
 
     def fit(self, brutemin=False):
+        if self.vary_amps:  # ampShift is fixed at 1 for the first fit
+            self.vary[-2] = False
+        self.nfree = int(self.vary[:-1].sum())
         if brutemin:
             n0, p0 = self.brute()
         else:
@@ -212,11 +239,17 @@ class VaryParamFitter(ToAFitter):
         starts[:, 0] = np.clip(n0, self.blo[0], self.bhi[0])
         starts[:, -1] = p0
         theta_hat, ll_max = self._maximise_batch(np.arange(self.nint), starts, self.vary)
+        if self.vary_amps:  # measureToAs.py:306-312: free ampShift from 1 and refit everything free
+            self.vary[-2] = True
+            self.nfree += 1
+            theta_hat[:, -2] = 1.0
+            theta_hat, ll_max = self._maximise_batch(np.arange(self.nint), theta_hat, self.vary)
         lo_err, up_err = self._scan(theta_hat, ll_max)
         rchi2 = self._reduced_chi2_theta(theta_hat)
         return {"phShi": theta_hat[:, -1].copy(), "phShi_LL": lo_err, "phShi_UL": up_err, "reducedChi2": rchi2,
                 "norm": theta_hat[:, 0].copy(), "LLmax": ll_max, "theta": theta_hat, "names": list(self.names),
-                "evaluations": self.evals.copy(), "ampShift": np.ones(self.nint)}
+                "evaluations": self.evals.copy(),
+                "ampShift": theta_hat[:, -2].copy() if self.vary_amps else np.ones(self.nint)}
 
     # ------------------------------------------------------------------ 1-sigma scan
     def _scan(self, theta_hat, ll_max):

@@ -566,3 +566,27 @@ def test_search_sets_equals_per_interval_search(gpu):
             ps = PeriodSearch(x[o[i]:o[i + 1]], np.array([fr[i]]), m, precision="f64")
             ref = ps.ztest() if stat == STAT_Z2 else ps.htest()
             close_rel(got[i:i + 1], ref, 1e-9)
+
+
+def test_readvaryparam_with_varyamps_vs_oracle(gpu):
+    """readvaryparam + varyAmps (measureToAs.py:306-312 after :727-801): norm and ph_2 freed by the template,
+    then ampShift freed in [0.01, 100] and everything refitted; the 1-sigma scan re-maximises all three. Against
+    the oracle's restatement (parity unpinned: no reference output exercises the combination)."""
+    from crimp_amd.measureToAs import measureToA_fourier
+    from crimp_amd.readPPtemplate import readPPtemplate
+    from crimp_amd.toafit_vary import VaryParamFitter
+    g, iv, _ = _golden_rows()
+    E = iv["ToA_exposure"].to_numpy()[g["ids"]]
+    tm = _vary_template(readPPtemplate(gpath("1e2259_template.txt")), {"norm", "ph_2"})
+    r = VaryParamFitter(g["folded"], g["offsets"], E, tm, vary_amps=True).fit()
+    i = 2
+    x = g["folded"][g["offsets"][i]:g["offsets"][i + 1]]
+    o = O.fit_toa_readvary(x, E[i], tm, vary_amps=True)
+    assert abs(r["phShi"][i] - o["phShi"]) / (2 * math.pi) < 1e-6
+    assert r["LLmax"][i] == pytest.approx(o["LLmax"], abs=1e-5)
+    assert r["LLmax"][i] >= o["LLmax"] - 1e-6
+    assert r["ampShift"][i] == pytest.approx(o["ampShift"], rel=1e-4)
+    assert r["phShi_LL"][i] == o["phShi_LL"] and r["phShi_UL"][i] == o["phShi_UL"]
+    assert r["reducedChi2"][i] == pytest.approx(o["reducedChi2"], rel=1e-4)
+    s = measureToA_fourier(tm, x, E[i], readvaryparam=True, varyAmps=True)
+    assert s["phShi"] == pytest.approx(r["phShi"][i], abs=1e-9)

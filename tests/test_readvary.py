@@ -8,7 +8,7 @@ import pandas as pd
 import pytest
 
 from conftest import gold, gpath
-from crimp_amd.measureToAs import defineinitialfitparam, measureToA_fourier
+from crimp_amd.measureToAs import defineinitialfitparam
 from crimp_amd.readPPtemplate import readPPtemplate
 from oracle import oracle as O
 
@@ -40,10 +40,23 @@ def test_defineinitialfitparam_readvaryparam():
     assert (p["phShift"].min, p["phShift"].max) == (-1.5 * np.pi, 1.5 * np.pi)
 
 
-def test_readvary_with_varyamps_is_rejected():
-    t = readPPtemplate(gpath("1e2259_template.txt"))
-    with pytest.raises(NotImplementedError):
-        measureToA_fourier(t, np.array([0.1, 0.2]), 10.0, varyAmps=True, readvaryparam=True)
+def test_oracle_readvary_with_varyamps_norm_only_is_the_varyamps_fit():
+    """readvaryparam + varyAmps (measureToAs.py:306-312 after :727-801) with only the norm free is the default
+    fit's varyAmps problem (norm, ampShift, phShift free; the norm bounds inactive): the two oracle
+    restatements agree. Parity beyond the oracle is unpinned (no reference output exercises either)."""
+    g = gold("toa_1e2259.npz")
+    iv = pd.read_csv(gpath("timIntToAs_1e2259.txt"), sep=r"\s+", comment="#")
+    E = iv["ToA_exposure"].to_numpy()[g["ids"]]
+    base = readPPtemplate(gpath("1e2259_template.txt"))
+    i = 2
+    x = g["folded"][g["offsets"][i]:g["offsets"][i + 1]]
+    o = O.fit_toa_readvary(x, E[i], _with_vary(base, {"norm"}), vary_amps=True)
+    d = O.fit_toa_vary_amps(x, E[i], base)
+    assert abs(o["phShi"] - d["phShi"]) / (2 * math.pi) < 1e-6
+    assert o["LLmax"] == pytest.approx(d["LLmax"], abs=1e-5)
+    assert o["ampShift"] == pytest.approx(d["ampShift"], rel=1e-4)
+    assert (o["phShi_LL"], o["phShi_UL"]) == (d["phShi_LL"], d["phShi_UL"])
+    assert o["reducedChi2"] * 13 == pytest.approx(d["reducedChi2"] * 12, rel=1e-4)  # dof 15-2 vs 15-3
 
 
 def test_oracle_readvary_norm_only_is_the_default_fit():
