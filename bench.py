@@ -1,16 +1,23 @@
-"""Benchmark: Z^2_2 photon x trial evaluations per second (BASELINE.json metric, config 3).
+"""Benchmark: Z^2_2 photon x trial evaluations per second (BASELINE.json metric, config 3), plus the ToA-fit and
+calcphase legs.
 
-One step = one complete Z^2_2 search of the config-3 workload per GPU: 1e7 synthetic pulsed
-photons (T = 1e6 s, p = 0.1, f0 = 7.123456789 Hz, seed 0) against 1e6 trial frequencies
-spaced 1/(10T), inputs resident in HBM, followed by the search's one exchange step (every
-rank's best trial gathered so that all ranks agree on the global best, ties -> lowest index).
-With N ranks each rank searches its own 1e6-trial slice of an N*1e6 grid (weak scaling);
-``value`` = all ranks' evaluations / max-over-ranks time.
+One step = one complete Z^2_2 search of the config-3 workload per GPU on the default (exact) path: 1e7 synthetic
+pulsed photons (T = 1e6 s, p = 0.1, f0 = 7.123456789 Hz, seed 0) against 1e6 trial frequencies spaced 1/(10T),
+inputs resident in HBM, followed by the search's one exchange step (every rank's best trial gathered so that all
+ranks agree on the global best, ties -> lowest index). With N ranks each rank searches its own 1e6-trial slice of
+an N*1e6 grid (weak scaling); ``value`` = all ranks' evaluations / max-over-ranks time.
 
-Also reported: the dominant kernel's roofline (algorithmic FLOP per launch / measured launch
-time: 8 real FLOP per photon x trial x harmonic, the complex multiply-accumulate of the
-factorised search), and the CPU oracle (oracle/liborc.so, OpenMP over trials) on
-a bounded sample of the same workload.
+Also reported:
+* ``roofline``: the exact kernel (k_search_exact) is bound by the i8 matrix-core issue rate: 8 MFMAs
+  (v_mfma_i32_32x32x32_i8, 65536 ops each) per 4 photons x 1024 trials x harmonic = 128 ops per
+  photon*trial*harmonic, against the 5.0 POP/s i8 dense peak; kernel time from hipEvents around the harmonic-sum
+  kernels on their stream; ``traffic`` from the same tree's rocprofv3 PMC pass (profiles/r02/pmc_traffic.json)
+  when it was taken on this workload;
+* ``cpu_baseline``: the oracle (oracle/liborc.so, fp64, OpenMP over trials) on a bounded sample;
+* ``fast_path``: the opt-in fp32 sin/cos path (precision="fast") on the same workload, for comparison;
+* ToA (config 5 per GPU): the device fit of 1250 intervals x 1e5 photons, and the end-to-end ``measure_intervals``
+  (interval selection, calcphase, fits, per-interval H-test) from host MJD arrays, with the oracle's fits on all
+  allowed host cores as its CPU baseline (a sample, extrapolated) and the fits' VALU roofline.
 """
 import argparse
 import json
@@ -23,15 +30,11 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-PEAK_F32_TFLOPS = 157.3         # MI355X_MICROARCH.md: FP32-input MFMA = FP32 vector peak
-PEAK_F16_DENSE_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16/F16 dense (no 2:1 sparsity)
-SPLIT_PRODUCTS = 4              # f16 hi/lo split: one fp32-exact product = four f16 products
-# HBM bytes per harmonic-sum launch of this workload from rocprofv3 PMC passes (profiles/): (2 x FETCH_SIZE
-# + WRITE_SIZE) KB x 1024, FETCH_SIZE doubled per the gfx950 correction in MI355X_MICROARCH.md (HBM section).
-PMC_TRAFFIC_BYTES = {"f16": (2 * 659900.0 + 2019000.0) * 1024,  # profiles/r1_final2/pmc_s64/pmc_summary.txt (64 splits)
-                     "f32": (2 * 588447.5625 + 153453.875) * 1024}  # profiles/r1/search_mfma_pmc_summary.json
-FLOP_PER_EVAL_HARM = 8.0
+PEAK_I8_TOPS = 5000.0           # MI355X_MICROARCH.md: I8 MFMA = 2x the BF16 dense rate (2.5 PF)
+OPS_PER_EVAL_HARM = 128.0       # 8 x v_mfma_i32_32x32x32_i8 (2*32*32*32 ops) per 4 photons x 1024 trials x harmonic
 PEAK_HBM_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E ~8 TB/s
+PEAK_VALU_SLOTS = 256 * 4 * 32 * 2.4e9   # lane-slots/s: 256 CUs x 4 SIMD-32 x 2.4 GHz
+PMC_FILE = os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json")
 
 
 def parse():
@@ -42,14 +45,26 @@ def parse():
     p.add_argument("--photons", type=int, default=10_000_000)
     p.add_argument("--trials", type=int, default=1_000_000, help="trial frequencies per GPU")
     p.add_argument("--nharm", type=int, default=2)
-    p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline legs")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--no-fast", action="store_true", help="skip the fast-path comparison")
     p.add_argument("--toa-intervals", type=int, default=1250, help="ToA intervals per GPU (config 5: 1e4 over 8)")
     p.add_argument("--toa-photons", type=int, default=100_000)
-    p.add_argument("--no-toa", action="store_true", help="skip the ToA-fit throughput leg")
+    p.add_argument("--no-toa", action="store_true", help="skip the ToA legs")
     p.add_argument("--calcphase-photons", type=int, default=100_000_000)
     p.add_argument("--no-calcphase", action="store_true", help="skip the calcphase (HBM-bound) leg")
     return p.parse_args()
+
+
+def host_cores():
+    """CPU threads this process may use: its affinity set, capped by OMP_NUM_THREADS when the host sets it (the
+    GPU box gives each GPU 16 of the machine's CPUs), and the machine's count for the record."""
+    try:
+        allowed = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        allowed = os.cpu_count() or 1
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return (min(allowed, omp) if omp > 0 else allowed), os.cpu_count()
 
 
 # 1E 2259+586 Fourier template (data/1e2259_template.txt), config 5 draws intervals from it
@@ -60,18 +75,27 @@ T2259 = {"model": "fourier", "norm": {"value": 17.060771467236613},
                 -0.1917798112304259, 0.8297144204463391]}
 
 
-def toa_leg(a, dev, world, rank):
-    """Config 5 (per GPU): intervals x photons drawn from the 1e2259 template with random true shifts,
-    brute grid + exact MLE + 1-sigma scan + redChi2 per interval (measureToA_fourier -bm); ``warmup``
-    untimed fits, then the mean over up to 3 timed fits of all intervals (max over ranks)."""
-    import torch
-    import torch.distributed as dist
-    from crimp_amd.synth import template_intervals_torch
-    from crimp_amd.toafit import ToAFitter
+def _tmpl():
     tm = {"model": "fourier", "norm": T2259["norm"]}
     for j, (am, ph) in enumerate(zip(T2259["amp"], T2259["ph"]), start=1):
         tm["amp_%d" % j] = {"value": am}
         tm["ph_%d" % j] = {"value": ph}
+    return tm
+
+
+def toa_leg(a, dev, world, rank):
+    """Config 5 (per GPU): intervals x photons drawn from the 1e2259 template with random true shifts,
+    brute grid + exact MLE + 1-sigma scan + redChi2 per interval (measureToA_fourier -bm).
+    (1) device fit of phases resident in HBM: ``warmup`` untimed fits, then the mean of up to 3 timed fits;
+    (2) end to end from host MJD arrays: measure_intervals (one upload of the times, interval selection,
+        calcphase, the fits, the per-interval H_5), one untimed and one timed call."""
+    import torch
+    import torch.distributed as dist
+    from crimp_amd.synth import template_intervals_torch
+    from crimp_amd.toafit import ToAFitter
+    from crimp_amd import _native as N
+    from crimp_amd.measureToAs import measure_intervals
+    tm = _tmpl()
     x, off, E, shifts = template_intervals_torch(a.toa_intervals, a.toa_photons, T2259["norm"]["value"],
                                                  T2259["amp"], T2259["ph"], seed=2 + rank, device=dev)
     for _ in range(max(a.warmup, 0)):  # untimed: code-object load, scratch-pool growth
@@ -85,23 +109,88 @@ def toa_leg(a, dev, world, rank):
         res = ToAFitter(x, off, E, tm).fit(brutemin=True)
     torch.cuda.synchronize()
     el = (time.perf_counter() - t1) / reps
+    # kernel split of one fit (hipEvents around the brute-grid and the fit kernels inside crimp_toa_fit)
+    from crimp_amd import ops
+    f = ToAFitter(x, off, E, tm)
+    ops.toa_fit(f.x, f.offsets, f.tpl, f._arr(f.E, np.float64), f.norm0, f.res, True, False,
+                flags=N.FLAG_TIME_KERNELS)
+    grid_ms, fit_ms = N.last_kernel_times()[:2]
     elt = torch.tensor([el], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(elt, op=dist.ReduceOp.MAX)
     d = np.angle(np.exp(1j * (res["phShi"] - shifts)))  # recovered vs true shift, wrapped
-    return {"toa_fits_per_s": a.toa_intervals * world / float(elt.item()),
-            "toa_config": "config5: %d intervals/GPU x %d photons, Fourier K=6 (1e2259), brute+MLE+1-sigma scan"
-                          % (a.toa_intervals, a.toa_photons),
-            "toa_seconds": float(elt.item()),
-            "toa_mean_likelihood_evaluations": float(np.mean(res["evaluations"])),
-            "toa_shift_recovery_rms_cycles": float(np.sqrt(np.mean(d ** 2)) / (2 * np.pi)),
-            "toa_median_sigma_cycles": float(np.median(res["phShi_LL"]) / (2 * np.pi)),
-            "toa_cpu_reference_fits_per_s": 0.42}
+    out = {"toa_fits_per_s": a.toa_intervals * world / float(elt.item()),
+           "toa_config": "config5: %d intervals/GPU x %d photons, Fourier K=6 (1e2259), brute+MLE+1-sigma scan"
+                         % (a.toa_intervals, a.toa_photons),
+           "toa_seconds": float(elt.item()),
+           "toa_mean_likelihood_evaluations": float(np.mean(res["evaluations"])),
+           "toa_shift_recovery_rms_cycles": float(np.sqrt(np.mean(d ** 2)) / (2 * np.pi)),
+           "toa_median_sigma_cycles": float(np.median(res["phShi_LL"]) / (2 * np.pi)),
+           "toa_kernel_ms": {"k_toa_grid": grid_ms, "k_toa_fit": fit_ms}}
+    # VALU roofline of the brute grid (the dominant ToA kernel): per photon and phShift, K fp32 FMA pairs for the
+    # template (2K slots) + per norm one add, one multiply and 1/4 of a quarter-rate log plus an add (2.5 + 1) slots:
+    # S = 2K + 20 * 3.5 = 82 slots (K = 6) per photon x phShift, 126 phShifts
+    slots = a.toa_intervals * a.toa_photons * 126 * (2 * 6 + 20 * 3.5)
+    ach = slots / (grid_ms * 1e-3)
+    out["toa_roofline"] = {"kernel": "k_toa_grid", "bound": "valu", "achieved": ach / 1e12, "peak": PEAK_VALU_SLOTS / 1e12,
+                           "unit": "Tslot/s", "frac": ach / PEAK_VALU_SLOTS,
+                           "note": "82 VALU lane-slots per photon x phShift (12 template FMAs + 20 norms x (add, mul, "
+                                   "1/4 v_log_f32 at 4 slots, add)) / k_toa_grid hipEvent time; 4 SIMD-32 x 256 CUs x "
+                                   "2.4 GHz peak"}
+    # end to end from host arrays: photon times t = (cycle + phase) / F0 around PEPOCH, intervals bracketing them
+    F0, pep = 0.5, 58000.0
+    cyc = torch.arange(x.numel(), device=dev, dtype=torch.float64)
+    tsec = (cyc + x) / F0
+    mjd = (pep + tsec / 86400.0).cpu().numpy()
+    offh = off.cpu().numpy()
+    starts = mjd[offh[:-1]] - 1e-9
+    ends = mjd[offh[1:] - 1] + 1e-9
+    del cyc, tsec
+    par = {"PEPOCH": pep, "F0": F0}
+    for k in range(1, 13):
+        par["F%d" % k] = 0.0
+    measure_intervals(mjd, par, tm, starts, ends, E, brutemin=True)   # untimed: allocation / code objects
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    r2 = measure_intervals(mjd, par, tm, starts, ends, E, brutemin=True)
+    torch.cuda.synchronize()
+    e2e = time.perf_counter() - t1
+    out["toa_e2e_fits_per_s"] = a.toa_intervals / e2e
+    out["toa_e2e_seconds"] = e2e
+    out["toa_e2e_note"] = ("measure_intervals from host MJD arrays (%d photons): upload, interval selection, calcphase, "
+                           "brute+MLE+1-sigma fits, redChi2, per-interval H_5 (measureToAs.py:168-226 minus file I/O)"
+                           % mjd.size)
+    out["toa_e2e_max_shift_diff_vs_device_fit_cycles"] = float(np.max(np.abs(
+        np.angle(np.exp(1j * (r2["phShi"] - res["phShi"]))))) / (2 * np.pi))
+    if not a.no_cpu and rank == 0:
+        out["toa_cpu_baseline"] = toa_cpu_baseline(x, off, E, tm, a.cpu_seconds)
+    return out
+
+
+def toa_cpu_baseline(x, off, E, tm, budget_s):
+    """The oracle's measureToA_fourier restatement (fp64 C likelihoods, OpenMP) on every allowed host core over
+    the first config-5 intervals until ``budget_s`` has passed; extrapolated as fits/s."""
+    from oracle import oracle as O
+    cores, visible = host_cores()
+    O.set_threads(cores)
+    xs = x[: int(off[min(8, off.numel() - 1)])].cpu().numpy()
+    oh = off[:9].cpu().numpy()
+    t1 = time.perf_counter()
+    done = 0
+    for i in range(min(8, oh.size - 1)):
+        O.fit_toa(xs[oh[i]:oh[i + 1]], E[i], tm, brutemin=True)
+        done += 1
+        if time.perf_counter() - t1 > budget_s:
+            break
+    el = time.perf_counter() - t1
+    return {"value": done / el, "unit": "ToA fits/s", "cores": cores, "host_cpus_visible": visible, "kind": "port",
+            "sample": "%d config-5 intervals (1e5 photons, brute+MLE+1-sigma scan), oracle fit_toa, %.1f s; "
+                      "reference log: 0.42 fits/s at 1e4 photons (BASELINE.md)" % (done, el)}
 
 
 def calcphase_leg(a, dev):
     """calcphase (calcphase.py:152-176) over 1e8 photons resident in HBM: 8 B read + 16 B written per photon
-    (SURVEY.md §8d), HBM-bound; hipEvents on the stream the library launches on (torch's current stream)."""
+    (SURVEY.md section 8d), HBM-bound; hipEvents on the stream the library launches on (torch's current stream)."""
     import torch
     from crimp_amd import ops
     from crimp_amd import _native as N
@@ -138,10 +227,11 @@ def calcphase_leg(a, dev):
 
 
 def cpu_baseline(t, f0, df, nharm, budget_s):
-    """Oracle (fp64 C restatement of periodsearch.py:57-71, OpenMP over trials) on a bounded sample."""
+    """Oracle (fp64 C restatement of periodsearch.py:57-71, OpenMP over trials) on a bounded sample, on every host
+    core this process may use."""
     from oracle import oracle as O
-    threads = min(16, os.cpu_count() or 1)
-    O.set_threads(threads)
+    cores, visible = host_cores()
+    O.set_threads(cores)
     n = min(t.size, 1_000_000)
     ts = np.ascontiguousarray(t[:n])
     m = 64
@@ -154,9 +244,21 @@ def cpu_baseline(t, f0, df, nharm, budget_s):
             break
         m = int(m * min(16.0, max(2.0, 1.2 * budget_s / max(el, 1e-3))))
     rate = n * m / el
-    return {"value": rate, "unit": "photon*trial evals/s", "cores": threads, "kind": "port",
+    return {"value": rate, "unit": "photon*trial evals/s", "cores": cores, "host_cpus_visible": visible, "kind": "port",
             "sample": "%d photons x %d trials of the same workload, Z^2_%d, oracle/liborc.so fp64, %.1f s" % (
                 n, m, nharm, el)}
+
+
+def pmc_traffic(photons, trials, nharm):
+    """HBM bytes per search of this workload from the tree's own rocprofv3 PMC pass (tools/pmc_exact.sh ->
+    profiles/r02/pmc_traffic.json), or None if that pass was not taken on this workload."""
+    try:
+        rec = json.load(open(PMC_FILE))
+    except (OSError, ValueError):
+        return None, None
+    if (rec.get("photons"), rec.get("trials"), rec.get("nharm")) != (photons, trials, nharm):
+        return None, None
+    return rec.get("bytes_per_search"), rec.get("source")
 
 
 def main():
@@ -187,11 +289,12 @@ def main():
     best = torch.zeros(2, dtype=torch.float64, device=dev)
     gathered = torch.zeros(world, 2, dtype=torch.float64, device=dev)
 
-    kms = []
+    kms, fixups = [], []
 
     def step():
         ops.search(t, t0, f, a.nharm, 0, out=out, flags=N.FLAG_TIME_KERNELS)
         kms.append(N.load().crimp_last_kernel_ms())
+        fixups.append(N.load().crimp_last_fixups())
         i = torch.argmax(out)
         best[0] = out[i]
         best[1] = (i + (g0 + (world * M) // 2)).to(torch.float64)  # global trial index
@@ -204,6 +307,7 @@ def main():
     for _ in range(a.warmup):
         step()
     kms.clear()
+    fixups.clear()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -232,11 +336,11 @@ def main():
 
     evals = float(a.photons) * M * world * a.steps
     value = evals / el
+    rec = None
     if rank == 0:
-        flop = FLOP_PER_EVAL_HARM * a.nharm * float(a.photons) * M
-        achieved = flop / (kern_ms * 1e-3) / 1e12
-        variant = "f32" if os.environ.get("CRIMP_MFMA", "").lower() == "f32" else "f16"
-        peak = PEAK_F32_TFLOPS if variant == "f32" else PEAK_F16_DENSE_TFLOPS / SPLIT_PRODUCTS
+        ops_per_launch = OPS_PER_EVAL_HARM * a.nharm * float(a.photons) * M
+        achieved = ops_per_launch / (kern_ms * 1e-3) / 1e12
+        traffic, tsrc = pmc_traffic(a.photons, M, a.nharm)
         rec = {
             "metric": "Z^2_2 photon*trial evals/sec (node)",
             "value": value,
@@ -248,26 +352,32 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": ("f32-input MFMA" if variant == "f32" else "f16 hi/lo-split MFMA (fp32-exact products)")
-                     + ", f32 sin/cos, f64 phase + sums",
+            "dtype": "int8 digits on i8 MFMA, exact int32/int64 sums (fp64 phase, 2^30 fixed-point cos/sin)",
             "data": "synthetic (seeded Poisson pulsed events, crimp_amd/synth.py)",
             "config": {"workload": "config3: synthetic %d photons x %d trials/GPU, Z^2_%d" % (a.photons, M, a.nharm),
                        "photons": a.photons, "trials_per_gpu": M, "nharm": a.nharm, "span_s": span, "f0": f0,
                        "trial_step_hz": df, "parallelism": "trial-sharded dp%d + all_gather(best)" % world,
                        "best_trial_index": best_idx, "best_power": float(gb[order[0], 0]),
-                       "search_path": os.environ.get("CRIMP_SEARCH", "auto")},
-            "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-                         "frac": achieved / peak,
-                         "traffic": PMC_TRAFFIC_BYTES[variant]
-                         if (a.photons, M, a.nharm) == (10_000_000, 1_000_000, 2) else None,
+                       "search_path": "exact (default precision)", "fp64_fixup_trials_per_step": float(np.mean(fixups))},
+            "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_I8_TOPS, "unit": "TFLOP/s",
+                         "frac": achieved / PEAK_I8_TOPS, "traffic": traffic,
                          "kernel_ms": kern_ms, "step_ms": step_ms,
-                         "note": "achieved = 8 FLOP (one complex MAC) per photon*trial*harmonic / mean duration of the "
-                                 "harmonic-sum kernels (hipEvents in libcrimp_hip on their stream); peak = "
-                                 + ("FP32-input MFMA" if variant == "f32" else
-                                    "F16 dense MFMA / 4 (four f16 products per fp32-exact product)")},
+                         "note": "int8 MFMA ops issued: 128 per photon*trial*harmonic (8 v_mfma_i32_32x32x32_i8 per 4 "
+                                 "photons x 1024 trials) / mean duration of the harmonic-sum kernels (hipEvents in "
+                                 "libcrimp_hip on their stream); peak = I8 dense MFMA (2x BF16 2.5 PF); 10 of every 16 "
+                                 "byte products are digit-level products (DESIGN.md); traffic: %s" % (
+                                     tsrc or "no PMC pass on this workload")},
         }
         if not a.no_cpu:
             rec["cpu_baseline"] = cpu_baseline(t_h, f0, df, a.nharm, a.cpu_seconds)
+        if not a.no_fast:  # the opt-in fp32 sin/cos path on the same inputs (not the metric)
+            ops.search(t, t0, f, a.nharm, 0, out=out, precision="fast")
+            torch.cuda.synchronize()
+            t2 = time.perf_counter()
+            ops.search(t, t0, f, a.nharm, 0, out=out, precision="fast")
+            torch.cuda.synchronize()
+            rec["fast_path"] = {"evals_per_s": float(a.photons) * M / (time.perf_counter() - t2),
+                                "precision": "fp32 sin/cos + f16-split MFMA: 1e-6 of the mean power, not per trial"}
     del t, f, out
     torch.cuda.empty_cache()
     if not a.no_calcphase and rank == 0:

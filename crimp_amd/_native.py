@@ -54,7 +54,8 @@ class Template(ctypes.Structure):
                 ("i0", ctypes.c_double * MAX_COMP), ("amp_shift", ctypes.c_double)]
 
 
-EXPORTS = ("crimp_version", "crimp_last_error", "crimp_last_kernel_ms", "crimp_last_fixups", "crimp_release_scratch",
+EXPORTS = ("crimp_version", "crimp_last_error", "crimp_last_kernel_ms", "crimp_last_kernel_times", "crimp_last_fixups",
+           "crimp_release_scratch",
            "crimp_device_count", "crimp_calcphase", "crimp_search", "crimp_search_sets", "crimp_toa_points",
            "crimp_toa_grid", "crimp_toa_fit", "crimp_toa_shape_points", "crimp_binphases")
 
@@ -80,6 +81,7 @@ def load(require_device=True):
             L.crimp_last_error.restype = ctypes.c_char_p
             L.crimp_last_kernel_ms.restype = ctypes.c_double
             L.crimp_last_fixups.restype = ctypes.c_int64
+            L.crimp_last_kernel_times.argtypes = [ctypes.POINTER(ctypes.c_double), i32]
             L.crimp_device_count.argtypes = [ctypes.POINTER(i32)]
             L.crimp_calcphase.argtypes = [P, i64, ctypes.POINTER(TimingModel), i32, P, P, u32, P]
             L.crimp_search.argtypes = [P, i64, ctypes.c_double, P, i64, P, i64, i32, i32, i64, i64, P, u32, P]
@@ -101,6 +103,14 @@ def load(require_device=True):
                                        "(there is no CPU fallback)")
             _dev_ok = True
     return _lib
+
+
+def last_kernel_times():
+    """Every timed span (ms) of the last native call made with FLAG_TIME_KERNELS (crimp_last_kernel_times)."""
+    L = load(require_device=False)
+    buf = (ctypes.c_double * 16)()
+    n = L.crimp_last_kernel_times(buf, 16)
+    return [buf[i] for i in range(min(n, 16))]
 
 
 def check(rc):

@@ -29,8 +29,10 @@
 static thread_local std::string g_err;
 static std::mutex g_mutex;
 
-// CRIMP_FLAG_TIME_KERNELS: hipEvents around the harmonic-sum kernels of the last search, or the calcphase kernel (ms)
+// CRIMP_FLAG_TIME_KERNELS: hipEvents around the timed spans of the last call (ms): the harmonic-sum kernels of a
+// search, the calcphase kernel, the brute-grid and the fit kernels of crimp_toa_fit
 static double g_last_kernel_ms = -1.0;
+static std::vector<double> g_kernel_times;
 // trials of the last crimp_search recomputed by the fp64 fix-up (exact path)
 static int64_t g_last_fixups = 0;
 struct KernelTimer {
@@ -47,8 +49,10 @@ struct KernelTimer {
         if (!on) return;
         (void)hipEventRecord(b, s);
         float ms = -1.0f;
-        if (hipEventSynchronize(b) == hipSuccess && hipEventElapsedTime(&ms, a, b) == hipSuccess)
-            g_last_kernel_ms = ms;
+        if (hipEventSynchronize(b) == hipSuccess && hipEventElapsedTime(&ms, a, b) == hipSuccess) {
+            if (g_kernel_times.empty()) g_last_kernel_ms = ms;
+            g_kernel_times.push_back(ms);
+        }
     }
     ~KernelTimer() {
         if (a) (void)hipEventDestroy(a);
@@ -922,6 +926,64 @@ __global__ __launch_bounds__(kSetBlock) void k_search_sets(const double* __restr
     if (tid == 0) out[set] = (stat == CRIMP_STAT_Z2) ? zsum * w : best;
 }
 
+// fp64 fix-up of a few trials over many photons (the exact path's flagged trials): block (t, split) sums the
+// harmonics k0 .. k0+G-1 of trial tidx[t] over photons of its split with fp64 sincospi of the exact phase of k0 and
+// fp64 angle addition (as k_search_f64), reduced across the block in a fixed order into part[split][2m][count].
+constexpr int kFixBlock = 256;
+template <int G, bool TWOD>
+__global__ __launch_bounds__(kFixBlock) void k_search_f64_few(
+    const double* __restrict__ dt, const double* __restrict__ dt2, int64_t n, int64_t chunk,
+    const double* __restrict__ freq, int64_t nf, const double* __restrict__ c2row, int64_t first,
+    const int64_t* __restrict__ tidx, int64_t count, int k0, int ncomp, double* __restrict__ part) {
+    __shared__ double red[kFixBlock / 64][2 * G];
+    const int64_t t = blockIdx.x;
+    const int64_t split = blockIdx.y;
+    const int64_t g = first + tidx[t];
+    const int64_t row = TWOD ? g / nf : 0;
+    const double f = freq[g - row * nf];
+    const double c2 = TWOD ? c2row[row] : 0.0;
+    const int64_t i0 = split * chunk;
+    const int64_t i1 = i0 + chunk < n ? i0 + chunk : n;
+    double C[G], S[G];
+#pragma unroll
+    for (int k = 0; k < G; ++k) C[k] = S[k] = 0.0;
+    for (int64_t i = i0 + threadIdx.x; i < i1; i += kFixBlock) {
+        const double ph = TWOD ? fma(f, dt[i], c2 * dt2[i]) : f * dt[i];
+        double s1 = 0.0, c1 = 1.0, s, c;
+        if (G > 1) sincospi(2.0 * (ph - rint(ph)), &s1, &c1);
+        if (k0 == 1 && G > 1) {
+            s = s1;
+            c = c1;
+        } else {
+            const double pk = ph * (double)k0;
+            sincospi(2.0 * (pk - rint(pk)), &s, &c);
+        }
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+            C[k] += c;
+            S[k] += s;
+            const double cn = fma(c, c1, -s * s1);
+            s = fma(s, c1, c * s1);
+            c = cn;
+        }
+    }
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+        const double cw = wave_sum(C[k]), sw = wave_sum(S[k]);
+        if (lane == 0) {
+            red[wid][2 * k] = cw;
+            red[wid][2 * k + 1] = sw;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 2 * G) {
+        double v = 0.0;
+        for (int w = 0; w < kFixBlock / 64; ++w) v += red[w][threadIdx.x];
+        part[(split * ncomp + 2 * (k0 - 1) + threadIdx.x) * count + t] = v;
+    }
+}
+
 #include "toa_fit.h"
 #include "toa_shape.h"
 
@@ -929,6 +991,12 @@ __global__ __launch_bounds__(kSetBlock) void k_search_sets(const double* __restr
 static hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 extern "C" double crimp_last_kernel_ms(void) { return g_last_kernel_ms; }
+
+extern "C" int crimp_last_kernel_times(double* ms, int32_t cap) {
+    const int n = (int)g_kernel_times.size();
+    for (int i = 0; i < n && i < cap; ++i) ms[i] = g_kernel_times[(size_t)i];
+    return n;
+}
 
 extern "C" int crimp_version(void) { return CRIMP_VERSION; }
 
@@ -965,6 +1033,10 @@ extern "C" int crimp_calcphase(const double* t_mjd, int64_t n, const crimp_timin
     ARGCHK(model->n_wave >= 0 && model->n_wave <= CRIMP_MAX_WAVE, "n_wave out of range");
     if (n == 0) return CRIMP_OK;
     std::lock_guard<std::mutex> lk(g_mutex);
+    if (flags & CRIMP_FLAG_TIME_KERNELS) {
+        g_kernel_times.clear();
+        g_last_kernel_ms = -1.0;
+    }
     const bool dev = flags & CRIMP_FLAG_DEVICE_PTRS;
     hipStream_t s = as_stream(stream);
     CPModel hm{};
@@ -1120,6 +1192,43 @@ static int direct_search(Scratch& sc, hipStream_t s, const double* dt, const dou
     return CRIMP_OK;
 }
 
+// fp64 fix-up of the trials first + tidx[t] (t < count), a few trials over all photons: photon splits of >= 4096
+// photons (up to 1024), one block per (trial, split), the splits combined by k_search_finalize into out[tidx[t]].
+static int fixup_search(Scratch& sc, hipStream_t s, const double* dt, const double* dt2, int64_t n, const double* freq,
+                        int64_t nf, const double* c2, bool twod, int nharm, int stat, int64_t first,
+                        const int64_t* tidx, int64_t count, double* out) {
+    const int64_t splits0 = std::max<int64_t>(1, std::min<int64_t>(1024, n / 4096));
+    const int64_t chunk = cdiv(n, splits0);
+    const int64_t splits = cdiv(n, chunk);
+    const int ncomp = 2 * nharm;
+    const int64_t cbmax = std::max<int64_t>(1, std::min<int64_t>(65535, part_budget() / (8 * splits * ncomp)));
+    double* part = nullptr;
+    HIPCHK(sc.alloc(&part, (size_t)(splits * ncomp * std::min<int64_t>(count, cbmax))));
+    for (int64_t b0 = 0; b0 < count; b0 += cbmax) {
+        const int64_t bc = std::min<int64_t>(cbmax, count - b0);
+        dim3 grid((unsigned)bc, (unsigned)splits);
+        for (int k0 = 1; k0 <= nharm;) {
+            const int rem = nharm - k0 + 1;
+            const int G = rem >= 8 ? 8 : rem >= 4 ? 4 : rem >= 2 ? 2 : 1;
+#define CRIMP_FX(GG)                                                                                                \
+    if (twod)                                                                                                       \
+        k_search_f64_few<GG, true><<<grid, kFixBlock, 0, s>>>(dt, dt2, n, chunk, freq, nf, c2, first, tidx + b0, bc, \
+                                                              k0, ncomp, part);                                     \
+    else                                                                                                            \
+        k_search_f64_few<GG, false><<<grid, kFixBlock, 0, s>>>(dt, dt2, n, chunk, freq, nf, c2, first, tidx + b0,   \
+                                                               bc, k0, ncomp, part)
+            if (G == 8) { CRIMP_FX(8); } else if (G == 4) { CRIMP_FX(4); } else if (G == 2) { CRIMP_FX(2); } else { CRIMP_FX(1); }
+#undef CRIMP_FX
+            HIPCHK(hipGetLastError());
+            k0 += G;
+        }
+        k_search_finalize<<<(unsigned)cdiv(bc, 256), 256, 0, s>>>(part, bc, (int)splits, nharm, stat, (double)n,
+                                                                 tidx + b0, out);
+        HIPCHK(hipGetLastError());
+    }
+    return CRIMP_OK;
+}
+
 // Arithmetic-progression check of the (device) frequency grid: 16 ulp of max|f| (k_ap_check). Writes delta
 // into ap[0] on the device (read by the factorised kernels) and returns whether the grid qualifies.
 static int grid_is_progression(Scratch& sc, hipStream_t s, const double* freq, int64_t nf, double** ap, bool* ok) {
@@ -1224,8 +1333,7 @@ static int exact_search(Scratch& sc, hipStream_t s, const double* dt, const doub
     HIPCHK(d2h(s, &nf_h, nflag, sizeof(int)));
     *nfixed = nf_h;
     if (nf_h == 0) return CRIMP_OK;
-    return direct_search(sc, s, dt, dt2, n, freq, nf, c2, twod, nharm, stat, first, flagged, nf_h, out, true, true,
-                         false, nullptr);
+    return fixup_search(sc, s, dt, dt2, n, freq, nf, c2, twod, nharm, stat, first, flagged, nf_h, out);
 }
 
 extern "C" int crimp_search(const double* t, int64_t n, double t0, const double* freq, int64_t nf,
@@ -1244,6 +1352,10 @@ extern "C" int crimp_search(const double* t, int64_t n, double t0, const double*
     ARGCHK(!(f64 && fast), "CRIMP_FLAG_F64 excludes the fast-path flags");
     if (count == 0) return CRIMP_OK;
     std::lock_guard<std::mutex> lk(g_mutex);
+    if (flags & CRIMP_FLAG_TIME_KERNELS) {
+        g_kernel_times.clear();
+        g_last_kernel_ms = -1.0;
+    }
     const bool dev = flags & CRIMP_FLAG_DEVICE_PTRS;
     hipStream_t s = as_stream(stream);
     g_last_fixups = 0;
@@ -1316,6 +1428,10 @@ extern "C" int crimp_search_sets(const double* t, const int64_t* offsets, int64_
     ARGCHK(nset <= 2147483647LL, "too many sets");
     if (nset == 0) return CRIMP_OK;
     std::lock_guard<std::mutex> lk(g_mutex);
+    if (flags & CRIMP_FLAG_TIME_KERNELS) {
+        g_kernel_times.clear();
+        g_last_kernel_ms = -1.0;
+    }
     const bool dev = flags & CRIMP_FLAG_DEVICE_PTRS;
     hipStream_t s = as_stream(stream);
     std::vector<int64_t> hoff((size_t)nset + 1);
@@ -1378,6 +1494,10 @@ extern "C" int crimp_toa_points(const double* x, const int64_t* offsets, int64_t
     if (rc) return rc;
     if (npts == 0) return CRIMP_OK;
     std::lock_guard<std::mutex> lk(g_mutex);
+    if (flags & CRIMP_FLAG_TIME_KERNELS) {
+        g_kernel_times.clear();
+        g_last_kernel_ms = -1.0;
+    }
     const bool dev = flags & CRIMP_FLAG_DEVICE_PTRS;
     hipStream_t s = as_stream(stream);
     // groups of <= 4 consecutive points sharing an interval (host needs the interval ids)
@@ -1474,6 +1594,10 @@ extern "C" int crimp_toa_fit(const double* x, const int64_t* offsets, int64_t ni
     const bool brutemin = options & CRIMP_TOA_BRUTE, vary_amps = options & CRIMP_TOA_VARY_AMPS;
     if (brutemin) ARGCHK(T.K <= kGridKMax, "brute grid supports at most 8 template components");
     std::lock_guard<std::mutex> lk(g_mutex);
+    if (flags & CRIMP_FLAG_TIME_KERNELS) {
+        g_kernel_times.clear();
+        g_last_kernel_ms = -1.0;
+    }
     const bool dev = flags & CRIMP_FLAG_DEVICE_PTRS;
     hipStream_t s = as_stream(stream);
     std::vector<int64_t> hoff((size_t)nint + 1);
@@ -1524,6 +1648,8 @@ extern "C" int crimp_toa_fit(const double* x, const int64_t* offsets, int64_t ni
             HIPCHK(sc.alloc(&dnrm, (size_t)(nint * nn)));
             HIPCHK(h2d(dphi, hphi.data(), nphi * sizeof(double)));
             HIPCHK(h2d(dnrm, hnrm.data(), nint * nn * sizeof(double)));
+            KernelTimer kg(s, flags & CRIMP_FLAG_TIME_KERNELS);  // brute grid: k_toa_grid + k_toa_grid_best
+            kg.start();
             for (int64_t i0 = 0; i0 < nint; i0 += 65535) {
                 const int64_t nb = std::min<int64_t>(65535, nint - i0);
                 int64_t maxn = 0;
@@ -1538,6 +1664,7 @@ extern "C" int crimp_toa_fit(const double* x, const int64_t* offsets, int64_t ni
                                                             dstart + 2 * i0);
                 HIPCHK(hipGetLastError());
             }
+            kg.stop();
         } else {  // Nelder-Mead starts from the template (norm0, phShift 0) (measureToAs.py:301)
             hstart.resize((size_t)(2 * nint));
             for (int64_t i = 0; i < nint; ++i) {
@@ -1546,6 +1673,8 @@ extern "C" int crimp_toa_fit(const double* x, const int64_t* offsets, int64_t ni
             }
             HIPCHK(h2d(dstart, hstart.data(), 2 * nint * sizeof(double)));
         }
+        KernelTimer kf(s, flags & CRIMP_FLAG_TIME_KERNELS);  // the fit kernel
+        kf.start();
         if (vary_amps) {
             k_toa_fit_amp<<<(unsigned)nint, kFitBlock, 0, s>>>(dx, doff, dT, de, dstart, C, dout);
         } else {
@@ -1554,6 +1683,7 @@ extern "C" int crimp_toa_fit(const double* x, const int64_t* offsets, int64_t ni
             k_toa_fit<<<(unsigned)nint, kFitBlock, 0, s>>>(dx, doff, dT, de, dstart, C, dout, hcache);
         }
         HIPCHK(hipGetLastError());
+        kf.stop();
         HIPCHK(copy_back(s, out, dout, (size_t)nint * 8, dev));
         HIPCHK(hipStreamSynchronize(s));
     }
@@ -1573,6 +1703,10 @@ extern "C" int crimp_toa_grid(const double* x, const int64_t* offsets, int64_t n
     if (rc) return rc;
     ARGCHK(T.K <= kGridKMax, "brute grid supports at most 8 template components");
     std::lock_guard<std::mutex> lk(g_mutex);
+    if (flags & CRIMP_FLAG_TIME_KERNELS) {
+        g_kernel_times.clear();
+        g_last_kernel_ms = -1.0;
+    }
     const bool dev = flags & CRIMP_FLAG_DEVICE_PTRS;
     hipStream_t s = as_stream(stream);
     std::vector<int64_t> hoff((size_t)nint + 1);
@@ -1648,6 +1782,10 @@ extern "C" int crimp_toa_shape_points(const double* x, const int64_t* offsets, i
         ARGCHK(pt_interval[p] >= 0 && pt_interval[p] < nint, "point interval out of range");
     }
     std::lock_guard<std::mutex> lk(g_mutex);
+    if (flags & CRIMP_FLAG_TIME_KERNELS) {
+        g_kernel_times.clear();
+        g_last_kernel_ms = -1.0;
+    }
     const bool dev = flags & CRIMP_FLAG_DEVICE_PTRS;
     hipStream_t s = as_stream(stream);
     std::vector<int64_t> hoff((size_t)nint + 1);
@@ -1709,6 +1847,10 @@ extern "C" int crimp_binphases(const double* x, const int64_t* offsets, int64_t 
     ARGCHK(x != nullptr && offsets != nullptr && edges != nullptr && counts != nullptr, "null argument");
     ARGCHK(nint <= 2147483647LL, "too many intervals");
     std::lock_guard<std::mutex> lk(g_mutex);
+    if (flags & CRIMP_FLAG_TIME_KERNELS) {
+        g_kernel_times.clear();
+        g_last_kernel_ms = -1.0;
+    }
     const bool dev = flags & CRIMP_FLAG_DEVICE_PTRS;
     hipStream_t s = as_stream(stream);
     int64_t ntot = 0;

@@ -33,22 +33,23 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kExTab = 4096;    // sin/cos table entries per turn
-#ifndef EX_CHUNK
-#define EX_CHUNK 32
-#endif
-constexpr int kExChunk = EX_CHUNK;  // photons per LDS chunk
+constexpr int kExChunk = 64;   // photons per LDS chunk (one barrier per chunk)
 constexpr int kExWaves = 8;     // waves (tiles) per block
 constexpr int kExBlock = 64 * kExWaves;
 constexpr int kExFold = 4096 / kExChunk;  // chunks between int32 -> int64 folds (4096 photons; overflow bound 2^31 at 16384)
 constexpr double kExUnit = 1.4551915228366852e-11;  // 2^-36: value of one unit of the int64 totals
 
 struct ExEntry {
-    int32_t sk, ck;  // rint(sin, cos * 2^30) - 0x4B400000 (the bias of the fp32 rounding trick below)
-    float s, c;      // fp32 sin, cos
+    int32_t sk, ck;  // rint(sin, cos(2 pi k / T) * 2^30) + 0x808080 - 0x4B400000: the fp32 rounding bias of ex_end and
+                     // the digit bias of ex_digits folded in
+    float s1, c1;    // sin, cos(2 pi k / T) * 2^30 * (2 pi / T): the residual rotation's first-order coefficients
 };
 
-// t in table units (turns * kExTab) -> (cos, sin) * 2^30 rounded to int32, in two halves so that the table
-// read of one photon can be issued ahead of the arithmetic of another (ex_begin / ex_end).
+// t in table units (turns * kExTab) -> the digit dwords of (cos, sin) * 2^30 (ex_digits of the rounded integers),
+// in two halves so that the table read of one photon can be issued ahead of the arithmetic of another.
+// x = 2 pi (k + y) / T, |y| <= 1/2: sin x = s_k + c_k sin(th) + s_k (cos(th) - 1) with th = 2 pi y / T, and to
+// 2^30 units  sin x * 2^30 = S_k + y (C1 - u S1),  cos x * 2^30 = C_k - y (S1 + u C1),  u = (pi / T) y,
+// (C1, S1 = (c_k, s_k) 2^30 2 pi / T); the dropped th^3/6 term is <= 0.08 units at the cell edge.
 struct ExArg {
     uint32_t idx;  // table index
     float y;       // residual in table steps, |y| <= 1/2
@@ -59,24 +60,39 @@ __device__ __forceinline__ ExArg ex_begin(double t) {
     const double kf = tm - M;
     return ExArg{(uint32_t)__double2loint(tm) & (kExTab - 1), (float)(t - kf)};  // t - kf is exact
 }
-__device__ __forceinline__ void ex_end(const ExEntry& e, float y, int32_t& yc, int32_t& ys) {
-    const float th = y * (6.2831853071795864769f / (float)kExTab);
-    const float th2 = th * th;
-    const float st = th * __builtin_fmaf(th2, -0.16666666666666666f, 1.0f);  // sin(th), error th^5/120
-    const float cm = th2 * -0.5f;                                           // cos(th) - 1, error th^4/24
-    const float dsn = __builtin_fmaf(e.c, st, e.s * cm);                    // sin(x) - s_k
-    const float dcs = __builtin_fmaf(-e.s, st, e.c * cm);                   // cos(x) - c_k
-    // |d * 2^30| < 2^22: the low mantissa bits of fma(d, 2^30, 1.5 * 2^23) are rint(d * 2^30) + 0x400000
-    ys = (int32_t)((uint32_t)e.sk + __float_as_uint(__builtin_fmaf(dsn, 1073741824.0f, 12582912.0f)));
-    yc = (int32_t)((uint32_t)e.ck + __float_as_uint(__builtin_fmaf(dcs, 1073741824.0f, 12582912.0f)));
+// -> digit dwords of cos (dc) and sin (ds)
+__device__ __forceinline__ void ex_end(const ExEntry& e, float y, uint32_t& dc, uint32_t& ds) {
+    const float u = y * (3.14159265358979323846f / (float)kExTab);
+    const float ts = __builtin_fmaf(-u, e.s1, e.c1);
+    const float tc = __builtin_fmaf(u, e.c1, e.s1);
+    // |value| < 2^22: the low mantissa bits of fma(y, t, 1.5 * 2^23) are rint(y t) + 0x400000
+    ds = ((uint32_t)e.sk + __float_as_uint(__builtin_fmaf(y, ts, 12582912.0f))) ^ 0x00808080u;
+    dc = ((uint32_t)e.ck + __float_as_uint(__builtin_fmaf(-y, tc, 12582912.0f))) ^ 0x00808080u;
 }
-__device__ __forceinline__ void ex_sincos(const ExEntry* __restrict__ tab, double t, int32_t& yc, int32_t& ys) {
+__device__ __forceinline__ void ex_sincos_digits(const ExEntry* __restrict__ tab, double t, uint32_t& dc,
+                                                 uint32_t& ds) {
     const ExArg g = ex_begin(t);
-    ex_end(tab[g.idx], g.y, yc, ys);
+    ex_end(tab[g.idx], g.y, dc, ds);
+}
+__device__ __forceinline__ ExEntry ex_entry(int i) {
+    double s, c;
+    sincospi((double)i * (2.0 / kExTab), &s, &c);
+    const double w = 1073741824.0 * (6.283185307179586476925 / kExTab);
+    ExEntry e;
+    e.s1 = (float)(s * w);
+    e.c1 = (float)(c * w);
+    e.sk = (int32_t)((uint32_t)(int32_t)rint(s * 1073741824.0) + 0x00808080u - 0x4B400000u);
+    e.ck = (int32_t)((uint32_t)(int32_t)rint(c * 1073741824.0) + 0x00808080u - 0x4B400000u);
+    return e;
 }
 
-__device__ __forceinline__ uint32_t ex_digits(int32_t y) { return ((uint32_t)y + 0x00808080u) ^ 0x00808080u; }
-__device__ __forceinline__ uint32_t ex_digits_neg(int32_t y) { return (0x00808080u - (uint32_t)y) ^ 0x00808080u; }
+// digit dword of -y from the digit dword of y: -y's balanced digits are the negated digits (with carries),
+// recomputed from the integer: y = (d ^ 0x808080) - 0x808080
+__device__ __forceinline__ uint32_t ex_neg_digits(uint32_t d) {
+    const uint32_t y = (d ^ 0x00808080u) - 0x00808080u;
+    return (0x00808080u - y) ^ 0x00808080u;
+}
+
 
 __device__ __forceinline__ int64_t ex_level_sum(int a3, int a4, int a5, int a6) {
     return (int64_t)a3 + ((int64_t)a4 << 8) + ((int64_t)a5 << 16) + ((int64_t)a6 << 24);
@@ -95,19 +111,7 @@ __global__ __launch_bounds__(kExBlock, 2) void k_search_exact(
     __shared__ double sdt2[TWOD ? 3 : 1][kExChunk];
     const int tid = threadIdx.x;
     const int lane = tid & 63, wv = tid >> 6;
-#ifdef EX_PRIO
-    if (wv >= kExWaves / 2) __builtin_amdgcn_s_setprio(1);  // the second-dispatched half wins issue arbitration
-#endif
-    for (int i = tid; i < kExTab; i += kExBlock) {
-        double s, c;
-        sincospi((double)i * (2.0 / kExTab), &s, &c);
-        ExEntry e;
-        e.s = (float)s;
-        e.c = (float)c;
-        e.sk = (int32_t)((uint32_t)(int32_t)rint(s * 1073741824.0) - 0x4B400000u);
-        e.ck = (int32_t)((uint32_t)(int32_t)rint(c * 1073741824.0) - 0x4B400000u);
-        tab[i] = e;
-    }
+    for (int i = tid; i < kExTab; i += kExBlock) tab[i] = ex_entry(i);
     const double kT = (double)kh * (double)kExTab;
     const int64_t T = (int64_t)blockIdx.x * kExWaves + wv;  // this wave's tile; waves past the end only produce V
     const bool active = T < ntiles;                          // wave-uniform
@@ -138,12 +142,12 @@ __global__ __launch_bounds__(kExBlock, 2) void k_search_exact(
 #pragma unroll
         for (int s = 0; s < kExChunk * 32 / kExBlock; ++s) {
             const int p = (tid >> 5) + (kExBlock / 32) * s;
-            int32_t yc, ys;
-            ex_sincos(tab, gbv * sdt[slot][p], yc, ys);
+            uint32_t dc, dsn;
+            ex_sincos_digits(tab, gbv * sdt[slot][p], dc, dsn);
             const bool live = i0 + (int64_t)c * kExChunk + p < i1;
-            const uint32_t rc = live ? __builtin_bswap32(ex_digits(yc)) : 0u;
-            const uint32_t rs = live ? __builtin_bswap32(ex_digits(ys)) : 0u;
-            const uint32_t rn = live ? __builtin_bswap32(ex_digits_neg(ys)) : 0u;
+            const uint32_t rc = live ? __builtin_bswap32(dc) : 0u;
+            const uint32_t rs = live ? __builtin_bswap32(dsn) : 0u;
+            const uint32_t rn = live ? __builtin_bswap32(ex_neg_digits(dsn)) : 0u;
             *(reinterpret_cast<uint2*>(&vre[vb][p >> 1][pb]) + (p & 1)) = make_uint2(rc, rn);
             *(reinterpret_cast<uint2*>(&vim[vb][p >> 1][pb]) + (p & 1)) = make_uint2(rs, rc);
         }
@@ -171,7 +175,12 @@ __global__ __launch_bounds__(kExBlock, 2) void k_search_exact(
         load_dt(c + 2, (c + 2) % 3);
         if (c + 1 < nch) produce(c + 1, (c + 1) % 3, vb ^ 1);
         if (active) {
-            auto mfmas = [&](int q, uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3) {
+#pragma unroll 2
+            for (int q = 0; q < kExChunk / 4; ++q) {
+                const int p0 = 4 * q + 2 * h;
+                uint32_t a0, a1, a2, a3;
+                ex_sincos_digits(tab, uphase(ds, p0), a0, a1);
+                ex_sincos_digits(tab, uphase(ds, p0 + 1), a2, a3);
                 const uint4 br = vre[vb][2 * q + h][ar], bi = vim[vb][2 * q + h][ar];
                 const i32x4 bre = {(int)br.x, (int)br.y, (int)br.z, (int)br.w};
                 const i32x4 bim = {(int)bi.x, (int)bi.y, (int)bi.z, (int)bi.w};
@@ -182,36 +191,7 @@ __global__ __launch_bounds__(kExBlock, 2) void k_search_exact(
                     acc[L][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A, bre, acc[L][0], 0, 0, 0);
                     acc[L][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A, bim, acc[L][1], 0, 0, 0);
                 }
-            };
-#ifdef EX_PIPE
-            // quad q+1's table reads are issued before quad q's MFMAs (their LDS latency hides behind them)
-            ExArg g0 = ex_begin(uphase(ds, 2 * h)), g1 = ex_begin(uphase(ds, 2 * h + 1));
-            ExEntry e0 = tab[g0.idx], e1 = tab[g1.idx];
-#pragma unroll
-            for (int q = 0; q < kExChunk / 4; ++q) {
-                int32_t uc0, us0, uc1, us1;
-                ex_end(e0, g0.y, uc0, us0);
-                ex_end(e1, g1.y, uc1, us1);
-                if (q + 1 < kExChunk / 4) {
-                    const int p0 = 4 * (q + 1) + 2 * h;
-                    g0 = ex_begin(uphase(ds, p0));
-                    g1 = ex_begin(uphase(ds, p0 + 1));
-                    e0 = tab[g0.idx];
-                    e1 = tab[g1.idx];
-                }
-                __builtin_amdgcn_sched_barrier(0);
-                mfmas(q, ex_digits(uc0), ex_digits(us0), ex_digits(uc1), ex_digits(us1));
             }
-#else
-#pragma unroll 2
-            for (int q = 0; q < kExChunk / 4; ++q) {
-                const int p0 = 4 * q + 2 * h;
-                int32_t uc0, us0, uc1, us1;
-                ex_sincos(tab, uphase(ds, p0), uc0, us0);
-                ex_sincos(tab, uphase(ds, p0 + 1), uc1, us1);
-                mfmas(q, ex_digits(uc0), ex_digits(us0), ex_digits(uc1), ex_digits(us1));
-            }
-#endif
             if ((c + 1) % kExFold == 0 || c + 1 == nch) {
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {

@@ -150,31 +150,67 @@ def select_intervals(TIMEMJD, starts, ends):
         np.int64)
 
 
+def _device_times(TIMEMJD):
+    """The photon times as one fp64 CUDA tensor (uploaded once), or None without a GPU."""
+    from ._native import _is_torch
+    import torch
+    if _is_torch(TIMEMJD):
+        return TIMEMJD.reshape(-1).to(torch.float64).contiguous() if TIMEMJD.is_cuda else None
+    if not torch.cuda.is_available():
+        return None
+    return torch.as_tensor(np.ascontiguousarray(TIMEMJD, dtype=np.float64), device="cuda")
+
+
 def measure_intervals(TIMEMJD, timMod, tempModPP, starts, ends, exposures, phShiftRes=1000, nbrBins=15, varyAmps=False,
                       brutemin=False, readvaryparam=False):
     """Batched core of measureToAs on in-memory arrays: per interval ToA_mid, fit dict entries, H power.
-    The timing model is parsed once; photons of all intervals are folded in one calcphase call, fitted in one
-    device fit, and H-tested (measureToAs.py:210-212) in one crimp_search_sets launch."""
+    The timing model is parsed once; the photon times go to the device once, where the intervals are selected
+    (binary search on the time-sorted photons, measureToAs.py:173-174), folded in one calcphase call, fitted in
+    one device fit and H-tested (:210-212) in one crimp_search_sets launch. Unsorted times take the reference's
+    mask on the host."""
+    import torch
     tmpl = readPPtemplate(tempModPP) if isinstance(tempModPP, str) else tempModPP
     model = str(tmpl["model"]).lower()
     tm = timMod if isinstance(timMod, dict) else ReadTimingModel(str(timMod)).readfulltimingmodel()[0]
-    allt, offs = select_intervals(TIMEMJD, starts, ends)
-    n = np.diff(offs)
-    if np.any(n <= 0):  # measureToAs.py:182 reads TIME_toa[-1] of every interval
-        raise IndexError("index -1 is out of bounds for axis 0 with size 0 (a ToA interval holds no photons)")
-    first, last = allt[offs[:-1]], allt[offs[1:] - 1]
+    starts = np.asarray(starts, dtype=np.float64)
+    ends = np.asarray(ends, dtype=np.float64)
+    T = _device_times(TIMEMJD)
+    if T is not None and (T.numel() < 2 or bool((T[1:] >= T[:-1]).all())):
+        lo = torch.searchsorted(T, torch.as_tensor(starts, device=T.device), right=False)
+        hi = torch.maximum(torch.searchsorted(T, torch.as_tensor(ends, device=T.device), right=True), lo)
+        n = (hi - lo).cpu().numpy()
+        offs = np.concatenate([[0], np.cumsum(n)]).astype(np.int64)
+        if np.any(n <= 0):  # measureToAs.py:182 reads TIME_toa[-1] of every interval
+            raise IndexError("index -1 is out of bounds for axis 0 with size 0 (a ToA interval holds no photons)")
+        rel = torch.arange(int(offs[-1]), device=T.device, dtype=torch.int64)
+        seg = torch.repeat_interleave(torch.arange(n.size, device=T.device), torch.as_tensor(n, device=T.device))
+        offs_d = torch.as_tensor(offs, device=T.device)
+        allt = T[lo[seg] + (rel - offs_d[seg])]
+        first, last = allt[offs_d[:-1]], allt[offs_d[1:] - 1]
+    else:
+        allt, offs = select_intervals(TIMEMJD if T is None else T.cpu().numpy(), starts, ends)
+        if np.any(np.diff(offs) <= 0):
+            raise IndexError("index -1 is out of bounds for axis 0 with size 0 (a ToA interval holds no photons)")
+        first, last = allt[offs[:-1]], allt[offs[1:] - 1]
+        if T is not None:
+            allt = torch.as_tensor(allt, device=T.device)
     mids = ((last - first) / 2) + first                 # measureToAs.py:182
+    mids = mids.cpu().numpy() if hasattr(mids, "cpu") else np.asarray(mids)
     _, folded = calcphase(allt, tm)
     if model in ("cauchy", "vonmises"):
         folded = folded * (2 * np.pi)                  # :195, :200
+    E = np.asarray(exposures, dtype=np.float64)
     if readvaryparam:
-        res = VaryParamFitter(folded, offs, np.asarray(exposures, dtype=np.float64), tmpl, phShiftRes,
-                              nbrBins, vary_amps=bool(varyAmps)).fit(brutemin=brutemin)
+        res = VaryParamFitter(folded, offs, E, tmpl, phShiftRes, nbrBins, vary_amps=bool(varyAmps)).fit(
+            brutemin=brutemin)
     else:
-        fit = ToAFitter(folded, offs, np.asarray(exposures, dtype=np.float64), tmpl, phShiftRes, nbrBins)
-        res = fit.fit(brutemin=brutemin, vary_amps=bool(varyAmps))
+        res = ToAFitter(folded, offs, E, tmpl, phShiftRes, nbrBins).fit(brutemin=brutemin, vary_amps=bool(varyAmps))
     freqs = np.atleast_1d(ephemTmjd(mids, tm)["freqAtTmjd"])          # :210
-    hp = ops.search_sets(allt * 86400, offs, freqs, 5, STAT_H)      # :211-212, one trial per interval
+    if hasattr(allt, "device"):
+        hp = ops.search_sets(allt * 86400, torch.as_tensor(offs, device=allt.device),
+                             torch.as_tensor(freqs, dtype=torch.float64, device=allt.device), 5, STAT_H).cpu().numpy()
+    else:
+        hp = ops.search_sets(allt * 86400, offs, freqs, 5, STAT_H)   # :211-212, one trial per interval
     res["ToA_mid"] = mids
     res["htestPow"] = np.asarray(hp)
     return res

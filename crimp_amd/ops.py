@@ -230,7 +230,7 @@ def toa_grid(x, offsets, tpl, norms, phis):
 TOA_BRUTE, TOA_VARY_AMPS = 1, 2
 
 
-def toa_fit(x, offsets, tpl, exposure, norm0, ph_shift_res=1000, brutemin=False, vary_amps=False):
+def toa_fit(x, offsets, tpl, exposure, norm0, ph_shift_res=1000, brutemin=False, vary_amps=False, flags=0):
     """Whole per-interval ToA fits on the device (crimp_toa_fit): [nint, 8] = norm, phShift, LLmax,
     phShift_LL, phShift_UL, likelihood evaluations, ampShift."""
     options = (TOA_BRUTE if brutemin else 0) | (TOA_VARY_AMPS if vary_amps else 0)
@@ -244,7 +244,7 @@ def toa_fit(x, offsets, tpl, exposure, norm0, ph_shift_res=1000, brutemin=False,
     outp = b.arg(out, np.float64, writable=True)
     with b.device_guard():
         N.check(L.crimp_toa_fit(xp, op, nint, ctypes.byref(tpl), ep, float(norm0), int(ph_shift_res), options, outp,
-                                b.flags(), b.stream()))
+                                b.flags(flags), b.stream()))
     return out.reshape(nint, 8)
 
 

@@ -87,6 +87,10 @@ const char* crimp_last_error(void);
  * the kernel of the last crimp_calcphase, made with CRIMP_FLAG_TIME_KERNELS; -1 if none. Measurement hook for
  * bench.py, not in the reference. */
 double crimp_last_kernel_ms(void);
+/* All timed spans of the last call made with CRIMP_FLAG_TIME_KERNELS (ms, in order: crimp_search -> the
+ * harmonic-sum kernels; crimp_calcphase -> the kernel; crimp_toa_fit -> the brute grid, the fit kernel); writes
+ * up to cap values, returns how many there are. Measurement hook for bench.py, not in the reference. */
+int crimp_last_kernel_times(double* ms, int32_t cap);
 /* Trials of the last crimp_search (default precision) whose power was recomputed by the fp64 fix-up. */
 int64_t crimp_last_fixups(void);
 /* Frees the library's idle cached device scratch on every device (not in the reference). */

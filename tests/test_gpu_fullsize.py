@@ -116,8 +116,10 @@ def test_trial_blocks_and_fixup(gpu, monkeypatch):
         r = np.load(out)
     z, z64, nfix = r["z"], r["z64"], int(r["nfix"])
     assert 0 < nfix < z.size
-    fixed = z == z64
-    assert fixed.sum() >= nfix                      # the flagged trials hold the fp64 kernel's values
+    # the flagged trials hold fp64 sums (the fix-up kernel's photon splits differ from the f64 path's, so equal to
+    # ~1e-15, where the exact kernel and the fp64 path differ by ~1e-9)
+    fixed = np.abs(z - z64) <= 1e-12 * np.abs(z64)
+    assert fixed.sum() >= nfix
     zr = O.search(pulsed_events(200000, 2.0e5, 7.123456789, pulsed_frac=0.05, seed=4),
                   f0 + np.arange(-1024, 1024) / 2.0e6, 2)
     assert _rel_err(z, zr).max() <= 1e-6
