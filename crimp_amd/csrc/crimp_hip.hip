@@ -518,6 +518,7 @@ __global__ __launch_bounds__(256) void k_search_finalize(const double* __restric
     out[map ? map[t] : t] = (stat == CRIMP_STAT_Z2) ? zsum * w : best;
 }
 
+#include "mfma_drain.h"
 #include "search_fast.h"
 #include "search_exact.h"
 

@@ -33,7 +33,7 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kExTab = 4096;    // sin/cos table entries per turn
-constexpr int kExChunk = 64;   // photons per LDS chunk (one barrier per chunk)
+constexpr int kExChunk = 64;    // photons per LDS chunk (one barrier per chunk)
 constexpr int kExWaves = 8;     // waves (tiles) per block
 constexpr int kExBlock = 64 * kExWaves;
 constexpr int kExFold = 4096 / kExChunk;  // chunks between int32 -> int64 folds (4096 photons; overflow bound 2^31 at 16384)
@@ -193,6 +193,7 @@ __global__ __launch_bounds__(kExBlock, 2) void k_search_exact(
                 }
             }
             if ((c + 1) % kExFold == 0 || c + 1 == nch) {
+                mfma_drain();
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     sre[r] += ex_level_sum(acc[0][0][r], acc[1][0][r], acc[2][0][r], acc[3][0][r]);

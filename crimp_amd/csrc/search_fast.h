@@ -199,6 +199,7 @@ __global__ __launch_bounds__(256, 2) void k_search_fast(
                                      re, im);
             }
         }
+        mfma_drain();
 #pragma unroll
         for (int g = 0; g < G; ++g)
 #pragma unroll

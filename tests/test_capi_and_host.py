@@ -26,6 +26,27 @@ def test_library_exports_every_declared_symbol():
     assert L.crimp_version() >= 1
 
 
+def test_mfma_results_not_read_early():
+    """The built search kernels read no MFMA result register within 64 issue cycles of the MFMA (the drain of
+    mfma_drain.h; tools/isa_hazards.py, tools/mb_hazard.hip): guards against a compiler or code change that moves
+    an accumulator read back next to the matrix pipe."""
+    import importlib.util
+    from crimp_amd import _native
+    if not os.path.exists(_native.LIB_PATH):
+        pytest.skip("library not built")
+    spec = importlib.util.spec_from_file_location("isa_hazards", os.path.join(ROOT, "tools", "isa_hazards.py"))
+    H = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(H)
+    funcs = H.disassemble(_native.LIB_PATH)
+    checked = 0
+    for name, insts in funcs.items():
+        if "k_search_exact" in name or "k_search_fast" in name:
+            assert any(op.startswith("v_mfma") for _, op, _, _ in insts), name
+            assert H.check_function(insts) == [], name
+            checked += 1
+    assert checked >= 8
+
+
 def test_hot_path_fails_loudly_without_gpu():
     import torch
     if torch.cuda.is_available():

@@ -111,7 +111,9 @@ def test_trial_blocks_and_fixup(gpu, monkeypatch):
     import os
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "fx.npz")
-        env = dict(os.environ, CRIMP_FIXUP_REL="1e-9")
+        # at 3e-8 the error bound (10 sigma of 2^30 roundings, ~2e-8 of Z for a noise trial at 2e5 photons)
+        # flags the low-power trials but not all of them
+        env = dict(os.environ, CRIMP_FIXUP_REL="3e-8")
         subprocess.run([sys.executable, "-c", code, out], check=True, env=env, timeout=300)
         r = np.load(out)
     z, z64, nfix = r["z"], r["z64"], int(r["nfix"])
