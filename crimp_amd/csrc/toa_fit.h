@@ -36,6 +36,12 @@ struct FitShared {
 
 // np.clip semantics (a NaN stays NaN)
 __device__ __forceinline__ double clipd(double v, double lo, double hi) { return v < lo ? lo : (v > hi ? hi : v); }
+// the 1-sigma bound kk * step + step / 2 (measureToAs.py:351, :376) rounded as numpy does: multiply, then add
+// (hipcc would otherwise fuse it into one fma and differ in the last bit)
+__device__ __forceinline__ double sigma_bound(int kk, double step) {
+#pragma clang fp contract(off)
+    return (double)kk * step + step / 2;
+}
 
 // Template-part cache modes of fit_eval: the norm profile of the 1-sigma scan evaluates one phShift at several
 // norms, and the template part h(x_i; phShift) of the model norm + h does not depend on the norm. The profile's
@@ -385,7 +391,7 @@ __global__ __launch_bounds__(kFitBlock) void k_toa_fit_amp(const double* __restr
                 break;
             }
         }
-        sig[s] = (double)kk * C.step + C.step / 2;
+        sig[s] = sigma_bound(kk, C.step);
     }
     if (threadIdx.x == 0) {
         double* o = out + iv * 8;
@@ -466,7 +472,7 @@ __global__ __launch_bounds__(kFitBlock) void k_toa_fit(const double* __restrict_
                 break;
             }
         }
-        sig[s] = (double)kk * C.step + C.step / 2;
+        sig[s] = sigma_bound(kk, C.step);
     }
     if (threadIdx.x == 0) {
         double* o = out + iv * 8;

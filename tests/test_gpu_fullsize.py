@@ -125,3 +125,103 @@ def test_trial_blocks_and_fixup(gpu, monkeypatch):
     zr = O.search(pulsed_events(200000, 2.0e5, 7.123456789, pulsed_frac=0.05, seed=4),
                   f0 + np.arange(-1024, 1024) / 2.0e6, 2)
     assert _rel_err(z, zr).max() <= 1e-6
+
+
+def _fit_vs_oracle(r, i, x, E, tm):
+    """One interval of a device fit against O.fit_toa (measureToAs.py:254-403 restated): phShift within 1e-6
+    cycles, the 1-sigma scan bounds identical (they are lattice values), redChi2 within 1e-6 relative."""
+    import math
+    o = O.fit_toa(x, E, tm, brutemin=True)
+    assert abs(r["phShi"][i] - o["phShi"]) / (2 * math.pi) <= 1e-6, (i, r["phShi"][i], o["phShi"])
+    assert r["phShi_LL"][i] == o["phShi_LL"] and r["phShi_UL"][i] == o["phShi_UL"], i
+    assert abs(r["reducedChi2"][i] - o["reducedChi2"]) <= 1e-6 * abs(o["reducedChi2"]), i
+    return o
+
+
+def _grid_margins(f):
+    """Relative gap between the best and the second-best point of each interval's brute grid (device grid, the
+    same LL assembly as ToAFitter.brute)."""
+    from crimp_amd import ops
+    from crimp_amd.toafit import _is_torch
+    nphi = int(np.ceil((2 * f.pb) / 0.05))
+    phis = np.arange(nphi) * 0.05 + (-f.pb)
+    norms = np.arange(20) * ((f.hi - f.lo) / 19.0) + f.lo
+    ln, hmin = ops.toa_grid(f.x, f.offsets, f.tpl, f._arr(np.tile(norms, (f.nint, 1)), np.float64),
+                            f._arr(phis, np.float64))
+    if _is_torch(ln):
+        ln, hmin = ln.cpu().numpy(), hmin.cpu().numpy()
+    N, E, nn = f.N[:, None, None], f.E[:, None, None], norms[None, :, None]
+    with np.errstate(divide="ignore", invalid="ignore"):
+        ll = -nn * E + N * np.log(nn * E) + (ln - N * np.log(nn))
+    ll = np.where(((hmin[:, None, :] + nn) > 0) & np.isfinite(ll), ll, -np.inf).reshape(f.nint, -1)
+    top2 = -np.sort(-ll, axis=1)[:, :2]
+    return (top2[:, 0] - top2[:, 1]) / np.abs(top2[:, 0])
+
+
+def test_config5_toas_vs_oracle(gpu):
+    """Config 5 per GPU: 1250 intervals x 1e5 photons (bench.py's workload, seed 2), batched device fits
+    (brute + MLE + 1-sigma scan + redChi2), compared with the oracle on sampled intervals -- including the
+    intervals whose fp32-evaluated brute grid has the closest top-two points (a lattice tie can hand the
+    maximiser a different start)."""
+    import os
+    from crimp_amd.readPPtemplate import readPPtemplate
+    from crimp_amd.synth import template_intervals_torch
+    from crimp_amd.toafit import ToAFitter
+    from conftest import gpath
+    O.set_threads(min(16, os.cpu_count() or 1))
+    tm = readPPtemplate(gpath("1e2259_template.txt"))
+    K = sum(1 for k in tm if k.startswith("amp_"))
+    amps = [tm["amp_%d" % j]["value"] for j in range(1, K + 1)]
+    phs = [tm["ph_%d" % j]["value"] for j in range(1, K + 1)]
+    x, off, E, shifts = template_intervals_torch(1250, 100_000, tm["norm"]["value"], amps, phs, seed=2, device=gpu)
+    f = ToAFitter(x, off, E, tm)
+    r = f.fit(brutemin=True)
+    d = np.angle(np.exp(1j * (r["phShi"] - shifts)))
+    assert np.sqrt(np.mean(d ** 2)) / (2 * np.pi) < 5e-3                # all 1250 recover their injected shift
+    margins = _grid_margins(ToAFitter(x, off, E, tm))
+    ties = [int(i) for i in np.argsort(margins)[:2]]
+    sample = sorted(set([0, 1, 417, 833, 1249, 600] + ties))
+    xh, oh = x.cpu().numpy(), off.cpu().numpy()
+    for i in sample:
+        _fit_vs_oracle(r, i, xh[oh[i]:oh[i + 1]], E[i], tm)
+    assert margins[ties[0]] < 1e-5       # the sample did include a near-tie of the lattice
+
+
+def _sample_template(tm, n, shift, rng):
+    """n phases in [0, 2 pi) from a Cauchy / von Mises template shifted by ``shift`` (rejection sampling on the
+    oracle's curve, templatemodels.py:166-185, 271-290)."""
+    tarr = O.template_arrays(tm)
+    n0 = tm["norm"]["value"]
+    ymax = 1.05 * O.curve(tarr, n0, shift, np.linspace(0, 2 * np.pi, 20001)).max()
+    out = np.empty(0)
+    while out.size < n:
+        xx = rng.uniform(0, 2 * np.pi, 3 * n)
+        keep = rng.uniform(0, ymax, xx.size) < O.curve(tarr, n0, shift, xx)
+        out = np.concatenate([out, xx[keep]])
+    return out[:n]
+
+
+def test_cauchy_vonmises_blocks_1e5(gpu):
+    """One Cauchy and one von Mises block (3 intervals x 1e5 photons each) fitted on the device against
+    O.fit_toa (measureToAs.py:406-548, :551-693)."""
+    import json
+    import os
+    from crimp_amd.toafit import ToAFitter
+    from conftest import gpath
+    O.set_threads(min(16, os.cpu_count() or 1))
+    tc = json.load(open(gpath("cauchy_vm_theta.json")))
+    rng = np.random.default_rng(7)
+    for model in ("cauchy", "vonmises"):
+        tm = {"model": model, "norm": {"value": tc["norm"], "vary": True}}
+        for j in (1, 2):
+            for nm in ("amp", "cen", "wid"):
+                tm["%s_%d" % (nm, j)] = {"value": tc["%s_%d" % (nm, j)], "vary": True}
+        n = 100_000
+        rate = tc["norm"] + (tc["amp_1"] + tc["amp_2"]) / (2 * np.pi)   # mean of the template over a turn
+        xs = [_sample_template(tm, n, s, rng) for s in (0.3, -2.0, 3.5)]
+        x = np.concatenate(xs)
+        off = np.arange(len(xs) + 1, dtype=np.int64) * n
+        E = np.full(len(xs), n / rate)
+        r = ToAFitter(x, off, E, tm).fit(brutemin=True)
+        for i in range(len(xs)):
+            _fit_vs_oracle(r, i, xs[i], E[i], tm)
