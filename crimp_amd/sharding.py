@@ -39,19 +39,33 @@ def _device_for_backend(dist):
 
 def _gpu_slice(time, t0, freq, nharm, stat, freq_dot, first, count):
     from . import ops
+    import torch
+    if isinstance(time, torch.Tensor) and freq_dot is not None and not isinstance(freq_dot, torch.Tensor):
+        freq_dot = torch.as_tensor(np.asarray(freq_dot, dtype=np.float64), device=time.device)
     return ops.search(time, t0, freq, nharm, stat, log10_negfdot=freq_dot, first=first, count=count)
+
+
+def _as_comm(local, dev):
+    """The rank's result as a float64 tensor on the collective's device, without a host round trip when it is
+    already a device tensor and the backend is nccl."""
+    import torch
+    if isinstance(local, torch.Tensor):
+        return local.to(device=dev, dtype=torch.float64)
+    return torch.as_tensor(np.asarray(local), dtype=torch.float64, device=dev)
 
 
 def sharded_search(time, freq, nharm=2, stat=0, freq_dot=None, gather="all", compute=None):
     """Z^2 (stat=0) / H (stat=1) over the fd-outer grid, sharded across the process group.
 
-    Returns the full power array (gather='all') or ``(best_power, best_flat_index)``
-    (gather='best'), identical on every rank.
+    Returns the full power array (gather='all'; a tensor on the rank's device when ``time`` is a device
+    tensor, else a numpy array) or ``(best_power, best_flat_index)`` (gather='best'), identical on every rank.
+    With the nccl backend the gather runs on the device buffers the search wrote (no host staging).
     """
     import torch
     dist, world, rank = _dist()
     compute = compute or _gpu_slice
-    if hasattr(time, "numel"):
+    as_tensor = isinstance(time, torch.Tensor)
+    if as_tensor:
         t0 = float((time[0] + time[-1]).item()) / 2
         nf = int(freq.numel())
     else:
@@ -61,12 +75,13 @@ def sharded_search(time, freq, nharm=2, stat=0, freq_dot=None, gather="all", com
     total = (nfd if nfd else 1) * nf
     first, count = shard_range(total, world, rank)
     local = compute(time, t0, freq, nharm, stat, freq_dot, first, count)
-    dev = _device_for_backend(dist)
-    loc = torch.as_tensor(np.asarray(local.cpu() if hasattr(local, "cpu") else local), dtype=torch.float64).to(dev)
+    dev = _device_for_backend(dist) if dist is not None else (
+        local.device if isinstance(local, torch.Tensor) else torch.device("cpu"))
+    loc = _as_comm(local, dev)
     if gather == "best":
         if count:
-            i = int(torch.argmax(loc).item())
-            mine = torch.tensor([loc[i].item(), float(first + i)], dtype=torch.float64, device=dev)
+            i = torch.argmax(loc)
+            mine = torch.stack([loc[i], (i + first).to(torch.float64)])
         else:
             mine = torch.tensor([-np.inf, float(total)], dtype=torch.float64, device=dev)
         if dist is None:
@@ -74,18 +89,24 @@ def sharded_search(time, freq, nharm=2, stat=0, freq_dot=None, gather="all", com
         else:
             allb = torch.empty(world * 2, dtype=torch.float64, device=dev)
             dist.all_gather_into_tensor(allb, mine)
-        b = allb.cpu().numpy().reshape(-1, 2)
-        k = np.lexsort((b[:, 1], -b[:, 0]))[0]
-        return float(b[k, 0]), int(b[k, 1])
+            allb = allb.reshape(world, 2)
+        # highest power, ties to the lowest flat index (np.argmax over the whole grid)
+        top = allb[:, 0].max()
+        idx = torch.where(allb[:, 0] == top, allb[:, 1], torch.full_like(allb[:, 1], np.inf)).min()
+        res = torch.stack([top, idx]).cpu().numpy()
+        return float(res[0]), int(res[1])
     if dist is None:
-        return loc.cpu().numpy()
+        return loc if as_tensor else loc.cpu().numpy()
     width = shard_range(total, world, 0)[1]
     buf = torch.full((width,), np.nan, dtype=torch.float64, device=dev)
     buf[:count] = loc
     allp = torch.empty(world * width, dtype=torch.float64, device=dev)
     dist.all_gather_into_tensor(allp, buf)
-    allp = allp.cpu().numpy().reshape(world, width)
-    return np.concatenate([allp[r, :shard_range(total, world, r)[1]] for r in range(world)])
+    allp = allp.reshape(world, width)
+    out = torch.cat([allp[r, :shard_range(total, world, r)[1]] for r in range(world)])
+    if as_tensor:
+        return out.to(time.device)
+    return out.cpu().numpy()
 
 
 def sharded_toa_fit(x, offsets, exposure, tmpl, brutemin=False, ph_shift_res=1000, nbr_bins=15, fitter=None):
@@ -93,14 +114,14 @@ def sharded_toa_fit(x, offsets, exposure, tmpl, brutemin=False, ph_shift_res=100
     import torch
     from .toafit import ToAFitter
     dist, world, rank = _dist()
-    off = np.asarray(offsets, dtype=np.int64)
+    off = np.asarray(offsets.cpu() if isinstance(offsets, torch.Tensor) else offsets, dtype=np.int64)
     nint = off.size - 1
     first, count = shard_range(nint, world, rank)
     keys = ("phShi", "phShi_LL", "phShi_UL", "reducedChi2", "norm", "LLmax")
     rec = np.full((shard_range(nint, world, 0)[1], len(keys)), np.nan)
     if count:
         sl = off[first:first + count + 1]
-        xs = np.asarray(x)[sl[0]:sl[-1]]
+        xs = x[int(sl[0]):int(sl[-1])] if isinstance(x, torch.Tensor) else np.asarray(x)[sl[0]:sl[-1]]
         fit = (fitter or ToAFitter)(xs, sl - sl[0], np.asarray(exposure)[first:first + count], tmpl, ph_shift_res,
                                     nbr_bins)
         r = fit.fit(brutemin=brutemin)

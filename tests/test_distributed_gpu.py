@@ -1,0 +1,74 @@
+"""The multi-GPU code path on one GPU: two gloo ranks on cuda:0 run sharding.py's default compute
+(_gpu_slice -> crimp_search on device tensors) and the real ToAFitter, and must give bit-identical results to
+the unsharded device search and fits computed in the same processes (the exact search is partition invariant;
+each ToA interval's fit is independent of the others in its batch). The nccl branch is the same code with
+the collective's buffers on the device; the 8-GPU scaling curve itself is run by the driver, not here."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out_path):
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from crimp_amd import ops
+    from crimp_amd.readPPtemplate import readPPtemplate
+    from crimp_amd.sharding import sharded_search, sharded_toa_fit
+    from crimp_amd.synth import pulsed_events, template_intervals_torch
+    from crimp_amd.toafit import ToAFitter
+    dev = torch.device("cuda", 0)
+    t_h = pulsed_events(200_000, 2.0e5, 7.123456789, pulsed_frac=0.05, seed=11)
+    f_h = 7.123456789 + (np.arange(40_000) - 20_000) / 2.0e6
+    fd = np.array([-12.0, -10.5])
+    t = torch.as_tensor(t_h, device=dev)
+    f = torch.as_tensor(f_h, device=dev)
+    full = sharded_search(t, f, 2, 0, freq_dot=fd, gather="all")
+    best = sharded_search(t, f, 3, 1, freq_dot=fd, gather="best")
+    t0 = float((t[0] + t[-1]).item()) / 2
+    fdd = torch.as_tensor(fd, device=dev)
+    ref = ops.search(t, t0, f, 2, 0, log10_negfdot=fdd)
+    refh = ops.search(t, t0, f, 3, 1, log10_negfdot=fdd).cpu().numpy()
+    tm = readPPtemplate(os.path.join(ROOT, "tests", "golden", "1e2259_template.txt"))
+    K = sum(1 for k in tm if k.startswith("amp_"))
+    x, off, E, _ = template_intervals_torch(9, 20_000, tm["norm"]["value"], [tm["amp_%d" % j]["value"] for j in
+                                            range(1, K + 1)], [tm["ph_%d" % j]["value"] for j in range(1, K + 1)],
+                                            seed=3, device=dev)
+    toa = sharded_toa_fit(x, off, E, tm, brutemin=True)
+    rtoa = ToAFitter(x, off, E, tm).fit(brutemin=True)
+    if rank == 0:
+        keys = sorted(toa)
+        np.savez(out_path, full=full.cpu().numpy(), full_is_dev=np.array(full.is_cuda), ref=ref.cpu().numpy(),
+                 best=np.array(best, dtype=np.float64), refh=refh, keys=np.array(keys),
+                 toa=np.stack([toa[k] for k in keys]), rtoa=np.stack([rtoa[k] for k in keys]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_gloo_ranks_on_gpu_bit_identical_to_unsharded(tmp_path):
+    out = str(tmp_path / "r.npz")
+    mp.spawn(_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    r = np.load(out)
+    assert bool(r["full_is_dev"])
+    np.testing.assert_array_equal(r["full"], r["ref"])
+    assert r["best"][0] == r["refh"].max() and int(r["best"][1]) == int(np.argmax(r["refh"]))
+    np.testing.assert_array_equal(r["toa"], r["rtoa"])

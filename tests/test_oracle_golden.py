@@ -1,12 +1,13 @@
 """The oracle (CPU restatement, test infrastructure) pinned against the reference's own outputs."""
 import json
 import math
+import os
 
 import numpy as np
 import pandas as pd
 import pytest
 
-from conftest import gold, gpath
+from conftest import ROOT, gold, gpath
 from oracle import oracle as O
 
 
@@ -91,3 +92,16 @@ def test_toa_fit_matches_reference_table():
         assert r["phShi_LL"] == pytest.approx(row["phShift_LL"], abs=1e-12)
         assert r["phShi_UL"] == pytest.approx(row["phShift_UL"], abs=1e-12)
         assert r["reducedChi2"] == pytest.approx(row["redChi2"], rel=5e-4)
+
+
+def test_oracle_clean_under_address_sanitizer():
+    """`make -C oracle asan`: every oracle entry point under -fsanitize=address,undefined."""
+    import shutil
+    import subprocess
+    if shutil.which("gcc") is None:
+        pytest.skip("no gcc")
+    r = subprocess.run(["make", "-s", "-B", "-C", os.path.join(ROOT, "oracle"), "asan"], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "ran clean" in r.stdout
+    assert "ERROR: AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr
