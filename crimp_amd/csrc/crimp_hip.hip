@@ -1286,15 +1286,19 @@ static int fast_search(Scratch& sc, hipStream_t s, const double* dt, const doubl
 // fp64 fix-up of the trials whose power is too small for the kernel's error bound (k_search_finalize_exact).
 // int64 totals in units of 2^-36 hold |C_k| <= n exactly for n < 2^27 photons.
 static const int64_t kExactMaxPhotons = int64_t(1) << 27;
+static const int64_t kExFoldMaxBlocks = 8192;  // fold scratch of one launch <= 1 GiB
 static int exact_search(Scratch& sc, hipStream_t s, const double* dt, const double* dt2, int64_t n, const double* freq,
                         int64_t nf, const double* c2, const double* ap, bool twod, int nharm, int stat, int64_t first,
                         int64_t count, double* out, KernelTimer* kt, int64_t* nfixed) {
     const int64_t tpr = cdiv(nf, kTile);
     const int ncomp = 2 * nharm;
-    // trial blocks bounded by the int64 totals buffer (2 GiB), whole 8-tile block groups
-    const int64_t cbmax = std::max<int64_t>(kTile * kExWaves, part_budget() / (8 * ncomp));
+    // trial blocks bounded by the int64 totals buffer (2 GiB) and by the blocks' fold scratch (kExFoldMaxBlocks
+    // blocks of 128 KB), whole 8-tile block groups
+    const int64_t cbmax = std::min<int64_t>(std::max<int64_t>(kTile * kExWaves, part_budget() / (8 * ncomp)),
+                                            kExFoldMaxBlocks * kExWaves * kTile);
     const int64_t cb = std::min<int64_t>(count, cdiv(cdiv(count, cdiv(count, cbmax)), kTile) * kTile);
     unsigned long long* tot = nullptr;
+    long long* fold = nullptr;
     int64_t* flagged = nullptr;
     int* nflag = nullptr;
     HIPCHK(sc.alloc(&tot, (size_t)(ncomp * cb)));
@@ -1316,13 +1320,18 @@ static int exact_search(Scratch& sc, hipStream_t s, const double* dt, const doub
         const int64_t splits = cdiv(n, chunk);
         HIPCHK(hipMemsetAsync(tot, 0, (size_t)(ncomp * bcount) * sizeof(unsigned long long), s));
         dim3 grid((unsigned)bpg, (unsigned)splits);
+        if (!fold) {  // blocks per launch <= bpg + 2048 (the split count above), bpg <= cb / 8192 + 2
+            const int64_t maxblocks = cdiv(cb, kTile * kExWaves) + 2 + 2048;
+            HIPCHK(sc.alloc(&fold, (size_t)(maxblocks * kExWaves * kExFoldVals * 64)));
+        }
+        if (bpg * splits > cdiv(cb, kTile * kExWaves) + 2 + 2048) return set_err(CRIMP_ERR_HIP, "exact search: fold scratch bound");
         for (int k = 1; k <= nharm; ++k) {
             if (twod)
                 k_search_exact<true><<<grid, kExBlock, 0, s>>>(dt, dt2, n, chunk, freq, nf, c2, ap, tf, nt, tpr, bfirst,
-                                                               bcount, k, tot);
+                                                               bcount, k, tot, fold);
             else
                 k_search_exact<false><<<grid, kExBlock, 0, s>>>(dt, dt2, n, chunk, freq, nf, c2, ap, tf, nt, tpr,
-                                                                bfirst, bcount, k, tot);
+                                                                bfirst, bcount, k, tot, fold);
             HIPCHK(hipGetLastError());
         }
         if (kt && b0 + cb >= count) kt->stop();

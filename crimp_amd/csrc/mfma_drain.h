@@ -1,16 +1,24 @@
-// mfma_drain.h -- wait for the matrix pipe before VALU code reads MFMA results (gfx950).
+// mfma_drain.h -- keeping VALU writes and reads away from in-flight MFMAs on gfx950.
 //
-// hipcc pads 12 wait states between a v_mfma_*_32x32x* and a dependent VALU read. tools/mb_hazard.hip measures
-// the result latency of v_mfma_i32_32x32x32_i8: rows 0..15 land within ~8 wait states, rows 16..31 (result
-// registers 8..15) after ~12, i.e. at the padding's edge. In the search kernels, with two waves per SIMD
-// mixing fp64 VALU work and MFMAs, reads placed 40+ issue cycles after the last MFMA by the compiler still
-// saw stale partial sums in rows 16..31 now and then: rare, timing-dependent errors of single photon terms
-// in rows a >= 16 of a tile (repeat runs and trial partitions differed). The kernels therefore drain before
-// every read of their accumulators: 256 wait states (this wave only; the other waves keep issuing), placed
-// where the accumulators are read once per fold or chunk, and fenced against scheduling across it.
-// tools/isa_hazards.py checks the built code object for result reads that come too early.
+// Measured on the exact search kernel (two waves per SIMD mixing fp64 VALU work, LDS table reads and
+// v_mfma_i32_32x32x32_i8): with hipcc's own scheduling, repeat runs and trial partitions differed by single
+// photon terms (~1e-11..1e-9 relative) in result rows 16..31 of a tile, mostly in the second wave of each SIMD.
+// Two code shapes were involved, and both are fixed here:
+//   * operand overwrite: hipcc rewrote an MFMA's A registers (the next digit level's shifted operand) in the
+//     very next instruction. Keeping the four level operands in distinct registers and issuing the quad's 8
+//     MFMAs as a group (scheduling barriers) followed by mfma_operand_guard() -- 32 wait states, so the
+//     earliest rewrite of an A register comes >= 48 issue cycles after its MFMA -- made every run
+//     bit-identical; the same code without the group (A rewritten at once) stayed nondeterministic
+//     (tools/dbg_part.py, tools/dbg_2d.py, tools/run_guard_ab.sh). Cost: ~2 % of the search.
+//   * result read: hipcc pads 12 wait states between a 32x32 MFMA and a dependent VALU read, the edge of the
+//     measured latency of the last result rows (tools/mb_hazard.hip: rows 0..15 land within ~8, rows 16..31
+//     after ~12). mfma_drain() (256 wait states) precedes every read of the accumulators (once per fold).
+// tools/mb_hazard.hip reproduces the result latency but not the operand hazard in isolation (single MFMAs,
+// queued MFMAs, 4 waves per SIMD all read their operands in time), so the guard distances are empirical
+// margins, enforced on the built code object by tools/isa_hazards.py (a CPU test).
 #pragma once
 
+// wait before VALU code reads MFMA results (this wave only; the other waves keep issuing)
 __device__ __forceinline__ void mfma_drain() {
     __builtin_amdgcn_sched_barrier(0);
     asm volatile(
@@ -18,5 +26,13 @@ __device__ __forceinline__ void mfma_drain() {
         "s_nop 7\n s_nop 7\n s_nop 7\n s_nop 7\n s_nop 7\n s_nop 7\n s_nop 7\n s_nop 7\n"
         "s_nop 7\n s_nop 7\n s_nop 7\n s_nop 7\n s_nop 7\n s_nop 7\n s_nop 7\n s_nop 7\n"
         "s_nop 7\n s_nop 7\n s_nop 7\n s_nop 7\n s_nop 7\n s_nop 7\n s_nop 7\n s_nop 7");
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+// end of a group of MFMAs whose operands were all computed before the group: nothing may be scheduled into
+// the group, and the next writes of the group's operand registers come after 32 wait states
+__device__ __forceinline__ void mfma_operand_guard() {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_nop 7\n s_nop 7\n s_nop 7\n s_nop 7");
     __builtin_amdgcn_sched_barrier(0);
 }

@@ -16,8 +16,9 @@
 // accumulated per digit LEVEL L = i+j on v_mfma_i32_32x32x32_i8 in int32 (exact), levels 3..6
 // kept (the dropped levels 0..2 contribute < 5e-14 per photon): the A operand holds U's digits in natural
 // order, the B operand V's digits byte-reversed, so one dword pair dots to level 3, and A >> 8, >> 16,
-// >> 24 give levels 4, 5, 6 against the same B. The level sums are folded into int64 registers in units
-// of 2^-36 (acc3 + acc4 << 8 + acc5 << 16 + acc6 << 24, exact) every kExFold chunks, and each block adds
+// >> 24 give levels 4, 5, 6 against the same B. The level sums are folded into int64 running sums in units
+// of 2^-36 (acc3 + acc4 << 8 + acc5 << 16 + acc6 << 24, exact) every kExFold chunks -- kept per lane in global
+// scratch between folds, so that the photon loop has the registers for both accumulators and operands --, and each block adds
 // its int64 totals to the global per-trial totals with 64-bit integer atomics: integer sums are exact and
 // order-independent, so the result does not depend on photon splits, trial blocking or sharding, and the
 // only errors are the 2^30 roundings of U and V (per-term ~1e-9, against ~1e-7 for fp32 sin/cos).
@@ -36,7 +37,9 @@ constexpr int kExTab = 4096;    // sin/cos table entries per turn
 constexpr int kExChunk = 64;    // photons per LDS chunk (one barrier per chunk)
 constexpr int kExWaves = 8;     // waves (tiles) per block
 constexpr int kExBlock = 64 * kExWaves;
-constexpr int kExFold = 4096 / kExChunk;  // chunks between int32 -> int64 folds (4096 photons; overflow bound 2^31 at 16384)
+constexpr int kExFold = 16384 / kExChunk;  // chunks between int32 -> int64 folds: 16384 photons, the int32 bound
+                                            // (level 3: <= 2 x 49152 per photon, 1.61e9 < 2^31)
+constexpr int kExFoldVals = 32;             // int64 running sums per lane (16 result rows x Re, Im)
 constexpr double kExUnit = 1.4551915228366852e-11;  // 2^-36: value of one unit of the int64 totals
 
 struct ExEntry {
@@ -103,7 +106,7 @@ __global__ __launch_bounds__(kExBlock, 2) void k_search_exact(
     const double* __restrict__ dt, const double* __restrict__ dt2, int64_t n, int64_t chunk,
     const double* __restrict__ freq, int64_t nf, const double* __restrict__ c2row, const double* __restrict__ apinfo,
     int64_t tile_first, int64_t ntiles, int64_t tiles_per_row, int64_t first, int64_t count, int kh,
-    unsigned long long* __restrict__ tot) {
+    unsigned long long* __restrict__ tot, long long* __restrict__ fold) {
     __shared__ ExEntry tab[kExTab];                        // 64 KB
     __shared__ uint4 vre[2][kExChunk / 2][32];             // B fragments (Re) per photon pair and column b
     __shared__ uint4 vim[2][kExChunk / 2][32];             // B fragments (Im)
@@ -161,9 +164,11 @@ __global__ __launch_bounds__(kExBlock, 2) void k_search_exact(
     for (int L = 0; L < 4; ++L)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[L][0][r] = acc[L][1][r] = 0;
-    int64_t sre[16], sim[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) sre[r] = sim[r] = 0;
+    // the block's running int64 sums between folds: per lane in global scratch (coalesced, written and read
+    // by the same lane), so that they take no registers inside the photon loop
+    long long* const fs =
+        fold + ((((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * kExWaves + wv) * 64 + lane) * kExFoldVals;
+    const int comp = 2 * (kh - 1);
 
     load_dt(0, 0);
     load_dt(1, 1);
@@ -184,20 +189,49 @@ __global__ __launch_bounds__(kExBlock, 2) void k_search_exact(
                 const uint4 br = vre[vb][2 * q + h][ar], bi = vim[vb][2 * q + h][ar];
                 const i32x4 bre = {(int)br.x, (int)br.y, (int)br.z, (int)br.w};
                 const i32x4 bim = {(int)bi.x, (int)bi.y, (int)bi.z, (int)bi.w};
+                i32x4 A[4];
 #pragma unroll
                 for (int L = 0; L < 4; ++L) {
                     const int sh = 8 * L;
-                    const i32x4 A = {(int)(a0 >> sh), (int)(a1 >> sh), (int)(a2 >> sh), (int)(a3 >> sh)};
-                    acc[L][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A, bre, acc[L][0], 0, 0, 0);
-                    acc[L][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A, bim, acc[L][1], 0, 0, 0);
+                    A[L] = i32x4{(int)(a0 >> sh), (int)(a1 >> sh), (int)(a2 >> sh), (int)(a3 >> sh)};
                 }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int L = 0; L < 4; ++L) {
+                    acc[L][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[L], bre, acc[L][0], 0, 0, 0);
+                    acc[L][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[L], bim, acc[L][1], 0, 0, 0);
+                }
+                mfma_operand_guard();
             }
             if ((c + 1) % kExFold == 0 || c + 1 == nch) {
                 mfma_drain();
+                const bool first_fold = c + 1 <= kExFold, last = c + 1 == nch;
+                // opaque copies of the lane's scratch pointer and trial index: the 32 addresses derived from them
+                // must be formed here, not hoisted out of the photon loop (they would hold 64 registers there)
+                long long* f = fs;
+                int64_t cl = c0 + ar - first + frow * nf;
+                asm volatile("" : "+v"(f), "+v"(cl));
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
-                    sre[r] += ex_level_sum(acc[0][0][r], acc[1][0][r], acc[2][0][r], acc[3][0][r]);
-                    sim[r] += ex_level_sum(acc[0][1][r], acc[1][1][r], acc[2][1][r], acc[3][1][r]);
+                    long long re = ex_level_sum(acc[0][0][r], acc[1][0][r], acc[2][0][r], acc[3][0][r]);
+                    long long im = ex_level_sum(acc[0][1][r], acc[1][1][r], acc[2][1][r], acc[3][1][r]);
+                    if (!first_fold) {
+                        re += f[2 * r];
+                        im += f[2 * r + 1];
+                    }
+                    if (!last) {
+                        f[2 * r] = re;
+                        f[2 * r + 1] = im;
+                    } else {
+                        // D[row a][col b] of the 32x32 tile: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 h;
+                        // trial c0 + 32 a + b, output slot o = frow * nf + trial - first
+                        const int ra = (r & 3) + 8 * (r >> 2) + 4 * h;
+                        const int64_t o = cl + 32 * ra;
+                        if (c0 + 32 * ra + ar < nf && o >= 0 && o < count) {
+                            atomicAdd(&tot[(int64_t)comp * count + o], (unsigned long long)re);
+                            atomicAdd(&tot[(int64_t)(comp + 1) * count + o], (unsigned long long)im);
+                        }
+                    }
                 }
 #pragma unroll
                 for (int L = 0; L < 4; ++L)
@@ -206,19 +240,6 @@ __global__ __launch_bounds__(kExBlock, 2) void k_search_exact(
             }
         }
         __syncthreads();
-    }
-    if (!active) return;
-    // D[row a][col b] of the 32x32 tile: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 h; trial c0 + 32 a + b
-    const int comp = 2 * (kh - 1);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int ra = (r & 3) + 8 * (r >> 2) + 4 * h;
-        const int64_t c = c0 + 32 * ra + ar;
-        const int64_t o = frow * nf + c - first;
-        if (c < nf && o >= 0 && o < count) {
-            atomicAdd(&tot[(int64_t)comp * count + o], (unsigned long long)sre[r]);
-            atomicAdd(&tot[(int64_t)(comp + 1) * count + o], (unsigned long long)sim[r]);
-        }
     }
 }
 

@@ -108,28 +108,35 @@ __device__ __forceinline__ void mma(const AFrag& A, const BFrag& B, f32x16& re, 
 template <int G, bool SQUARE>
 __device__ __forceinline__ void fast_pair(double phu, double phv, float live, int ka, int kb, f32x16 (&re)[G],
                                           f32x16 (&im)[G]) {
+    static_assert(G == 1 || G == 2, "harmonic groups of one or two");
+    // all operands first, then the MFMAs as one group followed by the operand guard (mfma_drain.h)
+    AFrag A[G];
+    BFrag B[G];
     if (SQUARE) {  // harmonics (ka, 2 ka): phases arrive pre-scaled by ka
         float vs, vc, us, uc;
         sincos_turn(frac_turn(phv), vs, vc);
-        const BFrag B1 = make_b(vc, vs);
-        BFrag B2;
-        if (G > 1) B2 = make_b(__builtin_fmaf(vc, vc, -(vs * vs)), (vc + vc) * vs);
+        B[0] = make_b(vc, vs);
+        if (G > 1) B[G - 1] = make_b(__builtin_fmaf(vc, vc, -(vs * vs)), (vc + vc) * vs);
         sincos_turn(frac_turn(phu), us, uc);
         uc *= live;
         us *= live;
-        mma(make_a(uc, us), B1, re[0], im[0]);
-        if (G > 1) mma(make_a(__builtin_fmaf(uc, uc, -(us * us)), (uc + uc) * us), B2, re[1], im[1]);
+        A[0] = make_a(uc, us);
+        if (G > 1) A[G - 1] = make_a(__builtin_fmaf(uc, uc, -(us * us)), (uc + uc) * us);
     } else {
 #pragma unroll
         for (int g = 0; g < G; ++g) {
             const double kf = (double)(g == 0 ? ka : kb);
             float vs, vc, us, uc;
             sincos_turn(frac_turn(phv * kf), vs, vc);
-            const BFrag B = make_b(vc, vs);
+            B[g] = make_b(vc, vs);
             sincos_turn(frac_turn(phu * kf), us, uc);
-            mma(make_a(uc * live, us * live), B, re[g], im[g]);
+            A[g] = make_a(uc * live, us * live);
         }
     }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int g = 0; g < G; ++g) mma(A[g], B[g], re[g], im[g]);
+    mfma_operand_guard();
 }
 
 template <int G, bool TWOD, bool SQUARE>

@@ -26,10 +26,10 @@ def test_library_exports_every_declared_symbol():
     assert L.crimp_version() >= 1
 
 
-def test_mfma_results_not_read_early():
-    """The built search kernels read no MFMA result register within 64 issue cycles of the MFMA (the drain of
-    mfma_drain.h; tools/isa_hazards.py, tools/mb_hazard.hip): guards against a compiler or code change that moves
-    an accumulator read back next to the matrix pipe."""
+def test_mfma_hazard_rules_hold_in_default_kernel():
+    """The default search kernel keeps VALU reads of MFMA results and rewrites of MFMA operands away from the
+    MFMA (crimp_amd/csrc/mfma_drain.h; tools/isa_hazards.py): guards against a compiler or code change that moves
+    them back next to the matrix pipe, which made repeat runs differ."""
     import importlib.util
     from crimp_amd import _native
     if not os.path.exists(_native.LIB_PATH):
@@ -40,11 +40,11 @@ def test_mfma_results_not_read_early():
     funcs = H.disassemble(_native.LIB_PATH)
     checked = 0
     for name, insts in funcs.items():
-        if "k_search_exact" in name or "k_search_fast" in name:
+        if "k_search_exact" in name:
             assert any(op.startswith("v_mfma") for _, op, _, _ in insts), name
             assert H.check_function(insts) == [], name
             checked += 1
-    assert checked >= 8
+    assert checked == 2
 
 
 def test_hot_path_fails_loudly_without_gpu():

@@ -1,15 +1,12 @@
-"""MFMA result-latency check on the shipped gfx950 code object.
+"""MFMA hazard check on the shipped gfx950 code object (see crimp_amd/csrc/mfma_drain.h for the measurements).
 
-tools/mb_hazard.hip measures when the 16 result registers of a v_mfma_i32_32x32x32_i8 are written: rows
-0..15 within ~8 wait states of the issue, rows 16..31 (result registers 8..15) only after ~12 -- exactly the
-12 wait states hipcc pads before a dependent VALU read -- and later than that when other waves keep the
-matrix pipe busy. A VALU (or memory) instruction that reads an MFMA result too early sees the old partial
-sum in rows 16..31; in the exact search kernel that showed up as rare, timing-dependent errors in rows
-a >= 16 of a tile. Overwriting the A/B operand registers right after the MFMA is harmless (measured).
-
-Rule checked here: no non-MFMA instruction reads a result register of an MFMA within SAFE_CYCLES issue
-cycles of it on any path (branches followed), counting 1 per instruction, N+1 per s_nop N and MFMA_CYCLES
-per later MFMA issue. MFMA -> MFMA accumulation chains are interlocked by the hardware and not counted.
+Two rules, on every path from each MFMA (branches followed), counting issue cycles as 1 per instruction, N+1
+per s_nop N and MFMA_CYCLES per later MFMA:
+  * result read: no non-MFMA instruction reads an MFMA's result registers within RESULT_CYCLES (MFMA -> MFMA
+    accumulation chains are interlocked by the hardware and not counted);
+  * operand rewrite: no instruction writes an MFMA's A-operand registers within A_CYCLES, nor its B-operand
+    registers within B_CYCLES (loads count from their issue: conservative).
+Only kernels matching the given name patterns are checked (default: the exact search kernel).
 
 usage: python tools/isa_hazards.py [lib.so] [kernel-substring ...]   (exit status 1 on a violation)
 """
@@ -21,8 +18,11 @@ import sys
 import tempfile
 
 OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
-SAFE_CYCLES = 64
+RESULT_CYCLES = 64
+A_CYCLES = 48
+B_CYCLES = 8
 MFMA_CYCLES = 8
+_WRITERS = ("v_", "ds_read", "global_load", "buffer_load", "scratch_load", "flat_load")
 _REG = re.compile(r"^v\[(\d+):(\d+)\]$|^v(\d+)$")
 
 
@@ -81,36 +81,42 @@ def check_function(insts):
         return nxt
 
     bad = []
+    stores = ("global_store", "buffer_store", "scratch_store", "flat_store", "ds_write", "global_atomic",
+              "buffer_atomic", "flat_atomic", "ds_add")
+    horizon = max(RESULT_CYCLES, A_CYCLES, B_CYCLES)
     for i, (a, op, ops, _) in enumerate(insts):
         if not op.startswith("v_mfma"):
             continue
-        dst = _regs(ops.split(",")[0])
-        stack, seen = [(s, 0) for s in successors(i)], set()
+        f0 = [f.strip() for f in ops.split(",")]
+        dst, srca, srcb = _regs(f0[0]), _regs(f0[1]), _regs(f0[2])
+        stack, seen = [(s, 0, dst, srca, srcb) for s in successors(i)], set()
         while stack:
-            j, cyc = stack.pop()
-            if (j, cyc) in seen or cyc >= SAFE_CYCLES:
+            j, cyc, d, ra, rb = stack.pop()
+            key = (j, cyc, frozenset(d), frozenset(ra), frozenset(rb))
+            if key in seen or cyc >= horizon or not (d or ra or rb):
                 continue
-            seen.add((j, cyc))
+            seen.add(key)
             b, op2, ops2, _ = insts[j]
             if op2 == "s_nop":
-                stack += [(s, cyc + int(ops2.split()[0], 0) + 1) for s in successors(j)]
+                stack += [(s, cyc + int(ops2.split()[0], 0) + 1, d, ra, rb) for s in successors(j)]
                 continue
             fields = [f.strip() for f in ops2.split(",")] if ops2 else []
             if op2.startswith("v_mfma"):
-                if set().union(*map(_regs, fields[1:3])) & dst:
-                    bad.append((a, b, op2, cyc))  # an MFMA operand (not the accumulator) from a fresh result
-                stack += [(s, cyc + MFMA_CYCLES) for s in successors(j)]
+                if cyc < RESULT_CYCLES and set().union(*map(_regs, fields[1:3])) & d:
+                    bad.append((a, b, op2 + " (result as operand)", cyc))
+                stack += [(s, cyc + MFMA_CYCLES, d, ra, rb) for s in successors(j)]
                 continue
-            # sources: every operand of a store/atomic/ds_write, all but the destination otherwise
-            stores = ("global_store", "buffer_store", "scratch_store", "flat_store", "ds_write", "global_atomic",
-                      "buffer_atomic", "flat_atomic", "ds_add")
             srcs = fields if op2.startswith(stores) else fields[1:]
-            if set().union(set(), *map(_regs, srcs)) & dst:
-                bad.append((a, b, op2, cyc))
-                continue
-            if set().union(set(), *map(_regs, fields[:1])) & dst:
-                continue  # result overwritten before being read
-            stack += [(s, cyc + 1) for s in successors(j)]
+            if cyc < RESULT_CYCLES and set().union(set(), *map(_regs, srcs)) & d:
+                bad.append((a, b, op2 + " (reads result)", cyc))
+                d = set()
+            w = _regs(fields[0]) if fields and op2.startswith(_WRITERS) else set()
+            if w & ra and cyc < A_CYCLES:
+                bad.append((a, b, op2 + " (rewrites A)", cyc))
+            if w & rb and cyc < B_CYCLES:
+                bad.append((a, b, op2 + " (rewrites B)", cyc))
+            d, ra, rb = d - w, ra - w, rb - w
+            stack += [(s, cyc + 1, d, ra, rb) for s in successors(j)]
     return bad
 
 
@@ -126,7 +132,7 @@ def main(argv):
             continue
         bad = check_function(insts)
         nm = sum(1 for _, op, _, _ in insts if op.startswith("v_mfma"))
-        print("%s: %d MFMAs, %d early result reads" % (name, nm, len(bad)))
+        print("%s: %d MFMAs, %d violations" % (name, nm, len(bad)))
         for v in bad[:10]:
             print("   mfma @%x  -> %s @%x after %d cycles" % (v[0], v[2], v[1], v[3]))
         nbad += len(bad)

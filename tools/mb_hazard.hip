@@ -99,6 +99,16 @@
         }                                                                                                 \
         for (int i = 0; i < 16; ++i) out[(blockIdx.x * blockDim.x + threadIdx.x) * 16 + i] = r[i];         \
     }                                                                                                     \
+    __global__ void k_warqa_##TAG(int* out) {                                                             \
+        int r[16];                                                                                        \
+        asm volatile(SETUP "v_mov_b32 v24, 0\n" BG8 MFMA W ZA LONGWAIT READOUT : OUTS : : CLOB2);            \
+        for (int i = 0; i < 16; ++i) out[(blockIdx.x * blockDim.x + threadIdx.x) * 16 + i] = r[i];         \
+    }                                                                                                     \
+    __global__ void k_warqb_##TAG(int* out) {                                                             \
+        int r[16];                                                                                        \
+        asm volatile(SETUP "v_mov_b32 v24, 0\n" BG8 MFMA W ZB LONGWAIT READOUT : OUTS : : CLOB2);            \
+        for (int i = 0; i < 16; ++i) out[(blockIdx.x * blockDim.x + threadIdx.x) * 16 + i] = r[i];         \
+    }                                                                                                     \
     __global__ void k_warb_##TAG(int* out) {                                                              \
         int r[16];                                                                                        \
         asm volatile(SETUP MFMA W ZB LONGWAIT READOUT : OUTS : : CLOB);                                   \
@@ -122,9 +132,10 @@ KERNELS(128, NOP64 NOP64)
 typedef void (*kfn)(int*);
 struct Case {
     int n;
-    kfn raw, wara, warb, rawl, opwa, opwb, chain, rawv;
+    kfn raw, wara, warb, rawl, opwa, opwb, chain, rawv, warqa, warqb;
 };
-#define CASE(T) {T, k_raw_##T, k_wara_##T, k_warb_##T, k_rawl_##T, k_opwa_##T, k_opwb_##T, k_chain_##T, k_rawv_##T}
+#define CASE(T) \
+    {T, k_raw_##T, k_wara_##T, k_warb_##T, k_rawl_##T, k_opwa_##T, k_opwb_##T, k_chain_##T, k_rawv_##T, k_warqa_##T, k_warqb_##T}
 
 static void report(const char* what, int n, const int* h, int nw = 1) {
     int bad = 0, badrow[32] = {0}, badreg[16] = {0};
@@ -152,19 +163,19 @@ int main() {
     int* d;
     hipMalloc(&d, (size_t)64 * 16 * nw * sizeof(int));
     static int h[64 * 16 * 16 * 256];
-    for (int rep = 0; rep < 3; ++rep)
+    for (int rep = 0; rep < 2; ++rep)
         for (const Case& c : cases) {
-            kfn fs[3] = {c.raw, c.wara, c.warb};
-            const char* names[3] = {"RAW", "WAR-A", "WAR-B"};
-            for (int k = 0; k < 3; ++k) {
+            kfn fs[5] = {c.raw, c.wara, c.warb, c.warqa, c.warqb};
+            const char* names[5] = {"RAW", "WAR-A", "WAR-B", "WARQ-A", "WARQ-B"};
+            for (int k = 0; k < 5; ++k) {
                 hipMemset(d, 0xff, 64 * 16 * sizeof(int));
                 hipLaunchKernelGGL(fs[k], dim3(1), dim3(64), 0, 0, d);
                 hipMemcpy(h, d, 64 * 16 * sizeof(int), hipMemcpyDeviceToHost);
                 report(names[k], c.n, h);
             }
-            kfn ls[5] = {c.rawl, c.opwa, c.opwb, c.chain, c.rawv};
-            const char* lnames[5] = {"RAW-4w", "OPWA4w", "OPWB4w", "CHN-4w", "RAW-VA"};
-            for (int k = 0; k < 5; ++k) {
+            kfn ls[7] = {c.rawl, c.opwa, c.opwb, c.chain, c.rawv, c.warqa, c.warqb};
+            const char* lnames[7] = {"RAW-4w", "OPWA4w", "OPWB4w", "CHN-4w", "RAW-VA", "WARQA4", "WARQB4"};
+            for (int k = 0; k < 7; ++k) {
                 hipMemset(d, 0xff, sizeof(h));
                 hipLaunchKernelGGL(ls[k], dim3(256), dim3(1024), 0, 0, d);
                 hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost);
