@@ -37,8 +37,13 @@ constexpr int kExTab = 4096;    // sin/cos table entries per turn
 constexpr int kExChunk = 64;    // photons per LDS chunk (one barrier per chunk)
 constexpr int kExWaves = 8;     // waves (tiles) per block
 constexpr int kExBlock = 64 * kExWaves;
-constexpr int kExFold = 16384 / kExChunk;  // chunks between int32 -> int64 folds: 16384 photons, the int32 bound
-                                            // (level 3: <= 2 x 49152 per photon, 1.61e9 < 2^31)
+// int32 headroom per photon and level (balanced digits, |top digit| <= 64): level 3 <= 2 x 49152, level 4
+// <= 2 x 32768, level 5 <= 2 x 16384, level 6 <= 2 x 4096. Every kExCarry chunks (16384 photons: level 3
+// reaches 1.61e9 < 2^31) the level sums are carried upward exactly (acc_L = 256 q + r, r in [0, 255]:
+// acc_L <- r, acc_{L+1} += q), which leaves level 6 growing by <= 2^27 per period; every kExFold chunks
+// (131072 photons, 8 periods: level 6 < 2^30 + carries) they are folded into the int64 running sums.
+constexpr int kExCarry = 16384 / kExChunk;
+constexpr int kExFold = 131072 / kExChunk;
 constexpr int kExFoldVals = 32;             // int64 running sums per lane (16 result rows x Re, Im)
 constexpr double kExUnit = 1.4551915228366852e-11;  // 2^-36: value of one unit of the int64 totals
 
@@ -167,7 +172,7 @@ __global__ __launch_bounds__(kExBlock, 2) void k_search_exact(
     // the block's running int64 sums between folds: per lane in global scratch (coalesced, written and read
     // by the same lane), so that they take no registers inside the photon loop
     long long* const fs =
-        fold + ((((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * kExWaves + wv) * 64 + lane) * kExFoldVals;
+        fold + (((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * kExWaves + wv) * (kExFoldVals * 64) + lane;
     const int comp = 2 * (kh - 1);
 
     load_dt(0, 0);
@@ -203,7 +208,21 @@ __global__ __launch_bounds__(kExBlock, 2) void k_search_exact(
                 }
                 mfma_operand_guard();
             }
-            if ((c + 1) % kExFold == 0 || c + 1 == nch) {
+            const bool fold_now = (c + 1) % kExFold == 0 || c + 1 == nch;
+            if (!fold_now && (c + 1) % kExCarry == 0) {
+                mfma_drain();
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+#pragma unroll
+                    for (int x = 0; x < 2; ++x)
+#pragma unroll
+                        for (int L = 0; L < 3; ++L) {
+                            const int q = acc[L][x][r] >> 8;  // floor division by 256
+                            acc[L][x][r] &= 255;
+                            acc[L + 1][x][r] += q;
+                        }
+            }
+            if (fold_now) {
                 mfma_drain();
                 const bool first_fold = c + 1 <= kExFold, last = c + 1 == nch;
                 // opaque copies of the lane's scratch pointer and trial index: the 32 addresses derived from them
@@ -216,12 +235,12 @@ __global__ __launch_bounds__(kExBlock, 2) void k_search_exact(
                     long long re = ex_level_sum(acc[0][0][r], acc[1][0][r], acc[2][0][r], acc[3][0][r]);
                     long long im = ex_level_sum(acc[0][1][r], acc[1][1][r], acc[2][1][r], acc[3][1][r]);
                     if (!first_fold) {
-                        re += f[2 * r];
-                        im += f[2 * r + 1];
+                        re += f[r * 64];
+                        im += f[(16 + r) * 64];
                     }
                     if (!last) {
-                        f[2 * r] = re;
-                        f[2 * r + 1] = im;
+                        f[r * 64] = re;
+                        f[(16 + r) * 64] = im;
                     } else {
                         // D[row a][col b] of the 32x32 tile: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 h;
                         // trial c0 + 32 a + b, output slot o = frow * nf + trial - first
