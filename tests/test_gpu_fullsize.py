@@ -51,23 +51,32 @@ def test_config3_full_size(gpu):
 
 
 def test_config4_full_photon_count_h20(gpu):
-    """1e8 photons with fdot, 2-D H-test m=20 on a trial sub-grid (the full 1e7-trial grid runs sharded on
-    8 GPUs in the bench configuration); oracle over all photons on sampled trials."""
+    """1e8 photons with fdot, 2-D H-test m=20 on a 3 x 8192 trial sub-grid (the full 1e7-trial grid runs sharded
+    on 8 GPUs in the bench configuration): oracle over all photons on 8 sampled trials (plain per-trial relative
+    error), and every fd row computed as its own trial range bit-identical to the whole grid."""
     import torch
     from crimp_amd import ops
     from crimp_amd.synth import pulsed_events
     n, span, f0, fdot = 100_000_000, 1.0e7, 7.123456789, -1.0e-12
     t_h = pulsed_events(n, span, f0, pulsed_frac=0.05, fdot=fdot, seed=1)
     df = 1.0 / (10.0 * span)
-    f_h = f0 + (np.arange(1024) - 512) * df
+    M = 8192
+    f_h = f0 + (np.arange(M) - M // 2) * df
     fd = np.array([-12.5, -12.0, -11.5])
     t = torch.as_tensor(t_h, device=gpu)
+    f = torch.as_tensor(f_h, device=gpu)
+    fdd = torch.as_tensor(fd, device=gpu)
     t0 = (t_h[0] + t_h[-1]) / 2
-    h = ops.search(t, t0, torch.as_tensor(f_h, device=gpu), 20, 1,
-                   log10_negfdot=torch.as_tensor(fd, device=gpu)).cpu().numpy().reshape(3, 1024)
+    hf = ops.search(t, t0, f, 20, 1, log10_negfdot=fdd).cpu().numpy()
+    h = hf.reshape(3, M)
     r, j = np.unravel_index(int(np.argmax(h)), h.shape)
-    assert r == 1 and j == 512                                # fdot = -1e-12 -> log10 = -12, f0 at index 512
-    sample = [(1, 512), (0, 100), (2, 900)]
+    assert r == 1 and j == M // 2                              # fdot = -1e-12 -> log10 = -12, f0 at index M/2
+    for row in range(3):                                       # row-sharded, as 3 ranks would compute it
+        hr = ops.search(t, t0, f, 20, 1, log10_negfdot=fdd, first=row * M, count=M).cpu().numpy()
+        np.testing.assert_array_equal(hr, h[row])
+    rng = np.random.default_rng(4)
+    sample = [(1, M // 2), (1, M // 2 + 1), (0, 100), (2, M - 1)] + [(int(a), int(b)) for a, b in
+                                                                       zip(rng.integers(0, 3, 4), rng.integers(0, M, 4))]
     for rr, jj in sample:
         ref = O.search(t_h, f_h[jj:jj + 1], 20, freq_dot=fd[rr:rr + 1], stat="h")[0]
         assert abs(h[rr, jj] - ref) <= 1e-6 * abs(ref), (rr, jj, h[rr, jj], ref)
