@@ -1305,7 +1305,7 @@ static int exact_search(Scratch& sc, hipStream_t s, const double* dt, const doub
     HIPCHK(sc.alloc(&flagged, (size_t)count));
     HIPCHK(sc.alloc(&nflag, 1));
     HIPCHK(hipMemsetAsync(nflag, 0, sizeof(int), s));
-    const double dc = 10.0 * std::sqrt((double)n) * 1e-9;  // 10-sigma bound on |error of C_k| (search_exact.h)
+    const double sigc = std::sqrt((double)n) * 1e-9;  // standard deviation of the error of C_k (search_exact.h)
     if (kt) kt->start();
     for (int64_t b0 = 0; b0 < count; b0 += cb) {
         const int64_t bfirst = first + b0, bcount = std::min<int64_t>(cb, count - b0);
@@ -1336,7 +1336,7 @@ static int exact_search(Scratch& sc, hipStream_t s, const double* dt, const doub
         }
         if (kt && b0 + cb >= count) kt->stop();
         k_search_finalize_exact<<<(unsigned)cdiv(bcount, 256), 256, 0, s>>>(
-            reinterpret_cast<const long long*>(tot), bcount, nharm, stat, (double)n, dc, fixup_rel(), b0, out + b0, nflag, flagged);
+            reinterpret_cast<const long long*>(tot), bcount, nharm, stat, (double)n, sigc, fixup_rel(), b0, out + b0, nflag, flagged);
         HIPCHK(hipGetLastError());
     }
     int nf_h = 0;

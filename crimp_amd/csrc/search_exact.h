@@ -264,31 +264,55 @@ __global__ __launch_bounds__(kExBlock, 2) void k_search_exact(
 
 // Statistic from the exact totals (periodsearch.py:67-69 and :120-123 in the reference's formula order), and
 // the fix-up list: trials whose power is too small for the kernel's error bound to guarantee 1e-6 relative.
-// Per-term error of U.V (2^30 roundings of both factors, fp32 residual rotation): |e| <= 3e-9, rms <= 1e-9;
-// the error of C_k is a sum of N such terms with random signs, so with kappa = 10 standard deviations
-// dC = 10 sqrt(N) 1e-9 (and the same for S_k), and |Z2_k error| <= (2/N)(2(|C| + |S|) dC + 2 dC^2).
+// Error model: per term of U.V (2^30 roundings of both factors, fp32 residual rotation) |e| <= 3e-9, rms <= 1e-9,
+// independent across photons and harmonics, so C_k and S_k carry errors of standard deviation
+// sc = sqrt(N) 1e-9 and Z2_k = (2/N)(C^2 + S^2) one of (4/N) sc sqrt(C^2 + S^2) (+ (2/N) 2 sc^2 bias). A sum of
+// harmonics i <= k (Z2, and H's cumulative g_k = sum_{i<=k} Z2_i - 4(k-1)) has standard deviation
+// (4/N) sc sqrt(sum_{i<=k} (C_i^2 + S_i^2)); the bound is kappa = 10 of them plus the bias. H = max_k g_k moves
+// by at most the bound of any g_k that can reach the maximum (g_k + err_k >= H - err_k*), so only those count.
 __global__ __launch_bounds__(256) void k_search_finalize_exact(const long long* __restrict__ tot, int64_t count, int m,
-                                                               int stat, double n, double dc, double rel, int64_t tbase,
+                                                               int stat, double n, double sc, double rel, int64_t tbase,
                                                                double* __restrict__ out, int* __restrict__ nflag,
                                                                int64_t* __restrict__ flagged) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= count) return;
-    const double w = 2.0 / n;
-    double zsum = 0.0, cum = 0.0, best = -INFINITY, err = 0.0;
-    for (int k = 0; k < m; ++k) {
+    const double w = 2.0 / n, kappa = 10.0;
+    const double lin = kappa * 2.0 * w * sc, quad = w * 2.0 * (kappa * sc) * (kappa * sc);
+    auto zk = [&](int k) {
         const double c = (double)tot[(int64_t)(2 * k) * count + t] * kExUnit;
         const double s = (double)tot[(int64_t)(2 * k + 1) * count + t] * kExUnit;
-        const double z = c * c + s * s;
-        err += w * (2.0 * (fabs(c) + fabs(s)) * dc + 2.0 * dc * dc);
-        if (stat == CRIMP_STAT_Z2) {
-            zsum += z;
-        } else {
+        return c * c + s * s;
+    };
+    double p, err;
+    if (stat == CRIMP_STAT_Z2) {
+        double zsum = 0.0;
+        for (int k = 0; k < m; ++k) zsum += zk(k);
+        p = zsum * w;
+        err = lin * sqrt(zsum) + m * quad;
+    } else {
+        double cum = 0.0, raw = 0.0, best = -INFINITY, ebest = 0.0;
+        for (int k = 0; k < m; ++k) {
+            const double z = zk(k);
             cum += z * w;
+            raw += z;
             const double v = cum - 4.0 * (double)k;
-            best = v > best ? v : best;
+            if (v > best) {
+                best = v;
+                ebest = lin * sqrt(raw) + (k + 1) * quad;
+            }
+        }
+        p = best;
+        err = ebest;
+        cum = 0.0;
+        raw = 0.0;
+        for (int k = 0; k < m; ++k) {  // every g_k that the errors could lift to the maximum
+            const double z = zk(k);
+            cum += z * w;
+            raw += z;
+            const double ek = lin * sqrt(raw) + (k + 1) * quad;
+            if (cum - 4.0 * (double)k + ek >= best - ebest) err = fmax(err, ek);
         }
     }
-    const double p = (stat == CRIMP_STAT_Z2) ? zsum * w : best;
     out[t] = p;
     if (!(err <= rel * fabs(p))) flagged[atomicAdd(nflag, 1)] = tbase + t;
 }
