@@ -234,3 +234,25 @@ def test_cauchy_vonmises_blocks_1e5(gpu):
         r = ToAFitter(x, off, E, tm).fit(brutemin=True)
         for i in range(len(xs)):
             _fit_vs_oracle(r, i, xs[i], E[i], tm)
+
+
+def test_exact_vs_f64_every_trial(gpu):
+    """The per-trial contract on every trial of larger grids, near-zero powers included: the default (exact +
+    fix-up) path against the fp64 path (itself within 1e-8 of the reference's outputs), 1e6 photons, Z^2_4 over
+    16384 trials and 2-D H_20 over 2 x 8192 trials."""
+    import torch
+    from crimp_amd import ops, _native as N
+    from crimp_amd.synth import pulsed_events
+    t_h = pulsed_events(1_000_000, 1.0e6, 7.123456789, pulsed_frac=0.02, fdot=-1e-12, seed=9)
+    t = torch.as_tensor(t_h, device=gpu)
+    t0 = (t_h[0] + t_h[-1]) / 2
+    f = torch.as_tensor(7.123456789 + (np.arange(16384) - 8192) / 1.0e7, device=gpu)
+    z = ops.search(t, t0, f, 4, 0).cpu().numpy()
+    z64 = ops.search(t, t0, f, 4, 0, precision="f64").cpu().numpy()
+    assert _rel_err(z, z64).max() <= 1e-6
+    fd = torch.as_tensor(np.array([-12.0, -11.0]), device=gpu)
+    h = ops.search(t, t0, f[4096:12288], 20, 1, log10_negfdot=fd).cpu().numpy()
+    nfix = N.load().crimp_last_fixups()
+    h64 = ops.search(t, t0, f[4096:12288], 20, 1, log10_negfdot=fd, precision="f64").cpu().numpy()
+    assert _rel_err(h, h64).max() <= 1e-6
+    assert nfix < h.size // 10
