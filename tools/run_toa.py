@@ -1,5 +1,6 @@
-"""Config-5 ToA fits on one GPU (brute + MLE + 1-sigma scan), timed after a warm-up; 
-a kernel experiment. NINT / NPH override the interval count and photons per interval."""
+"""Config-5 ToA fits on one GPU (brute + MLE + 1-sigma scan), timed after a warm-up, with the brute-grid and fit
+kernel times (hipEvents inside crimp_toa_fit). CRIMP_LIB selects a library build (A/B of kernel variants);
+NINT / NPH override the interval count and photons per interval."""
 import os
 import sys
 import time
@@ -10,6 +11,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from bench import T2259  # noqa: E402
 from crimp_amd.synth import template_intervals_torch  # noqa: E402
 from crimp_amd.toafit import ToAFitter  # noqa: E402
+from crimp_amd import ops, _native as N  # noqa: E402
+import numpy as np  # noqa: E402
 
 nint, nph = int(os.environ.get("NINT", 1250)), int(os.environ.get("NPH", 100_000))
 dev = torch.device("cuda", 0)
@@ -25,5 +28,8 @@ for rep in range(3):
     r = ToAFitter(x, off, E, tm).fit(brutemin=True)
     torch.cuda.synchronize()
     el = time.perf_counter() - t1
-    print("lib %s: %d x %d photons: %.1f ms, %.4g fits/s, phShi[0:3] %s" % (
-        "libcrimp_hip", nint, nph, el * 1e3, nint / el, r["phShi"][:3]), flush=True)
+    f = ToAFitter(x, off, E, tm)
+    ops.toa_fit(f.x, f.offsets, f.tpl, f._arr(f.E, np.float64), f.norm0, f.res, True, False, flags=N.FLAG_TIME_KERNELS)
+    g_ms, f_ms = N.last_kernel_times()[:2]
+    print("lib %s: %d x %d photons: %.1f ms (grid %.2f ms, fit %.2f ms), %.4g fits/s, phShi[0:3] %s" % (
+        os.path.basename(N.LIB_PATH), nint, nph, el * 1e3, g_ms, f_ms, nint / el, r["phShi"][:3]), flush=True)
