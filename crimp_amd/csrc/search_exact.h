@@ -146,19 +146,32 @@ __global__ __launch_bounds__(kExBlock, 2) void k_search_exact(
         }
     };
     // V digits of chunk c as B fragments; photons past the split get V = 0, so that their products vanish
-    auto produce = [&](int c, int slot, int vb) {
+    // one store address per thread: item s writes photon pp + 16 s, i.e. pair (pp >> 1) + 8 s (an immediate
+    // offset), half pp & 1 of the pair's uint4
+    const int pp = tid >> 5;
+    uint2* const wre = reinterpret_cast<uint2*>(&vre[0][pp >> 1][pb]) + (pp & 1);
+    uint2* const wim = reinterpret_cast<uint2*>(&vim[0][pp >> 1][pb]) + (pp & 1);
+    constexpr int kPairU2 = 32 * 2;                    // uint2 per photon pair row of 32 columns
+    constexpr int kBufU2 = (kExChunk / 2) * kPairU2;   // uint2 per buffer
+    auto produce_items = [&](int slot, int vb, int nlive, bool masked) {
 #pragma unroll
         for (int s = 0; s < kExChunk * 32 / kExBlock; ++s) {
-            const int p = (tid >> 5) + (kExBlock / 32) * s;
+            const int p = pp + (kExBlock / 32) * s;
             uint32_t dc, dsn;
             ex_sincos_digits(tab, gbv * sdt[slot][p], dc, dsn);
-            const bool live = i0 + (int64_t)c * kExChunk + p < i1;
-            const uint32_t rc = live ? __builtin_bswap32(dc) : 0u;
-            const uint32_t rs = live ? __builtin_bswap32(dsn) : 0u;
-            const uint32_t rn = live ? __builtin_bswap32(ex_neg_digits(dsn)) : 0u;
-            *(reinterpret_cast<uint2*>(&vre[vb][p >> 1][pb]) + (p & 1)) = make_uint2(rc, rn);
-            *(reinterpret_cast<uint2*>(&vim[vb][p >> 1][pb]) + (p & 1)) = make_uint2(rs, rc);
+            uint32_t rc = __builtin_bswap32(dc), rs = __builtin_bswap32(dsn),
+                     rn = __builtin_bswap32(ex_neg_digits(dsn));
+            if (masked && p >= nlive) rc = rs = rn = 0u;
+            wre[vb * kBufU2 + s * 8 * kPairU2] = make_uint2(rc, rn);
+            wim[vb * kBufU2 + s * 8 * kPairU2] = make_uint2(rs, rc);
         }
+    };
+    auto produce = [&](int c, int slot, int vb) {
+        const int64_t rest = i1 - (i0 + (int64_t)c * kExChunk);
+        if (rest >= kExChunk)
+            produce_items(slot, vb, kExChunk, false);  // every chunk but a split's last: no masks
+        else
+            produce_items(slot, vb, (int)rest, true);
     };
     auto uphase = [&](int ds, int p) -> double {
         return TWOD ? fma(fa, sdt[ds][p], c2 * sdt2[TWOD ? ds : 0][p]) : fa * sdt[ds][p];
