@@ -256,3 +256,25 @@ def test_exact_vs_f64_every_trial(gpu):
     h64 = ops.search(t, t0, f[4096:12288], 20, 1, log10_negfdot=fd, precision="f64").cpu().numpy()
     assert _rel_err(h, h64).max() <= 1e-6
     assert nfix < h.size // 10
+
+
+def test_exact_many_harmonics_and_ragged_partitions(gpu):
+    """H_64 on the exact path against the fp64 path on every trial, and a 2-D grid of rows that are not a whole
+    number of 1024-trial tiles split at arbitrary flat indices (mid-row, mid-tile): the pieces equal the whole
+    bit for bit."""
+    import torch
+    from crimp_amd import ops
+    from crimp_amd.synth import pulsed_events
+    t_h = pulsed_events(200_000, 2.0e5, 3.3, pulsed_frac=0.05, seed=12)
+    t = torch.as_tensor(t_h, device=gpu)
+    t0 = (t_h[0] + t_h[-1]) / 2
+    f = torch.as_tensor(3.3 + (np.arange(1000) - 500) / 2.0e6, device=gpu)
+    h = ops.search(t, t0, f, 64, 1).cpu().numpy()
+    h64 = ops.search(t, t0, f, 64, 1, precision="f64").cpu().numpy()
+    assert _rel_err(h, h64).max() <= 1e-6
+    fd = torch.as_tensor(np.array([-13.0, -12.0, -11.0]), device=gpu)
+    whole = ops.search(t, t0, f, 2, 0, log10_negfdot=fd).cpu().numpy()
+    cuts = [0, 1, 999, 1500, 2047, 2100, 3000]
+    parts = [ops.search(t, t0, f, 2, 0, log10_negfdot=fd, first=a, count=b - a).cpu().numpy()
+             for a, b in zip(cuts[:-1], cuts[1:])]
+    np.testing.assert_array_equal(np.concatenate(parts), whole)
