@@ -4,7 +4,7 @@ import glob
 import sys
 from collections import defaultdict
 
-root, pat = sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "k_search_mfma"
+root, pat = sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "k_search_exact"
 tot, durs = defaultdict(float), {}
 for fn in glob.glob(root + "/**/*counter_collection.csv", recursive=True):
     for row in csv.DictReader(open(fn)):
