@@ -278,3 +278,24 @@ def test_exact_many_harmonics_and_ragged_partitions(gpu):
     parts = [ops.search(t, t0, f, 2, 0, log10_negfdot=fd, first=a, count=b - a).cpu().numpy()
              for a, b in zip(cuts[:-1], cuts[1:])]
     np.testing.assert_array_equal(np.concatenate(parts), whole)
+
+
+def test_exact_path_photon_limit_routes_to_fp64(gpu):
+    """The exact kernel's int64 totals hold N < 2^27 photons; at N = 2^27 the search routes to the fp64 kernel
+    (bit-identical to precision='f64'), just below it takes the exact path (within 1e-6 of the fp64 path)."""
+    import torch
+    from crimp_amd import ops
+    g = torch.Generator(device=gpu)
+    g.manual_seed(5)
+    n = 1 << 27
+    t = 5.0e9 + torch.rand(n, generator=g, dtype=torch.float64, device=gpu) * 1.0e6
+    f = torch.as_tensor(1.7 + (np.arange(256) - 128) / 1.0e7, device=gpu)
+    t0 = 5.0e9 + 5.0e5
+    z_at = ops.search(t, t0, f, 2, 0).cpu().numpy()
+    z_at64 = ops.search(t, t0, f, 2, 0, precision="f64").cpu().numpy()
+    np.testing.assert_array_equal(z_at, z_at64)
+    tb = t[: n - 1]
+    z_below = ops.search(tb, t0, f, 2, 0).cpu().numpy()
+    z_below64 = ops.search(tb, t0, f, 2, 0, precision="f64").cpu().numpy()
+    assert _rel_err(z_below, z_below64).max() <= 1e-6
+    assert not np.array_equal(z_below, z_below64)       # a different (exact) kernel ran
