@@ -1287,18 +1287,50 @@ static int fast_search(Scratch& sc, hipStream_t s, const double* dt, const doubl
 // int64 totals in units of 2^-36 hold |C_k| <= n exactly for n < 2^27 photons.
 static const int64_t kExactMaxPhotons = int64_t(1) << 27;
 static const int64_t kExFoldMaxBlocks = 8192;  // fold scratch of one launch <= 1 GiB
+// Photon splits of the exact kernel (one 256-thread block per CU): >= 4096 photons per split and >= 8 rounds of
+// the device's CUs, and among those counts (up to 4x the smallest) the one whose last round of blocks is fullest:
+// a grid of 8.2 rounds runs as long as 9 (config 3: 123 block columns x 17 splits = 2091 blocks on 256 CUs wasted
+// 9 %; 29 splits = 3567 blocks fill 13.93 rounds).
+static void exact_splits(int64_t n, int64_t bpg, int64_t* chunk_out, int64_t* splits_out) {
+    static int ncu = 0;
+    if (!ncu) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+            ncu = 256;
+    }
+    const int64_t smax_n = std::max<int64_t>(1, std::min<int64_t>(cdiv(n, 4096), 65535));
+    const int64_t smax = std::max<int64_t>(1, std::min<int64_t>(smax_n, kExFoldMaxBlocks / bpg));
+    const int64_t smin = std::max<int64_t>(1, std::min<int64_t>(cdiv(8 * (int64_t)ncu, bpg), smax));
+    int64_t best_chunk = 0, best_splits = 0;
+    double best_eff = -1.0;
+    for (int64_t want = smin; want <= std::min<int64_t>(smax, 4 * smin); ++want) {
+        const int64_t chunk = cdiv(cdiv(n, want), kExChunk) * kExChunk;
+        const int64_t splits = cdiv(n, chunk);
+        const int64_t blocks = bpg * splits;
+        const double eff = (double)blocks / (double)(cdiv(blocks, ncu) * ncu);
+        if (eff > best_eff + 0.005) {
+            best_eff = eff;
+            best_chunk = chunk;
+            best_splits = splits;
+        }
+    }
+    *chunk_out = best_chunk;
+    *splits_out = best_splits;
+}
+
 static int exact_search(Scratch& sc, hipStream_t s, const double* dt, const double* dt2, int64_t n, const double* freq,
                         int64_t nf, const double* c2, const double* ap, bool twod, int nharm, int stat, int64_t first,
                         int64_t count, double* out, KernelTimer* kt, int64_t* nfixed) {
-    const int64_t tpr = cdiv(nf, kTile);
+    const int64_t tpr = cdiv(nf, kExTileTrials);
     const int ncomp = 2 * nharm;
     // trial blocks bounded by the int64 totals buffer (2 GiB) and by the blocks' fold scratch (kExFoldMaxBlocks
     // blocks of 128 KB), whole 8-tile block groups
-    const int64_t cbmax = std::min<int64_t>(std::max<int64_t>(kTile * kExWaves, part_budget() / (8 * ncomp)),
-                                            kExFoldMaxBlocks * kExWaves * kTile);
-    const int64_t cb = std::min<int64_t>(count, cdiv(cdiv(count, cdiv(count, cbmax)), kTile) * kTile);
+    const int64_t cbmax = std::min<int64_t>(std::max<int64_t>(kExTileTrials * kExWaves, part_budget() / (8 * ncomp)),
+                                            kExFoldMaxBlocks * kExWaves * kExTileTrials);
+    const int64_t cb = std::min<int64_t>(count, cdiv(cdiv(count, cdiv(count, cbmax)), kExTileTrials) * kExTileTrials);
     unsigned long long* tot = nullptr;
     long long* fold = nullptr;
+    int64_t fold_blocks = 0;
     int64_t* flagged = nullptr;
     int* nflag = nullptr;
     HIPCHK(sc.alloc(&tot, (size_t)(ncomp * cb)));
@@ -1310,21 +1342,19 @@ static int exact_search(Scratch& sc, hipStream_t s, const double* dt, const doub
     for (int64_t b0 = 0; b0 < count; b0 += cb) {
         const int64_t bfirst = first + b0, bcount = std::min<int64_t>(cb, count - b0);
         const int64_t last = bfirst + bcount - 1;
-        const int64_t tf = (bfirst / nf) * tpr + (bfirst % nf) / kTile;
-        const int64_t tl = (last / nf) * tpr + (last % nf) / kTile;
+        const int64_t tf = (bfirst / nf) * tpr + (bfirst % nf) / kExTileTrials;
+        const int64_t tl = (last / nf) * tpr + (last % nf) / kExTileTrials;
         const int64_t nt = tl - tf + 1;
         const int64_t bpg = cdiv(nt, kExWaves);
-        // photon splits: >= 8 rounds of the 256 CUs' block slots (one 512-thread block per CU), >= 4096 photons each
-        const int64_t want = std::max<int64_t>(1, std::min<int64_t>(cdiv(8 * 256, bpg), cdiv(n, 4096)));
-        const int64_t chunk = cdiv(cdiv(n, std::min<int64_t>(want, 65535)), kExChunk) * kExChunk;
-        const int64_t splits = cdiv(n, chunk);
+        int64_t chunk = 0, splits = 0;
+        exact_splits(n, bpg, &chunk, &splits);
         HIPCHK(hipMemsetAsync(tot, 0, (size_t)(ncomp * bcount) * sizeof(unsigned long long), s));
         dim3 grid((unsigned)bpg, (unsigned)splits);
-        if (!fold) {  // blocks per launch <= bpg + 2048 (the split count above), bpg <= cb / 8192 + 2
-            const int64_t maxblocks = cdiv(cb, kTile * kExWaves) + 2 + 2048;
-            HIPCHK(sc.alloc(&fold, (size_t)(maxblocks * kExWaves * kExFoldVals * 64)));
+        if (!fold) {  // sized by the first trial block, the largest (exact_splits keeps bpg * splits <= kExFoldMaxBlocks)
+            fold_blocks = bpg * splits;
+            HIPCHK(sc.alloc(&fold, (size_t)(fold_blocks * kExWaves * kExFoldVals * 64)));
         }
-        if (bpg * splits > cdiv(cb, kTile * kExWaves) + 2 + 2048) return set_err(CRIMP_ERR_HIP, "exact search: fold scratch bound");
+        if (bpg * splits > fold_blocks) return set_err(CRIMP_ERR_HIP, "exact search: fold scratch bound");
         for (int k = 1; k <= nharm; ++k) {
             if (twod)
                 k_search_exact<true><<<grid, kExBlock, 0, s>>>(dt, dt2, n, chunk, freq, nf, c2, ap, tf, nt, tpr, bfirst,

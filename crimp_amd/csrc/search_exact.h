@@ -30,13 +30,21 @@
 // (a, h) holds photons 4q+2h, 4q+2h+1 of quad q ({Ur, Ui} of each: 16 bytes = the K slice of one
 // i8 MFMA), so one quad costs 8 MFMAs (4 levels x Re/Im). V and dt are double/triple buffered so
 // that the producers of chunk c+1 run beside the MFMAs of chunk c with one barrier per chunk.
+#include <type_traits>
+
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kExTab = 4096;    // sin/cos table entries per turn
-constexpr int kExChunk = 64;    // photons per LDS chunk (one barrier per chunk)
-constexpr int kExWaves = 8;     // waves (tiles) per block
+constexpr int kExChunk = 32;    // photons per LDS chunk (one barrier per chunk)
+constexpr int kExQuads = kExChunk / 4;
+constexpr int kExWaves = 4;     // waves (tiles) per block: one per SIMD
 constexpr int kExBlock = 64 * kExWaves;
+constexpr int kExCols = 64;     // trial columns per tile: two 32-column B fragments
+constexpr int kExTileTrials = 32 * kExCols;           // trials per tile (32 rows)
+constexpr int kExItems = kExChunk * kExCols / kExBlock;  // V items per thread and chunk (= kExQuads)
+static_assert(kExItems == kExQuads, "one V item per pipeline group");
+constexpr int kExDtSlots = 4;   // photon-time ring: chunks c-1 (being retired) .. c+2
 // int32 headroom per photon and level (balanced digits, |top digit| <= 64): level 3 <= 2 x 49152, level 4
 // <= 2 x 32768, level 5 <= 2 x 16384, level 6 <= 2 x 4096. Every kExCarry chunks (16384 photons: level 3
 // reaches 1.61e9 < 2^31) the level sums are carried upward exactly (acc_L = 256 q + r, r in [0, 255]:
@@ -44,7 +52,7 @@ constexpr int kExBlock = 64 * kExWaves;
 // (131072 photons, 8 periods: level 6 < 2^30 + carries) they are folded into the int64 running sums.
 constexpr int kExCarry = 16384 / kExChunk;
 constexpr int kExFold = 131072 / kExChunk;
-constexpr int kExFoldVals = 32;             // int64 running sums per lane (16 result rows x Re, Im)
+constexpr int kExFoldVals = 64;             // int64 running sums per lane (2 fragments x 16 result rows x Re, Im)
 constexpr double kExUnit = 1.4551915228366852e-11;  // 2^-36: value of one unit of the int64 totals
 
 struct ExEntry {
@@ -68,14 +76,19 @@ __device__ __forceinline__ ExArg ex_begin(double t) {
     const double kf = tm - M;
     return ExArg{(uint32_t)__double2loint(tm) & (kExTab - 1), (float)(t - kf)};  // t - kf is exact
 }
-// -> digit dwords of cos (dc) and sin (ds)
-__device__ __forceinline__ void ex_end(const ExEntry& e, float y, uint32_t& dc, uint32_t& ds) {
+// -> digit dwords of cos (dc) and sin (ds), in two halves (ex_end_a: the rotation terms, ex_end_b: the digits)
+struct ExRot { float ts, tc; };
+__device__ __forceinline__ ExRot ex_end_a(const ExEntry& e, float y) {
     const float u = y * (3.14159265358979323846f / (float)kExTab);
-    const float ts = __builtin_fmaf(-u, e.s1, e.c1);
-    const float tc = __builtin_fmaf(u, e.c1, e.s1);
+    return ExRot{__builtin_fmaf(-u, e.s1, e.c1), __builtin_fmaf(u, e.c1, e.s1)};
+}
+__device__ __forceinline__ void ex_end_b(const ExEntry& e, float y, ExRot r, uint32_t& dc, uint32_t& ds) {
     // |value| < 2^22: the low mantissa bits of fma(y, t, 1.5 * 2^23) are rint(y t) + 0x400000
-    ds = ((uint32_t)e.sk + __float_as_uint(__builtin_fmaf(y, ts, 12582912.0f))) ^ 0x00808080u;
-    dc = ((uint32_t)e.ck + __float_as_uint(__builtin_fmaf(-y, tc, 12582912.0f))) ^ 0x00808080u;
+    ds = ((uint32_t)e.sk + __float_as_uint(__builtin_fmaf(y, r.ts, 12582912.0f))) ^ 0x00808080u;
+    dc = ((uint32_t)e.ck + __float_as_uint(__builtin_fmaf(-y, r.tc, 12582912.0f))) ^ 0x00808080u;
+}
+__device__ __forceinline__ void ex_end(const ExEntry& e, float y, uint32_t& dc, uint32_t& ds) {
+    ex_end_b(e, y, ex_end_a(e, y), dc, ds);
 }
 __device__ __forceinline__ void ex_sincos_digits(const ExEntry* __restrict__ tab, double t, uint32_t& dc,
                                                  uint32_t& ds) {
@@ -102,21 +115,73 @@ __device__ __forceinline__ uint32_t ex_neg_digits(uint32_t d) {
 }
 
 
+// Issue-order control for the pipelined photon loop. The MFMAs are volatile inline asm, so they keep their
+// program order with respect to each other, to LDS accesses and to the empty asm fences below; hipcc only moves
+// VALU work between them:
+//   ex_ready(x): x is computed before this point (pins a piece of work before the next MFMA);
+//   ex_open(x):  x is redefined here (work that depends on x starts after this point);
+//   ex_keep(x):  x's registers stay allocated until here. A quad's operands are kept until two MFMAs of the
+//                next group have issued, so no register an MFMA reads is rewritten within 64 cycles of its issue
+//                (the matrix pipe issues one 32x32x32 i8 MFMA per 32 cycles; mfma_drain.h for why it matters).
+// Operands are ready one whole group ahead, results are read only after mfma_drain(); hipcc inserts the LDS
+// waits (s_waitcnt) for the asm operands.
+// The wave's 16 int32 accumulator tiles live in AGPRs for the whole kernel, outside the compiler's register
+// model: tile m (level m >> 2, fragment (m >> 1) & 1, Re/Im m & 1) is a[16m : 16m + 15]. Only these asm helpers
+// touch AGPRs (the kernel has no spills, so hipcc never allocates them; ex_acc_zero's clobber makes the code
+// object reserve all 256), so the accumulators never move; tools/isa_hazards.py checks both on the built code.
+template <int M>
+__device__ __forceinline__ void ex_mfma(const i32x4& a, const i32x4& b) {
+    asm volatile("v_mfma_i32_32x32x32_i8 a[%c2:%c3], %0, %1, a[%c2:%c3]" ::"v"(a), "v"(b), "i"(16 * M),
+                 "i"(16 * M + 15));
+}
+template <int R>
+__device__ __forceinline__ int ex_acc_read(std::integral_constant<int, R>) {
+    int x;
+    asm volatile("v_accvgpr_read_b32 %0, a%c1" : "=v"(x) : "i"(R));
+    return x;
+}
+template <int R>
+__device__ __forceinline__ void ex_acc_write(std::integral_constant<int, R>, int x) {
+    asm volatile("v_accvgpr_write_b32 a%c0, %1" ::"i"(R), "v"(x));
+}
+template <int N, typename F>
+__device__ __forceinline__ void ex_static_for(F&& f) {
+    if constexpr (N > 0) {
+        ex_static_for<N - 1>(f);
+        f(std::integral_constant<int, N - 1>{});
+    }
+}
+template <int M, int R>
+using ex_areg = std::integral_constant<int, 16 * M + R>;
+__device__ __forceinline__ void ex_acc_zero() {
+    asm volatile("v_accvgpr_write_b32 a255, 0" ::: "a255");
+    ex_static_for<255>([&](auto r) { asm volatile("v_accvgpr_write_b32 a%c0, 0" ::"i"(decltype(r)::value)); });
+}
+__device__ __forceinline__ void ex_keep(const i32x4& x) { asm volatile("" ::"v"(x)); }
+__device__ __forceinline__ void ex_ready(const i32x4& x) { asm volatile("" ::"v"(x)); }
+__device__ __forceinline__ void ex_ready(uint32_t x, float y) { asm volatile("" ::"v"(x), "v"(y)); }
+__device__ __forceinline__ void ex_ready(uint32_t x, uint32_t y) { asm volatile("" ::"v"(x), "v"(y)); }
+__device__ __forceinline__ void ex_open(double& x) { asm volatile("" : "+v"(x)); }
+__device__ __forceinline__ void ex_open(float& x) { asm volatile("" : "+v"(x)); }
+__device__ __forceinline__ void ex_ready(float x, float y) { asm volatile("" ::"v"(x), "v"(y)); }
+__device__ __forceinline__ void ex_open(uint32_t& x, uint32_t& y) { asm volatile("" : "+v"(x), "+v"(y)); }
+
 __device__ __forceinline__ int64_t ex_level_sum(int a3, int a4, int a5, int a6) {
     return (int64_t)a3 + ((int64_t)a4 << 8) + ((int64_t)a5 << 16) + ((int64_t)a6 << 24);
 }
 
 template <bool TWOD>
-__global__ __launch_bounds__(kExBlock, 2) void k_search_exact(
+__global__ __launch_bounds__(kExBlock, 1) void k_search_exact(
     const double* __restrict__ dt, const double* __restrict__ dt2, int64_t n, int64_t chunk,
     const double* __restrict__ freq, int64_t nf, const double* __restrict__ c2row, const double* __restrict__ apinfo,
     int64_t tile_first, int64_t ntiles, int64_t tiles_per_row, int64_t first, int64_t count, int kh,
     unsigned long long* __restrict__ tot, long long* __restrict__ fold) {
-    __shared__ ExEntry tab[kExTab];                        // 64 KB
-    __shared__ uint4 vre[2][kExChunk / 2][32];             // B fragments (Re) per photon pair and column b
-    __shared__ uint4 vim[2][kExChunk / 2][32];             // B fragments (Im)
-    __shared__ double sdt[3][kExChunk];
-    __shared__ double sdt2[TWOD ? 3 : 1][kExChunk];
+    __shared__ ExEntry tab[kExTab];                          // 64 KB
+    // B fragments per photon pair and column b: two chunk buffers of kExChunk / 2 pairs, a ring of kExChunk pairs
+    __shared__ uint4 vre[kExChunk][kExCols];                 // {rev Vr, rev -Vi} of the pair's two photons
+    __shared__ uint4 vim[kExChunk][kExCols];                 // {rev Vi, rev Vr}
+    __shared__ double sdt[kExDtSlots * kExChunk];            // photon times: a ring of four chunks
+    __shared__ double sdt2[TWOD ? kExDtSlots * kExChunk : 1];
     const int tid = threadIdx.x;
     const int lane = tid & 63, wv = tid >> 6;
     for (int i = tid; i < kExTab; i += kExBlock) tab[i] = ex_entry(i);
@@ -125,153 +190,306 @@ __global__ __launch_bounds__(kExBlock, 2) void k_search_exact(
     const bool active = T < ntiles;                          // wave-uniform
     const int64_t gt = tile_first + (active ? T : 0);
     const int64_t frow = gt / tiles_per_row;
-    const int64_t c0 = (gt - frow * tiles_per_row) * 1024;
+    const int64_t c0 = (gt - frow * tiles_per_row) * kExTileTrials;
     const int ar = lane & 31, h = lane >> 5;
-    const int64_t ca = c0 + 32 * ar;
+    const int64_t ca = c0 + kExCols * ar;                    // U row a: trial c0 + 64 a
     const double fa = freq[ca < nf ? ca : nf - 1] * kT;
     const double c2 = TWOD ? c2row[frow] * kT : 0.0;
-    const int pb = tid & 31;                                  // producer: V_b for b = pb, photons (tid >> 5) + 16 s
+    const int pb = tid & (kExCols - 1);                      // producer: V_b for b = pb, photons (tid >> 6) + 4 s
+    const int pp = tid / kExCols;
     const double gbv = (double)pb * apinfo[0] * kT;
     const int64_t split = blockIdx.y;
     const int64_t i0 = split * chunk;
     const int64_t i1 = i0 + chunk < n ? i0 + chunk : n;
     const int nch = (int)((i1 - i0 + kExChunk - 1) / kExChunk);
 
-    auto load_dt = [&](int c, int slot) {
+    // photon times: thread tid < kExChunk loads photon tid of chunk c into a register one chunk before storing it
+    // into the ring, three chunks ahead of its use, so that no wave waits on global memory in the photon loop
+    auto fetch_dt = [&](int c, double& v, double& v2) {
+        const int64_t i = i0 + (int64_t)c * kExChunk + tid;
+        const bool ok = tid < kExChunk && c < nch && i < i1;
+        v = ok ? dt[i] : 0.0;
+        if (TWOD) v2 = ok ? dt2[i] : 0.0;
+    };
+    auto store_dt = [&](int c, double v, double v2) {
         if (tid < kExChunk) {
-            const int64_t i = i0 + (int64_t)c * kExChunk + tid;
-            const bool ok = c < nch && i < i1;
-            sdt[slot][tid] = ok ? dt[i] : 0.0;
-            if (TWOD) sdt2[TWOD ? slot : 0][tid] = ok ? dt2[i] : 0.0;
+            sdt[(c % kExDtSlots) * kExChunk + tid] = v;
+            if (TWOD) sdt2[TWOD ? (c % kExDtSlots) * kExChunk + tid : 0] = v2;
         }
     };
-    // V digits of chunk c as B fragments; photons past the split get V = 0, so that their products vanish
-    // one store address per thread: item s writes photon pp + 16 s, i.e. pair (pp >> 1) + 8 s (an immediate
-    // offset), half pp & 1 of the pair's uint4
-    const int pp = tid >> 5;
-    uint2* const wre = reinterpret_cast<uint2*>(&vre[0][pp >> 1][pb]) + (pp & 1);
-    uint2* const wim = reinterpret_cast<uint2*>(&vim[0][pp >> 1][pb]) + (pp & 1);
-    constexpr int kPairU2 = 32 * 2;                    // uint2 per photon pair row of 32 columns
-    constexpr int kBufU2 = (kExChunk / 2) * kPairU2;   // uint2 per buffer
-    auto produce_items = [&](int slot, int vb, int nlive, bool masked) {
-#pragma unroll
-        for (int s = 0; s < kExChunk * 32 / kExBlock; ++s) {
-            const int p = pp + (kExBlock / 32) * s;
-            uint32_t dc, dsn;
-            ex_sincos_digits(tab, gbv * sdt[slot][p], dc, dsn);
-            uint32_t rc = __builtin_bswap32(dc), rs = __builtin_bswap32(dsn),
-                     rn = __builtin_bswap32(ex_neg_digits(dsn));
-            if (masked && p >= nlive) rc = rs = rn = 0u;
-            wre[vb * kBufU2 + s * 8 * kPairU2] = make_uint2(rc, rn);
-            wim[vb * kBufU2 + s * 8 * kPairU2] = make_uint2(rs, rc);
-        }
-    };
-    auto produce = [&](int c, int slot, int vb) {
+    auto nlive_of = [&](int c) -> int {
         const int64_t rest = i1 - (i0 + (int64_t)c * kExChunk);
-        if (rest >= kExChunk)
-            produce_items(slot, vb, kExChunk, false);  // every chunk but a split's last: no masks
-        else
-            produce_items(slot, vb, (int)rest, true);
+        return rest < 0 ? 0 : (rest > kExChunk ? kExChunk : (int)rest);
     };
-    auto uphase = [&](int ds, int p) -> double {
-        return TWOD ? fma(fa, sdt[ds][p], c2 * sdt2[TWOD ? ds : 0][p]) : fa * sdt[ds][p];
+    // V items: item (chunk cj, index s) is photon pp + 4 s of chunk cj (so quad s) at column pb, stored as B
+    // fragment halves; photons past the split get V = 0, so that their products vanish
+    uint2* const wre = reinterpret_cast<uint2*>(&vre[pp >> 1][pb]) + (pp & 1);
+    uint2* const wim = reinterpret_cast<uint2*>(&vim[pp >> 1][pb]) + (pp & 1);
+    constexpr int kPairU2 = kExCols * 2;               // uint2 per photon pair row
+    struct VItem { double d; ExArg g; ExEntry e; ExRot r; uint32_t dc, dsn; };
+    // item (chunk cj, index s): all indices wave-uniform (scalar arithmetic), s a compile-time constant
+    auto v_read = [&](int cj, int s, VItem& it) { it.d = sdt[(cj & (kExDtSlots - 1)) * kExChunk + pp + 4 * s]; };
+    auto v_begin = [&](VItem& it) { it.g = ex_begin(gbv * it.d); };
+    auto v_table = [&](VItem& it) { it.e = tab[it.g.idx]; };
+    auto v_store = [&](VItem& it, int cj, int s, int nlive) {
+        const bool live = pp + 4 * s < nlive;
+        const uint32_t rc = live ? __builtin_bswap32(it.dc) : 0u, rs = live ? __builtin_bswap32(it.dsn) : 0u,
+                       rn = live ? __builtin_bswap32(ex_neg_digits(it.dsn)) : 0u;
+        // photon pp + 4 s of buffer cj & 1 = pair (pp >> 1) + 2 s + (cj & 1) kExChunk / 2
+        const int o = ((cj & 1) * (kExChunk / 2) + 2 * s) * kPairU2;
+        wre[o] = make_uint2(rc, rn);
+        wim[o] = make_uint2(rs, rc);
+    };
+    auto produce = [&](int cj, int s) {  // one whole item, outside the pipeline
+        VItem it;
+        v_read(cj, s, it);
+        v_begin(it);
+        v_table(it);
+        ex_end(it.e, it.g.y, it.dc, it.dsn);
+        v_store(it, cj, s, nlive_of(cj));
     };
 
-    i32x16 acc[4][2];
-#pragma unroll
-    for (int L = 0; L < 4; ++L)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[L][0][r] = acc[L][1][r] = 0;
+    // int32 level sums of the wave's 32 x 64 tile: AGPR tiles [level][fragment][Re, Im] (ex_mfma)
+    ex_acc_zero();
     // the block's running int64 sums between folds: per lane in global scratch (coalesced, written and read
     // by the same lane), so that they take no registers inside the photon loop
     long long* const fs =
         fold + (((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * kExWaves + wv) * (kExFoldVals * 64) + lane;
     const int comp = 2 * (kh - 1);
 
-    load_dt(0, 0);
-    load_dt(1, 1);
-    __syncthreads();  // table + first two dt chunks
-    produce(0, 0, 0);
+    // ---- software pipeline over quads (4 photons). Group (c, q) issues the 16 MFMAs of quad q of chunk c on
+    // operands prepared during the previous group and, in the gaps between them, finishes U of the next quad
+    // (table entries read one group earlier), starts U of the quad after (phase, table reads), reads the next
+    // quad's B fragments and the photon times three quads ahead, and computes one V item (item q + 1 of chunk
+    // c+1, or item 0 of chunk c+2). Every piece is pinned to its MFMA gap by ex_open / ex_ready, no LDS read is
+    // consumed within 3 MFMAs of its issue, and a gap carries <= ~6 VALU, so the matrix pipe sets the pace. The
+    // block's one barrier per chunk sits before group 7: by then the V items and photon times every wave reads
+    // next are written and the buffers it overwrites next are read, so the pipeline runs across chunk boundaries.
+    struct ExOps { i32x4 A[4]; i32x4 b[2][2]; };     // one quad's MFMA operands: U levels, B [fragment][Re, Im]
+    struct ExPend { ExEntry e0, e1; ExArg g0, g1; };  // a quad's table entries and residuals, awaiting ex_end
+    // photon times of quad q of chunk c (q may run into the next chunks: the slots form a ring)
+    auto read_dt = [&](int c, int q, double2& d, double2& d2) {
+        const int i = ((c % kExDtSlots) * kExChunk + 4 * q) & (kExDtSlots * kExChunk - 1);
+        d = *reinterpret_cast<const double2*>(&sdt[i + 2 * h]);
+        if (TWOD) d2 = *reinterpret_cast<const double2*>(&sdt2[TWOD ? i + 2 * h : 0]);
+    };
+    auto begin1 = [&](double d, double d2) -> ExArg { return ex_begin(TWOD ? fma(fa, d, c2 * d2) : fa * d); };
+    // B fragments of quad q of chunk c (q = kExQuads is quad 0 of chunk c+1)
+    auto read_b = [&](int c, int q, ExOps& o) {
+        const int pr = (((c & 1) * kExQuads + q) * 2 + h) & (kExChunk - 1);
+#pragma unroll
+        for (int f = 0; f < 2; ++f) {
+            const uint4 br = vre[pr][32 * f + ar], bi = vim[pr][32 * f + ar];
+            o.b[f][0] = i32x4{(int)br.x, (int)br.y, (int)br.z, (int)br.w};
+            o.b[f][1] = i32x4{(int)bi.x, (int)bi.y, (int)bi.z, (int)bi.w};
+        }
+    };
+    // one pipeline group; X = this quad's operands, Y = the previous quad's (kept 2 MFMAs, then overwritten with
+    // the next quad's); P = table entries of quad +1 (in) / +2 (out); D = photon times of quad +2 (in) / +3
+    // (out); it = V item j (photon time read in the previous group; on exit the time of item j + 1)
+    // V item of group q: (c+1, q+1) for q < 7, (c+2, 0) for q = 7; nl1, nl2 = live photons of chunks c+1, c+2
+    auto group = [&](ExOps& X, ExOps& Y, ExPend& P, double2& D, double2& D2, VItem& it, int c, int q, int nl1,
+                     int nl2) {
+        const int icj = q + 1 < kExItems ? c + 1 : c + 2, is = (q + 1) % kExItems;
+        const int ncj = q + 2 < kExItems ? c + 1 : c + 2, ns = (q + 2) % kExItems;
+#define EX_M(m) ex_mfma<m>(X.A[(m) >> 2], X.b[((m) >> 1) & 1][(m) & 1])
+        EX_M(0);
+        ex_open(D.x);
+        if (TWOD) ex_open(D2.x);
+        const ExArg g0 = begin1(D.x, D2.x);
+        ex_ready(g0.idx, g0.y);
+        EX_M(1);
+        ex_keep(Y.A[3]);  // read by the previous group's last MFMAs
+        ex_keep(Y.b[1][0]);
+        ex_keep(Y.b[1][1]);
+        ex_open(D.y);
+        if (TWOD) ex_open(D2.y);
+        const ExArg g1 = begin1(D.y, D2.y);
+        ex_ready(g1.idx, g1.y);
+        EX_M(2);
+        read_dt(c, q + 3, D, D2);  // consumed in the next group
+        read_b(c, q + 1, Y);
+        ex_open(it.d);
+        v_begin(it);
+        ex_ready(it.g.idx, it.g.y);
+        EX_M(3);
+        v_table(it);
+        ex_open(P.g0.y);
+        const ExRot r0 = ex_end_a(P.e0, P.g0.y);
+        ex_ready(r0.ts, r0.tc);
+        EX_M(4);
+        uint32_t a0, a1, a2, a3;
+        ex_end_b(P.e0, P.g0.y, r0, a0, a1);
+        ex_ready(a0, a1);
+        EX_M(5);
+        ex_keep(X.A[0]);  // last read by MFMA 3: operands stay allocated two MFMAs past their last reader
+        ex_open(P.g1.y);
+        const ExRot r1 = ex_end_a(P.e1, P.g1.y);
+        ex_ready(r1.ts, r1.tc);
+        EX_M(6);
+        ex_end_b(P.e1, P.g1.y, r1, a2, a3);
+        ex_ready(a2, a3);
+        EX_M(7);
+        ex_open(a0, a1);
+        ex_open(a2, a3);
+        Y.A[0] = i32x4{(int)a0, (int)a1, (int)a2, (int)a3};
+        Y.A[1] = i32x4{(int)(a0 >> 8), (int)(a1 >> 8), (int)(a2 >> 8), (int)(a3 >> 8)};
+        ex_ready(Y.A[0]);
+        ex_ready(Y.A[1]);
+        EX_M(8);
+        P.e0 = tab[g0.idx];  // the table entries of quad +2: consumed in the next group
+        P.e1 = tab[g1.idx];
+        P.g0 = g0;
+        P.g1 = g1;
+        Y.A[2] = i32x4{(int)(a0 >> 16), (int)(a1 >> 16), (int)(a2 >> 16), (int)(a3 >> 16)};
+        ex_ready(Y.A[2]);
+        EX_M(9);
+        ex_keep(X.A[1]);
+        Y.A[3] = i32x4{(int)(a0 >> 24), (int)(a1 >> 24), (int)(a2 >> 24), (int)(a3 >> 24)};
+        ex_ready(Y.A[3]);
+        EX_M(10);
+        ex_open(it.g.y);
+        it.r = ex_end_a(it.e, it.g.y);
+        ex_ready(it.r.ts, it.r.tc);
+        EX_M(11);
+        ex_end_b(it.e, it.g.y, it.r, it.dc, it.dsn);
+        ex_ready(it.dc, it.dsn);
+        EX_M(12);
+        v_store(it, icj, is, q + 1 < kExItems ? nl1 : nl2);
+        EX_M(13);
+        ex_keep(X.A[2]);
+        v_read(ncj, ns, it);  // the next group's item: used 5 MFMAs from here
+        EX_M(14);
+        EX_M(15);
+        ex_keep(X.b[0][0]);
+        ex_keep(X.b[0][1]);
+#undef EX_M
+    };
+
+    double pre = 0.0, pre2 = 0.0, v = 0.0, v2 = 0.0;
+#pragma unroll
+    for (int c = 0; c < kExDtSlots - 1; ++c) {
+        fetch_dt(c, v, v2);
+        store_dt(c, v, v2);
+    }
+    fetch_dt(kExDtSlots - 1, pre, pre2);
+    __syncthreads();  // table + the first three chunks' times
+#pragma unroll
+    for (int s = 0; s < kExItems; ++s) produce(0, s);  // chunk 0
+    produce(1, 0);                                      // and the first item of chunk 1
+    ExOps X, Y;
+    ExPend P;
+    VItem it;
+    double2 D, D2 = make_double2(0.0, 0.0);
+    if (active) {  // pipeline prologue: U of quad 0, table entries of quad 1, photon times of quad 2, V item 9
+        read_dt(0, 0, D, D2);
+        const ExArg g0 = begin1(D.x, D2.x), g1 = begin1(D.y, D2.y);
+        uint32_t a0, a1, a2, a3;
+        ex_end(tab[g0.idx], g0.y, a0, a1);
+        ex_end(tab[g1.idx], g1.y, a2, a3);
+#pragma unroll
+        for (int L = 0; L < 4; ++L) {
+            const int sh = 8 * L;
+            X.A[L] = i32x4{(int)(a0 >> sh), (int)(a1 >> sh), (int)(a2 >> sh), (int)(a3 >> sh)};
+        }
+        read_dt(0, 1, D, D2);
+        P.g0 = begin1(D.x, D2.x);
+        P.g1 = begin1(D.y, D2.y);
+        P.e0 = tab[P.g0.idx];
+        P.e1 = tab[P.g1.idx];
+        read_dt(0, 2, D, D2);
+        v_read(1, 1, it);
+    }
     __syncthreads();
+    if (active) {
+        read_b(0, 0, X);
+        Y = X;
+    }
     for (int c = 0; c < nch; ++c) {
-        const int ds = c % 3, vb = c & 1;
-        load_dt(c + 2, (c + 2) % 3);
-        if (c + 1 < nch) produce(c + 1, (c + 1) % 3, vb ^ 1);
+        // chunk c+3's times (fetched one chunk ago) into the slot of chunk c-1, read by every wave before the last
+        // barrier
+        store_dt(c + kExDtSlots - 1, pre, pre2);
+        fetch_dt(c + kExDtSlots, pre, pre2);
+        const int nl1 = nlive_of(c + 1), nl2 = nlive_of(c + 2);
         if (active) {
-#pragma unroll 2
-            for (int q = 0; q < kExChunk / 4; ++q) {
-                const int p0 = 4 * q + 2 * h;
-                uint32_t a0, a1, a2, a3;
-                ex_sincos_digits(tab, uphase(ds, p0), a0, a1);
-                ex_sincos_digits(tab, uphase(ds, p0 + 1), a2, a3);
-                const uint4 br = vre[vb][2 * q + h][ar], bi = vim[vb][2 * q + h][ar];
-                const i32x4 bre = {(int)br.x, (int)br.y, (int)br.z, (int)br.w};
-                const i32x4 bim = {(int)bi.x, (int)bi.y, (int)bi.z, (int)bi.w};
-                i32x4 A[4];
 #pragma unroll
-                for (int L = 0; L < 4; ++L) {
-                    const int sh = 8 * L;
-                    A[L] = i32x4{(int)(a0 >> sh), (int)(a1 >> sh), (int)(a2 >> sh), (int)(a3 >> sh)};
-                }
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int L = 0; L < 4; ++L) {
-                    acc[L][0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[L], bre, acc[L][0], 0, 0, 0);
-                    acc[L][1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[L], bim, acc[L][1], 0, 0, 0);
-                }
-                mfma_operand_guard();
+            for (int q = 0; q < kExQuads - 2; q += 2) {
+                group(X, Y, P, D, D2, it, c, q, nl1, nl2);
+                group(Y, X, P, D, D2, it, c, q + 1, nl1, nl2);
             }
+            group(X, Y, P, D, D2, it, c, kExQuads - 2, nl1, nl2);
+            __syncthreads();
+            group(Y, X, P, D, D2, it, c, kExQuads - 1, nl1, nl2);
             const bool fold_now = (c + 1) % kExFold == 0 || c + 1 == nch;
             if (!fold_now && (c + 1) % kExCarry == 0) {
                 mfma_drain();
-#pragma unroll
-                for (int r = 0; r < 16; ++r)
-#pragma unroll
-                    for (int x = 0; x < 2; ++x)
-#pragma unroll
-                        for (int L = 0; L < 3; ++L) {
-                            const int q = acc[L][x][r] >> 8;  // floor division by 256
-                            acc[L][x][r] &= 255;
-                            acc[L + 1][x][r] += q;
-                        }
+                ex_static_for<4>([&](auto fx) {  // fragment, Re/Im
+                    constexpr int t = decltype(fx)::value;
+                    ex_static_for<16>([&](auto rr) {
+                        constexpr int r = decltype(rr)::value;
+                        int l0 = ex_acc_read(ex_areg<t, r>{}), l1 = ex_acc_read(ex_areg<4 + t, r>{});
+                        int l2 = ex_acc_read(ex_areg<8 + t, r>{}), l3 = ex_acc_read(ex_areg<12 + t, r>{});
+                        l1 += l0 >> 8;  // floor division by 256
+                        l0 &= 255;
+                        l2 += l1 >> 8;
+                        l1 &= 255;
+                        l3 += l2 >> 8;
+                        l2 &= 255;
+                        ex_acc_write(ex_areg<t, r>{}, l0);
+                        ex_acc_write(ex_areg<4 + t, r>{}, l1);
+                        ex_acc_write(ex_areg<8 + t, r>{}, l2);
+                        ex_acc_write(ex_areg<12 + t, r>{}, l3);
+                    });
+                });
+                mfma_operand_guard();
             }
             if (fold_now) {
                 mfma_drain();
                 const bool first_fold = c + 1 <= kExFold, last = c + 1 == nch;
-                // opaque copies of the lane's scratch pointer and trial index: the 32 addresses derived from them
-                // must be formed here, not hoisted out of the photon loop (they would hold 64 registers there)
-                long long* f = fs;
+                // opaque copies of the lane's scratch pointer and trial index: the addresses derived from them
+                // must be formed here, not hoisted out of the photon loop
+                long long* fp = fs;
                 int64_t cl = c0 + ar - first + frow * nf;
-                asm volatile("" : "+v"(f), "+v"(cl));
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    long long re = ex_level_sum(acc[0][0][r], acc[1][0][r], acc[2][0][r], acc[3][0][r]);
-                    long long im = ex_level_sum(acc[0][1][r], acc[1][1][r], acc[2][1][r], acc[3][1][r]);
-                    if (!first_fold) {
-                        re += f[r * 64];
-                        im += f[(16 + r) * 64];
-                    }
-                    if (!last) {
-                        f[r * 64] = re;
-                        f[(16 + r) * 64] = im;
-                    } else {
-                        // D[row a][col b] of the 32x32 tile: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 h;
-                        // trial c0 + 32 a + b, output slot o = frow * nf + trial - first
-                        const int ra = (r & 3) + 8 * (r >> 2) + 4 * h;
-                        const int64_t o = cl + 32 * ra;
-                        if (c0 + 32 * ra + ar < nf && o >= 0 && o < count) {
-                            atomicAdd(&tot[(int64_t)comp * count + o], (unsigned long long)re);
-                            atomicAdd(&tot[(int64_t)(comp + 1) * count + o], (unsigned long long)im);
+                int64_t lim = nf - c0 - ar;  // trial c0 + 64 a + 32 f + ar is in the grid iff 64 a + 32 f < lim
+                asm volatile("" : "+v"(fp), "+v"(cl), "+v"(lim));
+                ex_static_for<2>([&](auto ff) {
+                    constexpr int f = decltype(ff)::value;
+                    ex_static_for<16>([&](auto rr) {
+                        constexpr int r = decltype(rr)::value;
+                        long long re = ex_level_sum(ex_acc_read(ex_areg<2 * f, r>{}), ex_acc_read(ex_areg<4 + 2 * f, r>{}),
+                                                    ex_acc_read(ex_areg<8 + 2 * f, r>{}), ex_acc_read(ex_areg<12 + 2 * f, r>{}));
+                        long long im = ex_level_sum(ex_acc_read(ex_areg<2 * f + 1, r>{}), ex_acc_read(ex_areg<5 + 2 * f, r>{}),
+                                                    ex_acc_read(ex_areg<9 + 2 * f, r>{}), ex_acc_read(ex_areg<13 + 2 * f, r>{}));
+                        long long* const fr = fp + (f * 32 + r) * 64;
+                        long long* const fi = fp + (f * 32 + 16 + r) * 64;
+                        if (!first_fold) {
+                            re += *fr;
+                            im += *fi;
                         }
-                    }
-                }
-#pragma unroll
-                for (int L = 0; L < 4; ++L)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) acc[L][0][r] = acc[L][1][r] = 0;
+                        if (!last) {
+                            *fr = re;
+                            *fi = im;
+                        } else {
+                            // D[row a][col] of fragment f: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 h;
+                            // trial c0 + 64 a + 32 f + col, output slot o = frow * nf + trial - first
+                            const int ra = (r & 3) + 8 * (r >> 2) + 4 * h;
+                            const int64_t off = kExCols * ra + 32 * f;
+                            const int64_t o = cl + off;
+                            if (off < lim && o >= 0 && o < count) {
+                                atomicAdd(&tot[(int64_t)comp * count + o], (unsigned long long)re);
+                                atomicAdd(&tot[(int64_t)(comp + 1) * count + o], (unsigned long long)im);
+                            }
+                        }
+                    });
+                });
+                ex_acc_zero();
+                mfma_operand_guard();
             }
+        } else {  // waves without a tile only produce V items, on the same barrier schedule
+            for (int q = 0; q < kExQuads - 1; ++q) produce(c + 1, q + 1);
+            __syncthreads();
+            produce(c + 2, 0);
         }
-        __syncthreads();
     }
 }
 

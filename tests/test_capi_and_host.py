@@ -43,6 +43,9 @@ def test_mfma_hazard_rules_hold_in_default_kernel():
         if "k_search_exact" in name:
             assert any(op.startswith("v_mfma") for _, op, _, _ in insts), name
             assert H.check_function(insts) == [], name
+            assert set(H.agpr_users(insts)) <= {"v_mfma_i32_32x32x32_i8", "v_accvgpr_read_b32",
+                                                 "v_accvgpr_write_b32"}, name
+            assert not any(op.startswith("scratch_") for _, op, _, _ in insts), name  # no spills
             checked += 1
     assert checked == 2
 

@@ -1,7 +1,8 @@
 """MFMA hazard check on the shipped gfx950 code object (see crimp_amd/csrc/mfma_drain.h for the measurements).
 
 Two rules, on every path from each MFMA (branches followed), counting issue cycles as 1 per instruction, N+1
-per s_nop N and MFMA_CYCLES per later MFMA:
+per s_nop N and MFMA_CYCLES per later MFMA (the matrix pipe issues one 32x32x32 i8 MFMA per 32 cycles:
+tools/mb_interleave.hip, profiles/r02/mb_interleave.txt); AGPRs (a0..a255) and VGPRs are both tracked:
   * result read: no non-MFMA instruction reads an MFMA's result registers within RESULT_CYCLES (MFMA -> MFMA
     accumulation chains are interlocked by the hardware and not counted);
   * operand rewrite: no instruction writes an MFMA's A-operand registers within A_CYCLES, nor its B-operand
@@ -21,18 +22,26 @@ OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
 RESULT_CYCLES = 64
 A_CYCLES = 48
 B_CYCLES = 8
-MFMA_CYCLES = 8
+MFMA_CYCLES = 32
 _WRITERS = ("v_", "ds_read", "global_load", "buffer_load", "scratch_load", "flat_load")
-_REG = re.compile(r"^v\[(\d+):(\d+)\]$|^v(\d+)$")
+_REG = re.compile(r"^([va])\[(\d+):(\d+)\]$|^([va])(\d+)$")
 
 
 def _regs(tok):
+    """Register numbers of an operand: VGPRs as 0..511, AGPRs as 1000 + n."""
     m = _REG.match(tok.strip())
     if not m:
         return set()
-    if m.group(3) is not None:
-        return {int(m.group(3))}
-    return set(range(int(m.group(1)), int(m.group(2)) + 1))
+    if m.group(5) is not None:
+        return {int(m.group(5)) + (1000 if m.group(4) == "a" else 0)}
+    base = 1000 if m.group(1) == "a" else 0
+    return set(range(base + int(m.group(2)), base + int(m.group(3)) + 1))
+
+
+def agpr_users(insts):
+    """Mnemonics of the instructions that name an AGPR (the exact kernel keeps its accumulators there, outside the
+    compiler's register model: only its MFMAs and accvgpr moves may touch them)."""
+    return sorted({op for _, op, ops, _ in insts if any(r >= 1000 for f in ops.split(",") for r in _regs(f))})
 
 
 def disassemble(lib):
