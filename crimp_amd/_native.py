@@ -24,6 +24,7 @@ FLAG_HW_SINCOS = 16
 FLAG_TIME_KERNELS = 128
 FLAG_F64 = 256
 FLAG_FAST = 512
+FLAG_NO_FIXUP = 1024
 
 STAT_Z2 = 0
 STAT_H = 1

@@ -1320,7 +1320,7 @@ static void exact_splits(int64_t n, int64_t bpg, int64_t* chunk_out, int64_t* sp
 
 static int exact_search(Scratch& sc, hipStream_t s, const double* dt, const double* dt2, int64_t n, const double* freq,
                         int64_t nf, const double* c2, const double* ap, bool twod, int nharm, int stat, int64_t first,
-                        int64_t count, double* out, KernelTimer* kt, int64_t* nfixed) {
+                        int64_t count, double* out, KernelTimer* kt, int64_t* nfixed, bool no_fixup) {
     const int64_t tpr = cdiv(nf, kExTileTrials);
     const int ncomp = 2 * nharm;
     // trial blocks bounded by the int64 totals buffer (2 GiB) and by the blocks' fold scratch (kExFoldMaxBlocks
@@ -1372,7 +1372,7 @@ static int exact_search(Scratch& sc, hipStream_t s, const double* dt, const doub
     int nf_h = 0;
     HIPCHK(d2h(s, &nf_h, nflag, sizeof(int)));
     *nfixed = nf_h;
-    if (nf_h == 0) return CRIMP_OK;
+    if (nf_h == 0 || no_fixup) return CRIMP_OK;
     return fixup_search(sc, s, dt, dt2, n, freq, nf, c2, twod, nharm, stat, first, flagged, nf_h, out);
 }
 
@@ -1447,7 +1447,8 @@ extern "C" int crimp_search(const double* t, int64_t n, double t0, const double*
             rc = fast_search(sc, s, ddt, ddt2, n, dfr, nf, dc2, ap, twod, nharm, stat, first, count, dout, &kt);
         } else if (factorised) {
             int64_t nfix = 0;
-            rc = exact_search(sc, s, ddt, ddt2, n, dfr, nf, dc2, ap, twod, nharm, stat, first, count, dout, &kt, &nfix);
+            rc = exact_search(sc, s, ddt, ddt2, n, dfr, nf, dc2, ap, twod, nharm, stat, first, count, dout, &kt, &nfix,
+                              (flags & CRIMP_FLAG_NO_FIXUP) != 0);
             g_last_fixups = nfix;
         } else {
             rc = direct_search(sc, s, ddt, ddt2, n, dfr, nf, dc2, twod, nharm, stat, first, nullptr, count, dout,

@@ -33,6 +33,7 @@
 #include <type_traits>
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x8 __attribute__((ext_vector_type(8)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kExTab = 4096;    // sin/cos table entries per turn
@@ -134,6 +135,11 @@ __device__ __forceinline__ void ex_mfma(const i32x4& a, const i32x4& b) {
     asm volatile("v_mfma_i32_32x32x32_i8 a[%c2:%c3], %0, %1, a[%c2:%c3]" ::"v"(a), "v"(b), "i"(16 * M),
                  "i"(16 * M + 15));
 }
+template <int M>
+__device__ __forceinline__ void ex_smfma(const i32x4& a, const i32x8& b, int idx) {
+    asm volatile("v_smfmac_i32_32x32x64_i8 a[%c3:%c4], %0, %1, %2" ::"v"(a), "v"(b), "v"(idx), "i"(16 * M),
+                 "i"(16 * M + 15));
+}
 template <int R>
 __device__ __forceinline__ int ex_acc_read(std::integral_constant<int, R>) {
     int x;
@@ -158,13 +164,19 @@ __device__ __forceinline__ void ex_acc_zero() {
     ex_static_for<255>([&](auto r) { asm volatile("v_accvgpr_write_b32 a%c0, 0" ::"i"(decltype(r)::value)); });
 }
 __device__ __forceinline__ void ex_keep(const i32x4& x) { asm volatile("" ::"v"(x)); }
+__device__ __forceinline__ void ex_keep(const i32x8& x) { asm volatile("" ::"v"(x)); }
 __device__ __forceinline__ void ex_ready(const i32x4& x) { asm volatile("" ::"v"(x)); }
 __device__ __forceinline__ void ex_ready(uint32_t x, float y) { asm volatile("" ::"v"(x), "v"(y)); }
 __device__ __forceinline__ void ex_ready(uint32_t x, uint32_t y) { asm volatile("" ::"v"(x), "v"(y)); }
 __device__ __forceinline__ void ex_open(double& x) { asm volatile("" : "+v"(x)); }
+__device__ __forceinline__ void ex_open(i32x4& x) { asm volatile("" : "+v"(x)); }
 __device__ __forceinline__ void ex_open(float& x) { asm volatile("" : "+v"(x)); }
 __device__ __forceinline__ void ex_ready(float x, float y) { asm volatile("" ::"v"(x), "v"(y)); }
 __device__ __forceinline__ void ex_open(uint32_t& x, uint32_t& y) { asm volatile("" : "+v"(x), "+v"(y)); }
+
+// level-4 operand: every digit dword shifted right by one byte (logical: the top byte becomes 0)
+typedef unsigned ex_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ i32x4 ex_shr8(i32x4 a) { return (i32x4)((ex_u32x4)a >> 8u); }
 
 __device__ __forceinline__ int64_t ex_level_sum(int a3, int a4, int a5, int a6) {
     return (int64_t)a3 + ((int64_t)a4 << 8) + ((int64_t)a5 << 16) + ((int64_t)a6 << 24);
@@ -181,7 +193,6 @@ __global__ __launch_bounds__(kExBlock, 1) void k_search_exact(
     __shared__ uint4 vre[kExChunk][kExCols];                 // {rev Vr, rev -Vi} of the pair's two photons
     __shared__ uint4 vim[kExChunk][kExCols];                 // {rev Vi, rev Vr}
     __shared__ double sdt[kExDtSlots * kExChunk];            // photon times: a ring of four chunks
-    __shared__ double sdt2[TWOD ? kExDtSlots * kExChunk : 1];
     const int tid = threadIdx.x;
     const int lane = tid & 63, wv = tid >> 6;
     for (int i = tid; i < kExTab; i += kExBlock) tab[i] = ex_entry(i);
@@ -205,17 +216,13 @@ __global__ __launch_bounds__(kExBlock, 1) void k_search_exact(
 
     // photon times: thread tid < kExChunk loads photon tid of chunk c into a register one chunk before storing it
     // into the ring, three chunks ahead of its use, so that no wave waits on global memory in the photon loop
-    auto fetch_dt = [&](int c, double& v, double& v2) {
+    auto fetch_dt = [&](int c, double& v) {
         const int64_t i = i0 + (int64_t)c * kExChunk + tid;
         const bool ok = tid < kExChunk && c < nch && i < i1;
         v = ok ? dt[i] : 0.0;
-        if (TWOD) v2 = ok ? dt2[i] : 0.0;
     };
-    auto store_dt = [&](int c, double v, double v2) {
-        if (tid < kExChunk) {
-            sdt[(c % kExDtSlots) * kExChunk + tid] = v;
-            if (TWOD) sdt2[TWOD ? (c % kExDtSlots) * kExChunk + tid : 0] = v2;
-        }
+    auto store_dt = [&](int c, double v) {
+        if (tid < kExChunk) sdt[(c % kExDtSlots) * kExChunk + tid] = v;
     };
     auto nlive_of = [&](int c) -> int {
         const int64_t rest = i1 - (i0 + (int64_t)c * kExChunk);
@@ -257,148 +264,268 @@ __global__ __launch_bounds__(kExBlock, 1) void k_search_exact(
         fold + (((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * kExWaves + wv) * (kExFoldVals * 64) + lane;
     const int comp = 2 * (kh - 1);
 
-    // ---- software pipeline over quads (4 photons). Group (c, q) issues the 16 MFMAs of quad q of chunk c on
-    // operands prepared during the previous group and, in the gaps between them, finishes U of the next quad
-    // (table entries read one group earlier), starts U of the quad after (phase, table reads), reads the next
-    // quad's B fragments and the photon times three quads ahead, and computes one V item (item q + 1 of chunk
-    // c+1, or item 0 of chunk c+2). Every piece is pinned to its MFMA gap by ex_open / ex_ready, no LDS read is
-    // consumed within 3 MFMAs of its issue, and a gap carries <= ~6 VALU, so the matrix pipe sets the pace. The
-    // block's one barrier per chunk sits before group 7: by then the V items and photon times every wave reads
-    // next are written and the buffers it overwrites next are read, so the pipeline runs across chunk boundaries.
-    struct ExOps { i32x4 A[4]; i32x4 b[2][2]; };     // one quad's MFMA operands: U levels, B [fragment][Re, Im]
-    struct ExPend { ExEntry e0, e1; ExArg g0, g1; };  // a quad's table entries and residuals, awaiting ex_end
+    // ---- software pipeline over quad PAIRS (8 photons). Pair group (c, p) issues the 24 MFMAs of quads 2p, 2p+1
+    // of chunk c -- levels 3 and 4 dense, one v_mfma_i32_32x32x32_i8 per quad, tile fragment and Re/Im; levels 5
+    // and 6 on the 2:4-sparse v_smfmac_i32_32x32x64_i8, one per fragment and Re/Im for both quads (their A bytes
+    // are (d2, d3, 0, 0) and (d3, 0, 0, 0), so the sparse form loses nothing and does the two quads' K = 64 in
+    // one instruction: 24 matrix instructions per pair instead of 32, tools/mb_power.hip for the energy) -- on
+    // operands prepared during the previous pair group. In the gaps between them it finishes U of the next pair
+    // (table entries read one group earlier), starts U of the pair after (phase, table reads), reads the next
+    // pair's B fragments and the photon times of the pair three ahead, and computes two V items. Every piece is
+    // pinned to its MFMA gap by ex_open / ex_ready, and no LDS read is consumed within 3 MFMAs of its issue. The
+    // block's one barrier per chunk sits before pair group 3: by then the V items and photon times every wave
+    // reads next are written and the buffers it overwrites next are read, so the pipeline runs across chunks.
+    //
+    // Sparse operand layout (tools/mb_smfmac_layout.hip, profiles/r02/smfmac_layout.txt): the instruction's
+    // logical K = 64 is [B lane-half 0 bytes 0..15 | half 1 bytes 0..15 | half 0 bytes 16..31 | half 1 bytes
+    // 16..31], and A lane-half h's 16 compressed bytes cover K 32h .. 32h+31. With B = {quad 2p's dense fragment,
+    // quad 2p+1's} the K order is (quad 0 half 0, quad 0 half 1, quad 1 half 0, quad 1 half 1), so lane-half 0 needs
+    // quad 0's level digits of both halves and lane-half 1 quad 1's: one v_permlane32_swap per compressed dword.
+    struct ExOps {                 // one pair's MFMA operands
+        i32x4 A3[2];               // dense level 3 per quad: U digits (level 4, the digits >> 8, is formed in the
+                                   // group that uses it)
+        i32x4 A5, A6;              // sparse levels 5, 6: compressed (d2, d3) / (d3, 0) per dword, lane-swapped
+        i32x8 b[2][2];             // B [fragment][Re, Im] = {quad 2p, quad 2p+1}
+    };
+    struct ExPend { ExEntry e[4]; ExArg g[4]; };  // the next pair's table entries: photon 2 quad + i of the lane
+    struct ExDt { double2 d[2]; };                // a pair's photon times, per quad
     // photon times of quad q of chunk c (q may run into the next chunks: the slots form a ring)
-    auto read_dt = [&](int c, int q, double2& d, double2& d2) {
+    auto read_dt = [&](int c, int q, double2& d) {
         const int i = ((c % kExDtSlots) * kExChunk + 4 * q) & (kExDtSlots * kExChunk - 1);
         d = *reinterpret_cast<const double2*>(&sdt[i + 2 * h]);
-        if (TWOD) d2 = *reinterpret_cast<const double2*>(&sdt2[TWOD ? i + 2 * h : 0]);
     };
-    auto begin1 = [&](double d, double d2) -> ExArg { return ex_begin(TWOD ? fma(fa, d, c2 * d2) : fa * d); };
-    // B fragments of quad q of chunk c (q = kExQuads is quad 0 of chunk c+1)
-    auto read_b = [&](int c, int q, ExOps& o) {
-        const int pr = (((c & 1) * kExQuads + q) * 2 + h) & (kExChunk - 1);
+    auto read_dt_pair = [&](int c, int p, ExDt& D) {
+        read_dt(c, 2 * p, D.d[0]);
+        read_dt(c, 2 * p + 1, D.d[1]);
+    };
+    // the phase in table units; the 2-D grid's dt^2 is formed here as d * d, bit-identical to the dt2 array
+    auto begin1 = [&](double d) -> ExArg { return ex_begin(TWOD ? fma(fa, d, c2 * (d * d)) : fa * d); };
+    // B fragments of pair p of chunk c (p = kExQuads / 2 is pair 0 of chunk c+1)
+    auto read_b = [&](int c, int p, ExOps& o) {
 #pragma unroll
         for (int f = 0; f < 2; ++f) {
-            const uint4 br = vre[pr][32 * f + ar], bi = vim[pr][32 * f + ar];
-            o.b[f][0] = i32x4{(int)br.x, (int)br.y, (int)br.z, (int)br.w};
-            o.b[f][1] = i32x4{(int)bi.x, (int)bi.y, (int)bi.z, (int)bi.w};
+            uint4 r[2], m[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int pr = (((c & 1) * kExQuads + 2 * p + i) * 2 + h) & (kExChunk - 1);
+                r[i] = vre[pr][32 * f + ar];
+                m[i] = vim[pr][32 * f + ar];
+            }
+            o.b[f][0] = i32x8{(int)r[0].x, (int)r[0].y, (int)r[0].z, (int)r[0].w,
+                              (int)r[1].x, (int)r[1].y, (int)r[1].z, (int)r[1].w};
+            o.b[f][1] = i32x8{(int)m[0].x, (int)m[0].y, (int)m[0].z, (int)m[0].w,
+                              (int)m[1].x, (int)m[1].y, (int)m[1].z, (int)m[1].w};
         }
     };
-    // one pipeline group; X = this quad's operands, Y = the previous quad's (kept 2 MFMAs, then overwritten with
-    // the next quad's); P = table entries of quad +1 (in) / +2 (out); D = photon times of quad +2 (in) / +3
-    // (out); it = V item j (photon time read in the previous group; on exit the time of item j + 1)
-    // V item of group q: (c+1, q+1) for q < 7, (c+2, 0) for q = 7; nl1, nl2 = live photons of chunks c+1, c+2
-    auto group = [&](ExOps& X, ExOps& Y, ExPend& P, double2& D, double2& D2, VItem& it, int c, int q, int nl1,
-                     int nl2) {
-        const int icj = q + 1 < kExItems ? c + 1 : c + 2, is = (q + 1) % kExItems;
-        const int ncj = q + 2 < kExItems ? c + 1 : c + 2, ns = (q + 2) % kExItems;
-#define EX_M(m) ex_mfma<m>(X.A[(m) >> 2], X.b[((m) >> 1) & 1][(m) & 1])
-        EX_M(0);
-        ex_open(D.x);
-        if (TWOD) ex_open(D2.x);
-        const ExArg g0 = begin1(D.x, D2.x);
-        ex_ready(g0.idx, g0.y);
-        EX_M(1);
-        ex_keep(Y.A[3]);  // read by the previous group's last MFMAs
-        ex_keep(Y.b[1][0]);
-        ex_keep(Y.b[1][1]);
-        ex_open(D.y);
-        if (TWOD) ex_open(D2.y);
-        const ExArg g1 = begin1(D.y, D2.y);
-        ex_ready(g1.idx, g1.y);
-        EX_M(2);
-        read_dt(c, q + 3, D, D2);  // consumed in the next group
-        read_b(c, q + 1, Y);
+    // U digits of photon i of a pair (quad i >> 1, photon i & 1 of the lane's two) -> a[quad][Ur, Ui of photon 0, 1]
+    auto u_end_a = [&](ExPend& P, int i) -> ExRot {
+        ex_open(P.g[i].y);
+        const ExRot r = ex_end_a(P.e[i], P.g[i].y);
+        ex_ready(r.ts, r.tc);
+        return r;
+    };
+    auto u_end_b = [&](ExPend& P, int i, ExRot r, uint32_t (&a)[2][4]) {
+        ex_end_b(P.e[i], P.g[i].y, r, a[i >> 1][2 * (i & 1)], a[i >> 1][2 * (i & 1) + 1]);
+        ex_ready(a[i >> 1][2 * (i & 1)], a[i >> 1][2 * (i & 1) + 1]);
+    };
+    // V item (chunk cj, index s): the phase half and the digit half
+    auto item_begin = [&](VItem& it) {
         ex_open(it.d);
         v_begin(it);
         ex_ready(it.g.idx, it.g.y);
-        EX_M(3);
-        v_table(it);
-        ex_open(P.g0.y);
-        const ExRot r0 = ex_end_a(P.e0, P.g0.y);
-        ex_ready(r0.ts, r0.tc);
-        EX_M(4);
-        uint32_t a0, a1, a2, a3;
-        ex_end_b(P.e0, P.g0.y, r0, a0, a1);
-        ex_ready(a0, a1);
-        EX_M(5);
-        ex_keep(X.A[0]);  // last read by MFMA 3: operands stay allocated two MFMAs past their last reader
-        ex_open(P.g1.y);
-        const ExRot r1 = ex_end_a(P.e1, P.g1.y);
-        ex_ready(r1.ts, r1.tc);
-        EX_M(6);
-        ex_end_b(P.e1, P.g1.y, r1, a2, a3);
-        ex_ready(a2, a3);
-        EX_M(7);
-        ex_open(a0, a1);
-        ex_open(a2, a3);
-        Y.A[0] = i32x4{(int)a0, (int)a1, (int)a2, (int)a3};
-        Y.A[1] = i32x4{(int)(a0 >> 8), (int)(a1 >> 8), (int)(a2 >> 8), (int)(a3 >> 8)};
-        ex_ready(Y.A[0]);
-        ex_ready(Y.A[1]);
-        EX_M(8);
-        P.e0 = tab[g0.idx];  // the table entries of quad +2: consumed in the next group
-        P.e1 = tab[g1.idx];
-        P.g0 = g0;
-        P.g1 = g1;
-        Y.A[2] = i32x4{(int)(a0 >> 16), (int)(a1 >> 16), (int)(a2 >> 16), (int)(a3 >> 16)};
-        ex_ready(Y.A[2]);
-        EX_M(9);
-        ex_keep(X.A[1]);
-        Y.A[3] = i32x4{(int)(a0 >> 24), (int)(a1 >> 24), (int)(a2 >> 24), (int)(a3 >> 24)};
-        ex_ready(Y.A[3]);
-        EX_M(10);
+    };
+    auto item_end = [&](VItem& it) {
         ex_open(it.g.y);
         it.r = ex_end_a(it.e, it.g.y);
-        ex_ready(it.r.ts, it.r.tc);
-        EX_M(11);
         ex_end_b(it.e, it.g.y, it.r, it.dc, it.dsn);
         ex_ready(it.dc, it.dsn);
-        EX_M(12);
-        v_store(it, icj, is, q + 1 < kExItems ? nl1 : nl2);
-        EX_M(13);
-        ex_keep(X.A[2]);
-        v_read(ncj, ns, it);  // the next group's item: used 5 MFMAs from here
-        EX_M(14);
-        EX_M(15);
+    };
+    const int kIdx = 0x44444444;  // sparse index: every group's two values at positions 0, 1
+#define EX_LO(v) __builtin_shufflevector(v, v, 0, 1, 2, 3)
+#define EX_HI(v) __builtin_shufflevector(v, v, 4, 5, 6, 7)
+    // one pair group; X = this pair's operands, Y = the previous pair's (kept 2 MFMAs past their last reader,
+    // then overwritten with the next pair's); P = table entries of pair +1 (in) / +2 (out); D = photon times of
+    // pair +2 (in) / +3 (out); I0, I1 = V items (photon time read one group earlier; on exit the next group's)
+    auto pgroup = [&](ExOps& X, ExOps& Y, ExPend& P, ExDt& D, VItem& I0, VItem& I1, int c, int p, int nl1,
+                      int nl2) {
+        // this group's items: (c+1, 2p+2), (c+1, 2p+3) for p < 3, (c+2, 0), (c+2, 1) for p = 3; next group's
+        const int icj = p + 1 < kExQuads / 2 ? c + 1 : c + 2, is = (2 * p + 2) % kExItems;
+        const int ncj = p + 2 < kExQuads / 2 ? c + 1 : c + 2, ns = (2 * p + 4) % kExItems;
+        const int inl = p + 1 < kExQuads / 2 ? nl1 : nl2;
+        ExArg g[4];
+        ex_mfma<0>(X.A3[0], EX_LO(X.b[0][0]));
+        ex_open(D.d[0].x);
+        g[0] = begin1(D.d[0].x);
+        ex_ready(g[0].idx, g[0].y);
+        ex_mfma<1>(X.A3[0], EX_LO(X.b[0][1]));
+        ex_keep(Y.A6);  // read by the previous group's last MFMAs
+        ex_keep(Y.b[1][0]);
+        ex_keep(Y.b[1][1]);
+        ex_open(D.d[0].y);
+        g[1] = begin1(D.d[0].y);
+        ex_ready(g[1].idx, g[1].y);
+        ex_mfma<2>(X.A3[0], EX_LO(X.b[1][0]));
+        read_b(c, p + 1, Y);  // consumed in the next group
+        ex_open(D.d[1].x);
+        g[2] = begin1(D.d[1].x);
+        ex_ready(g[2].idx, g[2].y);
+        ex_mfma<3>(X.A3[0], EX_LO(X.b[1][1]));
+        ex_open(D.d[1].y);
+        g[3] = begin1(D.d[1].y);
+        ex_ready(g[3].idx, g[3].y);
+        read_dt_pair(c, p + 3, D);  // consumed in the next group
+        ex_mfma<0>(X.A3[1], EX_HI(X.b[0][0]));
+        item_begin(I0);
+        ex_open(X.A3[0]);  // (an opaque copy: the shifts start here)
+        const i32x4 A40 = ex_shr8(X.A3[0]);
+        ex_ready(A40);
+        ex_mfma<1>(X.A3[1], EX_HI(X.b[0][1]));
+        ex_keep(X.A3[0]);
+        v_table(I0);
+        item_begin(I1);
+        ex_mfma<2>(X.A3[1], EX_HI(X.b[1][0]));
+        v_table(I1);
+        ex_open(X.A3[1]);
+        const i32x4 A41 = ex_shr8(X.A3[1]);
+        ex_ready(A41);
+        uint32_t a[2][4];
+        const ExRot r0 = u_end_a(P, 0);
+        ex_mfma<3>(X.A3[1], EX_HI(X.b[1][1]));
+        u_end_b(P, 0, r0, a);
+        ex_mfma<4>(A40, EX_LO(X.b[0][0]));
+        const ExRot r1 = u_end_a(P, 1);
+        ex_mfma<5>(A40, EX_LO(X.b[0][1]));
+        ex_keep(X.A3[1]);
+        u_end_b(P, 1, r1, a);
+        ex_mfma<6>(A40, EX_LO(X.b[1][0]));
+        const ExRot r2 = u_end_a(P, 2);
+        ex_mfma<7>(A40, EX_LO(X.b[1][1]));
+        u_end_b(P, 2, r2, a);
+        ex_mfma<4>(A41, EX_HI(X.b[0][0]));
+        const ExRot r3 = u_end_a(P, 3);
+        ex_mfma<5>(A41, EX_HI(X.b[0][1]));
+        ex_keep(A40);
+        u_end_b(P, 3, r3, a);
+        ex_mfma<6>(A41, EX_HI(X.b[1][0]));
+        // the next pair's operands: dense digits and >> 8, compressed level-5/6 bytes, lane-swapped
+        uint32_t c5[2][2], c6[2][2];
+#pragma unroll
+        for (int qd = 0; qd < 2; ++qd) {
+            ex_open(a[qd][0], a[qd][1]);
+            ex_open(a[qd][2], a[qd][3]);
+            Y.A3[qd] = i32x4{(int)a[qd][0], (int)a[qd][1], (int)a[qd][2], (int)a[qd][3]};
+#pragma unroll
+            for (int w = 0; w < 2; ++w) {
+                c5[qd][w] = __builtin_amdgcn_perm(a[qd][2 * w + 1], a[qd][2 * w], 0x07060302u);  // d2, d3 of each
+                c6[qd][w] = __builtin_amdgcn_perm(a[qd][2 * w + 1], a[qd][2 * w], 0x0C070C03u);  // d3, 0 of each
+            }
+        }
+        ex_ready(Y.A3[0]);
+        ex_mfma<7>(A41, EX_HI(X.b[1][1]));
+        ex_ready(Y.A3[1]);
+        ex_ready(c5[0][0], c5[0][1]);
+        ex_ready(c5[1][0], c5[1][1]);
+        ex_ready(c6[0][0], c6[0][1]);
+        ex_ready(c6[1][0], c6[1][1]);
+        ex_smfma<8>(X.A5, X.b[0][0], kIdx);
+        {
+            uint32_t s5[2][2], s6[2][2];
+#pragma unroll
+            for (int w = 0; w < 2; ++w) {
+                const auto t5 = __builtin_amdgcn_permlane32_swap(c5[0][w], c5[1][w], false, false);
+                const auto t6 = __builtin_amdgcn_permlane32_swap(c6[0][w], c6[1][w], false, false);
+                s5[0][w] = t5[0];
+                s5[1][w] = t5[1];
+                s6[0][w] = t6[0];
+                s6[1][w] = t6[1];
+            }
+            Y.A5 = i32x4{(int)s5[0][0], (int)s5[0][1], (int)s5[1][0], (int)s5[1][1]};
+            Y.A6 = i32x4{(int)s6[0][0], (int)s6[0][1], (int)s6[1][0], (int)s6[1][1]};
+        }
+        ex_ready(Y.A5);
+        ex_ready(Y.A6);
+        ex_smfma<9>(X.A5, X.b[0][1], kIdx);
+        ex_keep(A41);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {  // the table entries of pair +2: consumed in the next group
+            P.e[i] = tab[g[i].idx];
+            P.g[i] = g[i];
+        }
+        ex_smfma<10>(X.A5, X.b[1][0], kIdx);
+        item_end(I0);
+        ex_smfma<11>(X.A5, X.b[1][1], kIdx);
+        item_end(I1);
+        ex_smfma<12>(X.A6, X.b[0][0], kIdx);
+        v_store(I0, icj, is, inl);
+        ex_smfma<13>(X.A6, X.b[0][1], kIdx);
+        ex_keep(X.A5);
+        v_store(I1, icj, is + 1, inl);
+        ex_smfma<14>(X.A6, X.b[1][0], kIdx);
+        v_read(ncj, ns, I0);  // the next group's items
+        v_read(ncj, ns + 1, I1);
+        ex_smfma<15>(X.A6, X.b[1][1], kIdx);
         ex_keep(X.b[0][0]);
         ex_keep(X.b[0][1]);
-#undef EX_M
     };
+#undef EX_LO
+#undef EX_HI
 
-    double pre = 0.0, pre2 = 0.0, v = 0.0, v2 = 0.0;
+    double pre = 0.0, v = 0.0;
 #pragma unroll
     for (int c = 0; c < kExDtSlots - 1; ++c) {
-        fetch_dt(c, v, v2);
-        store_dt(c, v, v2);
+        fetch_dt(c, v);
+        store_dt(c, v);
     }
-    fetch_dt(kExDtSlots - 1, pre, pre2);
+    fetch_dt(kExDtSlots - 1, pre);
     __syncthreads();  // table + the first three chunks' times
 #pragma unroll
     for (int s = 0; s < kExItems; ++s) produce(0, s);  // chunk 0
-    produce(1, 0);                                      // and the first item of chunk 1
+    produce(1, 0);                                      // and the first two items of chunk 1
+    produce(1, 1);
     ExOps X, Y;
     ExPend P;
-    VItem it;
-    double2 D, D2 = make_double2(0.0, 0.0);
-    if (active) {  // pipeline prologue: U of quad 0, table entries of quad 1, photon times of quad 2, V item 9
-        read_dt(0, 0, D, D2);
-        const ExArg g0 = begin1(D.x, D2.x), g1 = begin1(D.y, D2.y);
-        uint32_t a0, a1, a2, a3;
-        ex_end(tab[g0.idx], g0.y, a0, a1);
-        ex_end(tab[g1.idx], g1.y, a2, a3);
+    ExDt D;
+    VItem I0, I1;
+    if (active) {  // pipeline prologue: U of pair 0, table entries of pair 1, photon times of pair 2, V items (1, 2..3)
+        ExDt D0;
+        read_dt_pair(0, 0, D0);
+        uint32_t a[2][4];
 #pragma unroll
-        for (int L = 0; L < 4; ++L) {
-            const int sh = 8 * L;
-            X.A[L] = i32x4{(int)(a0 >> sh), (int)(a1 >> sh), (int)(a2 >> sh), (int)(a3 >> sh)};
+        for (int i = 0; i < 4; ++i) {
+            const ExArg g = begin1((i & 1) ? D0.d[i >> 1].y : D0.d[i >> 1].x);
+            ex_end(tab[g.idx], g.y, a[i >> 1][2 * (i & 1)], a[i >> 1][2 * (i & 1) + 1]);
         }
-        read_dt(0, 1, D, D2);
-        P.g0 = begin1(D.x, D2.x);
-        P.g1 = begin1(D.y, D2.y);
-        P.e0 = tab[P.g0.idx];
-        P.e1 = tab[P.g1.idx];
-        read_dt(0, 2, D, D2);
-        v_read(1, 1, it);
+        uint32_t c5[2][2], c6[2][2];
+#pragma unroll
+        for (int qd = 0; qd < 2; ++qd) {
+            X.A3[qd] = i32x4{(int)a[qd][0], (int)a[qd][1], (int)a[qd][2], (int)a[qd][3]};
+#pragma unroll
+            for (int w = 0; w < 2; ++w) {
+                c5[qd][w] = __builtin_amdgcn_perm(a[qd][2 * w + 1], a[qd][2 * w], 0x07060302u);
+                c6[qd][w] = __builtin_amdgcn_perm(a[qd][2 * w + 1], a[qd][2 * w], 0x0C070C03u);
+            }
+        }
+        uint32_t s5[2][2], s6[2][2];
+#pragma unroll
+        for (int w = 0; w < 2; ++w) {
+            const auto t5 = __builtin_amdgcn_permlane32_swap(c5[0][w], c5[1][w], false, false);
+            const auto t6 = __builtin_amdgcn_permlane32_swap(c6[0][w], c6[1][w], false, false);
+            s5[0][w] = t5[0];
+            s5[1][w] = t5[1];
+            s6[0][w] = t6[0];
+            s6[1][w] = t6[1];
+        }
+        X.A5 = i32x4{(int)s5[0][0], (int)s5[0][1], (int)s5[1][0], (int)s5[1][1]};
+        X.A6 = i32x4{(int)s6[0][0], (int)s6[0][1], (int)s6[1][0], (int)s6[1][1]};
+        read_dt_pair(0, 1, D);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            P.g[i] = begin1((i & 1) ? D.d[i >> 1].y : D.d[i >> 1].x);
+            P.e[i] = tab[P.g[i].idx];
+        }
+        read_dt_pair(0, 2, D);
+        v_read(1, 2, I0);
+        v_read(1, 3, I1);
     }
     __syncthreads();
     if (active) {
@@ -408,18 +535,15 @@ __global__ __launch_bounds__(kExBlock, 1) void k_search_exact(
     for (int c = 0; c < nch; ++c) {
         // chunk c+3's times (fetched one chunk ago) into the slot of chunk c-1, read by every wave before the last
         // barrier
-        store_dt(c + kExDtSlots - 1, pre, pre2);
-        fetch_dt(c + kExDtSlots, pre, pre2);
+        store_dt(c + kExDtSlots - 1, pre);
+        fetch_dt(c + kExDtSlots, pre);
         const int nl1 = nlive_of(c + 1), nl2 = nlive_of(c + 2);
         if (active) {
-#pragma unroll
-            for (int q = 0; q < kExQuads - 2; q += 2) {
-                group(X, Y, P, D, D2, it, c, q, nl1, nl2);
-                group(Y, X, P, D, D2, it, c, q + 1, nl1, nl2);
-            }
-            group(X, Y, P, D, D2, it, c, kExQuads - 2, nl1, nl2);
+            pgroup(X, Y, P, D, I0, I1, c, 0, nl1, nl2);
+            pgroup(Y, X, P, D, I0, I1, c, 1, nl1, nl2);
+            pgroup(X, Y, P, D, I0, I1, c, 2, nl1, nl2);
             __syncthreads();
-            group(Y, X, P, D, D2, it, c, kExQuads - 1, nl1, nl2);
+            pgroup(Y, X, P, D, I0, I1, c, 3, nl1, nl2);
             const bool fold_now = (c + 1) % kExFold == 0 || c + 1 == nch;
             if (!fold_now && (c + 1) % kExCarry == 0) {
                 mfma_drain();
@@ -486,9 +610,10 @@ __global__ __launch_bounds__(kExBlock, 1) void k_search_exact(
                 mfma_operand_guard();
             }
         } else {  // waves without a tile only produce V items, on the same barrier schedule
-            for (int q = 0; q < kExQuads - 1; ++q) produce(c + 1, q + 1);
+            for (int s = 2; s < kExItems; ++s) produce(c + 1, s);
             __syncthreads();
             produce(c + 2, 0);
+            produce(c + 2, 1);
         }
     }
 }

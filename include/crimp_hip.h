@@ -45,6 +45,8 @@ extern "C" {
 #define CRIMP_FLAG_F64 256u         /* search: fp64 kernel on every grid */
 #define CRIMP_FLAG_FAST 512u        /* search: fp32 sin/cos kernels (f16-split MFMA / direct): ~1e-6 of the grid's
                                        mean power, not per trial; faster */
+#define CRIMP_FLAG_NO_FIXUP 1024u   /* search (diagnostic): the exact kernel's raw powers, without the fp64 fix-up
+                                       of the trials its error bound cannot certify (crimp_last_fixups counts them) */
 
 #define CRIMP_STAT_Z2 0 /* Z^2_m  (periodsearch.py:57-71, :73-106) */
 #define CRIMP_STAT_H 1  /* H-test (periodsearch.py:109-125)         */

@@ -41,13 +41,26 @@ def test_mfma_hazard_rules_hold_in_default_kernel():
     checked = 0
     for name, insts in funcs.items():
         if "k_search_exact" in name:
-            assert any(op.startswith("v_mfma") for _, op, _, _ in insts), name
+            assert any(op.startswith(("v_mfma", "v_smfmac")) for _, op, _, _ in insts), name
             assert H.check_function(insts) == [], name
-            assert set(H.agpr_users(insts)) <= {"v_mfma_i32_32x32x32_i8", "v_accvgpr_read_b32",
-                                                 "v_accvgpr_write_b32"}, name
+            assert set(H.agpr_users(insts)) <= {"v_mfma_i32_32x32x32_i8", "v_smfmac_i32_32x32x64_i8",
+                                                 "v_accvgpr_read_b32", "v_accvgpr_write_b32"}, name
             assert not any(op.startswith("scratch_") for _, op, _, _ in insts), name  # no spills
             checked += 1
     assert checked == 2
+
+
+def test_exact_kernel_accumulators_untouched_by_compiler():
+    """The exact kernel's accumulators live in AGPRs outside hipcc's register model (search_exact.h, ex_mfma):
+    the compiled kernels may not touch an AGPR themselves (a VGPR spilled to an AGPR would overwrite them)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("agpr_check", os.path.join(ROOT, "tools", "agpr_check.py"))
+    A = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(A)
+    res = A.compiler_agpr_accesses()
+    assert len(res) == 2
+    for name, bad in res.items():
+        assert bad == [], (name, bad[:4])
 
 
 def test_hot_path_fails_loudly_without_gpu():

@@ -150,10 +150,18 @@ def test_search_sharded_ranges_equal_full(gpu):
     f = 3.0 + np.arange(-300, 300) / 1.0e6
     fd = np.array([-12.0, -11.0])
     t0 = (t[0] + t[-1]) / 2
+    from crimp_amd import _native as N
     full = ops.search(t, t0, f, 2, 0, log10_negfdot=fd)
+    # the exact kernel, not its fp64 fix-up, must produce these (a broken exact kernel is hidden by a fix-up of
+    # every trial; at 5e4 photons and powers ~1 the error bound flags none)
+    assert N.load().crimp_last_fixups() <= 12
     parts = [ops.search(t, t0, f, 2, 0, log10_negfdot=fd, first=a, count=b - a)
              for a, b in ((0, 333), (333, 901), (901, 1200))]
     np.testing.assert_array_equal(np.concatenate(parts), full)
+    for twod in (None, fd):  # raw exact-kernel powers (fix-up off) within the kernel's error model of fp64
+        ref = ops.search(t, t0, f, 2, 0, log10_negfdot=twod, precision="f64")
+        z = ops.search(t, t0, f, 2, 0, log10_negfdot=twod, flags=N.FLAG_NO_FIXUP)
+        close_rel(z, ref, 1e-6)
 
 
 def test_sincos_variants_accuracy_report(gpu, monkeypatch, capsys):

@@ -94,7 +94,7 @@ def check_function(insts):
               "buffer_atomic", "flat_atomic", "ds_add")
     horizon = max(RESULT_CYCLES, A_CYCLES, B_CYCLES)
     for i, (a, op, ops, _) in enumerate(insts):
-        if not op.startswith("v_mfma"):
+        if not op.startswith(("v_mfma", "v_smfmac")):
             continue
         f0 = [f.strip() for f in ops.split(",")]
         dst, srca, srcb = _regs(f0[0]), _regs(f0[1]), _regs(f0[2])
@@ -110,7 +110,7 @@ def check_function(insts):
                 stack += [(s, cyc + int(ops2.split()[0], 0) + 1, d, ra, rb) for s in successors(j)]
                 continue
             fields = [f.strip() for f in ops2.split(",")] if ops2 else []
-            if op2.startswith("v_mfma"):
+            if op2.startswith(("v_mfma", "v_smfmac")):
                 if cyc < RESULT_CYCLES and set().union(*map(_regs, fields[1:3])) & d:
                     bad.append((a, b, op2 + " (result as operand)", cyc))
                 stack += [(s, cyc + MFMA_CYCLES, d, ra, rb) for s in successors(j)]
@@ -140,7 +140,7 @@ def main(argv):
         if not any(p in name for p in pats):
             continue
         bad = check_function(insts)
-        nm = sum(1 for _, op, _, _ in insts if op.startswith("v_mfma"))
+        nm = sum(1 for _, op, _, _ in insts if op.startswith(("v_mfma", "v_smfmac")))
         print("%s: %d MFMAs, %d violations" % (name, nm, len(bad)))
         for v in bad[:10]:
             print("   mfma @%x  -> %s @%x after %d cycles" % (v[0], v[2], v[1], v[3]))
