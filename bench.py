@@ -8,11 +8,13 @@ ranks agree on the global best, ties -> lowest index). With N ranks each rank se
 an N*1e6 grid (weak scaling); ``value`` = all ranks' evaluations / max-over-ranks time.
 
 Also reported:
-* ``roofline``: the exact kernel (k_search_exact) is bound by the i8 matrix-core issue rate: 8 MFMAs
-  (v_mfma_i32_32x32x32_i8, 65536 ops each) per 4 photons x 1024 trials x harmonic = 128 ops per
-  photon*trial*harmonic, against the 5.0 POP/s i8 dense peak; kernel time from hipEvents around the harmonic-sum
-  kernels on their stream; ``traffic`` from the same tree's rocprofv3 PMC pass (profiles/r02/pmc_traffic.json)
-  when it was taken on this workload;
+* ``roofline``: the exact kernel (k_search_exact) is bound by the i8 matrix cores. Per 4 photons x 2048 trials x
+  harmonic it issues 8 dense v_mfma_i32_32x32x32_i8 (65536 ops each) and 4 2:4-sparse v_smfmac_i32_32x32x64_i8
+  (131072 nominal ops each) = 128 ops per photon*trial*harmonic; both take 32 cycles of a SIMD's matrix pipe, so
+  the peak of this instruction mix is 2/3 x 5.0 + 1/3 x 10.0 = 6.67 POP/s (the i8 dense peak, 2x BF16's 2.5 PF,
+  and the 2:4-sparse peak, 2x dense) and ``frac`` is the matrix pipe's occupancy at the nominal 2.4 GHz; kernel
+  time from hipEvents around the harmonic-sum kernels on their stream; ``traffic`` from the same tree's rocprofv3
+  PMC pass (profiles/r02/pmc_traffic.json) when it was taken on this workload;
 * ``cpu_baseline``: the oracle (oracle/liborc.so, fp64, OpenMP over trials) on a bounded sample;
 * ``fast_path``: the opt-in fp32 sin/cos path (precision="fast") on the same workload, for comparison;
 * ToA (config 5 per GPU): the device fit of 1250 intervals x 1e5 photons, and the end-to-end ``measure_intervals``
@@ -30,8 +32,10 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-PEAK_I8_TOPS = 5000.0           # MI355X_MICROARCH.md: I8 MFMA = 2x the BF16 dense rate (2.5 PF)
-OPS_PER_EVAL_HARM = 128.0       # 8 x v_mfma_i32_32x32x32_i8 (2*32*32*32 ops) per 4 photons x 1024 trials x harmonic
+# MI355X_MICROARCH.md: I8 MFMA dense = 2x BF16 (2.5 PF) = 5.0 POP/s, 2:4 sparse 2x that; the exact kernel issues
+# 2 dense : 1 sparse instructions at 32 cycles each, so its mix peaks at (2 x 5.0 + 1 x 10.0) / 3 POP/s
+PEAK_I8_TOPS = (2 * 5000.0 + 10000.0) / 3
+OPS_PER_EVAL_HARM = 128.0       # (8 x 65536 dense + 4 x 131072 sparse ops) per 4 photons x 2048 trials x harmonic
 PEAK_HBM_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E ~8 TB/s
 PEAK_VALU_SLOTS = 256 * 4 * 32 * 2.4e9   # lane-slots/s: 256 CUs x 4 SIMD-32 x 2.4 GHz
 PMC_FILE = os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json")
@@ -362,10 +366,11 @@ def main():
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_I8_TOPS, "unit": "TFLOP/s",
                          "frac": achieved / PEAK_I8_TOPS, "traffic": traffic,
                          "kernel_ms": kern_ms, "step_ms": step_ms,
-                         "note": "int8 MFMA ops issued: 128 per photon*trial*harmonic (8 v_mfma_i32_32x32x32_i8 per 4 "
-                                 "photons x 1024 trials) / mean duration of the harmonic-sum kernels (hipEvents in "
-                                 "libcrimp_hip on their stream); peak = I8 dense MFMA (2x BF16 2.5 PF); 10 of every 16 "
-                                 "byte products are digit-level products (DESIGN.md); traffic: %s" % (
+                         "note": "int8 matrix ops issued: 128 per photon*trial*harmonic (8 v_mfma_i32_32x32x32_i8 + 4 "
+                                 "2:4-sparse v_smfmac_i32_32x32x64_i8 per 4 photons x 2048 trials) / mean duration of "
+                                 "the harmonic-sum kernels (hipEvents in libcrimp_hip on their stream); peak = that "
+                                 "2:1 dense:sparse instruction mix at 32 cycles each (I8 dense 5.0 POP/s, sparse 10.0): "
+                                 "frac = matrix-pipe occupancy at 2.4 GHz; traffic: %s" % (
                                      tsrc or "no PMC pass on this workload")},
         }
         if not a.no_cpu:
