@@ -83,10 +83,16 @@ __device__ __forceinline__ ExRot ex_end_a(const ExEntry& e, float y) {
     const float u = y * (3.14159265358979323846f / (float)kExTab);
     return ExRot{__builtin_fmaf(-u, e.s1, e.c1), __builtin_fmaf(u, e.c1, e.s1)};
 }
+// |value| < 2^22: the low mantissa bits of fma(y, t, 1.5 * 2^23) are rint(y t) + 0x400000
+__device__ __forceinline__ uint32_t ex_end_s(const ExEntry& e, float y, float ts) {
+    return ((uint32_t)e.sk + __float_as_uint(__builtin_fmaf(y, ts, 12582912.0f))) ^ 0x00808080u;
+}
+__device__ __forceinline__ uint32_t ex_end_c(const ExEntry& e, float y, float tc) {
+    return ((uint32_t)e.ck + __float_as_uint(__builtin_fmaf(-y, tc, 12582912.0f))) ^ 0x00808080u;
+}
 __device__ __forceinline__ void ex_end_b(const ExEntry& e, float y, ExRot r, uint32_t& dc, uint32_t& ds) {
-    // |value| < 2^22: the low mantissa bits of fma(y, t, 1.5 * 2^23) are rint(y t) + 0x400000
-    ds = ((uint32_t)e.sk + __float_as_uint(__builtin_fmaf(y, r.ts, 12582912.0f))) ^ 0x00808080u;
-    dc = ((uint32_t)e.ck + __float_as_uint(__builtin_fmaf(-y, r.tc, 12582912.0f))) ^ 0x00808080u;
+    ds = ex_end_s(e, y, r.ts);
+    dc = ex_end_c(e, y, r.tc);
 }
 __device__ __forceinline__ void ex_end(const ExEntry& e, float y, uint32_t& dc, uint32_t& ds) {
     ex_end_b(e, y, ex_end_a(e, y), dc, ds);
@@ -172,6 +178,7 @@ __device__ __forceinline__ void ex_open(double& x) { asm volatile("" : "+v"(x));
 __device__ __forceinline__ void ex_open(i32x4& x) { asm volatile("" : "+v"(x)); }
 __device__ __forceinline__ void ex_open(float& x) { asm volatile("" : "+v"(x)); }
 __device__ __forceinline__ void ex_ready(float x, float y) { asm volatile("" ::"v"(x), "v"(y)); }
+__device__ __forceinline__ void ex_ready(uint32_t x) { asm volatile("" ::"v"(x)); }
 __device__ __forceinline__ void ex_open(uint32_t& x, uint32_t& y) { asm volatile("" : "+v"(x), "+v"(y)); }
 
 // level-4 operand: every digit dword shifted right by one byte (logical: the top byte becomes 0)
@@ -188,7 +195,7 @@ __global__ __launch_bounds__(kExBlock, 1) void k_search_exact(
     const double* __restrict__ freq, int64_t nf, const double* __restrict__ c2row, const double* __restrict__ apinfo,
     int64_t tile_first, int64_t ntiles, int64_t tiles_per_row, int64_t first, int64_t count, int kh,
     unsigned long long* __restrict__ tot, long long* __restrict__ fold) {
-    __shared__ ExEntry tab[kExTab];                          // 64 KB
+    __shared__ ExEntry tab[kExTab + 1];                      // 64 KB; entry kExTab: cos = sin = 0 (dead photons)
     // B fragments per photon pair and column b: two chunk buffers of kExChunk / 2 pairs, a ring of kExChunk pairs
     __shared__ uint4 vre[kExChunk][kExCols];                 // {rev Vr, rev -Vi} of the pair's two photons
     __shared__ uint4 vim[kExChunk][kExCols];                 // {rev Vi, rev Vr}
@@ -196,6 +203,10 @@ __global__ __launch_bounds__(kExBlock, 1) void k_search_exact(
     const int tid = threadIdx.x;
     const int lane = tid & 63, wv = tid >> 6;
     for (int i = tid; i < kExTab; i += kExBlock) tab[i] = ex_entry(i);
+    if (tid == 0) {  // digits of exactly 0 whatever the residual: the biased zero integers, no rotation terms
+        const int32_t z = (int32_t)(0x00808080u - 0x4B400000u);
+        tab[kExTab] = ExEntry{z, z, 0.0f, 0.0f};
+    }
     const double kT = (double)kh * (double)kExTab;
     const int64_t T = (int64_t)blockIdx.x * kExWaves + wv;  // this wave's tile; waves past the end only produce V
     const bool active = T < ntiles;                          // wave-uniform
@@ -233,27 +244,34 @@ __global__ __launch_bounds__(kExBlock, 1) void k_search_exact(
     uint2* const wre = reinterpret_cast<uint2*>(&vre[pp >> 1][pb]) + (pp & 1);
     uint2* const wim = reinterpret_cast<uint2*>(&vim[pp >> 1][pb]) + (pp & 1);
     constexpr int kPairU2 = kExCols * 2;               // uint2 per photon pair row
-    struct VItem { double d; ExArg g; ExEntry e; ExRot r; uint32_t dc, dsn; };
+    struct VItem { double d; ExArg g; ExEntry e; ExRot r; uint32_t dc, dsn, rc, rs, rn; };
     // item (chunk cj, index s): all indices wave-uniform (scalar arithmetic), s a compile-time constant
     auto v_read = [&](int cj, int s, VItem& it) { it.d = sdt[(cj & (kExDtSlots - 1)) * kExChunk + pp + 4 * s]; };
-    auto v_begin = [&](VItem& it) { it.g = ex_begin(gbv * it.d); };
+    // a photon past the split (pp + 4 s >= nlive: wave-uniform) reads the zero entry, so its V digits are 0
+    auto v_begin = [&](VItem& it, int s, int nlive) {
+        it.g = ex_begin(gbv * it.d);
+        it.g.idx = pp + 4 * s < nlive ? it.g.idx : (uint32_t)kExTab;
+    };
     auto v_table = [&](VItem& it) { it.e = tab[it.g.idx]; };
-    auto v_store = [&](VItem& it, int cj, int s, int nlive) {
-        const bool live = pp + 4 * s < nlive;
-        const uint32_t rc = live ? __builtin_bswap32(it.dc) : 0u, rs = live ? __builtin_bswap32(it.dsn) : 0u,
-                       rn = live ? __builtin_bswap32(ex_neg_digits(it.dsn)) : 0u;
+    auto v_post = [&](VItem& it) {  // B fragment dwords: byte-reversed digits of Vr, Vi, -Vi
+        it.rc = __builtin_bswap32(it.dc);
+        it.rs = __builtin_bswap32(it.dsn);
+        it.rn = __builtin_bswap32(ex_neg_digits(it.dsn));
+    };
+    auto v_write = [&](VItem& it, int cj, int s) {
         // photon pp + 4 s of buffer cj & 1 = pair (pp >> 1) + 2 s + (cj & 1) kExChunk / 2
         const int o = ((cj & 1) * (kExChunk / 2) + 2 * s) * kPairU2;
-        wre[o] = make_uint2(rc, rn);
-        wim[o] = make_uint2(rs, rc);
+        wre[o] = make_uint2(it.rc, it.rn);
+        wim[o] = make_uint2(it.rs, it.rc);
     };
     auto produce = [&](int cj, int s) {  // one whole item, outside the pipeline
         VItem it;
         v_read(cj, s, it);
-        v_begin(it);
+        v_begin(it, s, nlive_of(cj));
         v_table(it);
         ex_end(it.e, it.g.y, it.dc, it.dsn);
-        v_store(it, cj, s, nlive_of(cj));
+        v_post(it);
+        v_write(it, cj, s);
     };
 
     // int32 level sums of the wave's 32 x 64 tile: AGPR tiles [level][fragment][Re, Im] (ex_mfma)
@@ -273,8 +291,9 @@ __global__ __launch_bounds__(kExBlock, 1) void k_search_exact(
     // (table entries read one group earlier), starts U of the pair after (phase, table reads), reads the next
     // pair's B fragments and the photon times of the pair three ahead, and computes two V items. Every piece is
     // pinned to its MFMA gap by ex_open / ex_ready, and no LDS read is consumed within 3 MFMAs of its issue. The
-    // block's one barrier per chunk sits before pair group 3: by then the V items and photon times every wave
-    // reads next are written and the buffers it overwrites next are read, so the pipeline runs across chunks.
+    // block's one barrier per chunk sits in pair group 3, before its read of the next chunk's first B fragments:
+    // by then the V items and photon times every wave reads next are written (four MFMAs earlier, so the barrier's
+    // LDS drain is free) and the buffers it overwrites next are read, so the pipeline runs across chunks.
     //
     // Sparse operand layout (tools/mb_smfmac_layout.hip, profiles/r02/smfmac_layout.txt): the instruction's
     // logical K = 64 is [B lane-half 0 bytes 0..15 | half 1 bytes 0..15 | half 0 bytes 16..31 | half 1 bytes
@@ -317,118 +336,162 @@ __global__ __launch_bounds__(kExBlock, 1) void k_search_exact(
                               (int)m[1].x, (int)m[1].y, (int)m[1].z, (int)m[1].w};
         }
     };
-    // U digits of photon i of a pair (quad i >> 1, photon i & 1 of the lane's two) -> a[quad][Ur, Ui of photon 0, 1]
-    auto u_end_a = [&](ExPend& P, int i) -> ExRot {
+    // Pieces of the pipeline, each pinned to one MFMA gap (ex_open on its input at the start, ex_ready on its output
+    // at the end). U photon i of a pair = photon i & 1 of the lane's two in quad i >> 1 -> digit dwords
+    // a[quad][Ur, Ui of photon 0, then of photon 1].
+    auto u_a = [&](ExPend& P, int i) -> ExRot {
         ex_open(P.g[i].y);
         const ExRot r = ex_end_a(P.e[i], P.g[i].y);
         ex_ready(r.ts, r.tc);
         return r;
     };
-    auto u_end_b = [&](ExPend& P, int i, ExRot r, uint32_t (&a)[2][4]) {
-        ex_end_b(P.e[i], P.g[i].y, r, a[i >> 1][2 * (i & 1)], a[i >> 1][2 * (i & 1) + 1]);
-        ex_ready(a[i >> 1][2 * (i & 1)], a[i >> 1][2 * (i & 1) + 1]);
+    auto u_s = [&](ExPend& P, int i, ExRot& r, uint32_t (&a)[2][4]) {
+        ex_open(r.ts);
+        a[i >> 1][2 * (i & 1) + 1] = ex_end_s(P.e[i], P.g[i].y, r.ts);
+        ex_ready(a[i >> 1][2 * (i & 1) + 1]);
     };
-    // V item (chunk cj, index s): the phase half and the digit half
-    auto item_begin = [&](VItem& it) {
+    auto u_c = [&](ExPend& P, int i, ExRot& r, uint32_t (&a)[2][4]) {
+        ex_open(r.tc);
+        a[i >> 1][2 * (i & 1)] = ex_end_c(P.e[i], P.g[i].y, r.tc);
+        ex_ready(a[i >> 1][2 * (i & 1)]);
+    };
+    auto item_begin = [&](VItem& it, int s, int nlive) {
         ex_open(it.d);
-        v_begin(it);
+        v_begin(it, s, nlive);
         ex_ready(it.g.idx, it.g.y);
     };
-    auto item_end = [&](VItem& it) {
+    auto item_a = [&](VItem& it) {
         ex_open(it.g.y);
         it.r = ex_end_a(it.e, it.g.y);
-        ex_end_b(it.e, it.g.y, it.r, it.dc, it.dsn);
-        ex_ready(it.dc, it.dsn);
+        ex_ready(it.r.ts, it.r.tc);
+    };
+    auto item_s = [&](VItem& it) {
+        ex_open(it.r.ts);
+        it.dsn = ex_end_s(it.e, it.g.y, it.r.ts);
+        ex_ready(it.dsn);
+    };
+    auto item_c = [&](VItem& it) {
+        ex_open(it.r.tc);
+        it.dc = ex_end_c(it.e, it.g.y, it.r.tc);
+        ex_ready(it.dc);
+    };
+    auto item_post = [&](VItem& it) {
+        ex_open(it.dc, it.dsn);
+        v_post(it);
+        ex_ready(it.rc, it.rs);
+        ex_ready(it.rn);
+    };
+    auto u_begin = [&](double& d) -> ExArg {
+        ex_open(d);
+        const ExArg g = begin1(d);
+        ex_ready(g.idx, g.y);
+        return g;
     };
     const int kIdx = 0x44444444;  // sparse index: every group's two values at positions 0, 1
 #define EX_LO(v) __builtin_shufflevector(v, v, 0, 1, 2, 3)
 #define EX_HI(v) __builtin_shufflevector(v, v, 4, 5, 6, 7)
     // one pair group; X = this pair's operands, Y = the previous pair's (kept 2 MFMAs past their last reader,
     // then overwritten with the next pair's); P = table entries of pair +1 (in) / +2 (out); D = photon times of
-    // pair +2 (in) / +3 (out); I0, I1 = V items (photon time read one group earlier; on exit the next group's)
+    // pair +2 (in) / +3 (out); I0, I1 = V items (photon time read one group earlier; on exit the next group's).
+    // Gap k = the gap after matrix instruction k; VALU per gap ~6 (the pieces above: begin 6, a 3, s 3, c 3).
     auto pgroup = [&](ExOps& X, ExOps& Y, ExPend& P, ExDt& D, VItem& I0, VItem& I1, int c, int p, int nl1,
-                      int nl2) {
+                      int nl2, bool sync) {
         // this group's items: (c+1, 2p+2), (c+1, 2p+3) for p < 3, (c+2, 0), (c+2, 1) for p = 3; next group's
         const int icj = p + 1 < kExQuads / 2 ? c + 1 : c + 2, is = (2 * p + 2) % kExItems;
         const int ncj = p + 2 < kExQuads / 2 ? c + 1 : c + 2, ns = (2 * p + 4) % kExItems;
         const int inl = p + 1 < kExQuads / 2 ? nl1 : nl2;
         ExArg g[4];
+        uint32_t a[2][4];
+        ExRot r[4];
         ex_mfma<0>(X.A3[0], EX_LO(X.b[0][0]));
-        ex_open(D.d[0].x);
-        g[0] = begin1(D.d[0].x);
-        ex_ready(g[0].idx, g[0].y);
+        g[0] = u_begin(D.d[0].x);                                // gap 0
         ex_mfma<1>(X.A3[0], EX_LO(X.b[0][1]));
         ex_keep(Y.A6);  // read by the previous group's last MFMAs
         ex_keep(Y.b[1][0]);
         ex_keep(Y.b[1][1]);
-        ex_open(D.d[0].y);
-        g[1] = begin1(D.d[0].y);
-        ex_ready(g[1].idx, g[1].y);
+        g[1] = u_begin(D.d[0].y);                                // gap 1
         ex_mfma<2>(X.A3[0], EX_LO(X.b[1][0]));
-        read_b(c, p + 1, Y);  // consumed in the next group
-        ex_open(D.d[1].x);
-        g[2] = begin1(D.d[1].x);
-        ex_ready(g[2].idx, g[2].y);
+        if (sync) __syncthreads();  // the chunk's barrier: after the previous group's V writes, before this read
+        read_b(c, p + 1, Y);                                     // gap 2: consumed in the next group
+        g[2] = u_begin(D.d[1].x);
         ex_mfma<3>(X.A3[0], EX_LO(X.b[1][1]));
-        ex_open(D.d[1].y);
-        g[3] = begin1(D.d[1].y);
-        ex_ready(g[3].idx, g[3].y);
-        read_dt_pair(c, p + 3, D);  // consumed in the next group
+        g[3] = u_begin(D.d[1].y);                                // gap 3
+        read_dt_pair(c, p + 3, D);                               //        consumed in the next group
         ex_mfma<0>(X.A3[1], EX_HI(X.b[0][0]));
-        item_begin(I0);
-        ex_open(X.A3[0]);  // (an opaque copy: the shifts start here)
-        const i32x4 A40 = ex_shr8(X.A3[0]);
-        ex_ready(A40);
+        item_begin(I0, is, inl);                                 // gap 4
         ex_mfma<1>(X.A3[1], EX_HI(X.b[0][1]));
         ex_keep(X.A3[0]);
-        v_table(I0);
-        item_begin(I1);
+        v_table(I0);                                             // gap 5
+        ex_open(X.A3[0]);
+        const i32x4 A40 = ex_shr8(X.A3[0]);
+        ex_ready(A40);
         ex_mfma<2>(X.A3[1], EX_HI(X.b[1][0]));
-        v_table(I1);
+        item_begin(I1, is + 1, inl);                             // gap 6
+        ex_mfma<3>(X.A3[1], EX_HI(X.b[1][1]));
+        v_table(I1);                                             // gap 7
         ex_open(X.A3[1]);
         const i32x4 A41 = ex_shr8(X.A3[1]);
         ex_ready(A41);
-        uint32_t a[2][4];
-        const ExRot r0 = u_end_a(P, 0);
-        ex_mfma<3>(X.A3[1], EX_HI(X.b[1][1]));
-        u_end_b(P, 0, r0, a);
         ex_mfma<4>(A40, EX_LO(X.b[0][0]));
-        const ExRot r1 = u_end_a(P, 1);
+        r[0] = u_a(P, 0);                                        // gap 8
+        u_s(P, 0, r[0], a);
         ex_mfma<5>(A40, EX_LO(X.b[0][1]));
         ex_keep(X.A3[1]);
-        u_end_b(P, 1, r1, a);
+        u_c(P, 0, r[0], a);                                      // gap 9
+        item_a(I0);
         ex_mfma<6>(A40, EX_LO(X.b[1][0]));
-        const ExRot r2 = u_end_a(P, 2);
+        r[1] = u_a(P, 1);                                        // gap 10
+        u_s(P, 1, r[1], a);
         ex_mfma<7>(A40, EX_LO(X.b[1][1]));
-        u_end_b(P, 2, r2, a);
+        u_c(P, 1, r[1], a);                                      // gap 11
+        item_a(I1);
         ex_mfma<4>(A41, EX_HI(X.b[0][0]));
-        const ExRot r3 = u_end_a(P, 3);
+        r[2] = u_a(P, 2);                                        // gap 12
+        u_s(P, 2, r[2], a);
         ex_mfma<5>(A41, EX_HI(X.b[0][1]));
         ex_keep(A40);
-        u_end_b(P, 3, r3, a);
+        u_c(P, 2, r[2], a);                                      // gap 13
+        item_s(I0);
         ex_mfma<6>(A41, EX_HI(X.b[1][0]));
-        // the next pair's operands: dense digits and >> 8, compressed level-5/6 bytes, lane-swapped
+        r[3] = u_a(P, 3);                                        // gap 14
+        u_s(P, 3, r[3], a);
+        ex_mfma<7>(A41, EX_HI(X.b[1][1]));
+        u_c(P, 3, r[3], a);                                      // gap 15
+        item_c(I0);
+        // the next pair's operands: dense digits, compressed level-5/6 bytes (lane-swapped below)
         uint32_t c5[2][2], c6[2][2];
+        ex_smfma<8>(X.A5, X.b[0][0], kIdx);
 #pragma unroll
-        for (int qd = 0; qd < 2; ++qd) {
+        for (int qd = 0; qd < 2; ++qd) {                         // gap 16
             ex_open(a[qd][0], a[qd][1]);
             ex_open(a[qd][2], a[qd][3]);
             Y.A3[qd] = i32x4{(int)a[qd][0], (int)a[qd][1], (int)a[qd][2], (int)a[qd][3]};
 #pragma unroll
-            for (int w = 0; w < 2; ++w) {
+            for (int w = 0; w < 2; ++w)
                 c5[qd][w] = __builtin_amdgcn_perm(a[qd][2 * w + 1], a[qd][2 * w], 0x07060302u);  // d2, d3 of each
-                c6[qd][w] = __builtin_amdgcn_perm(a[qd][2 * w + 1], a[qd][2 * w], 0x0C070C03u);  // d3, 0 of each
-            }
+            ex_ready(c5[qd][0], c5[qd][1]);
         }
         ex_ready(Y.A3[0]);
-        ex_mfma<7>(A41, EX_HI(X.b[1][1]));
         ex_ready(Y.A3[1]);
-        ex_ready(c5[0][0], c5[0][1]);
-        ex_ready(c5[1][0], c5[1][1]);
-        ex_ready(c6[0][0], c6[0][1]);
-        ex_ready(c6[1][0], c6[1][1]);
-        ex_smfma<8>(X.A5, X.b[0][0], kIdx);
-        {
+        item_s(I1);
+        ex_smfma<9>(X.A5, X.b[0][1], kIdx);
+        ex_keep(A41);
+#pragma unroll
+        for (int qd = 0; qd < 2; ++qd) {                         // gap 17
+#pragma unroll
+            for (int w = 0; w < 2; ++w)
+                c6[qd][w] = __builtin_amdgcn_perm(a[qd][2 * w + 1], a[qd][2 * w], 0x0C070C03u);  // d3, 0 of each
+            ex_ready(c6[qd][0], c6[qd][1]);
+        }
+        item_c(I1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {  // the table entries of pair +2: consumed in the next group
+            P.e[i] = tab[g[i].idx];
+            P.g[i] = g[i];
+        }
+
+        ex_smfma<10>(X.A5, X.b[1][0], kIdx);
+        {                                                        // gap 18
             uint32_t s5[2][2], s6[2][2];
 #pragma unroll
             for (int w = 0; w < 2; ++w) {
@@ -444,24 +507,16 @@ __global__ __launch_bounds__(kExBlock, 1) void k_search_exact(
         }
         ex_ready(Y.A5);
         ex_ready(Y.A6);
-        ex_smfma<9>(X.A5, X.b[0][1], kIdx);
-        ex_keep(A41);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {  // the table entries of pair +2: consumed in the next group
-            P.e[i] = tab[g[i].idx];
-            P.g[i] = g[i];
-        }
-        ex_smfma<10>(X.A5, X.b[1][0], kIdx);
-        item_end(I0);
         ex_smfma<11>(X.A5, X.b[1][1], kIdx);
-        item_end(I1);
+        item_post(I0);                                           // gap 19
         ex_smfma<12>(X.A6, X.b[0][0], kIdx);
-        v_store(I0, icj, is, inl);
+        item_post(I1);                                           // gap 20
         ex_smfma<13>(X.A6, X.b[0][1], kIdx);
         ex_keep(X.A5);
-        v_store(I1, icj, is + 1, inl);
+        v_write(I0, icj, is);                                    // gap 21
+        v_write(I1, icj, is + 1);
         ex_smfma<14>(X.A6, X.b[1][0], kIdx);
-        v_read(ncj, ns, I0);  // the next group's items
+        v_read(ncj, ns, I0);                                     // gap 22: the next group's items
         v_read(ncj, ns + 1, I1);
         ex_smfma<15>(X.A6, X.b[1][1], kIdx);
         ex_keep(X.b[0][0]);
@@ -539,11 +594,10 @@ __global__ __launch_bounds__(kExBlock, 1) void k_search_exact(
         fetch_dt(c + kExDtSlots, pre);
         const int nl1 = nlive_of(c + 1), nl2 = nlive_of(c + 2);
         if (active) {
-            pgroup(X, Y, P, D, I0, I1, c, 0, nl1, nl2);
-            pgroup(Y, X, P, D, I0, I1, c, 1, nl1, nl2);
-            pgroup(X, Y, P, D, I0, I1, c, 2, nl1, nl2);
-            __syncthreads();
-            pgroup(Y, X, P, D, I0, I1, c, 3, nl1, nl2);
+            pgroup(X, Y, P, D, I0, I1, c, 0, nl1, nl2, false);
+            pgroup(Y, X, P, D, I0, I1, c, 1, nl1, nl2, false);
+            pgroup(X, Y, P, D, I0, I1, c, 2, nl1, nl2, false);
+            pgroup(Y, X, P, D, I0, I1, c, 3, nl1, nl2, true);
             const bool fold_now = (c + 1) % kExFold == 0 || c + 1 == nch;
             if (!fold_now && (c + 1) % kExCarry == 0) {
                 mfma_drain();
