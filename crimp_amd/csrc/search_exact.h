@@ -116,9 +116,12 @@ __device__ __forceinline__ ExEntry ex_entry(int i) {
 
 // digit dword of -y from the digit dword of y: -y's balanced digits are the negated digits (with carries),
 // recomputed from the integer: y = (d ^ 0x808080) - 0x808080
+// ((0x808080 - y) ^ 0x808080 with y = (d ^ 0x808080) - 0x808080) = ((~(d ^ 0x808080) + 0x1010101) ^ 0x808080): an
+// xor-add and an xor (v_xad_u32, v_xor_b32)
 __device__ __forceinline__ uint32_t ex_neg_digits(uint32_t d) {
-    const uint32_t y = (d ^ 0x00808080u) - 0x00808080u;
-    return (0x00808080u - y) ^ 0x00808080u;
+    uint32_t x;  // hipcc does not form v_xad_u32 with two literal constants (one may be an SGPR, the other a VGPR)
+    asm("v_xad_u32 %0, %1, %2, %3" : "=v"(x) : "v"(d), "s"(0xFF7F7F7Fu), "v"(0x01010101u));
+    return x ^ 0x00808080u;
 }
 
 
@@ -219,6 +222,7 @@ __global__ __launch_bounds__(kExBlock, 1) void k_search_exact(
     const double c2 = TWOD ? c2row[frow] * kT : 0.0;
     const int pb = tid & (kExCols - 1);                      // producer: V_b for b = pb, photons (tid >> 6) + 4 s
     const int pp = tid / kExCols;
+    const int ppu = __builtin_amdgcn_readfirstlane(pp);      // = pp: the wave's index, made visibly uniform
     const double gbv = (double)pb * apinfo[0] * kT;
     const int64_t split = blockIdx.y;
     const int64_t i0 = split * chunk;
@@ -250,7 +254,7 @@ __global__ __launch_bounds__(kExBlock, 1) void k_search_exact(
     // a photon past the split (pp + 4 s >= nlive: wave-uniform) reads the zero entry, so its V digits are 0
     auto v_begin = [&](VItem& it, int s, int nlive) {
         it.g = ex_begin(gbv * it.d);
-        it.g.idx = pp + 4 * s < nlive ? it.g.idx : (uint32_t)kExTab;
+        it.g.idx = ppu + 4 * s < nlive ? it.g.idx : (uint32_t)kExTab;
     };
     auto v_table = [&](VItem& it) { it.e = tab[it.g.idx]; };
     auto v_post = [&](VItem& it) {  // B fragment dwords: byte-reversed digits of Vr, Vi, -Vi
