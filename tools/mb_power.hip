@@ -4,7 +4,9 @@
 // s_memrealtime around its loop, so the in-kernel clock is cycles / (realtime ticks / 100 MHz).
 // Patterns (A operand; B always random bytes):
 //   0 random bytes, 1 top byte zero (A >> 8), 2 two zero bytes (A >> 16), 3 one small byte (A >> 24 of a 30-bit
-//   digit word), 4 all zero, 5 sparse v_smfmac_i32_32x32x64_i8 (random compressed A, random B, 16x the B bytes)
+//   digit word), 4 all zero, 5 sparse v_smfmac_i32_32x32x64_i8 (random compressed A, random B, 16x the B bytes),
+//   6 dense v_mfma_i32_16x16x64_i8 on random operands (4 accumulators of 4 registers; ns per 16x16x64 instruction
+//   = half the MACs of a 32x32x32 one)
 // build: hipcc --offload-arch=gfx950 -O3 -o build/mb_power tools/mb_power.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -48,6 +50,10 @@ __global__ __launch_bounds__(256, 1) void k_pow(int iters, unsigned seed, long l
         for (int s = 0; s < 4; ++s) {
             if (PAT == 5)
                 asm volatile("v_smfmac_i32_32x32x64_i8 %0, %1, %2, %3" : "+v"(c[s]) : "v"(a[s]), "v"(b[s]), "v"(0x44444444));
+            else if (PAT == 6)
+                asm volatile("v_mfma_i32_16x16x64_i8 %0, %1, %2, %0"
+                             : "+v"(*reinterpret_cast<i32x4*>(&c[s]))
+                             : "v"(a[s]), "v"(i32x4{b[s][0], b[s][1], b[s][2], b[s][3]}));
             else
                 asm volatile("v_mfma_i32_32x32x32_i8 %0, %1, %2, %0" : "+v"(c[s]) : "v"(a[s]), "v"(i32x4{b[s][0], b[s][1], b[s][2], b[s][3]}));
         }
@@ -99,6 +105,7 @@ int main() {
         run<3>("dense, A one small byte", iters, st, out);
         run<4>("dense, A zero", iters, st, out);
         run<5>("sparse smfmac K=64, random", iters, st, out);
+        run<6>("dense 16x16x64, random", iters, st, out);
     }
     return 0;
 }
