@@ -85,6 +85,10 @@ def test_config4_full_photon_count_h20(gpu):
     for rr, jj in sample:
         ref = O.search(t_h, f_h[jj:jj + 1], 20, freq_dot=fd[rr:rr + 1], stat="h")[0]
         assert abs(h[rr, jj] - ref) <= 1e-6 * abs(ref), (rr, jj, h[rr, jj], ref)
+    # every trial of the peak row's central 1024 against the fp64 kernel over all 1e8 photons
+    w0 = M + M // 2 - 512
+    h64 = ops.search(t, t0, f, 20, 1, log10_negfdot=fdd, first=w0, count=1024, precision="f64").cpu().numpy()
+    assert _rel_err(hf[w0:w0 + 1024], h64).max() <= 1e-6
 
 
 def test_trial_blocks_and_fixup(gpu, monkeypatch):
