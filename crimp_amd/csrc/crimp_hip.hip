@@ -1287,6 +1287,8 @@ static int fast_search(Scratch& sc, hipStream_t s, const double* dt, const doubl
 // int64 totals in units of 2^-36 hold |C_k| <= n exactly for n < 2^27 photons.
 static const int64_t kExactMaxPhotons = int64_t(1) << 27;
 static const int64_t kExFoldMaxBlocks = 8192;  // fold scratch of one launch <= 1 GiB
+static const int64_t kExFoldPhotons = (int64_t)kExFold * kExChunk;  // photons between int64 folds (search_exact.h)
+static const int64_t kExNoFoldMaxBlocks = 131072;  // blocks per launch when splits need no fold scratch
 // Photon splits of the exact kernel (one 256-thread block per CU): >= 4096 photons per split and >= 8 rounds of
 // the device's CUs, and among those counts (up to 4x the smallest) the one whose last round of blocks is fullest:
 // a grid of 8.2 rounds runs as long as 9 (config 3: 123 block columns x 17 splits = 2091 blocks on 256 CUs wasted
@@ -1299,8 +1301,33 @@ static void exact_splits(int64_t n, int64_t bpg, int64_t* chunk_out, int64_t* sp
             ncu = 256;
     }
     const int64_t smax_n = std::max<int64_t>(1, std::min<int64_t>(cdiv(n, 4096), 65535));
+    const int64_t srounds = cdiv(8 * (int64_t)ncu, bpg);
+    // Preferred: splits of <= kExFoldPhotons photons, which never fold into the int64 scratch (a block's only
+    // global traffic is then its final atomics, 128 KB; each intermediate fold would add 128 KB each way).
+    const int64_t snofold = cdiv(n, kExFoldPhotons);
+    if (snofold <= 65535 && bpg * snofold <= kExNoFoldMaxBlocks) {
+        const int64_t lo = std::max<int64_t>(1, std::max<int64_t>(snofold, std::min<int64_t>(srounds, smax_n)));
+        int64_t best_chunk = 0, best_splits = 0;
+        double best_eff = -1.0;
+        for (int64_t want = lo; want <= std::min<int64_t>(smax_n, lo + lo / 4 + 1); ++want) {
+            const int64_t chunk = cdiv(cdiv(n, want), kExChunk) * kExChunk;
+            const int64_t splits = cdiv(n, chunk);
+            const int64_t blocks = bpg * splits;
+            const double eff = (double)blocks / (double)(cdiv(blocks, ncu) * ncu);
+            if (chunk <= kExFoldPhotons && eff > best_eff + 0.005) {
+                best_eff = eff;
+                best_chunk = chunk;
+                best_splits = splits;
+            }
+        }
+        if (best_splits > 0) {
+            *chunk_out = best_chunk;
+            *splits_out = best_splits;
+            return;
+        }
+    }
     const int64_t smax = std::max<int64_t>(1, std::min<int64_t>(smax_n, kExFoldMaxBlocks / bpg));
-    const int64_t smin = std::max<int64_t>(1, std::min<int64_t>(cdiv(8 * (int64_t)ncu, bpg), smax));
+    const int64_t smin = std::max<int64_t>(1, std::min<int64_t>(srounds, smax));
     int64_t best_chunk = 0, best_splits = 0;
     double best_eff = -1.0;
     for (int64_t want = smin; want <= std::min<int64_t>(smax, 4 * smin); ++want) {
@@ -1350,11 +1377,14 @@ static int exact_search(Scratch& sc, hipStream_t s, const double* dt, const doub
         exact_splits(n, bpg, &chunk, &splits);
         HIPCHK(hipMemsetAsync(tot, 0, (size_t)(ncomp * bcount) * sizeof(unsigned long long), s));
         dim3 grid((unsigned)bpg, (unsigned)splits);
-        if (!fold) {  // sized by the first trial block, the largest (exact_splits keeps bpg * splits <= kExFoldMaxBlocks)
+        // fold scratch only when a split is longer than one fold period (sized by the first trial block, the
+        // largest; exact_splits then keeps bpg * splits <= kExFoldMaxBlocks); shorter splits never touch it
+        const bool folds = chunk > kExFoldPhotons;
+        if (folds && !fold) {
             fold_blocks = bpg * splits;
             HIPCHK(sc.alloc(&fold, (size_t)(fold_blocks * kExWaves * kExFoldVals * 64)));
         }
-        if (bpg * splits > fold_blocks) return set_err(CRIMP_ERR_HIP, "exact search: fold scratch bound");
+        if (folds && bpg * splits > fold_blocks) return set_err(CRIMP_ERR_HIP, "exact search: fold scratch bound");
         for (int k = 1; k <= nharm; ++k) {
             if (twod)
                 k_search_exact<true><<<grid, kExBlock, 0, s>>>(dt, dt2, n, chunk, freq, nf, c2, ap, tf, nt, tpr, bfirst,
