@@ -1305,7 +1305,8 @@ static void exact_splits(int64_t n, int64_t bpg, int64_t* chunk_out, int64_t* sp
     // Preferred: splits of <= kExFoldPhotons photons, which never fold into the int64 scratch (a block's only
     // global traffic is then its final atomics, 128 KB; each intermediate fold would add 128 KB each way).
     const int64_t snofold = cdiv(n, kExFoldPhotons);
-    if (snofold <= 65535 && bpg * snofold <= kExNoFoldMaxBlocks) {
+    static const bool long_splits = getenv("CRIMP_EXACT_LONG_SPLITS") != nullptr;  // test hook: the fold path
+    if (!long_splits && snofold <= 65535 && bpg * snofold <= kExNoFoldMaxBlocks) {
         const int64_t lo = std::max<int64_t>(1, std::max<int64_t>(snofold, std::min<int64_t>(srounds, smax_n)));
         int64_t best_chunk = 0, best_splits = 0;
         double best_eff = -1.0;

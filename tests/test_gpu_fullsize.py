@@ -319,3 +319,36 @@ def test_exact_path_photon_limit_routes_to_fp64(gpu):
     z_below64 = ops.search(tb, t0, f, 2, 0, precision="f64").cpu().numpy()
     assert _rel_err(z_below, z_below64).max() <= 1e-6
     assert not np.array_equal(z_below, z_below64)       # a different (exact) kernel ran
+
+
+def test_exact_long_splits_fold_path_bit_identical(gpu):
+    """Splits longer than one fold period (131072 photons) keep int64 running sums in global scratch between
+    folds; the default split choice avoids them whenever it can, so a test hook (CRIMP_EXACT_LONG_SPLITS) forces
+    the earlier policy. The totals are exact integers, so both give the same powers bit for bit (4e6 photons: 1-D
+    Z^2_3 over 2e6 trials, splits of ~444k photons with three intermediate folds; 2-D H_8 over 2 x 524288
+    trials, ~250k photons and one)."""
+    import os
+    import subprocess
+    import sys
+    import tempfile
+    code = (
+        "import sys, numpy as np; sys.path.insert(0, %r); from crimp_amd import ops; "
+        "from crimp_amd.synth import pulsed_events; "
+        "import torch; t_h = pulsed_events(4000000, 1.0e6, 7.123456789, pulsed_frac=0.05, seed=6); "
+        "t = torch.as_tensor(t_h, device='cuda'); t0 = (t_h[0] + t_h[-1]) / 2; "
+        "f = torch.as_tensor(7.123456789 + np.arange(-1000000, 1000000) / 1.0e7, device='cuda'); "
+        "z = ops.search(t, t0, f, 3, 0).cpu().numpy(); "
+        "fd = torch.as_tensor(np.array([-13.0, -12.0]), device='cuda'); "
+        "h = ops.search(t, t0, f[:524288], 8, 1, log10_negfdot=fd).cpu().numpy(); "
+        "np.savez(sys.argv[1], z=z, h=h)") % (str(__import__("conftest").ROOT))
+    with tempfile.TemporaryDirectory() as d:
+        res = []
+        for hook in (False, True):
+            out = os.path.join(d, "ls%d.npz" % hook)
+            env = dict(os.environ)
+            if hook:
+                env["CRIMP_EXACT_LONG_SPLITS"] = "1"
+            subprocess.run([sys.executable, "-c", code, out], check=True, env=env, timeout=300)
+            res.append(np.load(out))
+    np.testing.assert_array_equal(res[0]["z"], res[1]["z"])
+    np.testing.assert_array_equal(res[0]["h"], res[1]["h"])
