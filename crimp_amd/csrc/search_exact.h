@@ -2,8 +2,8 @@
 // with EXACT integer accumulation (MI355X / gfx950).
 //
 // Trial grid: an arithmetic progression f_j = f_0 + j*delta (fd-outer rows for the 2-D grid). A tile of
-// 1024 trials j = c0 + 32a + b (a, b in 0..31) factorises (periodsearch.py:67, :93-98, :120):
-//     exp(2 pi i k (f_j dt + c2 dt^2)) = U_a * V_b,   U_a = exp(2 pi i k (f_{c0+32a} dt + c2 dt^2)),
+// 2048 trials j = c0 + 64a + b (a in 0..31, b in 0..63) factorises (periodsearch.py:67, :93-98, :120):
+//     exp(2 pi i k (f_j dt + c2 dt^2)) = U_a * V_b,   U_a = exp(2 pi i k (f_{c0+64a} dt + c2 dt^2)),
 //                                                   V_b = exp(2 pi i k (b delta) dt),
 // so C_k + i S_k of the tile is the complex matrix product sum_photons U_a V_b.
 //
@@ -13,23 +13,23 @@
 // integers (error <= ~1.3 units = 1.2e-9). Each integer is split into four balanced base-256 digits
 // (d3 2^24 + d2 2^16 + d1 2^8 + d0, d_i in [-128, 127], |d3| <= 64) packed in one dword by two
 // integer ops: digits(y) = (y + 0x808080) ^ 0x808080. A product U.V = sum_{i,j} d_i e_j 2^{8(i+j)} is
-// accumulated per digit LEVEL L = i+j on v_mfma_i32_32x32x32_i8 in int32 (exact), levels 3..6
-// kept (the dropped levels 0..2 contribute < 5e-14 per photon): the A operand holds U's digits in natural
-// order, the B operand V's digits byte-reversed, so one dword pair dots to level 3, and A >> 8, >> 16,
-// >> 24 give levels 4, 5, 6 against the same B. The level sums are folded into int64 running sums in units
-// of 2^-36 (acc3 + acc4 << 8 + acc5 << 16 + acc6 << 24, exact) every kExFold chunks -- kept per lane in global
-// scratch between folds, so that the photon loop has the registers for both accumulators and operands --, and each block adds
-// its int64 totals to the global per-trial totals with 64-bit integer atomics: integer sums are exact and
-// order-independent, so the result does not depend on photon splits, trial blocking or sharding, and the
-// only errors are the 2^30 roundings of U and V (per-term ~1e-9, against ~1e-7 for fp32 sin/cos).
+// accumulated per digit LEVEL L = i+j in int32 (exact), levels 3..6 kept (the dropped levels 0..2 contribute
+// < 5e-14 per photon): the A operand holds U's digits in natural order, the B operand V's digits byte-reversed,
+// so one dword pair dots to level 3 and A >> 8 to level 4 (dense v_mfma_i32_32x32x32_i8); levels 5 and 6 have
+// A bytes (d2, d3, 0, 0) and (d3, 0, 0, 0) and run on the 2:4-sparse v_smfmac_i32_32x32x64_i8, two quads per
+// instruction. The level sums are carried exactly between levels every 16384 photons and folded into int64
+// (acc3 + acc4 << 8 + acc5 << 16 + acc6 << 24, units of 2^-36) every 131072; each block adds its int64 totals to
+// the global per-trial totals with 64-bit integer atomics: integer sums are exact and order-independent, so the
+// result does not depend on photon splits, trial blocking or sharding, and the only errors are the 2^30
+// roundings of U and V (per-term ~1e-9, against ~1e-7 for fp32 sin/cos).
 //
-// Layout: one 512-thread block (8 waves, one 1024-trial tile per wave) per group of 8 consecutive tiles
-// and photon split. Per chunk of 32 photons the block stages dt in LDS, all 512 threads compute the
-// tile-independent V digits once for the 8 tiles (32 photons x 32 b, stored [photon][b] as
-// {rev Vr, rev -Vi, rev Vi, rev Vr}), and every wave computes its own U digits in registers; lane
-// (a, h) holds photons 4q+2h, 4q+2h+1 of quad q ({Ur, Ui} of each: 16 bytes = the K slice of one
-// i8 MFMA), so one quad costs 8 MFMAs (4 levels x Re/Im). V and dt are double/triple buffered so
-// that the producers of chunk c+1 run beside the MFMAs of chunk c with one barrier per chunk.
+// Layout: one 256-thread block per CU (4 waves, one per SIMD, one 32 x 64 tile each) per group of 4 consecutive
+// tiles and photon split; the 256 int32 accumulators of a wave live in AGPRs (ex_mfma). Per chunk of 32 photons
+// the block stages dt in LDS, all 256 threads compute the tile-independent V digits for the 4 tiles (32 photons x
+// 64 b, stored per photon pair and column as B fragments {rev Vr, rev -Vi} / {rev Vi, rev Vr}), and every wave
+// computes its own U digits in registers: lane (a, h) holds photons 4q+2h, 4q+2h+1 of quad q ({Ur, Ui} of each:
+// 16 bytes = the K slice of one i8 MFMA). A software pipeline over quad pairs (below) interleaves all of it with
+// the 24 matrix instructions of each pair.
 #include <type_traits>
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
