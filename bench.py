@@ -166,7 +166,7 @@ def toa_leg(a, dev, world, rank):
                            % mjd.size)
     out["toa_e2e_max_shift_diff_vs_device_fit_cycles"] = float(np.max(np.abs(
         np.angle(np.exp(1j * (r2["phShi"] - res["phShi"]))))) / (2 * np.pi))
-    if not a.no_cpu and rank == 0:
+    if not a.no_cpu and rank == 0 and world == 1:  # CPU baselines: rank 0 at N=1 only
         out["toa_cpu_baseline"] = toa_cpu_baseline(x, off, E, tm, a.cpu_seconds)
     return out
 
@@ -373,7 +373,7 @@ def main():
                                  "frac = matrix-pipe occupancy at 2.4 GHz; traffic: %s" % (
                                      tsrc or "no PMC pass on this workload")},
         }
-        if not a.no_cpu:
+        if not a.no_cpu and world == 1:  # rank 0 at N=1 only
             rec["cpu_baseline"] = cpu_baseline(t_h, f0, df, a.nharm, a.cpu_seconds)
         if not a.no_fast:  # the opt-in fp32 sin/cos path on the same inputs (not the metric)
             ops.search(t, t0, f, a.nharm, 0, out=out, precision="fast")
