@@ -693,12 +693,18 @@ __global__ __launch_bounds__(kPtsBlock) void k_toa_points(const double* __restri
 }
 
 // Brute grid (fp32 model and log2, fp64 fold every 32 photons). One lane per phShift value,
-// photons of a 128-photon tile broadcast from LDS; NN norms per lane.
+// photons of a 128-photon tile broadcast from LDS; NN norms per lane. The fp32 adds, multiplies and FMAs run
+// as packed pairs (v_pk_add/mul/fma_f32: two lane-ops per issue, the only way to the f32 VALU peak) -- the
+// template over photon pairs, the norm products over norm pairs -- with each lane's operation order unchanged,
+// so the sums are bit-identical to the scalar form.
 constexpr int kGridBlock = 128;
 constexpr int kGridNN = 20;
 constexpr int kGridKMax = 8;
 constexpr int kGridProd = 4;
 constexpr int64_t kGridTarget = 16384;  // brute-grid blocks per launch (toa_grid_partials)
+static_assert(kGridNN % 2 == 0 && kGridProd == 4, "norm pairs; photons in two pairs per product");
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 template <int KMAX>
 __global__ __launch_bounds__(kGridBlock) void k_toa_grid(const double* __restrict__ x,
@@ -707,7 +713,9 @@ __global__ __launch_bounds__(kGridBlock) void k_toa_grid(const double* __restric
                                                          int nnorm, int a0, int na, const double* __restrict__ phi,
                                                          int nphi, int64_t chunk, int nint,
                                                          double* __restrict__ lnsum, double* __restrict__ hmin) {
-    __shared__ float basis[kGridBlock][2 * KMAX];
+    // basis[2j (+1)][photon]: cos / sin of harmonic j+1 (Fourier) or of the phase (j = 0, other models);
+    // photons i, i+1 adjacent so that one 8-byte broadcast read gives a photon pair.
+    __shared__ __attribute__((aligned(16))) float basis[2 * KMAX][kGridBlock];
     const int tid = threadIdx.x;
     const int bphi = blockIdx.x * kGridBlock + tid;
     const int64_t iv = blockIdx.y;
@@ -733,9 +741,9 @@ __global__ __launch_bounds__(kGridBlock) void k_toa_grid(const double* __restric
             }
         }
     }
-    float nr[kGridNN];
+    f32x2 nr[kGridNN / 2];
 #pragma unroll
-    for (int a = 0; a < kGridNN; ++a) nr[a] = (a < na) ? (float)norm[iv * nnorm + a0 + a] : 1.0f;
+    for (int a = 0; a < kGridNN; ++a) nr[a / 2][a % 2] = (a < na) ? (float)norm[iv * nnorm + a0 + a] : 1.0f;
     double acc[kGridNN];
 #pragma unroll
     for (int a = 0; a < kGridNN; ++a) acc[a] = 0.0;
@@ -755,15 +763,15 @@ __global__ __launch_bounds__(kGridBlock) void k_toa_grid(const double* __restric
                 float cj = c1, sj = s1;
 #pragma unroll
                 for (int j = 0; j < KMAX; ++j) {
-                    basis[tid][2 * j] = cj;
-                    basis[tid][2 * j + 1] = sj;
+                    basis[2 * j][tid] = cj;
+                    basis[2 * j + 1][tid] = sj;
                     const float cn = __builtin_fmaf(cj, c1, -sj * s1);
                     sj = __builtin_fmaf(sj, c1, cj * s1);
                     cj = cn;
                 }
             } else {
-                basis[tid][0] = c1;
-                basis[tid][1] = s1;
+                basis[0][tid] = c1;
+                basis[1][tid] = s1;
             }
         }
         __syncthreads();
@@ -772,9 +780,9 @@ __global__ __launch_bounds__(kGridBlock) void k_toa_grid(const double* __restric
             if (model == CRIMP_MODEL_FOURIER) {
 #pragma unroll
                 for (int j = 0; j < KMAX; ++j)
-                    if (j < K) h = __builtin_fmaf(ca[j], basis[i][2 * j], __builtin_fmaf(cb[j], basis[i][2 * j + 1], h));
+                    if (j < K) h = __builtin_fmaf(ca[j], basis[2 * j][i], __builtin_fmaf(cb[j], basis[2 * j + 1][i], h));
             } else {
-                const float cx = basis[i][0], sx = basis[i][1];
+                const float cx = basis[0][i], sx = basis[1][i];
 #pragma unroll
                 for (int j = 0; j < KMAX; ++j) {
                     if (j < K) {
@@ -788,38 +796,56 @@ __global__ __launch_bounds__(kGridBlock) void k_toa_grid(const double* __restric
             }
             return h;
         };
-        for (int i0 = 0; i0 < cnt; i0 += 32) {
-            float pa[kGridNN];
+        // photons i, i+1 (i even): the Fourier template as packed FMAs, same order per photon as hval
+        auto hval2 = [&](int i) {
+            f32x2 h;
+            if (model == CRIMP_MODEL_FOURIER) {
+                h = f32x2{0.0f, 0.0f};
 #pragma unroll
-            for (int a = 0; a < kGridNN; ++a) pa[a] = 0.0f;
+                for (int j = 0; j < KMAX; ++j)
+                    if (j < K) {
+                        const f32x2 cj = *reinterpret_cast<const f32x2*>(&basis[2 * j][i]);
+                        const f32x2 sj = *reinterpret_cast<const f32x2*>(&basis[2 * j + 1][i]);
+                        h = __builtin_elementwise_fma(f32x2{ca[j], ca[j]}, cj,
+                                                      __builtin_elementwise_fma(f32x2{cb[j], cb[j]}, sj, h));
+                    }
+            } else {
+                h = f32x2{hval(i), hval(i + 1)};
+            }
+            return h;
+        };
+        for (int i0 = 0; i0 < cnt; i0 += 32) {
+            f32x2 pa[kGridNN / 2];
+#pragma unroll
+            for (int a = 0; a < kGridNN / 2; ++a) pa[a] = f32x2{0.0f, 0.0f};
             const int i1 = std::min(cnt, i0 + 32);
             int i = i0;
             // log2 of a product of kGridProd model values instead of kGridProd logs (v_log issues at quarter
             // rate): one photon costs an add and a multiply per norm plus 1/kGridProd of a log and an add.
             // Four factors of (norm + h) <= 2^31 cannot overflow fp32; the product adds <= 3 roundings.
             for (; i + kGridProd <= i1; i += kGridProd) {
-                float hv[kGridProd];
+                const f32x2 h01 = hval2(i), h23 = hval2(i + 2);
+                hmn = fminf(fminf(fminf(fminf(hmn, h01.x), h01.y), h23.x), h23.y);
 #pragma unroll
-                for (int j = 0; j < kGridProd; ++j) {
-                    hv[j] = hval(i + j);
-                    hmn = fminf(hmn, hv[j]);
-                }
-#pragma unroll
-                for (int a = 0; a < kGridNN; ++a) {
-                    float pr = nr[a] + hv[0];
-#pragma unroll
-                    for (int j = 1; j < kGridProd; ++j) pr *= nr[a] + hv[j];
-                    pa[a] += __builtin_amdgcn_logf(pr);
+                for (int b = 0; b < kGridNN / 2; ++b) {
+                    f32x2 pr = nr[b] + h01.x;
+                    pr *= nr[b] + h01.y;
+                    pr *= nr[b] + h23.x;
+                    pr *= nr[b] + h23.y;
+                    pa[b] += f32x2{__builtin_amdgcn_logf(pr.x), __builtin_amdgcn_logf(pr.y)};
                 }
             }
             for (; i < i1; ++i) {
                 const float h = hval(i);
                 hmn = fminf(hmn, h);
 #pragma unroll
-                for (int a = 0; a < kGridNN; ++a) pa[a] += __builtin_amdgcn_logf(nr[a] + h);
+                for (int b = 0; b < kGridNN / 2; ++b) {
+                    const f32x2 pr = nr[b] + h;
+                    pa[b] += f32x2{__builtin_amdgcn_logf(pr.x), __builtin_amdgcn_logf(pr.y)};
+                }
             }
 #pragma unroll
-            for (int a = 0; a < kGridNN; ++a) acc[a] += (double)pa[a];
+            for (int a = 0; a < kGridNN; ++a) acc[a] += (double)pa[a / 2][a % 2];
         }
     }
     if (bphi < nphi) {
