@@ -706,7 +706,9 @@ static_assert(kGridNN % 2 == 0 && kGridProd == 4, "norm pairs; photons in two pa
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
-template <int KMAX, int MODEL>  // the model is a template argument: registers only for its own coefficients
+// MODEL and (Fourier) the template size KF are template arguments: registers only for the model's own coefficients,
+// no per-harmonic branches; KF = 0 reads K from the template at run time.
+template <int KMAX, int MODEL, int KF>
 __global__ __launch_bounds__(kGridBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_toa_grid(const double* __restrict__ x,
                                                          const int64_t* __restrict__ offsets,
                                                          const TplDev* __restrict__ T, const double* __restrict__ norm,
@@ -721,7 +723,7 @@ __global__ __launch_bounds__(kGridBlock) __attribute__((amdgpu_waves_per_eu(4)))
     const int64_t iv = blockIdx.y;
     const int64_t split = blockIdx.z;
     constexpr int model = MODEL;
-    const int K = T->K;
+    const int K = KF > 0 ? KF : T->K;
     const double ph = phi[bphi < nphi ? bphi : nphi - 1];
     float ca[KMAX], cb[KMAX], amp[KMAX], chj[KMAX], kpj[KMAX];
 #pragma unroll
@@ -1654,7 +1656,7 @@ extern "C" int crimp_toa_points(const double* x, const int64_t* offsets, int64_t
 // Per-split brute-grid partial sums (k_toa_grid) for nint <= 65535 intervals of at most maxn photons:
 // pl[((split*nint + i)*nnorm + a)*nphi + b] (log2 sums), ph[(split*nint + i)*nphi + b] (min h).
 static int toa_grid_partials(Scratch& sc, hipStream_t s, const double* dx, const int64_t* doff, const TplDev* dT,
-                             int model, const double* dnrm, int64_t nnorm, const double* dphi, int64_t nphi, int64_t nint,
+                             int model, int K, const double* dnrm, int64_t nnorm, const double* dphi, int64_t nphi, int64_t nint,
                              int64_t maxn, double** pl, double** ph, int64_t* splits_out) {
     const int64_t pblocks = cdiv(nphi, kGridBlock);
     // photon splits: aim at kGridTarget blocks (2 waves each; 4 waves/SIMD fit, 2048 resident blocks), so
@@ -1672,11 +1674,24 @@ static int toa_grid_partials(Scratch& sc, hipStream_t s, const double* dx, const
     dim3 grid((unsigned)pblocks, (unsigned)nint, (unsigned)splits);
     for (int64_t a0 = 0; a0 < nnorm; a0 += kGridNN) {
         const int na = (int)std::min<int64_t>(kGridNN, nnorm - a0);
-#define CRIMP_LG(MD) k_toa_grid<kGridKMax, MD><<<grid, kGridBlock, 0, s>>>(dx, doff, dT, dnrm, (int)nnorm, (int)a0, na, \
-                                                                            dphi, (int)nphi, chunk, (int)nint, *pl, *ph)
-        if (model == CRIMP_MODEL_FOURIER) CRIMP_LG(CRIMP_MODEL_FOURIER);
-        else if (model == CRIMP_MODEL_CAUCHY) CRIMP_LG(CRIMP_MODEL_CAUCHY);
-        else CRIMP_LG(CRIMP_MODEL_VONMISES);
+#define CRIMP_LG(MD, KK) k_toa_grid<kGridKMax, MD, KK><<<grid, kGridBlock, 0, s>>>(dx, doff, dT, dnrm, (int)nnorm, (int)a0, \
+                                                                                na, dphi, (int)nphi, chunk, (int)nint, *pl, *ph)
+        if (model == CRIMP_MODEL_FOURIER) {
+            switch (K) {
+                case 1: CRIMP_LG(CRIMP_MODEL_FOURIER, 1); break;
+                case 2: CRIMP_LG(CRIMP_MODEL_FOURIER, 2); break;
+                case 3: CRIMP_LG(CRIMP_MODEL_FOURIER, 3); break;
+                case 4: CRIMP_LG(CRIMP_MODEL_FOURIER, 4); break;
+                case 5: CRIMP_LG(CRIMP_MODEL_FOURIER, 5); break;
+                case 6: CRIMP_LG(CRIMP_MODEL_FOURIER, 6); break;
+                case 7: CRIMP_LG(CRIMP_MODEL_FOURIER, 7); break;
+                default: CRIMP_LG(CRIMP_MODEL_FOURIER, 8); break;
+            }
+        } else if (model == CRIMP_MODEL_CAUCHY) {
+            CRIMP_LG(CRIMP_MODEL_CAUCHY, 0);
+        } else {
+            CRIMP_LG(CRIMP_MODEL_VONMISES, 0);
+        }
 #undef CRIMP_LG
         HIPCHK(hipGetLastError());
     }
@@ -1760,7 +1775,7 @@ extern "C" int crimp_toa_fit(const double* x, const int64_t* offsets, int64_t ni
                 for (int64_t i = i0; i < i0 + nb; ++i) maxn = std::max(maxn, hoff[i + 1] - hoff[i]);
                 double *pl = nullptr, *ph = nullptr;
                 int64_t splits = 0;
-                rc = toa_grid_partials(sc, s, dx, doff + i0, dT, T.model, dnrm + i0 * nn, nn, dphi, nphi, nb, maxn, &pl, &ph,
+                rc = toa_grid_partials(sc, s, dx, doff + i0, dT, T.model, T.K, dnrm + i0 * nn, nn, dphi, nphi, nb, maxn, &pl, &ph,
                                        &splits);
                 if (rc) return rc;
                 k_toa_grid_best<<<(unsigned)nb, 256, 0, s>>>(pl, ph, dnrm + i0 * nn, dphi, doff + i0, de + i0, (int)nn,
@@ -1839,7 +1854,7 @@ extern "C" int crimp_toa_grid(const double* x, const int64_t* offsets, int64_t n
         HIPCHK(h2d(dT, &T, sizeof(T)));
         double *pl = nullptr, *ph = nullptr;
         int64_t splits = 0;
-        rc = toa_grid_partials(sc, s, dx, doff, dT, T.model, dnrm, nnorm, dphi, nphi, nint, maxn, &pl, &ph, &splits);
+        rc = toa_grid_partials(sc, s, dx, doff, dT, T.model, T.K, dnrm, nnorm, dphi, nphi, nint, maxn, &pl, &ph, &splits);
         if (rc) return rc;
         // combine splits on the host in a fixed order (deterministic)
         std::vector<double> hl((size_t)(splits * nint * nnorm * nphi)), hh((size_t)(splits * nint * nphi));
