@@ -1380,53 +1380,67 @@ static int exact_search(Scratch& sc, hipStream_t s, const double* dt, const doub
                         int64_t count, double* out, KernelTimer* kt, int64_t* nfixed, bool no_fixup) {
     const int64_t tpr = cdiv(nf, kExTileTrials);
     const int ncomp = 2 * nharm;
-    // trial blocks bounded by the int64 totals buffer (2 GiB) and by the blocks' fold scratch (kExFoldMaxBlocks
-    // blocks of 128 KB), whole 8-tile block groups
-    const int64_t cbmax = std::min<int64_t>(std::max<int64_t>(kExTileTrials * kExWaves, part_budget() / (8 * ncomp)),
-                                            kExFoldMaxBlocks * kExWaves * kExTileTrials);
-    const int64_t cb = std::min<int64_t>(count, cdiv(cdiv(count, cdiv(count, cbmax)), kExTileTrials) * kExTileTrials);
+    // Trial blocks are bounded by the int64 totals buffer (part_budget) and by the tiles one launch may hold
+    // (<= kExFoldMaxBlocks block columns, so that a fold scratch stays <= 1 GiB: a 2-D grid's rows each start a
+    // new tile, so a block of short rows holds more tiles than its trial count suggests); whole tiles.
+    int64_t want = std::max<int64_t>(kExTileTrials, part_budget() / (8 * ncomp)), cb = 0;
+    struct Blk { int64_t bfirst, bcount, tf, nt, bpg, chunk, splits; };
+    std::vector<Blk> blks;
+    int64_t fold_blocks = 0;  // the largest bpg * splits of the blocks whose splits fold into the int64 scratch
+    for (;;) {
+        cb = std::min<int64_t>(count, cdiv(cdiv(count, cdiv(count, want)), kExTileTrials) * kExTileTrials);
+        blks.clear();
+        fold_blocks = 0;
+        bool fits = true;
+        for (int64_t b0 = 0; b0 < count && fits; b0 += cb) {
+            Blk k;
+            k.bfirst = first + b0;
+            k.bcount = std::min<int64_t>(cb, count - b0);
+            const int64_t last = k.bfirst + k.bcount - 1;
+            k.tf = (k.bfirst / nf) * tpr + (k.bfirst % nf) / kExTileTrials;
+            const int64_t tl = (last / nf) * tpr + (last % nf) / kExTileTrials;
+            k.nt = tl - k.tf + 1;
+            k.bpg = cdiv(k.nt, kExWaves);
+            fits = k.bpg <= kExFoldMaxBlocks;
+            exact_splits(n, k.bpg, &k.chunk, &k.splits);
+            if (k.chunk > kExFoldPhotons) fold_blocks = std::max<int64_t>(fold_blocks, k.bpg * k.splits);
+            blks.push_back(k);
+        }
+        if (fits) break;
+        if (cb <= kExTileTrials) return set_err(CRIMP_ERR_ARG, "exact search: trial block does not fit one launch");
+        want = cb / 2;
+    }
+    if (fold_blocks > kExFoldMaxBlocks) return set_err(CRIMP_ERR_HIP, "exact search: fold scratch bound");
     unsigned long long* tot = nullptr;
     long long* fold = nullptr;
-    int64_t fold_blocks = 0;
     int64_t* flagged = nullptr;
     int* nflag = nullptr;
     HIPCHK(sc.alloc(&tot, (size_t)(ncomp * cb)));
     HIPCHK(sc.alloc(&flagged, (size_t)count));
     HIPCHK(sc.alloc(&nflag, 1));
+    // fold scratch only when some block's splits are longer than one fold period; shorter splits never touch it
+    if (fold_blocks > 0) HIPCHK(sc.alloc(&fold, (size_t)(fold_blocks * kExWaves * kExFoldVals * 64)));
     HIPCHK(hipMemsetAsync(nflag, 0, sizeof(int), s));
     const double sigc = std::sqrt((double)n) * 1e-9;  // standard deviation of the error of C_k (search_exact.h)
     if (kt) kt->start();
-    for (int64_t b0 = 0; b0 < count; b0 += cb) {
-        const int64_t bfirst = first + b0, bcount = std::min<int64_t>(cb, count - b0);
-        const int64_t last = bfirst + bcount - 1;
-        const int64_t tf = (bfirst / nf) * tpr + (bfirst % nf) / kExTileTrials;
-        const int64_t tl = (last / nf) * tpr + (last % nf) / kExTileTrials;
-        const int64_t nt = tl - tf + 1;
-        const int64_t bpg = cdiv(nt, kExWaves);
-        int64_t chunk = 0, splits = 0;
-        exact_splits(n, bpg, &chunk, &splits);
-        HIPCHK(hipMemsetAsync(tot, 0, (size_t)(ncomp * bcount) * sizeof(unsigned long long), s));
-        dim3 grid((unsigned)bpg, (unsigned)splits);
-        // fold scratch only when a split is longer than one fold period (sized by the first trial block, the
-        // largest; exact_splits then keeps bpg * splits <= kExFoldMaxBlocks); shorter splits never touch it
-        const bool folds = chunk > kExFoldPhotons;
-        if (folds && !fold) {
-            fold_blocks = bpg * splits;
-            HIPCHK(sc.alloc(&fold, (size_t)(fold_blocks * kExWaves * kExFoldVals * 64)));
-        }
-        if (folds && bpg * splits > fold_blocks) return set_err(CRIMP_ERR_HIP, "exact search: fold scratch bound");
-        for (int k = 1; k <= nharm; ++k) {
+    for (size_t bi = 0; bi < blks.size(); ++bi) {
+        const Blk& k = blks[bi];
+        const int64_t b0 = k.bfirst - first;
+        HIPCHK(hipMemsetAsync(tot, 0, (size_t)(ncomp * k.bcount) * sizeof(unsigned long long), s));
+        dim3 grid((unsigned)k.bpg, (unsigned)k.splits);
+        for (int h = 1; h <= nharm; ++h) {
             if (twod)
-                k_search_exact<true><<<grid, kExBlock, 0, s>>>(dt, dt2, n, chunk, freq, nf, c2, ap, tf, nt, tpr, bfirst,
-                                                               bcount, k, tot, fold);
+                k_search_exact<true><<<grid, kExBlock, 0, s>>>(dt, dt2, n, k.chunk, freq, nf, c2, ap, k.tf, k.nt, tpr,
+                                                               k.bfirst, k.bcount, h, tot, fold);
             else
-                k_search_exact<false><<<grid, kExBlock, 0, s>>>(dt, dt2, n, chunk, freq, nf, c2, ap, tf, nt, tpr,
-                                                                bfirst, bcount, k, tot, fold);
+                k_search_exact<false><<<grid, kExBlock, 0, s>>>(dt, dt2, n, k.chunk, freq, nf, c2, ap, k.tf, k.nt, tpr,
+                                                                k.bfirst, k.bcount, h, tot, fold);
             HIPCHK(hipGetLastError());
         }
-        if (kt && b0 + cb >= count) kt->stop();
-        k_search_finalize_exact<<<(unsigned)cdiv(bcount, 256), 256, 0, s>>>(
-            reinterpret_cast<const long long*>(tot), bcount, nharm, stat, (double)n, sigc, fixup_rel(), b0, out + b0, nflag, flagged);
+        if (kt && bi + 1 == blks.size()) kt->stop();
+        k_search_finalize_exact<<<(unsigned)cdiv(k.bcount, 256), 256, 0, s>>>(
+            reinterpret_cast<const long long*>(tot), k.bcount, nharm, stat, (double)n, sigc, fixup_rel(), b0, out + b0,
+            nflag, flagged);
         HIPCHK(hipGetLastError());
     }
     int nf_h = 0;
@@ -1487,12 +1501,13 @@ extern "C" int crimp_search(const double* t, int64_t n, double t0, const double*
 
         // Routing by properties of the whole grid (not of this call's trial range), so that every shard of a
         // sharded search takes the kernel an unsharded search takes:
-        //   default: exact i8 kernel for progressions of >= 256 trials and < 2^27 photons, fp64 kernel otherwise;
-        //   fast:    f16-split MFMA kernel for progressions of >= 256 trials, fp32 direct kernel otherwise;
+        //   default: exact i8 kernel for progressions of >= 256 trials per row and < 2^27 photons, fp64 kernel
+        //            otherwise (a 2-D grid of short rows would fill its 2048-trial tiles with dead columns);
+        //   fast:    f16-split MFMA kernel for progressions of >= 256 trials per row, fp32 direct kernel otherwise;
         //   f64:     fp64 kernel.
         KernelTimer kt(s, flags & CRIMP_FLAG_TIME_KERNELS);
         bool factorised = !f64 && !(flags & CRIMP_FLAG_FORCE_DIRECT) &&
-                          (total >= 256 || (flags & CRIMP_FLAG_FORCE_MFMA)) && (fast || n < kExactMaxPhotons);
+                          (nf >= 256 || (flags & CRIMP_FLAG_FORCE_MFMA)) && (fast || n < kExactMaxPhotons);
         double* ap = nullptr;
         if (factorised) {
             bool ok = false;
@@ -1738,6 +1753,8 @@ extern "C" int crimp_toa_fit(const double* x, const int64_t* offsets, int64_t ni
     C.kcap = (double)ph_shift_res / 2.0;
     C.sum_amp = 0.0;
     for (int j = 0; j < tpl->ncomp; ++j) C.sum_amp += tpl->amp[j] * tpl->amp_shift;
+    C.amp_lo = T.model == CRIMP_MODEL_FOURIER ? 0.01 : 0.0;                                  // :308, :461, :605
+    C.amp_hi = T.model == CRIMP_MODEL_FOURIER ? 100.0 : T.model == CRIMP_MODEL_CAUCHY ? INFINITY : 500.0;
     {
         Scratch sc(s);
         const double *dx = nullptr, *de = nullptr;

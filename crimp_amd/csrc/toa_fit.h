@@ -23,6 +23,8 @@ struct FitCfg {
     double step;     // 2 pi / phShiftRes                                       (:320)
     double kcap;     // phShiftRes / 2                                          (:348, :373)
     double sum_amp;  // sum_j amp_j: cauchy / von Mises normalisation F = 2 pi norm + sum_amp
+    double amp_lo, amp_hi;  // ampShift bounds when varied: [0.01, 100] fourier (:308), [0, inf) cauchy (:461),
+                            // [0, 500] von Mises (:605)
 };
 
 struct FitEval {
@@ -188,8 +190,7 @@ __device__ double fit_profile(const double* __restrict__ x, int64_t a, int64_t b
 
 // ---------------------------------------------------------------- varyAmps (measureToAs.py:305-312)
 // With ampShift A free the model is norm + A*h, and the extended LL, its gradient and Hessian in
-// (norm, phShift, A) follow from 11 photon sums; ampShift is bounded to [0.01, 100] (:308).
-constexpr double kAmpLo = 0.01, kAmpHi = 100.0;
+// (norm, phShift, A) follow from 11 photon sums; ampShift is bounded by the model's [C.amp_lo, C.amp_hi].
 
 struct FitEval3 {
     double ll, g[3], H[6];  // H = {nn, np, nA, pp, pA, AA}
@@ -315,7 +316,7 @@ __device__ void fit_newton_dir3(const double* v, const FitEval3& e, int mask, do
 __device__ FitEval3 fit_ascent3(const double* __restrict__ x, int64_t a, int64_t b, const TplDev* __restrict__ T,
                                 double* v, int mask, int max_iter, double E, const FitCfg& C, FitShared& sh,
                                 FitShared3& s3, int& nev) {
-    const double lo[3] = {C.lo, -C.pb, kAmpLo}, hi[3] = {C.hi, C.pb, kAmpHi};
+    const double lo[3] = {C.lo, -C.pb, C.amp_lo}, hi[3] = {C.hi, C.pb, C.amp_hi};
     FitEval3 e = fit_eval3(x, a, b, T, v[0], v[1], v[2], E, C, sh, s3);
     ++nev;
     for (int it = 0; it < max_iter; ++it) {

@@ -14,8 +14,12 @@ The conversions keep the reference's operation order (``TIME / 86400 + MJDREF``,
 """
 import argparse
 import os
+import re
 
 import numpy as np
+
+# column keywords of a binary table header card (TTYPEn ... TDIMn): the new column's cards follow the last of them
+_COLKEY = re.compile(r"T(TYPE|FORM|UNIT|ZERO|SCAL|DISP|NULL|DIM)\d+")
 
 _CODES = {"L": ("u1", 1), "B": ("u1", 1), "I": (">i2", 2), "J": (">i4", 4), "K": (">i8", 8), "E": (">f4", 4),
           "D": (">f8", 8), "A": ("S1", 1)}
@@ -347,8 +351,7 @@ def add_column(path, extname, name, values):
                 c = _card("THEAP", int(hdr["THEAP"]) + 8 * nrow)
             new.append(c)
         # the new column's keywords go after the last existing column keyword
-        last = max(i for i, c in enumerate(new) if c[:5] in ("TTYPE", "TFORM", "TUNIT", "TZERO", "TSCAL", "TDISP",
-                                                              "TNULL", "TDIM"))
+        last = max(i for i, c in enumerate(new) if _COLKEY.match(c[:8]))
         new[last + 1:last + 1] = [_card("TTYPE%d" % (nf + 1), name), _card("TFORM%d" % (nf + 1), "D")]
         data = newrows.tobytes() + heap
         out.append(_block(new))

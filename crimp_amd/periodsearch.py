@@ -9,8 +9,9 @@ Z2pow] plus the matching DataFrame, where ``freq_dot`` holds log10|fdot| of a
 negative fdot (:95). ``twod_htest`` is this package's extension (H-test on the
 same 2-D grid).
 
-All statistics come from ``crimp_search`` (csrc/crimp_hip.hip section 4 and
-csrc/search_mfma.h); there is no NumPy fallback.
+All statistics come from ``crimp_search`` (csrc/crimp_hip.hip section 4, the default
+exact kernel in csrc/search_exact.h, the opt-in fast kernel in csrc/search_fast.h);
+there is no NumPy fallback.
 """
 import numpy as np
 
@@ -19,9 +20,15 @@ from ._native import STAT_H, STAT_Z2, _is_torch
 
 
 class PeriodSearch:
-    """``precision`` (keyword, not in the reference): None/"fast" is the default MFMA/fp32-sin-cos path
-    (within 1e-6 of the grid's power scale); "f64" evaluates every term in fp64 like the reference
-    (within ~1e-9 relative on every trial, including near-zero bins)."""
+    """``precision`` (keyword, not in the reference):
+
+    * None (default): the exact path -- on arithmetic-progression grids of >= 256 trials per row and < 2^27 photons
+      the i8-MFMA kernel with exact integer sums of 2^30 fixed-point cos/sin (~1e-9 relative per trial), plus an
+      fp64 recomputation of every trial that its 10-sigma error bound cannot place within 1e-6 relative; other
+      grids take the fp64 kernel. Per-trial contract: 1e-6 relative of the reference's fp64 value, except where
+      the reference's own argument rounding is larger (noise-level H at config-4 arguments; DESIGN.md section 8);
+    * "f64": every term in fp64 like the reference (~1e-9 relative on every trial, near-zero bins included);
+    * "fast": fp32 sin/cos on f16-split MFMA, within 1e-6 of the grid's mean power (not per trial)."""
 
     def __init__(self, time, freq, nbrHarm: int = 2, *, precision=None):
         self.time = time

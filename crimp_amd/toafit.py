@@ -21,7 +21,9 @@ iterates:
 4. redChi2 from the ``binphases`` profile (device histogram, numpy.histogram
    edge semantics) against the best-fit curve, dof = nbrBins - 2 (:385-393).
 
-Only ``readvaryparam=False, varyAmps=False`` (the CLI defaults) are implemented.
+``varyAmps`` (a free ampShift, :305-312) runs on the device too (``k_toa_fit_amp``: (norm, ampShift)
+re-profiled at every scan step); ``readvaryparam`` (free template parameters, :727-801) is driven from
+``toafit_vary.py`` on device likelihood/gradient sums.
 """
 import math
 
@@ -309,7 +311,7 @@ class ToAFitter:
     # ------------------------------------------------------------------ drivers
     def fit(self, brutemin=False, vary_amps=False):
         """Every interval's fit in one device call (crimp_toa_fit: one workgroup per interval runs steps 1-3),
-        then the redChi2 of step 4. ``vary_amps``: ampShift free in [0.01, 100] after the (norm, phShift) fit,
+        then the redChi2 of step 4. ``vary_amps``: ampShift free (Fourier [0.01, 100], Cauchy [0, inf), von Mises [0, 500]) after the (norm, phShift) fit,
         re-profiled with the norm in the 1-sigma scan, one more free parameter in redChi2 (:305-312)."""
         r = ops.toa_fit(self.x, self.offsets, self.tpl, self._arr(self.E, np.float64), self.norm0, self.res, brutemin,
                         vary_amps)

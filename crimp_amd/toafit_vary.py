@@ -13,7 +13,8 @@ is a copy of the best-fit parameters, :319), and redChi2 counts the free paramet
 :733-748 does (norm and the freed template parameters -- not phShift).
 
 ``varyAmps`` together with ``readvaryparam`` (:306-312 after :727-801): once the freed parameters are fitted,
-ampShift (a common factor on every template amplitude) is freed in [0.01, 100] from 1 and everything free is
+ampShift (a common factor on every template amplitude) is freed from 1 within its model's bounds (Fourier
+[0.01, 100] :308, Cauchy [0, inf) :461, von Mises [0, 500] :605) and everything free is
 maximised again; the 1-sigma scan then re-maximises ampShift too, and redChi2 counts one more free parameter.
 The parameter vector is then [norm, template..., ampShift, phShift].
 
@@ -28,6 +29,9 @@ import numpy as np
 
 from . import ops
 from . import _native as N
+
+# ampShift bounds when varyAmps frees it: measureToAs.py:308 (Fourier), :461 (Cauchy), :605 (von Mises)
+AMP_SHIFT_BOUNDS = {"fourier": (0.01, 100.0), "cauchy": (0.0, math.inf), "vonmises": (0.0, 500.0)}
 from .toafit import CHI2_1SIG_1DOF, TWO_PI, ToAFitter
 
 
@@ -53,11 +57,12 @@ class VaryParamFitter(ToAFitter):
                 lo.append(l)
                 hi.append(h)
                 vary.append(bool(tmpl[nm]["vary"]))
-        if self.vary_amps:  # measureToAs.py:308: ampShift 1 in [0.01, 100], freed after the first fit
+        if self.vary_amps:  # measureToAs.py:308, :461, :605: ampShift 1 in its model's bounds, freed after the first fit
+            alo, ahi = AMP_SHIFT_BOUNDS[m]
             names.append("ampShift")
             val.append(1.0)
-            lo.append(0.01)
-            hi.append(100.0)
+            lo.append(alo)
+            hi.append(ahi)
             vary.append(False)
         names.append("phShift")
         val.append(0.0)

@@ -26,6 +26,14 @@
 
 #define ORC_PI 3.141592653589793238462643383279502884
 
+/* The search sums use fma() and rint() on every term: built for FMA3 hosts (hardware fma, roundsd via AVX) with a baseline
+ * clone selected at load time on older hosts (the library is built here and runs on the GPU box's host too). */
+#if defined(__x86_64__) && defined(__GNUC__)
+#define ORC_CLONES __attribute__((target_clones("fma", "default")))
+#else
+#define ORC_CLONES
+#endif
+
 /* ------------------------------------------------------------------------ */
 /* Timing model (values of the .par dictionary, readtimingmodel.py:212-233)  */
 /* ------------------------------------------------------------------------ */
@@ -111,30 +119,124 @@ void orc_calcphase(const double* t, int64_t n, const orc_model* m, int parts, do
  *   2-D: 2*(kk+1)*pi*(f*(t-t0) + (0.5*(-1*10**fd))*(t-t0)**2)
  * stat 0 = Z^2_m; stat 1 = H (max of cumsum(Z^2_k) - 4*(k-1)).
  * out is [nfd*nf] with fd outer, f inner (periodsearch.py:264-278). nfd==0 => 1-D. */
+/* cos(a), sin(a) of the fp64 argument a, as accurate as libm's (a few 1e-16 absolute) but without libm's slow
+ * large-argument path (glibc switches to Payne-Hanek reduction above ~1e8 rad, where the config-4 arguments
+ * 2 pi k f dt ~ 4e9 rad live: ~110 ns per term). Reduction by 2 pi = P1 + P2 (+ < 6e-33): with k = rint(a / 2 pi),
+ * a - k P1 is a multiple of 2^-50 below 4 in magnitude for |a| < 2^40, so the fma is exact; k P2 <= 2^38 x 2.5e-16
+ * adds one rounding of the reduced angle. The argument itself is the reference's, unchanged. */
+/* sin, cos of |x| <= pi/4 + 1e-9: Taylor series to x^17 / x^18 (truncation < 1e-19), Horner in fp64 (~1 ulp) */
+static inline __attribute__((always_inline)) void orc_sincos_small(double x, double* s, double* c) {
+    const double x2 = x * x;
+    double ps = 1.0 / 355687428096000.0;                 /* 1/17! */
+    ps = fma(ps, -x2, 1.0 / 1307674368000.0);            /* 1/15! */
+    ps = fma(ps, -x2, 1.0 / 6227020800.0);               /* 1/13! */
+    ps = fma(ps, -x2, 1.0 / 39916800.0);                 /* 1/11! */
+    ps = fma(ps, -x2, 1.0 / 362880.0);
+    ps = fma(ps, -x2, 1.0 / 5040.0);
+    ps = fma(ps, -x2, 1.0 / 120.0);
+    ps = fma(ps, -x2, 1.0 / 6.0);
+    *s = fma(-x * x2, ps, x);
+    double pc = 1.0 / 6402373705728000.0;                /* 1/18! */
+    pc = fma(pc, -x2, 1.0 / 20922789888000.0);           /* 1/16! */
+    pc = fma(pc, -x2, 1.0 / 87178291200.0);              /* 1/14! */
+    pc = fma(pc, -x2, 1.0 / 479001600.0);                /* 1/12! */
+    pc = fma(pc, -x2, 1.0 / 3628800.0);
+    pc = fma(pc, -x2, 1.0 / 40320.0);
+    pc = fma(pc, -x2, 1.0 / 720.0);
+    pc = fma(pc, -x2, 1.0 / 24.0);
+    pc = fma(pc, -x2, 0.5);
+    *c = fma(-x2, pc, 1.0);
+}
+
+/* cos/sin of r - q pi/2 -> of r by the quadrant q (mod 4) */
+static inline __attribute__((always_inline)) void orc_quadrant(double s0, double c0, int64_t q, double* c, double* s) {
+    switch ((int)(q & 3)) {
+        case 0: *c = c0; *s = s0; break;
+        case 1: *c = -s0; *s = c0; break;
+        case 2: *c = -c0; *s = -s0; break;
+        default: *c = s0; *s = -c0; break;
+    }
+}
+
+static inline __attribute__((always_inline)) void orc_cossin(double a, double* c, double* s) {
+    /* 2 pi = P1 + P2 (+ < 6e-33), pi/2 = H1 + H2 (+ < 2e-33) */
+    static const double P1 = 6.283185307179586232, P2 = 2.4492935982947063e-16, INV = 0.15915494309189535;
+    static const double H1 = 1.5707963267948966, H2 = 6.123233995736766e-17, INVH = 0.6366197723675814;
+    if (!(fabs(a) < 1099511627776.0)) {
+        *c = cos(a);
+        *s = sin(a);
+        return;
+    }
+    const double k = rint(a * INV);
+    const double r = fma(-k, P2, fma(-k, P1, a));   /* |r| <= pi + 1e-15 */
+    const double q = rint(r * INVH);                 /* quadrant, |q| <= 2 */
+    const double x = fma(-q, H2, fma(-q, H1, r));    /* |x| <= pi/4 + 1e-15; fma(-q, H1, r) exact */
+    double s0, c0;
+    orc_sincos_small(x, &s0, &c0);
+    orc_quadrant(s0, c0, (int64_t)q, c, s);
+}
+
 /* Harmonic sums of one trial over photons [i0, i1) (the inner loops of periodsearch.py:66-69,
  * :97-100 and :118-121). */
-static void trial_sums(const double* time, int64_t i0, int64_t i1, double t0, double f, double c2, int twod,
+ORC_CLONES static void trial_sums(const double* time, int64_t i0, int64_t i1, double t0, double f, double c2, int twod,
                        int k, double* sc_out, double* ss_out) {
     double pre = 2.0 * (double)(k + 1) * ORC_PI;
-    double sc = 0.0, ss = 0.0;
+    double sc = 0.0, ss = 0.0, c, s;
     if (twod) {
         for (int64_t i = i0; i < i1; ++i) {
             double dt = time[i] - t0;
             double a = pre * (f * dt + c2 * (dt * dt));
-            sc += cos(a);
-            ss += sin(a);
+            orc_cossin(a, &c, &s);
+            sc += c;
+            ss += s;
         }
     } else {
         double pf = pre * f;
         for (int64_t i = i0; i < i1; ++i) {
             double a = pf * (time[i] - t0);
-            sc += cos(a);
-            ss += sin(a);
+            orc_cossin(a, &c, &s);
+            sc += c;
+            ss += s;
         }
     }
     *sc_out = sc;
     *ss_out = ss;
 }
+
+/* The same sums with the EXACT argument of the given inputs: phase in cycles (k+1)(f dt + c2 dt^2) carried in
+ * double-double (error-free products by fma), reduced to a centred fraction before the 2 pi multiply. This is the
+ * value the reference's formula has on these fp64 inputs in exact arithmetic -- the reference's own fp64 argument
+ * rounds by ~2^-53 of |a| per term (up to ~1e-6 rad at config 4), which this variant measures. Not a restatement
+ * of any reference routine: it is the yardstick both the reference and the device kernels are measured against. */
+ORC_CLONES static void trial_sums_true(const double* time, int64_t i0, int64_t i1, double t0, double f, double c2, int twod,
+                            int k, double* sc_out, double* ss_out) {
+    const double kk = (double)(k + 1);
+    double sc = 0.0, ss = 0.0, c, s;
+    for (int64_t i = i0; i < i1; ++i) {
+        const double dt = time[i] - t0;              /* exact: t and t0 within a factor 2 (Sterbenz) */
+        double uh = f * dt, ul = fma(f, dt, -uh);    /* f dt = uh + ul exactly */
+        if (twod) {
+            const double d2h = dt * dt, d2l = fma(dt, dt, -d2h);
+            const double wh = c2 * d2h, wl = fma(c2, d2h, -wh) + c2 * d2l;
+            const double sh = uh + wh, bb = sh - uh;  /* two-sum of uh + wh */
+            const double se = (uh - (sh - bb)) + (wh - bb);
+            uh = sh;
+            ul = ul + wl + se;
+        }
+        const double ph = kk * uh, pl = fma(kk, uh, -ph) + kk * ul;
+        const double fr = (ph - rint(ph)) + pl;      /* ph - rint(ph) is exact */
+        const double q = rint(4.0 * fr);             /* quadrant: fr = q/4 + y, |y| <= 1/8 (+ 1e-9) */
+        double s0, c0;
+        orc_sincos_small(2.0 * ORC_PI * (fr - 0.25 * q), &s0, &c0);   /* fr - q/4 is exact */
+        orc_quadrant(s0, c0, (int64_t)q, &c, &s);
+        sc += c;
+        ss += s;
+    }
+    *sc_out = sc;
+    *ss_out = ss;
+}
+
+typedef void (*orc_sums_fn)(const double*, int64_t, int64_t, double, double, double, int, int, double*, double*);
 
 static double combine(const double* z, int nharm, int stat, int64_t n) {
     if (stat == 0) {
@@ -155,8 +257,9 @@ static double combine(const double* z, int nharm, int stat, int64_t n) {
  * parallel over (trial, harmonic, photon block) with a FIXED block count, blocks summed in
  * order, so the result does not depend on the thread count either. */
 #define ORC_PBLOCKS 256
-static void orc_search_photon_blocked(const double* time, int64_t n, double t0, const double* freq, int64_t nf,
-                                      const double* fd, int64_t nfd, int nharm, int stat, double* out) {
+static void orc_search_photon_blocked(orc_sums_fn sums, const double* time, int64_t n, double t0,
+                                      const double* freq, int64_t nf, const double* fd, int64_t nfd, int nharm,
+                                      int stat, double* out) {
     int64_t rows = nfd > 0 ? nfd : 1;
     int64_t total = rows * nf;
     int64_t nb = ORC_PBLOCKS, bs = (n + nb - 1) / nb;
@@ -170,7 +273,7 @@ static void orc_search_photon_blocked(const double* time, int64_t n, double t0, 
                 int64_t i0 = b * bs, i1 = i0 + bs < n ? i0 + bs : n;
                 double* o = part + 2 * ((idx * nharm + k) * nb + b);
                 if (i0 >= i1) { o[0] = o[1] = 0.0; continue; }
-                trial_sums(time, i0, i1, t0, freq[j], c2, nfd > 0, k, o, o + 1);
+                sums(time, i0, i1, t0, freq[j], c2, nfd > 0, k, o, o + 1);
             }
     double* z = (double*)malloc(sizeof(double) * (size_t)nharm);
     for (int64_t idx = 0; idx < total; ++idx) {
@@ -186,12 +289,12 @@ static void orc_search_photon_blocked(const double* time, int64_t n, double t0, 
     free(part);
 }
 
-void orc_search(const double* time, int64_t n, double t0, const double* freq, int64_t nf,
-                const double* fd, int64_t nfd, int nharm, int stat, double* out) {
+static void orc_search_with(orc_sums_fn sums, const double* time, int64_t n, double t0, const double* freq,
+                            int64_t nf, const double* fd, int64_t nfd, int nharm, int stat, double* out) {
     int64_t rows = nfd > 0 ? nfd : 1;
     int64_t total = rows * nf;
     if (total < 64 && n >= (1 << 22)) {
-        orc_search_photon_blocked(time, n, t0, freq, nf, fd, nfd, nharm, stat, out);
+        orc_search_photon_blocked(sums, time, n, t0, freq, nf, fd, nfd, nharm, stat, out);
         return;
     }
 #pragma omp parallel
@@ -200,46 +303,33 @@ void orc_search(const double* time, int64_t n, double t0, const double* freq, in
 #pragma omp for schedule(dynamic, 1)
         for (int64_t idx = 0; idx < total; ++idx) {
             int64_t r = idx / nf, j = idx % nf;
-            double f = freq[j];
             double c2 = nfd > 0 ? 0.5 * (-1.0 * pow(10.0, fd[r])) : 0.0;
             for (int k = 0; k < nharm; ++k) {
-                double pre = 2.0 * (double)(k + 1) * ORC_PI;
-                double sc = 0.0, ss = 0.0;
-                if (nfd > 0) {
-                    for (int64_t i = 0; i < n; ++i) {
-                        double dt = time[i] - t0;
-                        double a = pre * (f * dt + c2 * (dt * dt));
-                        sc += cos(a);
-                        ss += sin(a);
-                    }
-                } else {
-                    double pf = pre * f;
-                    for (int64_t i = 0; i < n; ++i) {
-                        double a = pf * (time[i] - t0);
-                        sc += cos(a);
-                        ss += sin(a);
-                    }
-                }
+                double sc, ss;
+                sums(time, 0, n, t0, freq[j], c2, nfd > 0, k, &sc, &ss);
                 z[k] = sc * sc + ss * ss;
             }
-            double res;
-            if (stat == 0) {
-                double s = 0.0;
-                for (int k = 0; k < nharm; ++k) s += z[k];
-                res = s * (2.0 / (double)n);
-            } else {
-                double cum = 0.0, best = -INFINITY;
-                for (int k = 0; k < nharm; ++k) {
-                    cum += z[k] * (2.0 / (double)n);
-                    double v = cum - 4.0 * (double)k;
-                    if (v > best) best = v;
-                }
-                res = best;
-            }
-            out[idx] = res;
+            out[idx] = combine(z, nharm, stat, n);
         }
         free(z);
     }
+}
+
+void orc_search(const double* time, int64_t n, double t0, const double* freq, int64_t nf,
+                const double* fd, int64_t nfd, int nharm, int stat, double* out) {
+    orc_search_with(trial_sums, time, n, t0, freq, nf, fd, nfd, nharm, stat, out);
+}
+
+/* Same statistic with exact arguments (trial_sums_true): the yardstick for the argument-rounding analysis of the
+ * full-size parity tests, not a reference routine. */
+void orc_search_true(const double* time, int64_t n, double t0, const double* freq, int64_t nf,
+                     const double* fd, int64_t nfd, int nharm, int stat, double* out) {
+    orc_search_with(trial_sums_true, time, n, t0, freq, nf, fd, nfd, nharm, stat, out);
+}
+
+/* cos/sin of orc_cossin for a vector of arguments (CPU test of the reduction against libm) */
+ORC_CLONES void orc_cossin_vec(const double* a, int64_t n, double* c, double* s) {
+    for (int64_t i = 0; i < n; ++i) orc_cossin(a[i], c + i, s + i);
 }
 
 /* ------------------------------------------------------------------------ */
