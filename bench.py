@@ -19,7 +19,10 @@ Also reported:
 * ``fast_path``: the opt-in fp32 sin/cos path (precision="fast") on the same workload, for comparison;
 * ToA (config 5 per GPU): the device fit of 1250 intervals x 1e5 photons, and the end-to-end ``measure_intervals``
   (interval selection, calcphase, fits, per-interval H-test) from host MJD arrays, with the oracle's fits on all
-  allowed host cores as its CPU baseline (a sample, extrapolated) and the fits' VALU roofline.
+  allowed host cores as its CPU baseline (a sample, extrapolated) and the fits' VALU roofline;
+* ``config4``: 1e8 photons, 2-D H_20, the first 131072 trials of this rank's shard of the 1e7-trial grid;
+* ``config2``: ``measureToAs`` on the bundled events, ToAs 35-41, FITS -> table (the reference's published rate).
+The multi-GPU search step is ``sharding.sharded_search(gather="best")``, the path tests/test_distributed_*.py test.
 """
 import argparse
 import json
@@ -57,6 +60,10 @@ def parse():
     p.add_argument("--no-toa", action="store_true", help="skip the ToA legs")
     p.add_argument("--calcphase-photons", type=int, default=100_000_000)
     p.add_argument("--no-calcphase", action="store_true", help="skip the calcphase (HBM-bound) leg")
+    p.add_argument("--no-config2", action="store_true", help="skip the config-2 measureToAs leg")
+    p.add_argument("--no-config4", action="store_true", help="skip the config-4 (1e8 photons, H_20) leg")
+    p.add_argument("--c4-photons", type=int, default=100_000_000)
+    p.add_argument("--c4-trials", type=int, default=131072, help="config-4 trials timed per GPU")
     return p.parse_args()
 
 
@@ -192,6 +199,119 @@ def toa_cpu_baseline(x, off, E, tm, budget_s):
                       "reference log: 0.42 fits/s at 1e4 photons (BASELINE.md)" % (done, el)}
 
 
+def config2_leg(a):
+    """BASELINE config 2, the reference's one published rate: ``measureToAs`` (measureToAs.py:64-251) on the bundled
+    1e2259 events (a FITS file written from tests/golden/events_1e2259.npz, the EVENTS rows of
+    data/1e2259_ni1020600110.fits), .par, template and interval file, ``-el 1 -eh 5 -bm -ts 35 -te 41``: FITS read,
+    energy filter, interval selection, calcphase, 7 brute+MLE+1-sigma fits, H_5, the table, .txt and the residual
+    PDF. One untimed call, then the median of 3. The reference's log quotes 84 ToAs in 202 s = 0.42 fits/s
+    (data/ToAs_2259.log:1,23); the oracle's fit_toa (fp64 C + SciPy) on the same 7 intervals and host cores sits
+    beside it."""
+    import tempfile
+    import pandas as pd
+    from crimp_amd.eventfile import write_events_fits
+    from crimp_amd.measureToAs import measureToAs
+    from crimp_amd.readPPtemplate import readPPtemplate
+    G = os.path.join(ROOT, "tests", "golden")
+    ev = np.load(os.path.join(G, "events_1e2259.npz"))
+    ref = pd.read_csv(os.path.join(G, "ToAs_2259.txt"), sep=r"\s+", comment="#")
+    ref = ref[(ref["ToA"] >= 35) & (ref["ToA"] <= 41)].reset_index(drop=True)
+    times = []
+    with tempfile.TemporaryDirectory() as d:
+        fits = os.path.join(d, "ev.fits")
+        write_events_fits(fits, ev["TIME"], ev["PI"], int(ev["MJDREFI"]), float(ev["MJDREFF"]))
+        args = (fits, os.path.join(G, "1e2259.par"), os.path.join(G, "1e2259_template.txt"),
+                os.path.join(G, "timIntToAs_1e2259.txt"))
+        kw = dict(eneLow=1, eneHigh=5, toaStart=35, toaEnd=41, brutemin=True, toaFile=os.path.join(d, "ToAs"))
+        tab = measureToAs(*args, **kw)   # untimed: code objects, scratch pool, matplotlib import
+        for _ in range(3):
+            t1 = time.perf_counter()
+            tab = measureToAs(*args, **kw)
+            times.append(time.perf_counter() - t1)
+    el = float(np.median(times))
+    nfit = len(tab)
+    dphi = float(np.max(np.abs(tab["phShift"].to_numpy() - ref["phShift"].to_numpy())) / (2 * np.pi))
+    out = {"fits_per_s": nfit / el, "seconds": el, "toas": nfit,
+           "max_phShift_diff_vs_reference_table_cycles": dphi,
+           "phShift_LL_UL_identical_to_reference_table": bool(
+               np.array_equal(tab["phShift_LL"].to_numpy(), ref["phShift_LL"].to_numpy()) and
+               np.array_equal(tab["phShift_UL"].to_numpy(), ref["phShift_UL"].to_numpy())),
+           "reference_log_fits_per_s": 84 / 202.0,
+           "note": "measureToAs FITS -> table incl. .txt and residual PDF, ToAs 35-41 of the worked example "
+                   "(data/ToAs_2259.txt); reference: 84 ToAs in 202 s (data/ToAs_2259.log:1,23), author's machine"}
+    if not a.no_cpu:
+        from oracle import oracle as O
+        cores, visible = host_cores()
+        O.set_threads(cores)
+        g = np.load(os.path.join(G, "toa_1e2259.npz"))
+        iv = pd.read_csv(os.path.join(G, "timIntToAs_1e2259.txt"), sep=r"\s+", comment="#")
+        E = iv["ToA_exposure"].to_numpy()[g["ids"]]
+        tm = readPPtemplate(os.path.join(G, "1e2259_template.txt"))
+        t1 = time.perf_counter()
+        for i in range(len(g["ids"])):
+            O.fit_toa(g["folded"][g["offsets"][i]:g["offsets"][i + 1]], E[i], tm, brutemin=True)
+        el = time.perf_counter() - t1
+        out["cpu_baseline"] = {"value": len(g["ids"]) / el, "unit": "ToA fits/s", "cores": cores,
+                               "host_cpus_visible": visible, "kind": "port",
+                               "sample": "the same 7 intervals (folded phases of tests/golden/toa_1e2259.npz), oracle "
+                                         "fit_toa with brute start, %.1f s" % el}
+    return out
+
+
+def config4_leg(a, dev, world, rank):
+    """BASELINE config 4 on this rank's shard: 1e8 photons (T = 1e7 s, p = 0.05, fdot = -1e-12, seed 1), 2-D H_20
+    over 1e5 f (step 1/(10 T)) x 100 log10|fdot| rows linspace(-13.5, -11.5, 100) = 1e7 trials split over the ranks
+    (sharding.shard_range, fd-outer flat index); the first ``c4_trials`` trials of the rank's shard are timed
+    (the whole 1.25e6-trial shard of one of 8 GPUs takes ~14x longer). Default (exact) path; one untimed search,
+    then one timed; evals/s summed over ranks / max-over-ranks time."""
+    import torch
+    import torch.distributed as dist
+    from crimp_amd import ops
+    from crimp_amd import _native as N
+    from crimp_amd.sharding import shard_range
+    from crimp_amd.synth import pulsed_events
+    n, span, f0, fdot, M = a.c4_photons, 1.0e7, 7.123456789, -1.0e-12, 100_000
+    t1 = time.perf_counter()
+    t_h = pulsed_events(n, span, f0, pulsed_frac=0.05, fdot=fdot, seed=1)
+    gen_s = time.perf_counter() - t1
+    t = torch.as_tensor(t_h, device=dev)
+    t0 = (t_h[0] + t_h[-1]) / 2
+    del t_h
+    f = torch.as_tensor(f0 + (np.arange(M) - M // 2) / (10.0 * span), device=dev)
+    fd = torch.as_tensor(np.linspace(-13.5, -11.5, 100), device=dev)
+    first, count = shard_range(100 * M, world, rank)
+    count = min(count, a.c4_trials)
+    ops.search(t, t0, f, 20, 1, log10_negfdot=fd, first=first, count=count)   # untimed
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    h = ops.search(t, t0, f, 20, 1, log10_negfdot=fd, first=first, count=count, flags=N.FLAG_TIME_KERNELS)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t1
+    kms = N.load().crimp_last_kernel_ms()
+    nfix = N.load().crimp_last_fixups()
+    best = int(torch.argmax(h).item())
+    elt = torch.tensor([el], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elt, op=dist.ReduceOp.MAX)
+    el = float(elt.item())
+    ops_launch = OPS_PER_EVAL_HARM * 20 * float(n) * count
+    ach = ops_launch / (kms * 1e-3) / 1e12
+    del t, f, fd, h
+    torch.cuda.empty_cache()
+    return {"evals_per_s": float(n) * count * world / el, "unit": "photon*trial evals/s (H_20)", "seconds": el,
+            "kernel_ms": kms, "trials_per_gpu_timed": count, "photons": n, "first_flat_trial": first,
+            "fp64_fixup_trials": nfix, "best_flat_trial_in_timed_range": first + best,
+            "photon_generation_s": gen_s,
+            "roofline": {"bound": "mfma", "achieved": ach, "peak": PEAK_I8_TOPS, "unit": "TFLOP/s",
+                         "frac": ach / PEAK_I8_TOPS,
+                         "note": "128 int8 matrix ops per photon*trial*harmonic x 20 harmonics / k_search_exact "
+                                 "hipEvent time (the harmonic launches of the search)"},
+            "workload": "config4: 1e8 photons, H_20, 2-D grid 1e5 f x 100 fdot = 1e7 trials sharded over %d rank(s); "
+                        "first %d trials of the rank's shard timed" % (world, count)}
+
+
 def calcphase_leg(a, dev):
     """calcphase (calcphase.py:152-176) over 1e8 photons resident in HBM: 8 B read + 16 B written per photon
     (SURVEY.md section 8d), HBM-bound; hipEvents on the stream the library launches on (torch's current stream)."""
@@ -284,29 +404,23 @@ def main():
     t_h = pulsed_events(a.photons, span, f0, pulsed_frac=0.1, seed=0)
     df = 1.0 / (10.0 * span)
     M = a.trials
-    g0 = rank * M - (world * M) // 2          # this rank's slice of the N*M grid centred on f0
-    f_h = f0 + (np.arange(M) + g0) * df
+    # the whole N*M grid centred on f0; sharding.sharded_search gives this rank trials [rank*M, (rank+1)*M)
+    f_h = f0 + (np.arange(world * M) - (world * M) // 2) * df
     t = torch.as_tensor(t_h, device=dev)
     f = torch.as_tensor(f_h, device=dev)
-    out = torch.empty(M, dtype=torch.float64, device=dev)
-    t0 = (t_h[0] + t_h[-1]) / 2
-    best = torch.zeros(2, dtype=torch.float64, device=dev)
-    gathered = torch.zeros(world, 2, dtype=torch.float64, device=dev)
+    from crimp_amd.sharding import sharded_search, shard_range
+    assert shard_range(world * M, world, rank) == (rank * M, M)
 
-    kms, fixups = [], []
+    kms, fixups, bests = [], [], []
 
     def step():
-        ops.search(t, t0, f, a.nharm, 0, out=out, flags=N.FLAG_TIME_KERNELS)
+        # the tested multi-GPU path (tests/test_distributed_*.py): this rank's slice through crimp_search, then one
+        # all_gather of every rank's (best power, flat index); ties -> lowest index
+        b = sharded_search(t, f, a.nharm, 0, gather="best", flags=N.FLAG_TIME_KERNELS)
         kms.append(N.load().crimp_last_kernel_ms())
         fixups.append(N.load().crimp_last_fixups())
-        i = torch.argmax(out)
-        best[0] = out[i]
-        best[1] = (i + (g0 + (world * M) // 2)).to(torch.float64)  # global trial index
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, best)
-        else:
-            gathered[0] = best
-        return gathered
+        bests.append(b)
+        return b
 
     for _ in range(a.warmup):
         step()
@@ -321,7 +435,7 @@ def main():
     t1 = time.perf_counter()
     for k in range(a.steps):
         evs[k][0].record(stream)
-        g = step()
+        step()
         evs[k][1].record(stream)
     torch.cuda.synchronize()
     if world > 1:
@@ -334,9 +448,7 @@ def main():
     el = float(elt.item())
     step_ms = float(np.mean([s.elapsed_time(e) for s, e in evs]))
     kern_ms = float(np.mean(kms))  # hipEvents around the harmonic-sum kernels, on the stream they run on
-    gb = g.cpu().numpy()
-    order = np.lexsort((gb[:, 1], -gb[:, 0]))
-    best_idx = int(gb[order[0], 1])
+    best_pow, best_idx = bests[-1]
 
     evals = float(a.photons) * M * world * a.steps
     value = evals / el
@@ -360,8 +472,9 @@ def main():
             "data": "synthetic (seeded Poisson pulsed events, crimp_amd/synth.py)",
             "config": {"workload": "config3: synthetic %d photons x %d trials/GPU, Z^2_%d" % (a.photons, M, a.nharm),
                        "photons": a.photons, "trials_per_gpu": M, "nharm": a.nharm, "span_s": span, "f0": f0,
-                       "trial_step_hz": df, "parallelism": "trial-sharded dp%d + all_gather(best)" % world,
-                       "best_trial_index": best_idx, "best_power": float(gb[order[0], 0]),
+                       "trial_step_hz": df,
+                       "parallelism": "trial-sharded dp%d: sharding.sharded_search + all_gather(best)" % world,
+                       "best_trial_index": best_idx, "best_power": float(best_pow),
                        "search_path": "exact (default precision)", "fp64_fixup_trials_per_step": float(np.mean(fixups))},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_I8_TOPS, "unit": "TFLOP/s",
                          "frac": achieved / PEAK_I8_TOPS, "traffic": traffic,
@@ -376,14 +489,16 @@ def main():
         if not a.no_cpu and world == 1:  # rank 0 at N=1 only
             rec["cpu_baseline"] = cpu_baseline(t_h, f0, df, a.nharm, a.cpu_seconds)
         if not a.no_fast:  # the opt-in fp32 sin/cos path on the same inputs (not the metric)
-            ops.search(t, t0, f, a.nharm, 0, out=out, precision="fast")
+            t0 = (t_h[0] + t_h[-1]) / 2
+            out = torch.empty(M, dtype=torch.float64, device=dev)
+            ops.search(t, t0, f, a.nharm, 0, first=rank * M, count=M, out=out, precision="fast")
             torch.cuda.synchronize()
             t2 = time.perf_counter()
-            ops.search(t, t0, f, a.nharm, 0, out=out, precision="fast")
+            ops.search(t, t0, f, a.nharm, 0, first=rank * M, count=M, out=out, precision="fast")
             torch.cuda.synchronize()
             rec["fast_path"] = {"evals_per_s": float(a.photons) * M / (time.perf_counter() - t2),
                                 "precision": "fp32 sin/cos + f16-split MFMA: 1e-6 of the mean power, not per trial"}
-    del t, f, out
+    del t, f
     torch.cuda.empty_cache()
     if not a.no_calcphase and rank == 0:
         rec["calcphase"] = calcphase_leg(a, dev)
@@ -391,6 +506,12 @@ def main():
         toa = toa_leg(a, dev, world, rank)
         if rank == 0:
             rec.update(toa)
+    if not a.no_config4:
+        c4 = config4_leg(a, dev, world, rank)
+        if rank == 0:
+            rec["config4"] = c4
+    if not a.no_config2 and rank == 0:
+        rec["config2"] = config2_leg(a)
     if rank == 0:
         print(json.dumps(rec), flush=True)
     if world > 1:

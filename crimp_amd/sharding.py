@@ -7,9 +7,9 @@ ranks, one collective per search.
                        per-trial powers (``gather='all'``, every rank gets the full array) or one
                        ``all_gather`` of each rank's best (power, index) (``gather='best'``);
                        ties resolve to the lowest flat index, as ``np.argmax`` does;
-* ``sharded_toa_fit``  each rank fits a contiguous block of intervals; one ``all_gather`` of the
-                       per-interval result records.
-Photon arrays are replicated (every rank holds all photons; 8 B/photon). The collectives go
+* ``sharded_toa_fit``  each rank fits a contiguous block of intervals, loading only their photons
+                       (``interval_shard``); one ``all_gather`` of the per-interval result records.
+The search's photon arrays are replicated (every rank holds all photons; 8 B/photon). The collectives go
 through ``torch.distributed`` (backend ``nccl`` = RCCL over xGMI on the GPU box; ``gloo`` in the
 CPU tests). ``compute`` hooks let the CPU tests drive the same collective logic without a GPU.
 """
@@ -37,12 +37,12 @@ def _device_for_backend(dist):
     return torch.device("cpu")
 
 
-def _gpu_slice(time, t0, freq, nharm, stat, freq_dot, first, count):
+def _gpu_slice(time, t0, freq, nharm, stat, freq_dot, first, count, flags=0):
     from . import ops
     import torch
     if isinstance(time, torch.Tensor) and freq_dot is not None and not isinstance(freq_dot, torch.Tensor):
         freq_dot = torch.as_tensor(np.asarray(freq_dot, dtype=np.float64), device=time.device)
-    return ops.search(time, t0, freq, nharm, stat, log10_negfdot=freq_dot, first=first, count=count)
+    return ops.search(time, t0, freq, nharm, stat, log10_negfdot=freq_dot, first=first, count=count, flags=flags)
 
 
 def _as_comm(local, dev):
@@ -54,16 +54,18 @@ def _as_comm(local, dev):
     return torch.as_tensor(np.asarray(local), dtype=torch.float64, device=dev)
 
 
-def sharded_search(time, freq, nharm=2, stat=0, freq_dot=None, gather="all", compute=None):
+def sharded_search(time, freq, nharm=2, stat=0, freq_dot=None, gather="all", compute=None, flags=0):
     """Z^2 (stat=0) / H (stat=1) over the fd-outer grid, sharded across the process group.
 
     Returns the full power array (gather='all'; a tensor on the rank's device when ``time`` is a device
     tensor, else a numpy array) or ``(best_power, best_flat_index)`` (gather='best'), identical on every rank.
     With the nccl backend the gather runs on the device buffers the search wrote (no host staging).
+    ``flags`` go to the rank's crimp_search call (e.g. FLAG_TIME_KERNELS for bench.py).
     """
+    import functools
     import torch
     dist, world, rank = _dist()
-    compute = compute or _gpu_slice
+    compute = compute or functools.partial(_gpu_slice, flags=flags)
     as_tensor = isinstance(time, torch.Tensor)
     if as_tensor:
         t0 = float((time[0] + time[-1]).item()) / 2
@@ -109,19 +111,37 @@ def sharded_search(time, freq, nharm=2, stat=0, freq_dot=None, gather="all", com
     return out.cpu().numpy()
 
 
+def interval_shard(offsets, world, rank):
+    """(first interval, interval count, first photon, photon end) of ``rank``'s contiguous block of intervals:
+    the photon range [a, b) is all that rank has to load."""
+    off = np.asarray(offsets, dtype=np.int64)
+    first, count = shard_range(off.size - 1, world, rank)
+    return first, count, int(off[first]), int(off[first + count])
+
+
 def sharded_toa_fit(x, offsets, exposure, tmpl, brutemin=False, ph_shift_res=1000, nbr_bins=15, fitter=None):
-    """Fit interval blocks per rank; one all_gather of (phShi, LL, UL, redChi2, norm, LLmax)."""
+    """Fit interval blocks per rank; one all_gather of (phShi, LL, UL, redChi2, norm, LLmax).
+
+    ``offsets`` (nint + 1, global) and ``exposure`` (nint) describe every interval. ``x`` supplies the photons:
+    the whole concatenated array (host or device; the rank slices out its own range and uploads only that), or a
+    callable ``x(a, b)`` returning photons [a, b) -- e.g. a slice of a memory-mapped file -- so that a rank never
+    holds more than its own intervals' photons (``interval_shard`` gives the range)."""
     import torch
     from .toafit import ToAFitter
     dist, world, rank = _dist()
     off = np.asarray(offsets.cpu() if isinstance(offsets, torch.Tensor) else offsets, dtype=np.int64)
     nint = off.size - 1
-    first, count = shard_range(nint, world, rank)
+    first, count, pa, pb = interval_shard(off, world, rank)
     keys = ("phShi", "phShi_LL", "phShi_UL", "reducedChi2", "norm", "LLmax")
     rec = np.full((shard_range(nint, world, 0)[1], len(keys)), np.nan)
     if count:
         sl = off[first:first + count + 1]
-        xs = x[int(sl[0]):int(sl[-1])] if isinstance(x, torch.Tensor) else np.asarray(x)[sl[0]:sl[-1]]
+        if callable(x):
+            xs = x(pa, pb)
+        elif isinstance(x, torch.Tensor):
+            xs = x[pa:pb]
+        else:
+            xs = np.asarray(x)[pa:pb]
         fit = (fitter or ToAFitter)(xs, sl - sl[0], np.asarray(exposure)[first:first + count], tmpl, ph_shift_res,
                                     nbr_bins)
         r = fit.fit(brutemin=brutemin)

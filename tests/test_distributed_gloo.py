@@ -54,6 +54,17 @@ def _worker(rank, world, port, out_path):
     tmpl = {"model": "fourier", "norm": {"value": 10.0}, "amp_1": {"value": 2.0}, "ph_1": {"value": 0.3},
             "amp_2": {"value": 1.0}, "ph_2": {"value": -1.0}}
     toa = sharded_toa_fit(x, off, E, tmpl, brutemin=True, fitter=_OracleFitter)
+    # per-rank photon loading: the rank asks only for its own intervals' photon range
+    asked = []
+
+    def load(a, b):
+        asked.append((a, b))
+        return x[a:b].copy()
+    toa2 = sharded_toa_fit(load, off, E, tmpl, brutemin=True, fitter=_OracleFitter)
+    from crimp_amd.sharding import interval_shard
+    _, _, pa, pb = interval_shard(off, world, rank)
+    assert asked == [(pa, pb)] and pb - pa < x.size
+    assert np.array_equal(toa2["phShi"], toa["phShi"])
     if rank == 0:
         np.savez(out_path, full=full, best=np.array(best), phShi=toa["phShi"], LL=toa["phShi_LL"])
     dist.barrier()

@@ -72,3 +72,54 @@ def test_two_gloo_ranks_on_gpu_bit_identical_to_unsharded(tmp_path):
     np.testing.assert_array_equal(r["full"], r["ref"])
     assert r["best"][0] == r["refh"].max() and int(r["best"][1]) == int(np.argmax(r["refh"]))
     np.testing.assert_array_equal(r["toa"], r["rtoa"])
+
+
+def _nccl_worker(rank, world, port, out_path):
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    from crimp_amd import ops
+    from crimp_amd.readPPtemplate import readPPtemplate
+    from crimp_amd.sharding import sharded_search, sharded_toa_fit
+    from crimp_amd.synth import pulsed_events, template_intervals_torch
+    from crimp_amd.toafit import ToAFitter
+    t_h = pulsed_events(200_000, 2.0e5, 7.123456789, pulsed_frac=0.05, seed=11)
+    f = torch.as_tensor(7.123456789 + (np.arange(40_000) - 20_000) / 2.0e6, device=dev)
+    fd = np.array([-12.0, -10.5])
+    t = torch.as_tensor(t_h, device=dev)
+    full = sharded_search(t, f, 2, 0, freq_dot=fd, gather="all")
+    best = sharded_search(t, f, 3, 1, freq_dot=fd, gather="best")
+    t0 = float((t[0] + t[-1]).item()) / 2
+    fdd = torch.as_tensor(fd, device=dev)
+    ref = ops.search(t, t0, f, 2, 0, log10_negfdot=fdd)
+    refh = ops.search(t, t0, f, 3, 1, log10_negfdot=fdd).cpu().numpy()
+    tm = readPPtemplate(os.path.join(ROOT, "tests", "golden", "1e2259_template.txt"))
+    K = sum(1 for k in tm if k.startswith("amp_"))
+    x, off, E, _ = template_intervals_torch(5, 20_000, tm["norm"]["value"], [tm["amp_%d" % j]["value"] for j in
+                                            range(1, K + 1)], [tm["ph_%d" % j]["value"] for j in range(1, K + 1)],
+                                            seed=3, device=dev)
+    toa = sharded_toa_fit(x, off, E, tm, brutemin=True)
+    rtoa = ToAFitter(x, off, E, tm).fit(brutemin=True)
+    keys = sorted(toa)
+    np.savez(out_path, full=full.cpu().numpy(), full_is_dev=np.array(full.is_cuda), ref=ref.cpu().numpy(),
+             best=np.array(best, dtype=np.float64), refh=refh, backend=np.array(dist.get_backend()),
+             toa=np.stack([toa[k] for k in keys]), rtoa=np.stack([rtoa[k] for k in keys]))
+    dist.destroy_process_group()
+
+
+def test_nccl_backend_single_rank_on_gpu(tmp_path):
+    """The nccl (RCCL) branch of sharding.py -- collective buffers on the device, the best-trial selection on the
+    device -- executed for real: one rank (RCCL needs one GPU per rank, and this box has one), results equal to
+    the unsharded device search and fits."""
+    out = str(tmp_path / "n.npz")
+    mp.spawn(_nccl_worker, args=(1, _free_port(), out), nprocs=1, join=True)
+    r = np.load(out)
+    assert str(r["backend"]) == "nccl" and bool(r["full_is_dev"])
+    np.testing.assert_array_equal(r["full"], r["ref"])
+    assert r["best"][0] == r["refh"].max() and int(r["best"][1]) == int(np.argmax(r["refh"]))
+    np.testing.assert_array_equal(r["toa"], r["rtoa"])

@@ -1,0 +1,149 @@
+"""The exact search path's per-trial certificate under inputs that correlate its 2^30 roundings, the routing and
+trial-blocking edge cases of crimp_search, and varyAmps bounds per template model.
+
+The exact kernel (csrc/search_exact.h) flags for the fp64 fix-up every trial whose 10-sigma error bound (an
+independent-rounding model: per-term rms 1e-9) cannot place it within 1e-6 relative. These tests hold the model to
+inputs built to break the independence -- photon times on a 1/(4096 f0) lattice (every photon's phase lands on the
+same table cells with zero residual rotation), every photon duplicated, a 90 %-pulsed source -- by comparing every
+trial with the fp64 path (itself ~1e-9 of the reference, tests/test_gpu_parity.py): the default result (fix-up on)
+at plain 1e-6, and the raw kernel (FLAG_NO_FIXUP) at plain 1e-6 on every trial the certificate passed."""
+import math
+import os
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(got, ref):
+    return np.abs(got - ref) / np.abs(ref)
+
+
+def _correlated_inputs():
+    from crimp_amd.synth import pulsed_events
+    f0, n = 7.123456789, 1_000_000
+    base = pulsed_events(n, 1.0e6, f0, pulsed_frac=0.1, seed=21)
+    q = 1.0 / (4096.0 * f0)
+    quant = np.round(base / q) * q                           # times on the table lattice of the fundamental
+    half = pulsed_events(n // 2, 1.0e6, f0, pulsed_frac=0.1, seed=22)
+    dup = np.sort(np.concatenate([half, half]))              # every photon twice
+    strong = pulsed_events(n, 1.0e6, f0, pulsed_frac=0.9, seed=23)
+    return f0, {"quantised": quant, "duplicated": dup, "pulsed90": strong}
+
+
+@pytest.mark.parametrize("nharm,stat", [(2, 0), (20, 1)])
+def test_certificate_holds_on_correlated_inputs(gpu, nharm, stat):
+    import torch
+    from crimp_amd import ops, _native as N
+    f0, inputs = _correlated_inputs()
+    f = torch.as_tensor(f0 + (np.arange(8192) - 4096) / 1.0e7, device=gpu)
+    for name, t_h in inputs.items():
+        t = torch.as_tensor(t_h, device=gpu)
+        t0 = (t_h[0] + t_h[-1]) / 2
+        z = ops.search(t, t0, f, nharm, stat).cpu().numpy()
+        nfix = N.load().crimp_last_fixups()
+        raw = ops.search(t, t0, f, nharm, stat, flags=N.FLAG_NO_FIXUP).cpu().numpy()
+        z64 = ops.search(t, t0, f, nharm, stat, precision="f64").cpu().numpy()
+        e = _rel(z, z64)
+        assert e.max() <= 1e-6, (name, e.max(), int(e.argmax()))
+        flagged = z != raw                                   # the fix-up rewrote exactly the flagged trials
+        assert flagged.sum() <= nfix, (name, flagged.sum(), nfix)
+        er = _rel(raw[~flagged], z64[~flagged])
+        assert er.max() <= 1e-6, (name, "raw kernel on a certified trial", er.max())
+        assert nfix <= 64, (name, nfix)                      # a kernel regression would flag most trials
+        assert int(np.argmax(z)) == int(np.argmax(z64))
+        print("%s m=%d: max rel %.2e (raw certified %.2e), fix-ups %d" % (name, nharm, e.max(), er.max(), nfix))
+
+
+def _run_child(code, env_extra, out):
+    env = dict(os.environ, **env_extra)
+    subprocess.run([sys.executable, "-c", code, out], check=True, env=env, timeout=300)
+    return np.load(out)
+
+
+def test_fold_path_many_ragged_trial_blocks_2d(gpu):
+    """Splits longer than one fold period (CRIMP_EXACT_LONG_SPLITS) over a 2-D grid cut into many trial blocks
+    (CRIMP_SEARCH_BUDGET_MB=1: 8192 trials per block) whose rows (3000 trials: one full tile and a ragged one)
+    start at every offset inside a block: the fold scratch is sized over all blocks and the powers equal the
+    default search's bit for bit (integer sums)."""
+    code = ("import sys, numpy as np; sys.path.insert(0, %r); from crimp_amd import ops, _native as N; "
+            "from crimp_amd.synth import pulsed_events; import torch; "
+            "t_h = pulsed_events(3000000, 1.0e6, 7.123456789, pulsed_frac=0.05, seed=31); "
+            "t = torch.as_tensor(t_h, device='cuda'); t0 = (t_h[0] + t_h[-1]) / 2; "
+            "f = torch.as_tensor(7.123456789 + (np.arange(3000) - 1500) / 1.0e7, device='cuda'); "
+            "fd = torch.as_tensor(np.linspace(-13.0, -11.0, 40), device='cuda'); "
+            "h = ops.search(t, t0, f, 8, 1, log10_negfdot=fd, first=1234, count=100000).cpu().numpy(); "
+            "np.savez(sys.argv[1], h=h)") % (str(__import__("conftest").ROOT))
+    with tempfile.TemporaryDirectory() as d:
+        a = _run_child(code, {}, os.path.join(d, "a.npz"))
+        b = _run_child(code, {"CRIMP_EXACT_LONG_SPLITS": "1", "CRIMP_SEARCH_BUDGET_MB": "1"}, os.path.join(d, "b.npz"))
+    np.testing.assert_array_equal(a["h"], b["h"])
+
+
+def test_short_rows_2d_route_to_fp64(gpu):
+    """A 2-D grid of 2-trial rows (300 rows) would fill 2048-trial tiles with dead columns: it takes the fp64
+    kernel (bit-identical to precision='f64'); 256-trial rows still take the exact kernel."""
+    import torch
+    from crimp_amd import ops
+    from crimp_amd.synth import pulsed_events
+    t_h = pulsed_events(200_000, 2.0e5, 3.3, pulsed_frac=0.05, seed=12)
+    t = torch.as_tensor(t_h, device=gpu)
+    t0 = (t_h[0] + t_h[-1]) / 2
+    fd = torch.as_tensor(np.linspace(-13.0, -10.0, 300), device=gpu)
+    f2 = torch.as_tensor(3.3 + np.arange(2) / 2.0e6, device=gpu)
+    z = ops.search(t, t0, f2, 2, 0, log10_negfdot=fd).cpu().numpy()
+    z64 = ops.search(t, t0, f2, 2, 0, log10_negfdot=fd, precision="f64").cpu().numpy()
+    np.testing.assert_array_equal(z, z64)
+    f256 = torch.as_tensor(3.3 + np.arange(256) / 2.0e6, device=gpu)
+    z = ops.search(t, t0, f256, 2, 0, log10_negfdot=fd[:4]).cpu().numpy()
+    z64 = ops.search(t, t0, f256, 2, 0, log10_negfdot=fd[:4], precision="f64").cpu().numpy()
+    assert not np.array_equal(z, z64) and _rel(z, z64).max() <= 1e-6
+
+
+def _sample_template(tm, n, shift, rng):
+    tarr = O.template_arrays(tm)
+    n0 = tm["norm"]["value"]
+    ymax = 1.05 * O.curve(tarr, n0, shift, np.linspace(0, 2 * np.pi, 20001)).max()
+    out = np.empty(0)
+    while out.size < n:
+        xx = rng.uniform(0, 2 * np.pi, 3 * n)
+        keep = rng.uniform(0, ymax, xx.size) < O.curve(tarr, n0, shift, xx)
+        out = np.concatenate([out, xx[keep]])
+    return out[:n]
+
+
+def test_vary_amps_bounds_per_model(gpu):
+    """varyAmps frees ampShift in [0.01, 100] for Fourier (measureToAs.py:308), [0, inf) for Cauchy (:461) and
+    [0, 500] for von Mises (:605). Photons drawn from a template whose amplitudes are 150x the fitting template's
+    push ampShift to ~150: Cauchy and von Mises fit it freely, Fourier stops at 100. Device fits (k_toa_fit_amp)
+    against the oracle's restatement (parity unpinned beyond the oracle: no reference output uses varyAmps)."""
+    import json
+    from crimp_amd.toafit import ToAFitter
+    from conftest import gpath
+    O.set_threads(min(16, os.cpu_count() or 1))
+    tc = json.load(open(gpath("cauchy_vm_theta.json")))
+    rng = np.random.default_rng(17)
+    n = 10_000
+    for model in ("cauchy", "vonmises"):
+        gen = {"model": model, "norm": {"value": tc["norm"], "vary": True}}
+        fit = {"model": model, "norm": {"value": tc["norm"], "vary": True}}
+        for j in (1, 2):
+            for nm in ("amp", "cen", "wid"):
+                v = tc["%s_%d" % (nm, j)]
+                gen["%s_%d" % (nm, j)] = {"value": v, "vary": True}
+                fit["%s_%d" % (nm, j)] = {"value": v / 150.0 if nm == "amp" else v, "vary": True}
+        x = _sample_template(gen, n, 0.4, rng)
+        rate = tc["norm"] + (tc["amp_1"] + tc["amp_2"]) / (2 * np.pi)
+        E = n / rate
+        r = ToAFitter(x, np.array([0, n], dtype=np.int64), np.array([E]), fit).fit(brutemin=True, vary_amps=True)
+        o = O.fit_toa_vary_amps(x, E, fit, brutemin=True)
+        assert r["ampShift"][0] > 100.0, (model, r["ampShift"][0])
+        assert r["ampShift"][0] == pytest.approx(o["ampShift"], rel=1e-5), model
+        assert abs(r["phShi"][0] - o["phShi"]) / (2 * math.pi) < 1e-6, model
+        assert r["phShi_LL"][0] == o["phShi_LL"] and r["phShi_UL"][0] == o["phShi_UL"], model

@@ -12,8 +12,13 @@ stop_on_fault() {  # rc 0 ok, 1 = test failures (not a fault); anything else: st
     if [ "$rc" -ne 0 ] && [ "$rc" -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit "$rc"; fi
 }
 STEPS=${STEPS:-tests,smoke,bench,prof}
+if [[ $STEPS == *c4w* ]]; then  # config-4 parity windows against the committed oracle values
+  timeout -k 10 300 python -u tools/config4_windows.py > "$OUT/c4w.json" 2> "$OUT/c4w.err"
+  stop_on_fault $? c4w
+  head -c 600 "$OUT/c4w.json"; echo
+fi
 if [[ $STEPS == *tests* ]]; then
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -rs --timeout 120 --timeout-method thread ${PYTEST_ARGS:-} ${PYTEST_K:+-k "$PYTEST_K"} > "$OUT/pytest_gpu.log" 2>&1
+  timeout -k 10 900 python -u -m pytest tests -m gpu ${PYTEST_X--x} -v -rs --durations=15 --timeout 180 --timeout-method thread ${PYTEST_ARGS:-} ${PYTEST_K:+-k "$PYTEST_K"} > "$OUT/pytest_gpu.log" 2>&1
   stop_on_fault $? pytest
   tail -5 "$OUT/pytest_gpu.log"
 fi
