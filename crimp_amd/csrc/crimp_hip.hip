@@ -703,12 +703,14 @@ constexpr int kGridKMax = 8;
 constexpr int kGridProd = 4;
 constexpr int64_t kGridTarget = 16384;  // brute-grid blocks per launch (toa_grid_partials)
 static_assert(kGridNN % 2 == 0 && kGridProd == 4, "norm pairs; photons in two pairs per product");
+constexpr int kGridNNSmall = 4;  // the pruned brute grid's norms per lane (crimp_toa_fit)
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // MODEL and (Fourier) the template size KF are template arguments: registers only for the model's own coefficients,
-// no per-harmonic branches; KF = 0 reads K from the template at run time.
-template <int KMAX, int MODEL, int KF>
+// no per-harmonic branches; KF = 0 reads K from the template at run time. NN (even, <= kGridNN) norms per lane:
+// the device fit evaluates only the norms that can hold each phShift's maximum (crimp_toa_fit), usually 2.
+template <int KMAX, int MODEL, int KF, int NN>
 __global__ __launch_bounds__(kGridBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_toa_grid(const double* __restrict__ x,
                                                          const int64_t* __restrict__ offsets,
                                                          const TplDev* __restrict__ T, const double* __restrict__ norm,
@@ -744,12 +746,12 @@ __global__ __launch_bounds__(kGridBlock) __attribute__((amdgpu_waves_per_eu(4)))
             }
         }
     }
-    f32x2 nr[kGridNN / 2];
+    f32x2 nr[NN / 2];
 #pragma unroll
-    for (int a = 0; a < kGridNN; ++a) nr[a / 2][a % 2] = (a < na) ? (float)norm[iv * nnorm + a0 + a] : 1.0f;
-    double acc[kGridNN];
+    for (int a = 0; a < NN; ++a) nr[a / 2][a % 2] = (a < na) ? (float)norm[iv * nnorm + a0 + a] : 1.0f;
+    double acc[NN];
 #pragma unroll
-    for (int a = 0; a < kGridNN; ++a) acc[a] = 0.0;
+    for (int a = 0; a < NN; ++a) acc[a] = 0.0;
     float hmn = INFINITY;
     const int64_t beg = offsets[iv] + split * chunk;
     const int64_t end = std::min<int64_t>(offsets[iv + 1], beg + chunk);
@@ -818,9 +820,9 @@ __global__ __launch_bounds__(kGridBlock) __attribute__((amdgpu_waves_per_eu(4)))
             return h;
         };
         for (int i0 = 0; i0 < cnt; i0 += 32) {
-            f32x2 pa[kGridNN / 2];
+            f32x2 pa[NN / 2];
 #pragma unroll
-            for (int a = 0; a < kGridNN / 2; ++a) pa[a] = f32x2{0.0f, 0.0f};
+            for (int a = 0; a < NN / 2; ++a) pa[a] = f32x2{0.0f, 0.0f};
             const int i1 = std::min(cnt, i0 + 32);
             int i = i0;
             // log2 of a product of kGridProd model values instead of kGridProd logs (v_log issues at quarter
@@ -830,7 +832,7 @@ __global__ __launch_bounds__(kGridBlock) __attribute__((amdgpu_waves_per_eu(4)))
                 const f32x2 h01 = hval2(i), h23 = hval2(i + 2);
                 hmn = fminf(fminf(fminf(fminf(hmn, h01.x), h01.y), h23.x), h23.y);
 #pragma unroll
-                for (int b = 0; b < kGridNN / 2; ++b) {
+                for (int b = 0; b < NN / 2; ++b) {
                     f32x2 pr = nr[b] + h01.x;
                     pr *= nr[b] + h01.y;
                     pr *= nr[b] + h23.x;
@@ -842,18 +844,18 @@ __global__ __launch_bounds__(kGridBlock) __attribute__((amdgpu_waves_per_eu(4)))
                 const float h = hval(i);
                 hmn = fminf(hmn, h);
 #pragma unroll
-                for (int b = 0; b < kGridNN / 2; ++b) {
+                for (int b = 0; b < NN / 2; ++b) {
                     const f32x2 pr = nr[b] + h;
                     pa[b] += f32x2{__builtin_amdgcn_logf(pr.x), __builtin_amdgcn_logf(pr.y)};
                 }
             }
 #pragma unroll
-            for (int a = 0; a < kGridNN; ++a) acc[a] += (double)pa[a / 2][a % 2];
+            for (int a = 0; a < NN; ++a) acc[a] += (double)pa[a / 2][a % 2];
         }
     }
     if (bphi < nphi) {
 #pragma unroll
-        for (int a = 0; a < kGridNN; ++a)
+        for (int a = 0; a < NN; ++a)
             if (a < na) lnsum[((split * nint + iv) * nnorm + a0 + a) * nphi + bphi] = acc[a];
         if (a0 == 0) hmin[(split * nint + iv) * nphi + bphi] = (double)hmn;
     }
@@ -1598,6 +1600,27 @@ static int make_tpl(const crimp_template* tpl, TplDev* T) {
     return CRIMP_OK;
 }
 
+// Bounds hmin <= h <= hmax of the template part h = model - norm over every phase and phShift
+// (templatemodels.py:64-82, :166-185, :271-290 with TplDev's folded amplitudes)
+static void tpl_bounds(const TplDev& T, double* hmin, double* hmax) {
+    double lo = 0.0, hi = 0.0;
+    for (int j = 0; j < T.K; ++j) {
+        const double a = std::fabs(T.amp[j]);
+        if (T.model == CRIMP_MODEL_FOURIER) {
+            lo -= a;
+            hi += a;
+        } else if (T.model == CRIMP_MODEL_CAUCHY) {  // a / (cosh w - cos u), cos u in [-1, 1]
+            lo += T.amp[j] / (T.ch[j] + 1.0);
+            hi += T.amp[j] / (T.ch[j] - 1.0);
+        } else {                                     // a exp(k cos u)
+            lo += T.amp[j] * std::exp(-T.kap[j]);
+            hi += T.amp[j] * std::exp(T.kap[j]);
+        }
+    }
+    *hmin = std::min(lo, hi);
+    *hmax = std::max(lo, hi);
+}
+
 extern "C" int crimp_toa_points(const double* x, const int64_t* offsets, int64_t nint, const crimp_template* tpl,
                                 const int64_t* pt_interval, const double* pt_norm, const double* pt_phi, int64_t npts,
                                 double* out, uint32_t flags, void* stream) {
@@ -1687,10 +1710,14 @@ static int toa_grid_partials(Scratch& sc, hipStream_t s, const double* dx, const
     HIPCHK(sc.alloc(pl, (size_t)(splits * nint * nnorm * nphi)));
     HIPCHK(sc.alloc(ph, (size_t)(splits * nint * nphi)));
     dim3 grid((unsigned)pblocks, (unsigned)nint, (unsigned)splits);
-    for (int64_t a0 = 0; a0 < nnorm; a0 += kGridNN) {
-        const int na = (int)std::min<int64_t>(kGridNN, nnorm - a0);
-#define CRIMP_LG(MD, KK) k_toa_grid<kGridKMax, MD, KK><<<grid, kGridBlock, 0, s>>>(dx, doff, dT, dnrm, (int)nnorm, (int)a0, \
-                                                                                na, dphi, (int)nphi, chunk, (int)nint, *pl, *ph)
+    // norms per lane: 2 or kGridNNSmall for a pruned grid (crimp_toa_fit), otherwise kGridNN per launch
+    const int nn = nnorm <= 2 ? 2 : nnorm <= kGridNNSmall ? kGridNNSmall : kGridNN;
+    for (int64_t a0 = 0; a0 < nnorm; a0 += nn) {
+        const int na = (int)std::min<int64_t>(nn, nnorm - a0);
+#define CRIMP_LG1(MD, KK, NNV) k_toa_grid<kGridKMax, MD, KK, NNV><<<grid, kGridBlock, 0, s>>>(dx, doff, dT, dnrm, (int)nnorm, \
+                                                                                (int)a0, na, dphi, (int)nphi, chunk, (int)nint, *pl, *ph)
+#define CRIMP_LG(MD, KK) do { if (nn == 2) CRIMP_LG1(MD, KK, 2); else if (nn == kGridNNSmall) CRIMP_LG1(MD, KK, kGridNNSmall); \
+                              else CRIMP_LG1(MD, KK, kGridNN); } while (0)
         if (model == CRIMP_MODEL_FOURIER) {
             switch (K) {
                 case 1: CRIMP_LG(CRIMP_MODEL_FOURIER, 1); break;
@@ -1708,6 +1735,7 @@ static int toa_grid_partials(Scratch& sc, hipStream_t s, const double* dx, const
             CRIMP_LG(CRIMP_MODEL_VONMISES, 0);
         }
 #undef CRIMP_LG
+#undef CRIMP_LG1
         HIPCHK(hipGetLastError());
     }
     *splits_out = splits;
@@ -1776,14 +1804,57 @@ extern "C" int crimp_toa_fit(const double* x, const int64_t* offsets, int64_t ni
             const int64_t nn = 20;
             hphi.resize((size_t)nphi);
             for (int64_t k = 0; k < nphi; ++k) hphi[(size_t)k] = (double)k * 0.05 + (-C.pb);
-            hnrm.resize((size_t)(nint * nn));
-            for (int64_t a = 0; a < nn; ++a) hnrm[(size_t)a] = (double)a * ((C.hi - C.lo) / (double)(nn - 1)) + C.lo;
-            for (int64_t i = 1; i < nint; ++i) std::memcpy(&hnrm[(size_t)(i * nn)], &hnrm[0], nn * sizeof(double));
+            std::vector<double> grid_n((size_t)nn);
+            for (int64_t a = 0; a < nn; ++a) grid_n[(size_t)a] = (double)a * ((C.hi - C.lo) / (double)(nn - 1)) + C.lo;
+            // Pruned norm axis. At fixed phShift the extended LL is -nE + sum_i ln(n + h_i) + const (every model:
+            // templatemodels.py:109-121, :213-226, :318-329), strictly concave in n, with its maximum n* where
+            // sum_i 1/(n* + h_i) = E, so n* lies in [N/E - hmax, N/E - hmin] for any bounds hmin <= h_i <= hmax. The
+            // lattice maximum over the norms at that phShift is then at one of the grid norms adjacent to that
+            // interval: every other grid norm is strictly lower (a whole grid step, ~26 norm units, from a
+            // bracketing one), so the brute grid's argmax (lmfit brute, measureToAs.py:292-295) is found among them.
+            // Config 5 and the worked example: 2 of the 20 norms.
+            double hlo = 0.0, hhi = 0.0;
+            tpl_bounds(T, &hlo, &hhi);
+            std::vector<double> hexp((size_t)nint);
+            if (dev) {
+                HIPCHK(d2h(s, hexp.data(), exposure, nint * sizeof(double)));
+                HIPCHK(hipStreamSynchronize(s));
+            } else {
+                std::memcpy(hexp.data(), exposure, nint * sizeof(double));
+            }
+            std::vector<int64_t> alo((size_t)nint), acnt((size_t)nint);
+            int64_t ncand = 1;
+            for (int64_t i = 0; i < nint; ++i) {
+                const double r = (double)(hoff[i + 1] - hoff[i]) / hexp[(size_t)i];
+                const double lo_n = r - hhi, hi_n = r - hlo, eps = 1e-9 * (1.0 + std::fabs(r) + hhi - hlo);
+                int64_t a0 = 0, a1 = nn - 1;
+                if (std::isfinite(lo_n) && std::isfinite(hi_n) && hexp[(size_t)i] > 0.0) {
+                    while (a0 + 1 < nn && grid_n[(size_t)(a0 + 1)] <= lo_n - eps) ++a0;
+                    while (a1 > a0 && grid_n[(size_t)(a1 - 1)] >= hi_n + eps) --a1;
+                }
+                alo[(size_t)i] = a0;
+                acnt[(size_t)i] = a1 - a0 + 1;
+                ncand = std::max(ncand, a1 - a0 + 1);
+            }
+            if (ncand > kGridNNSmall || getenv("CRIMP_TOA_FULL_GRID")) {  // (test hook: evaluate all 20 norms)
+                for (int64_t i = 0; i < nint; ++i) {
+                    alo[(size_t)i] = 0;
+                    acnt[(size_t)i] = nn;
+                }
+                ncand = nn;
+            }
+            // compacted per-interval norms: the candidates in grid order, padded by repeating the last (a repeat
+            // comes later in norm-outer order, so it never wins a tie)
+            const int64_t nc = ncand <= 2 ? 2 : ncand <= kGridNNSmall ? kGridNNSmall : ncand;
+            hnrm.resize((size_t)(nint * nc));
+            for (int64_t i = 0; i < nint; ++i)
+                for (int64_t c = 0; c < nc; ++c)
+                    hnrm[(size_t)(i * nc + c)] = grid_n[(size_t)(alo[(size_t)i] + std::min(c, acnt[(size_t)i] - 1))];
             double *dphi = nullptr, *dnrm = nullptr;
             HIPCHK(sc.alloc(&dphi, (size_t)nphi));
-            HIPCHK(sc.alloc(&dnrm, (size_t)(nint * nn)));
+            HIPCHK(sc.alloc(&dnrm, (size_t)(nint * nc)));
             HIPCHK(h2d(dphi, hphi.data(), nphi * sizeof(double)));
-            HIPCHK(h2d(dnrm, hnrm.data(), nint * nn * sizeof(double)));
+            HIPCHK(h2d(dnrm, hnrm.data(), nint * nc * sizeof(double)));
             KernelTimer kg(s, flags & CRIMP_FLAG_TIME_KERNELS);  // brute grid: k_toa_grid + k_toa_grid_best
             kg.start();
             for (int64_t i0 = 0; i0 < nint; i0 += 65535) {
@@ -1792,12 +1863,12 @@ extern "C" int crimp_toa_fit(const double* x, const int64_t* offsets, int64_t ni
                 for (int64_t i = i0; i < i0 + nb; ++i) maxn = std::max(maxn, hoff[i + 1] - hoff[i]);
                 double *pl = nullptr, *ph = nullptr;
                 int64_t splits = 0;
-                rc = toa_grid_partials(sc, s, dx, doff + i0, dT, T.model, T.K, dnrm + i0 * nn, nn, dphi, nphi, nb, maxn, &pl, &ph,
+                rc = toa_grid_partials(sc, s, dx, doff + i0, dT, T.model, T.K, dnrm + i0 * nc, nc, dphi, nphi, nb, maxn, &pl, &ph,
                                        &splits);
                 if (rc) return rc;
-                k_toa_grid_best<<<(unsigned)nb, 256, 0, s>>>(pl, ph, dnrm + i0 * nn, dphi, doff + i0, de + i0, (int)nn,
+                k_toa_grid_best<<<(unsigned)nb, 256, 0, s>>>(pl, ph, dnrm + i0 * nc, dphi, doff + i0, de + i0, (int)nc,
                                                             (int)nphi, (int)nb, (int)splits, T.model, C.sum_amp,
-                                                            dstart + 2 * i0);
+                                                            grid_n[0], dstart + 2 * i0);
                 HIPCHK(hipGetLastError());
             }
             kg.stop();

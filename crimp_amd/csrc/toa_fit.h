@@ -490,12 +490,13 @@ __global__ __launch_bounds__(kFitBlock) void k_toa_fit(const double* __restrict_
 
 // lmfit brute maximum per interval from k_toa_grid's per-split partial sums (toafit.brute): splits combined in
 // a fixed order, the reference LL formed for every (norm, phShift) lattice point, -inf where the model is not
-// positive, first maximum in norm-outer order (scipy.optimize.brute / np.argmax).
+// positive, first maximum in norm-outer order (scipy.optimize.brute / np.argmax). ``norm`` holds each interval's
+// candidate norms (a contiguous run of the grid, in grid order: crimp_toa_fit's pruning), so the order is kept.
 __global__ __launch_bounds__(256) void k_toa_grid_best(const double* __restrict__ pl, const double* __restrict__ ph,
                                                        const double* __restrict__ norm, const double* __restrict__ phi,
                                                        const int64_t* __restrict__ offsets,
                                                        const double* __restrict__ expo, int nnorm, int nphi, int nint,
-                                                       int splits, int model, double sum_amp,
+                                                       int splits, int model, double sum_amp, double norm_first,
                                                        double* __restrict__ start) {
     __shared__ double bv[4];
     __shared__ int bi[4];
@@ -546,8 +547,12 @@ __global__ __launch_bounds__(256) void k_toa_grid_best(const double* __restrict_
                 best = bv[ww];
                 bidx = bi[ww];
             }
-        if (bidx == 0x7fffffff) bidx = 0;
-        start[2 * iv] = norm[iv * nnorm + bidx / nphi];
-        start[2 * iv + 1] = phi[bidx % nphi];
+        if (bidx == 0x7fffffff) {  // no finite point: the full lattice's first point (norm_first, phi[0])
+            start[2 * iv] = norm_first;
+            start[2 * iv + 1] = phi[0];
+        } else {
+            start[2 * iv] = norm[iv * nnorm + bidx / nphi];
+            start[2 * iv + 1] = phi[bidx % nphi];
+        }
     }
 }

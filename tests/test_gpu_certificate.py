@@ -147,3 +147,37 @@ def test_vary_amps_bounds_per_model(gpu):
         assert r["ampShift"][0] == pytest.approx(o["ampShift"], rel=1e-5), model
         assert abs(r["phShi"][0] - o["phShi"]) / (2 * math.pi) < 1e-6, model
         assert r["phShi_LL"][0] == o["phShi_LL"] and r["phShi_UL"][0] == o["phShi_UL"], model
+
+
+def test_pruned_brute_grid_equals_full_grid(gpu):
+    """crimp_toa_fit evaluates only the brute-grid norms that can hold a phShift's maximum (the extended LL is
+    strictly concave in norm). The fits must equal, bit for bit, the fits that evaluate all 20
+    norms of lmfit's grid (CRIMP_TOA_FULL_GRID test hook; read per call, so one process runs both): config-5-style
+    Fourier intervals and the Cauchy / von Mises templates, the device records compared whole."""
+    import json
+    from crimp_amd.synth import template_intervals_torch
+    from crimp_amd.toafit import ToAFitter
+    from conftest import gpath
+    from bench import T2259, _tmpl
+    x, off, E, _ = template_intervals_torch(300, 100_000, T2259["norm"]["value"], T2259["amp"], T2259["ph"], seed=5,
+                                            device=gpu)
+    cases = [(x, off, E, _tmpl())]
+    tc = json.load(open(gpath("cauchy_vm_theta.json")))
+    rng = np.random.default_rng(3)
+    for model in ("cauchy", "vonmises"):
+        tm = {"model": model, "norm": {"value": tc["norm"], "vary": True}}
+        for j in (1, 2):
+            for nm in ("amp", "cen", "wid"):
+                tm["%s_%d" % (nm, j)] = {"value": tc["%s_%d" % (nm, j)], "vary": True}
+        xs = [_sample_template(tm, 20_000, s, rng) for s in (0.3, -2.0, 3.5, 1.0)]
+        rate = tc["norm"] + (tc["amp_1"] + tc["amp_2"]) / (2 * np.pi)
+        cases.append((np.concatenate(xs), np.arange(5, dtype=np.int64) * 20_000, np.full(4, 20_000 / rate), tm))
+    for xx, oo, ee, tm in cases:
+        a = ToAFitter(xx, oo, ee, tm).fit(brutemin=True)
+        os.environ["CRIMP_TOA_FULL_GRID"] = "1"
+        try:
+            b = ToAFitter(xx, oo, ee, tm).fit(brutemin=True)
+        finally:
+            del os.environ["CRIMP_TOA_FULL_GRID"]
+        for k in ("phShi", "phShi_LL", "phShi_UL", "reducedChi2", "norm", "LLmax"):
+            np.testing.assert_array_equal(a[k], b[k], err_msg="%s %s" % (tm["model"], k))
