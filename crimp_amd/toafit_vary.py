@@ -18,10 +18,15 @@ ampShift (a common factor on every template amplitude) is freed from 1 within it
 maximised again; the 1-sigma scan then re-maximises ampShift too, and redChi2 counts one more free parameter.
 The parameter vector is then [norm, template..., ampShift, phShift].
 
-Deviation: with ``brutemin`` the reference hands every free parameter to lmfit's brute grid (20
-points per bounded parameter without a ``brute_step``: 20^k x 126 evaluations). Here the brute start
-is the (norm, phShift) grid of the default path with the template's shape, then the full local
-maximisation.
+``brutemin`` (:292-295): lmfit's brute over every free parameter -- 20 points on [min, max] for each bounded
+parameter without a ``brute_step`` (norm, amp_k, ph_k, wid_k), steps of 0.05 for cen_k and phShift -- and its first
+maximum in C order of the parameters (norm, template parameters in insertion order, phShift). Each template of the
+lattice is one device brute-grid launch (``crimp_toa_grid``: every norm x phShift of every interval), so up to
+``BRUTE_MAX_TEMPLATE_PARAMS`` = 2 freed template parameters (<= 625 templates) are covered exactly; with more the
+start is the (norm, phShift) lattice at the template's values (a documented deviation). Lattice points whose LL is
+not finite (a von Mises width of 0) are skipped. Parity unpinned: lmfit (absent) aborts brute after
+max_nfev = 1e4 evaluations (:294), which any lattice with a freed template parameter exceeds, and the point it then
+hands to Nelder-Mead depends on the lmfit version; the oracle restates the lattice maximum (oracle.readvary_brute).
 """
 import math
 
@@ -29,10 +34,21 @@ import numpy as np
 
 from . import ops
 from . import _native as N
+from ._native import _is_torch
+from .toafit import CHI2_1SIG_1DOF, TWO_PI, ToAFitter
 
 # ampShift bounds when varyAmps frees it: measureToAs.py:308 (Fourier), :461 (Cauchy), :605 (von Mises)
 AMP_SHIFT_BOUNDS = {"fourier": (0.01, 100.0), "cauchy": (0.0, math.inf), "vonmises": (0.0, 500.0)}
-from .toafit import CHI2_1SIG_1DOF, TWO_PI, ToAFitter
+BRUTE_MAX_TEMPLATE_PARAMS = 2   # freed template parameters the full brute lattice covers (20^k templates)
+
+
+def mgrid_axis(lo, hi, step=None, ns=20):
+    """One axis of lmfit's brute lattice as scipy.optimize.brute builds it with np.mgrid: ``slice(lo, hi, step)``
+    (arange semantics, hi excluded) for a parameter with a ``brute_step``, ``slice(lo, hi, complex(Ns))`` (Ns
+    points, both bounds included) otherwise (lmfit Minimizer.brute, Ns = 20)."""
+    if step is None:
+        return np.mgrid[slice(lo, hi, complex(ns))]
+    return np.mgrid[slice(lo, hi, step)]
 
 
 class VaryParamFitter(ToAFitter):
@@ -232,17 +248,64 @@ class VaryParamFitter(ToAFitter):
         th[:, idx] = Z
         return th, F
 
+    def brute_lattice(self):
+        """Start vectors [nint, len(theta)] from lmfit's brute lattice over every free parameter (module docstring),
+        or None when more than BRUTE_MAX_TEMPLATE_PARAMS template parameters are free."""
+        import itertools
+        names, th0 = self.names, self.theta0
+        tp = [i for i in range(1, len(names) - 1) if self.vary[i] and names[i] != "ampShift"]
+        if len(tp) > BRUTE_MAX_TEMPLATE_PARAMS:
+            return None
+        axes = [mgrid_axis(self.blo[i], self.bhi[i], 0.05 if names[i].startswith("cen_") else None) for i in tp]
+        norms = mgrid_axis(self.blo[0], self.bhi[0]) if self.vary[0] else np.array([th0[0]])
+        phis = mgrid_axis(-self.pb, self.pb, 0.05)
+        combos = list(itertools.product(*axes))
+        nn, nc, nphi = norms.size, len(combos), phis.size
+        ll = np.full((self.nint, nn, nc, nphi), -np.inf)
+        Np, E = self.N[:, None, None], self.E[:, None, None]
+        nv = norms[None, :, None]
+        step = 2 if self.model == "fourier" else 3
+        for c, combo in enumerate(combos):
+            th = th0.copy()
+            th[tp] = combo
+            if self.model == "vonmises" and np.any(th[3:3 + 3 * self.K:3] <= 0):
+                continue                      # width 0: I0(1/w^2) overflows, the reference's LL is NaN there
+            tpl, amps, _ = self._template(th)
+            ln, hmin = ops.toa_grid(self.x, self.offsets, tpl, self._arr(np.tile(norms, (self.nint, 1)), np.float64),
+                                    self._arr(phis, np.float64))
+            if _is_torch(ln):
+                ln, hmin = ln.cpu().numpy(), hmin.cpu().numpy()
+            with np.errstate(divide="ignore", invalid="ignore", over="ignore"):
+                if self.model == "fourier":
+                    v = -nv * E + Np * np.log(nv * E) + (ln - Np * np.log(nv))
+                else:
+                    F = TWO_PI * nv + float(np.sum(th[1:1 + step * self.K:step]))
+                    v = -F * E / TWO_PI + Np * np.log(F * E / TWO_PI) + (ln - Np * np.log(F))
+                valid = (hmin[:, None, :] + nv) > 0
+            ll[:, :, c, :] = np.where(valid & np.isfinite(v), v, -np.inf)
+        flat = ll.reshape(self.nint, -1)
+        idx = np.argmax(flat, axis=1)                                 # first maximum in C order (np.argmin of -LL)
+        a, c, b = np.unravel_index(idx, (nn, nc, nphi))
+        starts = np.tile(th0, (self.nint, 1))
+        starts[:, 0] = norms[a]
+        for i in range(self.nint):
+            starts[i, tp] = combos[c[i]]
+        starts[:, -1] = phis[b]
+        return starts
+
     def fit(self, brutemin=False):
         if self.vary_amps:  # ampShift is fixed at 1 for the first fit
             self.vary[-2] = False
         self.nfree = int(self.vary[:-1].sum())
-        if brutemin:
-            n0, p0 = self.brute()
-        else:
-            n0, p0 = np.full(self.nint, self.norm0), np.zeros(self.nint)
-        starts = np.tile(self.theta0, (self.nint, 1))
-        starts[:, 0] = np.clip(n0, self.blo[0], self.bhi[0])
-        starts[:, -1] = p0
+        starts = self.brute_lattice() if brutemin else None
+        if starts is None:
+            if brutemin:    # more free template parameters than the lattice covers: the (norm, phShift) lattice
+                n0, p0 = self.brute()
+            else:
+                n0, p0 = np.full(self.nint, self.norm0), np.zeros(self.nint)
+            starts = np.tile(self.theta0, (self.nint, 1))
+            starts[:, 0] = np.clip(n0, self.blo[0], self.bhi[0])
+            starts[:, -1] = p0
         theta_hat, ll_max = self._maximise_batch(np.arange(self.nint), starts, self.vary)
         if self.vary_amps:  # measureToAs.py:306-312: free ampShift from 1 and refit everything free
             self.vary[-2] = True

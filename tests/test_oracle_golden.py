@@ -105,3 +105,19 @@ def test_oracle_clean_under_address_sanitizer():
     assert r.returncode == 0, r.stdout + r.stderr
     assert "ran clean" in r.stdout
     assert "ERROR: AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr
+
+
+def test_brute_lattice_axes_follow_mgrid():
+    """lmfit's brute lattice axes (scipy.optimize.brute through np.mgrid): 20 points with both bounds for a bounded
+    parameter without a brute_step, arange semantics for phShift / cen_k (brute_step 0.05); the product's size for
+    the default Fourier fit is measureToAs.py's 126 x 20."""
+    from crimp_amd.toafit_vary import mgrid_axis
+    import math
+    a = O.mgrid_axis(-math.pi, math.pi, 0.05)
+    assert a.size == 126 and a[0] == -math.pi and a[-1] < math.pi
+    b = O.mgrid_axis(0.0, 1000.0)
+    assert b.size == 20 and b[0] == 0.0 and abs(b[-1] - 1000.0) < 1e-9   # mgrid: 999.9999999999999
+    c = O.mgrid_axis(1.0 - 0.6, 1.0 + 0.6, 0.05)
+    np.testing.assert_array_equal(c, np.arange(c.size) * 0.05 + 0.4)
+    for args in ((-math.pi, math.pi, 0.05), (0.0, 1000.0), (0.4, 1.6, 0.05), (-1.5 * math.pi, 1.5 * math.pi, 0.05)):
+        np.testing.assert_array_equal(mgrid_axis(*args), O.mgrid_axis(*args))
