@@ -118,6 +118,6 @@ def test_brute_lattice_axes_follow_mgrid():
     b = O.mgrid_axis(0.0, 1000.0)
     assert b.size == 20 and b[0] == 0.0 and abs(b[-1] - 1000.0) < 1e-9   # mgrid: 999.9999999999999
     c = O.mgrid_axis(1.0 - 0.6, 1.0 + 0.6, 0.05)
-    np.testing.assert_array_equal(c, np.arange(c.size) * 0.05 + 0.4)
+    assert c.size == 25 and np.allclose(c, np.arange(c.size) * 0.05 + 0.4, rtol=0, atol=1e-15)
     for args in ((-math.pi, math.pi, 0.05), (0.0, 1000.0), (0.4, 1.6, 0.05), (-1.5 * math.pi, 1.5 * math.pi, 0.05)):
         np.testing.assert_array_equal(mgrid_axis(*args), O.mgrid_axis(*args))
