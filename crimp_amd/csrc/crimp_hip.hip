@@ -569,6 +569,35 @@ __device__ __forceinline__ void photon_sincos(int model, double xv, double& s1, 
         sincos(xv, &s1, &c1);
 }
 
+// The same sin/cos from a 4096-entry fp64 table in LDS (k_toa_points and the fit kernels; CRIMP_FIT_TABLE=0 keeps
+// the library sincospi / sincos): r = x in turns (x / 2 pi for radians), k = rint(4096 r), delta = 2 pi (r - k / 4096)
+// (the subtraction is exact), |delta| <= pi / 4096, cos/sin(delta) by their Taylor series to delta^4 / delta^5
+// (truncation < 3e-22), rotated by the table entry: ~2 ulp, against ~30 fp64 operations of the library call.
+#ifndef CRIMP_FIT_TABLE
+#define CRIMP_FIT_TABLE 1
+#endif
+constexpr int kSinTab = 4096;
+__device__ __forceinline__ void sintab_fill(double2* tab) {
+    for (int i = threadIdx.x; i < kSinTab; i += blockDim.x) {
+        double sv, cv;
+        sincospi((double)i * (2.0 / kSinTab), &sv, &cv);
+        tab[i] = make_double2(cv, sv);
+    }
+    __syncthreads();
+}
+__device__ __forceinline__ void photon_sincos_tab(int model, const double2* __restrict__ tab, double xv, double& s1,
+                                                  double& c1) {
+    const double r = (model == CRIMP_MODEL_FOURIER) ? xv : xv * 0.15915494309189533577;
+    const double k = rint(r * (double)kSinTab);
+    const double d = fma(-k, 1.0 / kSinTab, r) * 6.283185307179586476925;
+    const double d2 = d * d;
+    const double cd = fma(d2, fma(d2, 1.0 / 24.0, -0.5), 1.0);
+    const double sd = d * fma(d2, fma(d2, 1.0 / 120.0, -1.0 / 6.0), 1.0);
+    const double2 e = tab[(int)(int64_t)k & (kSinTab - 1)];
+    s1 = fma(e.y, cd, e.x * sd);
+    c1 = fma(e.x, cd, -(e.y * sd));
+}
+
 // h = model - norm at one photon and its first two phShift derivatives h1, h2 (templatemodels.py:64-82,
 // :166-185, :271-290), from the photon's (s1, c1) and one point's coefficient rows c0[], cs[].
 __device__ __forceinline__ void tpl_terms(const TplDev* __restrict__ T, int model, int K, const double* c0,
@@ -627,6 +656,10 @@ __global__ __launch_bounds__(kPtsBlock) void k_toa_points(const double* __restri
                                                           const double* __restrict__ pt_phi, double* __restrict__ out) {
     __shared__ double coef[kPtsPerGroup][2][CRIMP_MAX_COMP];
     __shared__ double red[kPtsBlock / 64][kPtsPerGroup][8];
+#if CRIMP_FIT_TABLE
+    __shared__ double2 stab[kSinTab];
+    sintab_fill(stab);
+#endif
     const int gi = blockIdx.x;
     const int64_t iv = grp_int[gi];
     const int64_t p0 = grp_first[gi];
@@ -652,7 +685,11 @@ __global__ __launch_bounds__(kPtsBlock) void k_toa_points(const double* __restri
     const int64_t a = offsets[iv], b = offsets[iv + 1];
     for (int64_t i = a + tid; i < b; i += kPtsBlock) {
         double s1, c1;
+#if CRIMP_FIT_TABLE
+        photon_sincos_tab(model, stab, x[i], s1, c1);
+#else
         photon_sincos(model, x[i], s1, c1);
+#endif
 #pragma unroll
         for (int p = 0; p < kPtsPerGroup; ++p) {
             if (p >= np) break;
@@ -704,94 +741,121 @@ constexpr int kGridProd = 4;
 constexpr int64_t kGridTarget = 16384;  // brute-grid blocks per launch (toa_grid_partials)
 static_assert(kGridNN % 2 == 0 && kGridProd == 4, "norm pairs; photons in two pairs per product");
 constexpr int kGridNNSmall = 4;  // the pruned brute grid's norms per lane (crimp_toa_fit)
+#ifndef CRIMP_GRID_PPL
+#define CRIMP_GRID_PPL 2
+#endif
+constexpr int kGridPPL = CRIMP_GRID_PPL;  // phShift values per lane of the pruned grid (k_toa_grid)
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // MODEL and (Fourier) the template size KF are template arguments: registers only for the model's own coefficients,
 // no per-harmonic branches; KF = 0 reads K from the template at run time. NN (even, <= kGridNN) norms per lane:
 // the device fit evaluates only the norms that can hold each phShift's maximum (crimp_toa_fit), usually 2.
-template <int KMAX, int MODEL, int KF, int NN>
+// PPL phShift values per lane (1 or 2; the block has kGridBlock / PPL threads and always covers kGridBlock phShift
+// values): with 2, every broadcast basis read feeds twice the FMAs. Each (phShift, norm) sum is formed in the same
+// operation order whatever PPL, so the sums are bit-identical.
+template <int KMAX, int MODEL, int KF, int NN, int PPL>
 __global__ __launch_bounds__(kGridBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_toa_grid(const double* __restrict__ x,
                                                          const int64_t* __restrict__ offsets,
                                                          const TplDev* __restrict__ T, const double* __restrict__ norm,
                                                          int nnorm, int a0, int na, const double* __restrict__ phi,
                                                          int nphi, int64_t chunk, int nint,
                                                          double* __restrict__ lnsum, double* __restrict__ hmin) {
-    // basis[2j (+1)][photon]: cos / sin of harmonic j+1 (Fourier) or of the phase (j = 0, other models);
-    // photons i, i+1 adjacent so that one 8-byte broadcast read gives a photon pair.
-    __shared__ __attribute__((aligned(16))) float basis[2 * KMAX][kGridBlock];
+    constexpr int TB = kGridBlock / PPL;  // threads per block
+    // bas[pair][2j (+1)] = {photon 2 pair, photon 2 pair + 1}: cos / sin of harmonic j+1 (Fourier) or of the phase
+    // (j = 0, other models). A photon pair's whole basis is 16 K contiguous bytes, read by broadcast ds_read_b128
+    // (cos and sin of one harmonic for both photons) at immediate offsets from one address per pair.
+    __shared__ __attribute__((aligned(16))) f32x2 bas[kGridBlock / 2][2 * KMAX];
+    float* const basf = reinterpret_cast<float*>(&bas[0][0]);
+    auto bset = [&](int photon, int row, float v) { basf[((photon >> 1) * 2 * KMAX + row) * 2 + (photon & 1)] = v; };
+    auto bget = [&](int photon, int row) { return basf[((photon >> 1) * 2 * KMAX + row) * 2 + (photon & 1)]; };
     const int tid = threadIdx.x;
-    const int bphi = blockIdx.x * kGridBlock + tid;
     const int64_t iv = blockIdx.y;
     const int64_t split = blockIdx.z;
     constexpr int model = MODEL;
     const int K = KF > 0 ? KF : T->K;
-    const double ph = phi[bphi < nphi ? bphi : nphi - 1];
-    float ca[KMAX], cb[KMAX], amp[KMAX], chj[KMAX], kpj[KMAX];
+    int bphi[PPL];
+    float ca[PPL][KMAX], cb[PPL][KMAX], amp[KMAX], chj[KMAX], kpj[KMAX];
 #pragma unroll
-    for (int j = 0; j < KMAX; ++j) {
-        ca[j] = cb[j] = amp[j] = chj[j] = kpj[j] = 0.0f;
-        if (j < K) {
-            if (model == CRIMP_MODEL_FOURIER) {
-                const double d = T->loc[j] - (double)(j + 1) * ph;
-                ca[j] = (float)(T->amp[j] * cos(d));
-                cb[j] = (float)(-T->amp[j] * sin(d));
-            } else {
-                const double d = T->loc[j] + ph;
-                ca[j] = (float)cos(d);
-                cb[j] = (float)sin(d);
-                amp[j] = (float)T->amp[j];
-                chj[j] = (float)T->ch[j];
-                kpj[j] = (float)(T->kap[j] * 1.4426950408889634);  // exp(k*cu) = exp2(k*log2e*cu)
+    for (int p = 0; p < PPL; ++p) {
+        bphi[p] = blockIdx.x * kGridBlock + p * TB + tid;
+        const double ph = phi[bphi[p] < nphi ? bphi[p] : nphi - 1];
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j) {
+            ca[p][j] = cb[p][j] = 0.0f;
+            if (p == 0) amp[j] = chj[j] = kpj[j] = 0.0f;
+            if (j < K) {
+                if (model == CRIMP_MODEL_FOURIER) {
+                    const double d = T->loc[j] - (double)(j + 1) * ph;
+                    ca[p][j] = (float)(T->amp[j] * cos(d));
+                    cb[p][j] = (float)(-T->amp[j] * sin(d));
+                } else {
+                    const double d = T->loc[j] + ph;
+                    ca[p][j] = (float)cos(d);
+                    cb[p][j] = (float)sin(d);
+                    if (p == 0) {
+                        amp[j] = (float)T->amp[j];
+                        chj[j] = (float)T->ch[j];
+                        kpj[j] = (float)(T->kap[j] * 1.4426950408889634);  // exp(k*cu) = exp2(k*log2e*cu)
+                    }
+                }
             }
         }
     }
     f32x2 nr[NN / 2];
 #pragma unroll
     for (int a = 0; a < NN; ++a) nr[a / 2][a % 2] = (a < na) ? (float)norm[iv * nnorm + a0 + a] : 1.0f;
-    double acc[NN];
+    double acc[PPL][NN];
+    float hmn[PPL];
 #pragma unroll
-    for (int a = 0; a < NN; ++a) acc[a] = 0.0;
-    float hmn = INFINITY;
+    for (int p = 0; p < PPL; ++p) {
+        hmn[p] = INFINITY;
+#pragma unroll
+        for (int a = 0; a < NN; ++a) acc[p][a] = 0.0;
+    }
     const int64_t beg = offsets[iv] + split * chunk;
     const int64_t end = std::min<int64_t>(offsets[iv + 1], beg + chunk);
     for (int64_t base = beg; base < end; base += kGridBlock) {
         const int cnt = (int)std::min<int64_t>(kGridBlock, end - base);
         __syncthreads();
-        if (tid < cnt) {
-            const double xv = x[base + tid];
-            double rv = (model == CRIMP_MODEL_FOURIER) ? xv : xv * 0.15915494309189533577;  // cycles
-            rv -= rint(rv);
-            float s1, c1;
-            sincos_rev_poly((float)rv, s1, c1);
-            if (model == CRIMP_MODEL_FOURIER) {
-                float cj = c1, sj = s1;
 #pragma unroll
-                for (int j = 0; j < KMAX; ++j) {
-                    basis[2 * j][tid] = cj;
-                    basis[2 * j + 1][tid] = sj;
-                    const float cn = __builtin_fmaf(cj, c1, -sj * s1);
-                    sj = __builtin_fmaf(sj, c1, cj * s1);
-                    cj = cn;
+        for (int q = 0; q < PPL; ++q) {
+            const int ph_i = tid + q * TB;  // photon of the tile this thread fills
+            if (ph_i < cnt) {
+                const double xv = x[base + ph_i];
+                double rv = (model == CRIMP_MODEL_FOURIER) ? xv : xv * 0.15915494309189533577;  // cycles
+                rv -= rint(rv);
+                float s1, c1;
+                sincos_rev_poly((float)rv, s1, c1);
+                if (model == CRIMP_MODEL_FOURIER) {
+                    float cj = c1, sj = s1;
+#pragma unroll
+                    for (int j = 0; j < KMAX; ++j) {
+                        bset(ph_i, 2 * j, cj);
+                        bset(ph_i, 2 * j + 1, sj);
+                        const float cn = __builtin_fmaf(cj, c1, -sj * s1);
+                        sj = __builtin_fmaf(sj, c1, cj * s1);
+                        cj = cn;
+                    }
+                } else {
+                    bset(ph_i, 0, c1);
+                    bset(ph_i, 1, s1);
                 }
-            } else {
-                basis[0][tid] = c1;
-                basis[1][tid] = s1;
             }
         }
         __syncthreads();
-        auto hval = [&](int i) {
+        auto hval = [&](int p, int i) {
             float h = 0.0f;
             if (model == CRIMP_MODEL_FOURIER) {
 #pragma unroll
                 for (int j = 0; j < KMAX; ++j)
-                    if (j < K) h = __builtin_fmaf(ca[j], basis[2 * j][i], __builtin_fmaf(cb[j], basis[2 * j + 1][i], h));
+                    if (j < K) h = __builtin_fmaf(ca[p][j], bget(i, 2 * j), __builtin_fmaf(cb[p][j], bget(i, 2 * j + 1), h));
             } else {
-                const float cx = basis[0][i], sx = basis[1][i];
+                const float cx = bget(i, 0), sx = bget(i, 1);
 #pragma unroll
                 for (int j = 0; j < KMAX; ++j) {
                     if (j < K) {
-                        const float cu = __builtin_fmaf(cx, ca[j], sx * cb[j]);
+                        const float cu = __builtin_fmaf(cx, ca[p][j], sx * cb[p][j]);
                         if (model == CRIMP_MODEL_CAUCHY)
                             h += amp[j] * __builtin_amdgcn_rcpf(chj[j] - cu);
                         else
@@ -801,63 +865,80 @@ __global__ __launch_bounds__(kGridBlock) __attribute__((amdgpu_waves_per_eu(4)))
             }
             return h;
         };
-        // photons i, i+1 (i even): the Fourier template as packed FMAs, same order per photon as hval
-        auto hval2 = [&](int i) {
-            f32x2 h;
+        // photons i, i+1 (i even) for every phShift of the lane: the Fourier template as packed FMAs, same order per
+        // photon as hval; one basis read serves all PPL phShifts
+        auto hval2 = [&](int i, f32x2 (&h)[PPL]) {
             if (model == CRIMP_MODEL_FOURIER) {
-                h = f32x2{0.0f, 0.0f};
+#pragma unroll
+                for (int p = 0; p < PPL; ++p) h[p] = f32x2{0.0f, 0.0f};
 #pragma unroll
                 for (int j = 0; j < KMAX; ++j)
                     if (j < K) {
-                        const f32x2 cj = *reinterpret_cast<const f32x2*>(&basis[2 * j][i]);
-                        const f32x2 sj = *reinterpret_cast<const f32x2*>(&basis[2 * j + 1][i]);
-                        h = __builtin_elementwise_fma(f32x2{ca[j], ca[j]}, cj,
-                                                      __builtin_elementwise_fma(f32x2{cb[j], cb[j]}, sj, h));
+                        const f32x2 cj = bas[i >> 1][2 * j], sj = bas[i >> 1][2 * j + 1];   // i is even
+#pragma unroll
+                        for (int p = 0; p < PPL; ++p)
+                            h[p] = __builtin_elementwise_fma(f32x2{ca[p][j], ca[p][j]}, cj,
+                                                             __builtin_elementwise_fma(f32x2{cb[p][j], cb[p][j]}, sj, h[p]));
                     }
             } else {
-                h = f32x2{hval(i), hval(i + 1)};
+#pragma unroll
+                for (int p = 0; p < PPL; ++p) h[p] = f32x2{hval(p, i), hval(p, i + 1)};
             }
-            return h;
         };
         for (int i0 = 0; i0 < cnt; i0 += 32) {
-            f32x2 pa[NN / 2];
+            f32x2 pa[PPL][NN / 2];
 #pragma unroll
-            for (int a = 0; a < NN / 2; ++a) pa[a] = f32x2{0.0f, 0.0f};
+            for (int p = 0; p < PPL; ++p)
+#pragma unroll
+                for (int a = 0; a < NN / 2; ++a) pa[p][a] = f32x2{0.0f, 0.0f};
             const int i1 = std::min(cnt, i0 + 32);
             int i = i0;
             // log2 of a product of kGridProd model values instead of kGridProd logs (v_log issues at quarter
             // rate): one photon costs an add and a multiply per norm plus 1/kGridProd of a log and an add.
             // Four factors of (norm + h) <= 2^31 cannot overflow fp32; the product adds <= 3 roundings.
             for (; i + kGridProd <= i1; i += kGridProd) {
-                const f32x2 h01 = hval2(i), h23 = hval2(i + 2);
-                hmn = fminf(fminf(fminf(fminf(hmn, h01.x), h01.y), h23.x), h23.y);
+                f32x2 h01[PPL], h23[PPL];
+                hval2(i, h01);
+                hval2(i + 2, h23);
 #pragma unroll
-                for (int b = 0; b < NN / 2; ++b) {
-                    f32x2 pr = nr[b] + h01.x;
-                    pr *= nr[b] + h01.y;
-                    pr *= nr[b] + h23.x;
-                    pr *= nr[b] + h23.y;
-                    pa[b] += f32x2{__builtin_amdgcn_logf(pr.x), __builtin_amdgcn_logf(pr.y)};
+                for (int p = 0; p < PPL; ++p) {
+                    hmn[p] = fminf(fminf(fminf(fminf(hmn[p], h01[p].x), h01[p].y), h23[p].x), h23[p].y);
+#pragma unroll
+                    for (int b = 0; b < NN / 2; ++b) {
+                        f32x2 pr = nr[b] + h01[p].x;
+                        pr *= nr[b] + h01[p].y;
+                        pr *= nr[b] + h23[p].x;
+                        pr *= nr[b] + h23[p].y;
+                        pa[p][b] += f32x2{__builtin_amdgcn_logf(pr.x), __builtin_amdgcn_logf(pr.y)};
+                    }
                 }
             }
             for (; i < i1; ++i) {
-                const float h = hval(i);
-                hmn = fminf(hmn, h);
 #pragma unroll
-                for (int b = 0; b < NN / 2; ++b) {
-                    const f32x2 pr = nr[b] + h;
-                    pa[b] += f32x2{__builtin_amdgcn_logf(pr.x), __builtin_amdgcn_logf(pr.y)};
+                for (int p = 0; p < PPL; ++p) {
+                    const float h = hval(p, i);
+                    hmn[p] = fminf(hmn[p], h);
+#pragma unroll
+                    for (int b = 0; b < NN / 2; ++b) {
+                        const f32x2 pr = nr[b] + h;
+                        pa[p][b] += f32x2{__builtin_amdgcn_logf(pr.x), __builtin_amdgcn_logf(pr.y)};
+                    }
                 }
             }
 #pragma unroll
-            for (int a = 0; a < NN; ++a) acc[a] += (double)pa[a / 2][a % 2];
+            for (int p = 0; p < PPL; ++p)
+#pragma unroll
+                for (int a = 0; a < NN; ++a) acc[p][a] += (double)pa[p][a / 2][a % 2];
         }
     }
-    if (bphi < nphi) {
 #pragma unroll
-        for (int a = 0; a < NN; ++a)
-            if (a < na) lnsum[((split * nint + iv) * nnorm + a0 + a) * nphi + bphi] = acc[a];
-        if (a0 == 0) hmin[(split * nint + iv) * nphi + bphi] = (double)hmn;
+    for (int p = 0; p < PPL; ++p) {
+        if (bphi[p] < nphi) {
+#pragma unroll
+            for (int a = 0; a < NN; ++a)
+                if (a < na) lnsum[((split * nint + iv) * nnorm + a0 + a) * nphi + bphi[p]] = acc[p][a];
+            if (a0 == 0) hmin[(split * nint + iv) * nphi + bphi[p]] = (double)hmn[p];
+        }
     }
 }
 
@@ -1714,10 +1795,11 @@ static int toa_grid_partials(Scratch& sc, hipStream_t s, const double* dx, const
     const int nn = nnorm <= 2 ? 2 : nnorm <= kGridNNSmall ? kGridNNSmall : kGridNN;
     for (int64_t a0 = 0; a0 < nnorm; a0 += nn) {
         const int na = (int)std::min<int64_t>(nn, nnorm - a0);
-#define CRIMP_LG1(MD, KK, NNV) k_toa_grid<kGridKMax, MD, KK, NNV><<<grid, kGridBlock, 0, s>>>(dx, doff, dT, dnrm, (int)nnorm, \
-                                                                                (int)a0, na, dphi, (int)nphi, chunk, (int)nint, *pl, *ph)
-#define CRIMP_LG(MD, KK) do { if (nn == 2) CRIMP_LG1(MD, KK, 2); else if (nn == kGridNNSmall) CRIMP_LG1(MD, KK, kGridNNSmall); \
-                              else CRIMP_LG1(MD, KK, kGridNN); } while (0)
+#define CRIMP_LG1(MD, KK, NNV, PP) k_toa_grid<kGridKMax, MD, KK, NNV, PP><<<grid, kGridBlock / PP, 0, s>>>(dx, doff, dT, dnrm, \
+                                                          (int)nnorm, (int)a0, na, dphi, (int)nphi, chunk, (int)nint, *pl, *ph)
+#define CRIMP_LG(MD, KK) do { if (nn == 2) CRIMP_LG1(MD, KK, 2, kGridPPL); \
+                              else if (nn == kGridNNSmall) CRIMP_LG1(MD, KK, kGridNNSmall, kGridPPL); \
+                              else CRIMP_LG1(MD, KK, kGridNN, 1); } while (0)
         if (model == CRIMP_MODEL_FOURIER) {
             switch (K) {
                 case 1: CRIMP_LG(CRIMP_MODEL_FOURIER, 1); break;

@@ -34,7 +34,22 @@ struct FitEval {
 struct FitShared {
     double red[kFitBlock / 64][8];
     double coef[2][CRIMP_MAX_COMP];
+#if CRIMP_FIT_TABLE
+    double2 tab[kSinTab];  // photon_sincos_tab (filled once per workgroup)
+#endif
 };
+__device__ __forceinline__ void fit_sincos(int model, FitShared& sh, double xv, double& s1, double& c1) {
+#if CRIMP_FIT_TABLE
+    photon_sincos_tab(model, sh.tab, xv, s1, c1);
+#else
+    photon_sincos(model, xv, s1, c1);
+#endif
+}
+__device__ __forceinline__ void fit_shared_init(FitShared& sh) {
+#if CRIMP_FIT_TABLE
+    sintab_fill(sh.tab);
+#endif
+}
 
 // np.clip semantics (a NaN stays NaN)
 __device__ __forceinline__ double clipd(double v, double lo, double hi) { return v < lo ? lo : (v > hi ? hi : v); }
@@ -90,7 +105,7 @@ __device__ FitEval fit_eval(const double* __restrict__ x, int64_t a, int64_t b, 
         }
     } else for (int64_t i = a + tid; i < b; i += kFitBlock) {
         double s1, c1, h, h1, h2;
-        photon_sincos(model, x[i], s1, c1);
+        fit_sincos(model, sh, x[i], s1, c1);
         tpl_terms(T, model, K, sh.coef[0], sh.coef[1], s1, c1, h, h1, h2);
         if (hmode == kHStore) hc[i] = h;
         const double mv = n + h;
@@ -215,7 +230,7 @@ __device__ FitEval3 fit_eval3(const double* __restrict__ x, int64_t a, int64_t b
     double mn = INFINITY;
     for (int64_t i = a + tid; i < b; i += kFitBlock) {
         double s1, c1, h, h1, h2;
-        photon_sincos(model, x[i], s1, c1);
+        fit_sincos(model, sh, x[i], s1, c1);
         tpl_terms(T, model, K, sh.coef[0], sh.coef[1], s1, c1, h, h1, h2);
         const double mv = n + A * h;
         const double q = 1.0 / mv;
@@ -357,6 +372,7 @@ __global__ __launch_bounds__(kFitBlock) void k_toa_fit_amp(const double* __restr
                                                            double* __restrict__ out) {
     __shared__ FitShared sh;
     __shared__ FitShared3 s3;
+    fit_shared_init(sh);
     const int64_t iv = blockIdx.x;
     const int64_t a = offsets[iv], b = offsets[iv + 1];
     const double E = expo[iv];
@@ -414,6 +430,7 @@ __global__ __launch_bounds__(kFitBlock) void k_toa_fit(const double* __restrict_
                                                        const double* __restrict__ start, FitCfg C,
                                                        double* __restrict__ out, double* __restrict__ hcache) {
     __shared__ FitShared sh;
+    fit_shared_init(sh);
     const int64_t iv = blockIdx.x;
     const int64_t a = offsets[iv], b = offsets[iv + 1];
     const double E = expo[iv];
