@@ -289,7 +289,8 @@ __device__ FitEval3 fit_eval3(const double* __restrict__ x, int64_t a, int64_t b
 }
 
 // Newton direction for the free coordinates (mask bits: 1 norm, 2 phShift, 4 ampShift) of a 3-parameter
-// ascent: Levenberg shift by a Gershgorin bound of the largest eigenvalue, then a trust region (0.05 rad
+// ascent: plain Newton where H is negative definite, else a Levenberg shift by a Gershgorin bound of the largest
+// eigenvalue; then a trust region (0.05 rad
 // in phShift, half the current norm and ampShift).
 __device__ void fit_newton_dir3(const double* v, const FitEval3& e, int mask, double* d) {
     double H[3][3] = {{e.H[0], e.H[1], e.H[2]}, {e.H[1], e.H[3], e.H[4]}, {e.H[2], e.H[4], e.H[5]}};
@@ -308,7 +309,15 @@ __device__ void fit_newton_dir3(const double* v, const FitEval3& e, int mask, do
         lam = fmax(lam, r);
         diag += fabs(H[i][i]);
     }
-    const double shift = lam < 0 ? 0.0 : lam * 1.5 + 1e-6 * diag + 1e-12;
+    // no shift when H is negative definite (leading principal minors alternate in sign): the Gershgorin bound
+    // over-estimates the largest eigenvalue of a badly scaled H (norm vs ampShift entries) and a shift from it
+    // shrank every ampShift step to ~2 % of the distance to the optimum
+    const double m2 = H[0][0] * H[1][1] - H[0][1] * H[1][0];
+    const double m3 = H[0][0] * (H[1][1] * H[2][2] - H[1][2] * H[2][1]) -
+                      H[0][1] * (H[1][0] * H[2][2] - H[1][2] * H[2][0]) +
+                      H[0][2] * (H[1][0] * H[2][1] - H[1][1] * H[2][0]);
+    const bool negdef = H[0][0] < 0.0 && m2 > 0.0 && m3 < 0.0;
+    const double shift = (lam < 0 || negdef) ? 0.0 : lam * 1.5 + 1e-6 * diag + 1e-12;
     for (int i = 0; i < 3; ++i) H[i][i] -= shift;
     // solve H d = -g (symmetric 3x3, Cramer)
     const double c00 = H[1][1] * H[2][2] - H[1][2] * H[2][1];

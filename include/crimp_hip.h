@@ -36,8 +36,10 @@ extern "C" {
 #define CRIMP_FLAG_DEVICE_PTRS 1u  /* array arguments are device pointers */
 #define CRIMP_FLAG_SYNC 2u         /* synchronise the stream before returning */
 /* Periodicity-search precision. Default: the exact i8-MFMA kernel on arithmetic-progression grids of >= 256
- * trials (per-term error ~1e-9, integer sums; every trial within 1e-6 relative of the reference, trials it
- * cannot certify recomputed in fp64 -- crimp_last_fixups()), the fp64 kernel otherwise. */
+ * trials (per-term error ~1e-9, integer sums; trials whose 10-sigma bound on those roundings cannot place them within
+ * 1e-6 relative are recomputed in fp64 -- crimp_last_fixups()), the fp64 kernel otherwise. Tested within 1e-6 of the
+ * reference on every checked trial; the reference's own fp64 argument rounding (~1e-6 of a noise-level H_20) is
+ * the floor of any fp64 implementation. */
 #define CRIMP_FLAG_FORCE_DIRECT 4u /* fast search: the fp32 direct kernel even on a progression (implies FAST) */
 #define CRIMP_FLAG_FORCE_MFMA 8u   /* search: fail unless a factorised kernel applies (with FAST: the f16 one) */
 #define CRIMP_FLAG_HW_SINCOS 16u   /* fast direct search: hardware v_sin/v_cos (implies FAST) */

@@ -5,8 +5,9 @@ The exact kernel (csrc/search_exact.h) flags for the fp64 fix-up every trial who
 independent-rounding model: per-term rms 1e-9) cannot place it within 1e-6 relative. These tests hold the model to
 inputs built to break the independence -- photon times on a 1/(4096 f0) lattice (every photon's phase lands on the
 same table cells with zero residual rotation), every photon duplicated, a 90 %-pulsed source -- by comparing every
-trial with the fp64 path (itself ~1e-9 of the reference, tests/test_gpu_parity.py): the default result (fix-up on)
-at plain 1e-6, and the raw kernel (FLAG_NO_FIXUP) at plain 1e-6 on every trial the certificate passed."""
+trial with the fp64 path, and the trials where that differs by more than 1e-6 with the oracle in the reference's
+operation order: the default result (fix-up on) at plain 1e-6, and the raw kernel (FLAG_NO_FIXUP) at plain 1e-6 on
+every trial the certificate passed."""
 import math
 import os
 import subprocess
@@ -37,12 +38,32 @@ def _correlated_inputs():
     return f0, {"quantised": quant, "duplicated": dup, "pulsed90": strong}
 
 
+def _within_1e6_of_reference(got, z64, t_h, f_h, nharm, stat, name, what):
+    """Every trial within 1e-6 relative of the fp64 path or, where it is not, of the oracle in the reference's
+    operation order. At m = 20 two fp64 evaluations with different argument roundings (the reference's
+    2 pi k f dt, the fp64 kernel's angle additions, the exact kernel's f_j dt) differ by ~2^-53 of the k = 20
+    argument per term, which moves a noise-level H by up to ~1e-6 (duplicated photons double it coherently):
+    there the reference itself is the yardstick. Measured (tools/diag_cert.py): duplicated photons, H_20, trial
+    7429: exact 4.9e-7 from the reference, the fp64 kernel 1.7e-6 from the exact path, the reference 2.5e-6 from
+    the exact-argument value."""
+    e = _rel(got, z64)
+    off = np.flatnonzero(e > 1e-6)
+    assert off.size <= 32, (name, what, off.size)
+    if off.size:
+        ref = O.search(t_h, f_h[off], nharm, stat="h" if stat else "z2")
+        er = _rel(got[off], ref)
+        assert er.max() <= 1e-6, (name, what, er.max(), int(off[er.argmax()]))
+    return e, off.size
+
+
 @pytest.mark.parametrize("nharm,stat", [(2, 0), (20, 1)])
 def test_certificate_holds_on_correlated_inputs(gpu, nharm, stat):
     import torch
     from crimp_amd import ops, _native as N
+    O.set_threads(min(16, os.cpu_count() or 1))
     f0, inputs = _correlated_inputs()
-    f = torch.as_tensor(f0 + (np.arange(8192) - 4096) / 1.0e7, device=gpu)
+    f_h = f0 + (np.arange(8192) - 4096) / 1.0e7
+    f = torch.as_tensor(f_h, device=gpu)
     for name, t_h in inputs.items():
         t = torch.as_tensor(t_h, device=gpu)
         t0 = (t_h[0] + t_h[-1]) / 2
@@ -50,15 +71,16 @@ def test_certificate_holds_on_correlated_inputs(gpu, nharm, stat):
         nfix = N.load().crimp_last_fixups()
         raw = ops.search(t, t0, f, nharm, stat, flags=N.FLAG_NO_FIXUP).cpu().numpy()
         z64 = ops.search(t, t0, f, nharm, stat, precision="f64").cpu().numpy()
-        e = _rel(z, z64)
-        assert e.max() <= 1e-6, (name, e.max(), int(e.argmax()))
+        e, noff = _within_1e6_of_reference(z, z64, t_h, f_h, nharm, stat, name, "default")
         flagged = z != raw                                   # the fix-up rewrote exactly the flagged trials
         assert flagged.sum() <= nfix, (name, flagged.sum(), nfix)
-        er = _rel(raw[~flagged], z64[~flagged])
-        assert er.max() <= 1e-6, (name, "raw kernel on a certified trial", er.max())
+        cert = np.flatnonzero(~flagged)
+        er, _ = _within_1e6_of_reference(raw[cert], z64[cert], t_h, f_h[cert], nharm, stat, name,
+                                         "raw kernel on a certified trial")
         assert nfix <= 64, (name, nfix)                      # a kernel regression would flag most trials
         assert int(np.argmax(z)) == int(np.argmax(z64))
-        print("%s m=%d: max rel %.2e (raw certified %.2e), fix-ups %d" % (name, nharm, e.max(), er.max(), nfix))
+        print("%s m=%d: max rel vs fp64 %.2e (raw certified %.2e), %d checked against the oracle, fix-ups %d" % (
+            name, nharm, e.max(), er.max(), noff, nfix))
 
 
 def _run_child(code, env_extra, out):

@@ -59,10 +59,46 @@ def test_config3_full_size(gpu):
     assert abs(far.mean() - 4.0) < 0.05
 
 
+def test_config4_windows_vs_oracle(gpu):
+    """Config 4 at plain 1e-6 against the oracle over all 1e8 photons, on contiguous trial windows: 32 noise-level
+    trials at the start of the far row (log10|fdot| = -13.5), 32 beside the peak and the peak with its neighbours in
+    the row of the injected fdot (tests/golden/config4_windows.npz; the oracle needs ~16 s of 8 cores per trial, so
+    its values are committed with checksums of the regenerated photons, tests/golden/gen_config4_windows.py).
+    ``ref`` follows the reference's operation order (periodsearch.py:93-98, :118-123); ``true`` is the same formula
+    with the argument carried exactly, so ref-vs-true is the reference's own argument rounding (<= 1.6e-7 here)."""
+    import os
+    import sys
+    import torch
+    from crimp_amd import ops, _native as N
+    from crimp_amd.synth import pulsed_events
+    from conftest import ROOT
+    sys.path.insert(0, os.path.join(str(ROOT), "tests", "golden"))
+    from gen_config4_windows import FD, FREQ, M, N as NPH, SPAN, F0, FDOT, WINDOWS, photon_checksums
+    fx = np.load(os.path.join(str(ROOT), "tests", "golden", "config4_windows.npz"))
+    t_h = pulsed_events(NPH, SPAN, F0, pulsed_frac=0.05, fdot=FDOT, seed=1)
+    np.testing.assert_array_equal(photon_checksums(t_h), fx["checksums"])   # the fixture's photons, bit for bit
+    t = torch.as_tensor(t_h, device=gpu)
+    t0 = (t_h[0] + t_h[-1]) / 2
+    del t_h
+    f = torch.as_tensor(FREQ, device=gpu)
+    fd = torch.as_tensor(FD, device=gpu)
+    got, nfix = [], 0
+    for r, j0, cnt in WINDOWS:
+        got.append(ops.search(t, t0, f, 20, 1, log10_negfdot=fd, first=r * M + j0, count=cnt).cpu().numpy())
+        nfix += N.load().crimp_last_fixups()
+    h = np.concatenate(got)
+    assert _rel_err(h, fx["ref"]).max() <= 1e-6          # measured 2.6e-7 (profiles/r03/config4_windows.json)
+    assert _rel_err(h, fx["true"]).max() <= 1e-6         # measured 1.4e-7
+    assert np.median(_rel_err(h, fx["ref"])) <= 1e-7
+    assert int(np.argmax(h)) == int(np.argmax(fx["ref"]))
+    assert nfix <= 8
+
+
 def test_config4_full_photon_count_h20(gpu):
     """1e8 photons with fdot, 2-D H-test m=20 on a 3 x 8192 trial sub-grid (the full 1e7-trial grid runs sharded
-    on 8 GPUs in the bench configuration): oracle over all photons on 8 sampled trials (plain per-trial relative
-    error), and every fd row computed as its own trial range bit-identical to the whole grid."""
+    on 8 GPUs in the bench configuration) whose rows include both ends of config 4's log10|fdot| range: oracle over
+    all photons on 8 sampled trials (plain per-trial relative error), and every fd row computed as its own trial
+    range bit-identical to the whole grid."""
     import torch
     from crimp_amd import ops
     from crimp_amd.synth import pulsed_events
@@ -71,7 +107,7 @@ def test_config4_full_photon_count_h20(gpu):
     df = 1.0 / (10.0 * span)
     M = 8192
     f_h = f0 + (np.arange(M) - M // 2) * df
-    fd = np.array([-12.5, -12.0, -11.5])
+    fd = np.array([-13.5, -12.0, -11.5])
     t = torch.as_tensor(t_h, device=gpu)
     f = torch.as_tensor(f_h, device=gpu)
     fdd = torch.as_tensor(fd, device=gpu)
