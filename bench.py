@@ -40,7 +40,8 @@ sys.path.insert(0, ROOT)
 PEAK_I8_TOPS = (2 * 5000.0 + 10000.0) / 3
 OPS_PER_EVAL_HARM = 128.0       # (8 x 65536 dense + 4 x 131072 sparse ops) per 4 photons x 2048 trials x harmonic
 PEAK_HBM_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E ~8 TB/s
-PEAK_VALU_SLOTS = 256 * 4 * 32 * 2.4e9   # lane-slots/s: 256 CUs x 4 SIMD-32 x 2.4 GHz
+PEAK_VALU_SLOTS = 256 * 4 * 32 * 2.4e9   # fp32 lane-ops/s: 256 CUs x 4 SIMD-32 x 2.4 GHz
+PEAK_F64_OPS = 256 * 64 * 2.4e9          # fp64 FMA-rate lane-ops/s: half the fp32 rate (78.6 TFLOP/s fp64 vector)
 PMC_FILE = os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json")
 
 
@@ -138,16 +139,39 @@ def toa_leg(a, dev, world, rank):
            "toa_shift_recovery_rms_cycles": float(np.sqrt(np.mean(d ** 2)) / (2 * np.pi)),
            "toa_median_sigma_cycles": float(np.median(res["phShi_LL"]) / (2 * np.pi)),
            "toa_kernel_ms": {"k_toa_grid": grid_ms, "k_toa_fit": fit_ms}}
-    # VALU roofline of the brute grid (the dominant ToA kernel): per photon and phShift, K fp32 FMA pairs for the
-    # template (2K slots) + per norm one add, one multiply and 1/4 of a quarter-rate log plus an add (2.5 + 1) slots:
-    # S = 2K + 20 * 3.5 = 82 slots (K = 6) per photon x phShift, 126 phShifts
-    slots = a.toa_intervals * a.toa_photons * 126 * (2 * 6 + 20 * 3.5)
-    ach = slots / (grid_ms * 1e-3)
-    out["toa_roofline"] = {"kernel": "k_toa_grid", "bound": "valu", "achieved": ach / 1e12, "peak": PEAK_VALU_SLOTS / 1e12,
-                           "unit": "Tslot/s", "frac": ach / PEAK_VALU_SLOTS,
-                           "note": "82 VALU lane-slots per photon x phShift (12 template FMAs + 20 norms x (add, mul, "
-                                   "1/4 v_log_f32 at 4 slots, add)) / k_toa_grid hipEvent time; 4 SIMD-32 x 256 CUs x "
-                                   "2.4 GHz peak"}
+    # Algorithmic VALU work (SURVEY.md section 8d's lane-slot model). Brute grid: per photon x
+    # phShift, the K-term template as 2K fp32 FMAs, one min, and per evaluated norm an add, 3/4 of a multiply (log2 of a
+    # product of four factors), 1/4 of a quarter-rate v_log_f32 (4 slots) and 1/4 of an add: S_grid = 2K + 1 + 3 NN,
+    # NN = norms evaluated per phShift (the pruned candidates, crimp_last_toa_grid_norms); fp32 peak = 256 CUs x 4
+    # SIMDs x 32 lanes x 2.4 GHz = 7.86e13 lane-ops/s (packed or not). Fit: per photon and likelihood pass, in fp64
+    # operations (FMA rate, half the fp32 rate: 3.93e13/s): table sin/cos 14, per harmonic the Chebyshev step (2)
+    # and h, h', h'' (7) = 9K, the model add 1, the reciprocal 5 (v_rcp_f64 + two Newton steps), ln as 1/4 of a fp64
+    # log (~29) + a multiply = 8.25, 6 sums and fmin 9 -> S_full = 37 + 9K; a pass that reads the cached template
+    # part (norm re-profile of the 1-sigma scan): S_cached = 17 (the add, reciprocal, ln, two sums and fmin). Passes
+    # per interval from the fit's own counters.
+    K = len(T2259["amp"])
+    nn = int(N.load().crimp_last_toa_grid_norms())
+    nphi = 126
+    nph_tot = float(a.toa_intervals) * a.toa_photons
+    g_slots = nph_tot * nphi * (2 * K + 1 + 3 * nn)
+    g_ach = g_slots / (grid_ms * 1e-3)
+    out["toa_roofline"] = {"kernel": "k_toa_grid", "bound": "valu", "achieved": g_ach / 1e12,
+                           "peak": PEAK_VALU_SLOTS / 1e12, "unit": "Tlane-op/s (fp32)", "frac": g_ach / PEAK_VALU_SLOTS,
+                           "norms_evaluated": nn, "slots_per_photon_phshift": 2 * K + 1 + 3 * nn,
+                           "note": "S_grid = 2K + 1 + 3 NN fp32 lane-op slots per photon x phShift (v_log_f32 at 4) x "
+                                   "1250 x 1e5 photons x 126 phShifts / brute-grid hipEvent time (k_toa_grid + "
+                                   "k_toa_grid_best); peak 256 CU x 4 SIMD x 32 lanes x 2.4 GHz"}
+    fev = np.asarray(res["evaluations"], dtype=np.float64)
+    fca = np.asarray(res["cached_evaluations"], dtype=np.float64)
+    f_ops = float(np.sum((fev - fca) * (37 + 9 * K) + fca * 17) * a.toa_photons)
+    f_ach = f_ops / (fit_ms * 1e-3)
+    out["toa_fit_roofline"] = {"kernel": "k_toa_fit", "bound": "valu", "achieved": f_ach / 1e12,
+                               "peak": PEAK_F64_OPS / 1e12, "unit": "Tlane-op/s (fp64)", "frac": f_ach / PEAK_F64_OPS,
+                               "full_passes_per_interval": float(np.mean(fev - fca)),
+                               "cached_passes_per_interval": float(np.mean(fca)),
+                               "note": "S_full = 37 + 9K fp64 ops per photon and likelihood pass, S_cached = 17 for "
+                                       "a pass over the cached template part; passes from the fit's own counters / "
+                                       "k_toa_fit hipEvent time; peak fp64 FMA rate 256 CU x 64 lanes x 2.4 GHz"}
     # end to end from host arrays: photon times t = (cycle + phase) / F0 around PEPOCH, intervals bracketing them
     F0, pep = 0.5, 58000.0
     cyc = torch.arange(x.numel(), device=dev, dtype=torch.float64)

@@ -35,6 +35,7 @@ static double g_last_kernel_ms = -1.0;
 static std::vector<double> g_kernel_times;
 // trials of the last crimp_search recomputed by the fp64 fix-up (exact path)
 static int64_t g_last_fixups = 0;
+static int64_t g_last_grid_norms = 0;  // brute-grid norms evaluated per phShift by the last crimp_toa_fit
 struct KernelTimer {
     hipEvent_t a = nullptr, b = nullptr;
     hipStream_t s;
@@ -573,6 +574,9 @@ __device__ __forceinline__ void photon_sincos(int model, double xv, double& s1, 
 // the library sincospi / sincos): r = x in turns (x / 2 pi for radians), k = rint(4096 r), delta = 2 pi (r - k / 4096)
 // (the subtraction is exact), |delta| <= pi / 4096, cos/sin(delta) by their Taylor series to delta^4 / delta^5
 // (truncation < 3e-22), rotated by the table entry: ~2 ulp, against ~30 fp64 operations of the library call.
+#ifndef CRIMP_FIT_GENERIC
+#define CRIMP_FIT_GENERIC 0
+#endif
 #ifndef CRIMP_FIT_TABLE
 #define CRIMP_FIT_TABLE 1
 #endif
@@ -598,6 +602,22 @@ __device__ __forceinline__ void photon_sincos_tab(int model, const double2* __re
     c1 = fma(e.x, cd, -(e.y * sd));
 }
 
+// 1/v for the likelihood sums: v_rcp_f64 and two Newton steps (5 fp64 operations instead of the ~10 of a correctly
+// rounded division; within 1 ulp). The fit kernels and k_toa_points use the same, so the device-driven and the
+// host-driven fits sum identical terms.
+#ifndef CRIMP_FIT_EXACT_DIV
+#define CRIMP_FIT_EXACT_DIV 0
+#endif
+__device__ __forceinline__ double lk_rcp(double v) {
+#if CRIMP_FIT_EXACT_DIV
+    return 1.0 / v;
+#else
+    double r = __builtin_amdgcn_rcp(v);
+    r = fma(fma(-v, r, 1.0), r, r);
+    return fma(fma(-v, r, 1.0), r, r);
+#endif
+}
+
 // h = model - norm at one photon and its first two phShift derivatives h1, h2 (templatemodels.py:64-82,
 // :166-185, :271-290), from the photon's (s1, c1) and one point's coefficient rows c0[], cs[].
 __device__ __forceinline__ void tpl_terms(const TplDev* __restrict__ T, int model, int K, const double* c0,
@@ -607,17 +627,22 @@ __device__ __forceinline__ void tpl_terms(const TplDev* __restrict__ T, int mode
     h1 = 0.0;
     h2 = 0.0;
     if (model == CRIMP_MODEL_FOURIER) {
-        double cj = c1, sj = s1;
+        // cos, sin of harmonic j+1 by the Chebyshev recurrence c_{j+1} = 2 c_1 c_j - c_{j-1} (one fma each instead of
+        // the four operations of an angle addition; error <= ~K^2 ulp)
+        const double tc = c1 + c1;
+        double cj = c1, sj = s1, cp = 1.0, sp = 0.0;
         for (int j = 0; j < K; ++j) {
             const double al = c0[j], be = cs[j];
-            const double tj = al * cj + be * sj;
+            const double tj = fma(al, cj, be * sj);
             const double jj = (double)(j + 1);
             h += tj;
-            h2 -= jj * jj * tj;
-            h1 += jj * (al * sj - be * cj);
-            const double cn = cj * c1 - sj * s1;
-            sj = sj * c1 + cj * s1;
+            h2 = fma(-(jj * jj), tj, h2);
+            h1 = fma(jj, fma(al, sj, -(be * cj)), h1);
+            const double cn = fma(tc, cj, -cp), sn = fma(tc, sj, -sp);
+            cp = cj;
+            sp = sj;
             cj = cn;
+            sj = sn;
         }
     } else {
         for (int j = 0; j < K; ++j) {
@@ -639,6 +664,33 @@ __device__ __forceinline__ void tpl_terms(const TplDev* __restrict__ T, int mode
                 h1 += kp * su * v;
                 h2 += (-kp * cu + kp * kp * su * su) * v;
             }
+        }
+    }
+}
+
+// The Fourier branch of tpl_terms for a template size fixed at compile time (the device fit kernel): the same
+// per-photon operation order, coefficient rows held in registers, the harmonic loop unrolled.
+template <int KF>
+__device__ __forceinline__ void tpl_terms_fourier(const double (&al)[KF], const double (&be)[KF], double s1, double c1,
+                                                  double& h, double& h1, double& h2) {
+    h = 0.0;
+    h1 = 0.0;
+    h2 = 0.0;
+    const double tc = c1 + c1;
+    double cj = c1, sj = s1, cp = 1.0, sp = 0.0;
+#pragma unroll
+    for (int j = 0; j < KF; ++j) {
+        const double tj = fma(al[j], cj, be[j] * sj);
+        const double jj = (double)(j + 1);
+        h += tj;
+        h2 = fma(-(jj * jj), tj, h2);
+        h1 = fma(jj, fma(al[j], sj, -(be[j] * cj)), h1);
+        if (j + 1 < KF) {
+            const double cn = fma(tc, cj, -cp), sn = fma(tc, sj, -sp);
+            cp = cj;
+            sp = sj;
+            cj = cn;
+            sj = sn;
         }
     }
 }
@@ -696,7 +748,7 @@ __global__ __launch_bounds__(kPtsBlock) void k_toa_points(const double* __restri
             double h, h1, h2;
             tpl_terms(T, model, K, coef[p][0], coef[p][1], s1, c1, h, h1, h2);
             const double mv = nrm[p] + h;
-            const double q = 1.0 / mv;
+            const double q = lk_rcp(mv);
             acc[p][0] += log(mv);
             acc[p][1] += q;
             acc[p][2] += h1 * q;
@@ -1114,6 +1166,7 @@ extern "C" int crimp_last_kernel_times(double* ms, int32_t cap) {
 extern "C" int crimp_version(void) { return CRIMP_VERSION; }
 
 extern "C" int64_t crimp_last_fixups(void) { return g_last_fixups; }
+extern "C" int64_t crimp_last_toa_grid_norms(void) { return g_last_grid_norms; }
 
 extern "C" int crimp_release_scratch(void) {
     std::lock_guard<std::mutex> lk(g_mutex);
@@ -1844,6 +1897,7 @@ extern "C" int crimp_toa_fit(const double* x, const int64_t* offsets, int64_t ni
     }
     const bool dev = flags & CRIMP_FLAG_DEVICE_PTRS;
     hipStream_t s = as_stream(stream);
+    g_last_grid_norms = 0;
     std::vector<int64_t> hoff((size_t)nint + 1);
     if (dev) {
         HIPCHK(d2h(s, hoff.data(), offsets, (nint + 1) * sizeof(int64_t)));
@@ -1928,6 +1982,7 @@ extern "C" int crimp_toa_fit(const double* x, const int64_t* offsets, int64_t ni
             // compacted per-interval norms: the candidates in grid order, padded by repeating the last (a repeat
             // comes later in norm-outer order, so it never wins a tie)
             const int64_t nc = ncand <= 2 ? 2 : ncand <= kGridNNSmall ? kGridNNSmall : ncand;
+            g_last_grid_norms = nc;
             hnrm.resize((size_t)(nint * nc));
             for (int64_t i = 0; i < nint; ++i)
                 for (int64_t c = 0; c < nc; ++c)
@@ -1969,7 +2024,29 @@ extern "C" int crimp_toa_fit(const double* x, const int64_t* offsets, int64_t ni
         } else {
             double* hcache = nullptr;  // per-photon template part for the norm profiles of the 1-sigma scan
             HIPCHK(sc.alloc(&hcache, (size_t)hoff[nint]));
-            k_toa_fit<<<(unsigned)nint, kFitBlock, 0, s>>>(dx, doff, dT, de, dstart, C, dout, hcache);
+#define CRIMP_LF(MD, KK) k_toa_fit<MD, KK><<<(unsigned)nint, kFitBlock, 0, s>>>(dx, doff, dT, de, dstart, C, dout, hcache)
+            if (T.model == CRIMP_MODEL_FOURIER) {
+#if CRIMP_FIT_GENERIC  // A/B build: the template size read at run time
+                CRIMP_LF(CRIMP_MODEL_FOURIER, 0);
+#else
+                switch (T.K) {
+                    case 1: CRIMP_LF(CRIMP_MODEL_FOURIER, 1); break;
+                    case 2: CRIMP_LF(CRIMP_MODEL_FOURIER, 2); break;
+                    case 3: CRIMP_LF(CRIMP_MODEL_FOURIER, 3); break;
+                    case 4: CRIMP_LF(CRIMP_MODEL_FOURIER, 4); break;
+                    case 5: CRIMP_LF(CRIMP_MODEL_FOURIER, 5); break;
+                    case 6: CRIMP_LF(CRIMP_MODEL_FOURIER, 6); break;
+                    case 7: CRIMP_LF(CRIMP_MODEL_FOURIER, 7); break;
+                    case 8: CRIMP_LF(CRIMP_MODEL_FOURIER, 8); break;
+                    default: CRIMP_LF(CRIMP_MODEL_FOURIER, 0); break;
+                }
+#endif
+            } else if (T.model == CRIMP_MODEL_CAUCHY) {
+                CRIMP_LF(CRIMP_MODEL_CAUCHY, 0);
+            } else {
+                CRIMP_LF(CRIMP_MODEL_VONMISES, 0);
+            }
+#undef CRIMP_LF
         }
         HIPCHK(hipGetLastError());
         kf.stop();

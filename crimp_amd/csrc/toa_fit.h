@@ -70,12 +70,15 @@ constexpr int kFitProd = 4;  // model values per fp64 log in fit_eval
 
 // Reference extended LL (templatemodels.py:109-121, :213-226, :318-329) with its (norm, phShift) gradient and
 // Hessian at (n, phi), from one pass over photons x[a, b) (as toafit.ToAFitter.evaluate assembles them).
-// kHLoad passes return the LL and the norm derivatives only (gp, hnp, hpp are 0).
+// kHLoad passes return the LL and the norm derivatives only (gp, hnp, hpp are 0). MODEL and (Fourier) the template
+// size KF are compile-time (KF = 0: K from the template at run time), as in k_toa_grid.
+template <int MODEL, int KF>
 __device__ FitEval fit_eval(const double* __restrict__ x, int64_t a, int64_t b, const TplDev* __restrict__ T, double n,
                             double phi, double E, const FitCfg& C, FitShared& sh, double* __restrict__ hc = nullptr,
                             int hmode = kHNone) {
     const int tid = threadIdx.x;
-    const int model = T->model, K = T->K;
+    constexpr int model = MODEL;
+    const int K = KF > 0 ? KF : T->K;
     __syncthreads();  // the previous evaluation's readers are done with sh
     if (tid < K) tpl_coef(T, tid, phi, sh.coef[0][tid], sh.coef[1][tid]);
     __syncthreads();
@@ -97,19 +100,31 @@ __device__ FitEval fit_eval(const double* __restrict__ x, int64_t a, int64_t b, 
     if (hmode == kHLoad) {
         for (int64_t i = a + tid; i < b; i += kFitBlock) {
             const double mv = n + hc[i];
-            const double q = 1.0 / mv;
+            const double q = lk_rcp(mv);
             lnacc(mv);
             acc[1] += q;
             acc[3] -= q * q;
             mn = fmin(mn, mv);
         }
-    } else for (int64_t i = a + tid; i < b; i += kFitBlock) {
+    } else {
+      [[maybe_unused]] double al[KF > 0 ? KF : 1], be[KF > 0 ? KF : 1];
+      if constexpr (MODEL == CRIMP_MODEL_FOURIER && KF > 0) {
+#pragma unroll
+          for (int j = 0; j < KF; ++j) {
+              al[j] = sh.coef[0][j];
+              be[j] = sh.coef[1][j];
+          }
+      }
+      for (int64_t i = a + tid; i < b; i += kFitBlock) {
         double s1, c1, h, h1, h2;
         fit_sincos(model, sh, x[i], s1, c1);
-        tpl_terms(T, model, K, sh.coef[0], sh.coef[1], s1, c1, h, h1, h2);
+        if constexpr (MODEL == CRIMP_MODEL_FOURIER && KF > 0)
+            tpl_terms_fourier<KF>(al, be, s1, c1, h, h1, h2);
+        else
+            tpl_terms(T, model, K, sh.coef[0], sh.coef[1], s1, c1, h, h1, h2);
         if (hmode == kHStore) hc[i] = h;
         const double mv = n + h;
-        const double q = 1.0 / mv;
+        const double q = lk_rcp(mv);
         lnacc(mv);
         acc[1] += q;
         acc[2] += h1 * q;
@@ -117,6 +132,7 @@ __device__ FitEval fit_eval(const double* __restrict__ x, int64_t a, int64_t b, 
         acc[4] -= h1 * q * q;
         acc[5] += h2 * q - h1 * h1 * q * q;
         mn = fmin(mn, mv);
+      }
     }
     if (np) acc[0] += log(pr);
     const int w = tid >> 6, lane = tid & 63;
@@ -174,12 +190,13 @@ __device__ void fit_newton_dir(double n, const FitEval& e, double& dn, double& d
 
 // toafit.profile_norm: max over norm in [lo, hi] of LL(norm, phi) at fixed phi (1-D Newton, concave)
 // hc: per-photon template-part cache (nullptr: recompute every pass).
+template <int MODEL, int KF>
 __device__ double fit_profile(const double* __restrict__ x, int64_t a, int64_t b, const TplDev* __restrict__ T,
                               double phi, double n_start, double E, const FitCfg& C, FitShared& sh, int& nev,
-                              double* __restrict__ hc = nullptr) {
+                              double* __restrict__ hc = nullptr, int* ncached = nullptr) {
     double n = clipd(n_start, C.lo, C.hi);
     const int hm = hc ? kHLoad : kHNone;
-    FitEval e = fit_eval(x, a, b, T, n, phi, E, C, sh, hc, hc ? kHStore : kHNone);
+    FitEval e = fit_eval<MODEL, KF>(x, a, b, T, n, phi, E, C, sh, hc, hc ? kHStore : kHNone);
     ++nev;
     for (int it = 0; it < 30; ++it) {
         const bool bad = !isfinite(e.ll);
@@ -187,13 +204,15 @@ __device__ double fit_profile(const double* __restrict__ x, int64_t a, int64_t b
         step = clipd(step, -0.5 * n, 0.5 * n);
         if (bad) step = 0.5 * n;  // infeasible: model <= 0 somewhere, raise the norm
         double nn = clipd(n + step, C.lo, C.hi);
-        FitEval e2 = fit_eval(x, a, b, T, nn, phi, E, C, sh, hc, hm);
+        FitEval e2 = fit_eval<MODEL, KF>(x, a, b, T, nn, phi, E, C, sh, hc, hm);
         ++nev;
+        if (ncached && hc) ++*ncached;
         const bool worse = isfinite(e.ll) && (!isfinite(e2.ll) || e2.ll < e.ll - 1e-12 * fabs(e.ll));
         if (worse) {  // damp an overshoot
             nn = clipd(n + 0.25 * step, C.lo, C.hi);
-            e2 = fit_eval(x, a, b, T, nn, phi, E, C, sh, hc, hm);
+            e2 = fit_eval<MODEL, KF>(x, a, b, T, nn, phi, E, C, sh, hc, hm);
             ++nev;
+            if (ncached && hc) ++*ncached;
         }
         const bool conv = fabs(nn - n) <= 1e-13 * fmax(1.0, n);
         n = nn;
@@ -233,7 +252,7 @@ __device__ FitEval3 fit_eval3(const double* __restrict__ x, int64_t a, int64_t b
         fit_sincos(model, sh, x[i], s1, c1);
         tpl_terms(T, model, K, sh.coef[0], sh.coef[1], s1, c1, h, h1, h2);
         const double mv = n + A * h;
-        const double q = 1.0 / mv;
+        const double q = lk_rcp(mv);
         const double q2 = q * q;
         acc[0] += log(mv);
         acc[1] += q;
@@ -433,8 +452,17 @@ __global__ __launch_bounds__(kFitBlock) void k_toa_fit_amp(const double* __restr
 }
 
 // One workgroup per interval: ascent from start[iv], then the 1-sigma scan on both sides.
-// out[iv*8 + 0..6] = norm, phShift, LLmax, phShift_LL, phShift_UL, likelihood evaluations, ampShift (1).
-__global__ __launch_bounds__(kFitBlock) void k_toa_fit(const double* __restrict__ x, const int64_t* __restrict__ offsets,
+// out[iv*8 + 0..7] = norm, phShift, LLmax, phShift_LL, phShift_UL, likelihood evaluations, ampShift (1), and how
+// many of those evaluations read the cached template part (bench.py's algorithmic work count).
+// Waves per SIMD of the fit kernel: 4 (two 512-thread workgroups per CU, 66 KB of LDS each) holds it to 128 VGPRs;
+// hipcc then calls fit_eval out of line and spills only around those calls (once per likelihood pass), and the
+// photon loops run at twice the occupancy: 14.9 -> 13.2 ms per 1250 config-5 fits, records bit-identical
+// (profiles/r03/ab_fit_tmpl.log; CRIMP_FIT_WPE=2 is the all-inline 221-VGPR build)
+#ifndef CRIMP_FIT_WPE
+#define CRIMP_FIT_WPE 4
+#endif
+template <int MODEL, int KF>
+__global__ __launch_bounds__(kFitBlock) __attribute__((amdgpu_waves_per_eu(CRIMP_FIT_WPE))) void k_toa_fit(const double* __restrict__ x, const int64_t* __restrict__ offsets,
                                                        const TplDev* __restrict__ T, const double* __restrict__ expo,
                                                        const double* __restrict__ start, FitCfg C,
                                                        double* __restrict__ out, double* __restrict__ hcache) {
@@ -443,9 +471,9 @@ __global__ __launch_bounds__(kFitBlock) void k_toa_fit(const double* __restrict_
     const int64_t iv = blockIdx.x;
     const int64_t a = offsets[iv], b = offsets[iv + 1];
     const double E = expo[iv];
-    int nev = 0;
+    int nev = 0, ncached = 0;
     double n = start[2 * iv], p = start[2 * iv + 1];
-    FitEval e = fit_eval(x, a, b, T, n, p, E, C, sh);
+    FitEval e = fit_eval<MODEL, KF>(x, a, b, T, n, p, E, C, sh);
     ++nev;
     for (int it = 0; it < 60; ++it) {  // toafit.maximise
         double dn, dp;
@@ -456,7 +484,7 @@ __global__ __launch_bounds__(kFitBlock) void k_toa_fit(const double* __restrict_
         for (int ls = 0; ls < 40; ++ls) {
             tn = clipd(n + t * dn, C.lo, C.hi);
             tp = clipd(p + t * dp, -C.pb, C.pb);
-            e2 = fit_eval(x, a, b, T, tn, tp, E, C, sh);
+            e2 = fit_eval<MODEL, KF>(x, a, b, T, tn, tp, E, C, sh);
             ++nev;
             if (isfinite(e2.ll) && e2.ll >= e.ll - 1e-12 * fabs(e.ll)) {
                 ok = true;
@@ -480,7 +508,7 @@ __global__ __launch_bounds__(kFitBlock) void k_toa_fit(const double* __restrict_
         for (int k = 1;; ++k) {
             const double target = phat + (double)(side * k) * C.step;
             double ph;
-            if (T->model == CRIMP_MODEL_FOURIER) {
+            if (MODEL == CRIMP_MODEL_FOURIER) {
                 // the first step past +-pi is clipped to the bound; later ones move the bound (:332-334, :357-359)
                 const bool beyond = side < 0 ? (target <= -M_PI) : (target >= M_PI);
                 if (beyond && !past) {
@@ -492,7 +520,7 @@ __global__ __launch_bounds__(kFitBlock) void k_toa_fit(const double* __restrict_
             } else {
                 ph = clipd(target, -C.pb, C.pb);
             }
-            const double llk = fit_profile(x, a, b, T, ph, nhat, E, C, sh, nev, hcache);
+            const double llk = fit_profile<MODEL, KF>(x, a, b, T, ph, nhat, E, C, sh, nev, hcache, &ncached);
             const double diff = llmax - llk;
             if (diff > kHalfChi2OneSigma || (double)(k + 1) > C.kcap) {
                 kk = k + 1;
@@ -510,7 +538,7 @@ __global__ __launch_bounds__(kFitBlock) void k_toa_fit(const double* __restrict_
         o[4] = sig[1];
         o[5] = (double)nev;
         o[6] = 1.0;
-        o[7] = 0.0;
+        o[7] = (double)ncached;
     }
 }
 

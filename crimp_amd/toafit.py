@@ -321,7 +321,8 @@ class ToAFitter:
         n_hat, phi_hat, amp = r[:, 0].copy(), r[:, 1].copy(), r[:, 6].copy()
         rchi2 = self.reduced_chi2(n_hat, phi_hat, nfree=3 if vary_amps else 2, amp_shift=amp)
         return {"phShi": phi_hat, "phShi_LL": r[:, 3].copy(), "phShi_UL": r[:, 4].copy(), "reducedChi2": rchi2,
-                "norm": n_hat, "LLmax": r[:, 2].copy(), "evaluations": r[:, 5].copy(), "ampShift": amp}
+                "norm": n_hat, "LLmax": r[:, 2].copy(), "evaluations": r[:, 5].copy(), "ampShift": amp,
+                "cached_evaluations": r[:, 7].copy()}
 
     def fit_host(self, brutemin=False):
         """The same fit driven from the host, one batched likelihood launch per iteration (cross-check of fit)."""
