@@ -534,7 +534,10 @@ struct TplDev {
 };
 
 constexpr int kPtsPerGroup = 4;
-constexpr int kPtsBlock = 512;  // = kFitBlock: the device fit driver strides and reduces as k_toa_points
+#ifndef CRIMP_PTS_BLOCK
+#define CRIMP_PTS_BLOCK 512
+#endif
+constexpr int kPtsBlock = CRIMP_PTS_BLOCK;  // = kFitBlock: the device fit driver strides and reduces as k_toa_points
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
