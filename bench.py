@@ -14,7 +14,7 @@ Also reported:
   the peak of this instruction mix is 2/3 x 5.0 + 1/3 x 10.0 = 6.67 POP/s (the i8 dense peak, 2x BF16's 2.5 PF,
   and the 2:4-sparse peak, 2x dense) and ``frac`` is the matrix pipe's occupancy at the nominal 2.4 GHz; kernel
   time from hipEvents around the harmonic-sum kernels on their stream; ``traffic`` from the same tree's rocprofv3
-  PMC pass (profiles/r02/pmc_traffic.json) when it was taken on this workload;
+  PMC pass (profiles/r03/pmc_traffic.json, tools/pmc_round.sh) when it was taken on this workload;
 * ``cpu_baseline``: the oracle (oracle/liborc.so, fp64, OpenMP over trials) on a bounded sample;
 * ``fast_path``: the opt-in fp32 sin/cos path (precision="fast") on the same workload, for comparison;
 * ToA (config 5 per GPU): the device fit of 1250 intervals x 1e5 photons, and the end-to-end ``measure_intervals``
@@ -42,7 +42,7 @@ OPS_PER_EVAL_HARM = 128.0       # (8 x 65536 dense + 4 x 131072 sparse ops) per 
 PEAK_HBM_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E ~8 TB/s
 PEAK_VALU_SLOTS = 256 * 4 * 32 * 2.4e9   # fp32 lane-ops/s: 256 CUs x 4 SIMD-32 x 2.4 GHz
 PEAK_F64_OPS = 256 * 64 * 2.4e9          # fp64 FMA-rate lane-ops/s: half the fp32 rate (78.6 TFLOP/s fp64 vector)
-PMC_FILE = os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r03", "pmc_traffic.json")
 
 
 def parse():
@@ -399,7 +399,7 @@ def cpu_baseline(t, f0, df, nharm, budget_s):
 
 def pmc_traffic(photons, trials, nharm):
     """HBM bytes per search of this workload from the tree's own rocprofv3 PMC pass (tools/pmc_exact.sh ->
-    profiles/r02/pmc_traffic.json), or None if that pass was not taken on this workload."""
+    profiles/r03/pmc_traffic.json), or None if that pass was not taken on this workload."""
     try:
         rec = json.load(open(PMC_FILE))
     except (OSError, ValueError):
