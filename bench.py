@@ -145,10 +145,12 @@ def toa_leg(a, dev, world, rank):
     # NN = norms evaluated per phShift (the pruned candidates, crimp_last_toa_grid_norms); fp32 peak = 256 CUs x 4
     # SIMDs x 32 lanes x 2.4 GHz = 7.86e13 lane-ops/s (packed or not). Fit: per photon and likelihood pass, in fp64
     # operations (FMA rate, half the fp32 rate: 3.93e13/s): table sin/cos 14, per harmonic the Chebyshev step (2)
-    # and h, h', h'' (7) = 9K, the model add 1, the reciprocal 5 (v_rcp_f64 + two Newton steps), ln as 1/4 of a fp64
-    # log (~29) + a multiply = 8.25, 6 sums and fmin 9 -> S_full = 37 + 9K; a pass that reads the cached template
-    # part (norm re-profile of the 1-sigma scan): S_cached = 17 (the add, reciprocal, ln, two sums and fmin). Passes
-    # per interval from the fit's own counters.
+    # and h, h', h'' (7) = 9K, the model add 1, the reciprocal 5 (v_rcp_f64 + two Newton steps), ln as 1/8 of a fp64
+    # log (~29) + a multiply = 4.6, 6 sums and fmin 9 -> S_full = 33 + 9K (the Newton ascent's passes); the first
+    # pass of each 1-sigma-scan norm profile forms h alone (5 per harmonic, 3 sums): S_store = 27 + 5K; a pass that
+    # reads the cached template part: S_cached = 13 (the add, reciprocal, ln, two sums and fmin). Passes per interval
+    # from the fit's own counters: cached ones in out[7]; one store pass per scan step, kk - 1 per side where the
+    # side's sigma is kk step + step / 2.
     K = len(T2259["amp"])
     nn = int(N.load().crimp_last_toa_grid_norms())
     nphi = 126
@@ -163,14 +165,18 @@ def toa_leg(a, dev, world, rank):
                                    "k_toa_grid_best); peak 256 CU x 4 SIMD x 32 lanes x 2.4 GHz"}
     fev = np.asarray(res["evaluations"], dtype=np.float64)
     fca = np.asarray(res["cached_evaluations"], dtype=np.float64)
-    f_ops = float(np.sum((fev - fca) * (37 + 9 * K) + fca * 17) * a.toa_photons)
+    step = 2 * np.pi / f.res
+    fst = (np.rint((res["phShi_LL"] - step / 2) / step) - 1) + (np.rint((res["phShi_UL"] - step / 2) / step) - 1)
+    fnw = fev - fca - fst
+    f_ops = float(np.sum(fnw * (33 + 9 * K) + fst * (27 + 5 * K) + fca * 13) * a.toa_photons)
     f_ach = f_ops / (fit_ms * 1e-3)
     out["toa_fit_roofline"] = {"kernel": "k_toa_fit", "bound": "valu", "achieved": f_ach / 1e12,
                                "peak": PEAK_F64_OPS / 1e12, "unit": "Tlane-op/s (fp64)", "frac": f_ach / PEAK_F64_OPS,
-                               "full_passes_per_interval": float(np.mean(fev - fca)),
+                               "newton_passes_per_interval": float(np.mean(fnw)),
+                               "store_passes_per_interval": float(np.mean(fst)),
                                "cached_passes_per_interval": float(np.mean(fca)),
-                               "note": "S_full = 37 + 9K fp64 ops per photon and likelihood pass, S_cached = 17 for "
-                                       "a pass over the cached template part; passes from the fit's own counters / "
+                               "note": "S_full = 33 + 9K fp64 ops per photon and Newton pass, S_store = 27 + 5K for a "
+                                       "scan profile's first pass, S_cached = 13 for a pass over the cached template part; passes from the fit's own counters / "
                                        "k_toa_fit hipEvent time; peak fp64 FMA rate 256 CU x 64 lanes x 2.4 GHz"}
     # end to end from host arrays: photon times t = (cycle + phase) / F0 around PEPOCH, intervals bracketing them
     F0, pep = 0.5, 58000.0

@@ -698,6 +698,26 @@ __device__ __forceinline__ void tpl_terms_fourier(const double (&al)[KF], const 
     }
 }
 
+// h alone (no phShift derivatives), bit-identical to tpl_terms_fourier's h
+template <int KF>
+__device__ __forceinline__ void tpl_value_fourier(const double (&al)[KF], const double (&be)[KF], double s1, double c1,
+                                                  double& h) {
+    h = 0.0;
+    const double tc = c1 + c1;
+    double cj = c1, sj = s1, cp = 1.0, sp = 0.0;
+#pragma unroll
+    for (int j = 0; j < KF; ++j) {
+        h += fma(al[j], cj, be[j] * sj);
+        if (j + 1 < KF) {
+            const double cn = fma(tc, cj, -cp), sn = fma(tc, sj, -sp);
+            cp = cj;
+            sp = sj;
+            cj = cn;
+            sj = sn;
+        }
+    }
+}
+
 // One block per group of <= 4 points of one interval; lanes stride the photons. fp64.
 // Coefficient table per point (LDS): fourier  a_j = A cos(ph_j - j phi), b_j = -A sin(ph_j - j phi)
 //                                    cauchy/vm a_j = cos(cen_j + phi),   b_j = sin(cen_j + phi)

@@ -66,11 +66,16 @@ __device__ __forceinline__ double sigma_bound(int kk, double step) {
 // later passes read it instead of recomputing sin/cos and the template terms. The stored value is the
 // recomputed one bit for bit, so the sums are unchanged.
 enum : int { kHNone = 0, kHStore = 1, kHLoad = 2 };
-constexpr int kFitProd = 4;  // model values per fp64 log in fit_eval
+// model values per fp64 log: 8 (12.03 -> 11.33 ms per 1250 config-5 fits, profiles/r03/ab_fit_store_prod8.log);
+// exact for model values in (1e-38, 1e38), where no product of 8 leaves the fp64 range
+#ifndef CRIMP_FIT_PROD
+#define CRIMP_FIT_PROD 8
+#endif
+constexpr int kFitProd = CRIMP_FIT_PROD;  // model values per fp64 log in fit_eval
 
 // Reference extended LL (templatemodels.py:109-121, :213-226, :318-329) with its (norm, phShift) gradient and
 // Hessian at (n, phi), from one pass over photons x[a, b) (as toafit.ToAFitter.evaluate assembles them).
-// kHLoad passes return the LL and the norm derivatives only (gp, hnp, hpp are 0). MODEL and (Fourier) the template
+// kHStore and kHLoad passes return the LL and the norm derivatives only (gp, hnp, hpp are 0). MODEL and (Fourier) the template
 // size KF are compile-time (KF = 0: K from the template at run time), as in k_toa_grid.
 template <int MODEL, int KF>
 __device__ FitEval fit_eval(const double* __restrict__ x, int64_t a, int64_t b, const TplDev* __restrict__ T, double n,
@@ -85,8 +90,8 @@ __device__ FitEval fit_eval(const double* __restrict__ x, int64_t a, int64_t b, 
     double acc[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
     double mn = INFINITY;
     // sum of ln(model) as ln of products of kFitProd consecutive (per thread) model values: one fp64 log per
-    // kFitProd photons; a product of <= 4 model values in (1e-75, 1e75) stays in the fp64 range and adds <= 3
-    // roundings (~3e-16 relative). A non-positive model makes the LL -inf through min(model) below.
+    // kFitProd photons; a product of <= 8 model values in (1e-38, 1e38) stays in the fp64 range and adds <= 7
+    // roundings (~8e-16 relative). A non-positive model makes the LL -inf through min(model) below.
     double pr = 1.0;
     int np = 0;
     auto lnacc = [&](double mv) {
@@ -115,14 +120,34 @@ __device__ FitEval fit_eval(const double* __restrict__ x, int64_t a, int64_t b, 
               be[j] = sh.coef[1][j];
           }
       }
-      for (int64_t i = a + tid; i < b; i += kFitBlock) {
+      if (hmode == kHStore) {
+        // the first pass of a norm profile: the profile reads only LL, dLL/dnorm and d2LL/dnorm2, so the phShift
+        // derivatives h', h'' are not formed (the Fourier template: 5 instead of 9 operations per harmonic); h and
+        // the sums are formed exactly as in the full pass
+        for (int64_t i = a + tid; i < b; i += kFitBlock) {
+            double s1, c1, h;
+            fit_sincos(model, sh, x[i], s1, c1);
+            if constexpr (MODEL == CRIMP_MODEL_FOURIER && KF > 0) {
+                tpl_value_fourier<KF>(al, be, s1, c1, h);
+            } else {
+                double h1, h2;
+                tpl_terms(T, model, K, sh.coef[0], sh.coef[1], s1, c1, h, h1, h2);
+            }
+            hc[i] = h;
+            const double mv = n + h;
+            const double q = lk_rcp(mv);
+            lnacc(mv);
+            acc[1] += q;
+            acc[3] -= q * q;
+            mn = fmin(mn, mv);
+        }
+      } else for (int64_t i = a + tid; i < b; i += kFitBlock) {
         double s1, c1, h, h1, h2;
         fit_sincos(model, sh, x[i], s1, c1);
         if constexpr (MODEL == CRIMP_MODEL_FOURIER && KF > 0)
             tpl_terms_fourier<KF>(al, be, s1, c1, h, h1, h2);
         else
             tpl_terms(T, model, K, sh.coef[0], sh.coef[1], s1, c1, h, h1, h2);
-        if (hmode == kHStore) hc[i] = h;
         const double mv = n + h;
         const double q = lk_rcp(mv);
         lnacc(mv);
