@@ -338,8 +338,8 @@ def config4_leg(a, dev, world, rank):
                          "frac": ach / PEAK_I8_TOPS,
                          "note": "128 int8 matrix ops per photon*trial*harmonic x 20 harmonics / k_search_exact "
                                  "hipEvent time (the harmonic launches of the search)"},
-            "workload": "config4: 1e8 photons, H_20, 2-D grid 1e5 f x 100 fdot = 1e7 trials sharded over %d rank(s); "
-                        "first %d trials of the rank's shard timed" % (world, count)}
+            "workload": "config4: %.3g photons, H_20, 2-D grid 1e5 f x 100 fdot = 1e7 trials sharded over %d rank(s); "
+                        "first %d trials of the rank's shard timed" % (n, world, count)}
 
 
 def calcphase_leg(a, dev):
@@ -422,10 +422,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # CRIMP_BENCH_REHEARSE=1: every rank on cuda:0 over gloo, to run the N > 1 code path (sharded search, gathers,
+    # max-over-ranks timing) on a one-GPU box; the numbers of such a run are not a scaling measurement
+    rehearse = os.environ.get("CRIMP_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
     from crimp_amd import ops
     from crimp_amd import _native as N
     from crimp_amd.synth import pulsed_events
