@@ -42,6 +42,7 @@ OPS_PER_EVAL_HARM = 128.0       # (8 x 65536 dense + 4 x 131072 sparse ops) per 
 PEAK_HBM_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E ~8 TB/s
 PEAK_VALU_SLOTS = 256 * 4 * 32 * 2.4e9   # fp32 lane-ops/s: 256 CUs x 4 SIMD-32 x 2.4 GHz
 PEAK_F64_OPS = 256 * 64 * 2.4e9          # fp64 FMA-rate lane-ops/s: half the fp32 rate (78.6 TFLOP/s fp64 vector)
+PEAK_F16_TFLOPS = 2500.0                 # MI355X_MICROARCH.md: dense F16/BF16 MFMA ~2.5 PFLOP/s
 PMC_FILE = os.path.join(ROOT, "profiles", "r03", "pmc_traffic.json")
 
 
@@ -139,11 +140,13 @@ def toa_leg(a, dev, world, rank):
            "toa_shift_recovery_rms_cycles": float(np.sqrt(np.mean(d ** 2)) / (2 * np.pi)),
            "toa_median_sigma_cycles": float(np.median(res["phShi_LL"]) / (2 * np.pi)),
            "toa_kernel_ms": {"k_toa_grid": grid_ms, "k_toa_fit": fit_ms}}
-    # Algorithmic VALU work (SURVEY.md section 8d's lane-slot model). Brute grid: per photon x
-    # phShift, the K-term template as 2K fp32 FMAs, one min, and per evaluated norm an add, 3/4 of a multiply (log2 of a
-    # product of four factors), 1/4 of a quarter-rate v_log_f32 (4 slots) and 1/4 of an add: S_grid = 2K + 1 + 3 NN,
-    # NN = norms evaluated per phShift (the pruned candidates, crimp_last_toa_grid_norms); fp32 peak = 256 CUs x 4
-    # SIMDs x 32 lanes x 2.4 GHz = 7.86e13 lane-ops/s (packed or not). Fit: per photon and likelihood pass, in fp64
+    # Algorithmic work (SURVEY.md section 8d's lane-slot model). Brute grid (k_toa_grid_mf): the
+    # template part h of every photon x phShift point is a (photons x 2K) . (2K x phShifts) product on the f16 matrix
+    # cores (each fp32 factor as hi + lo f16, four products per term: 8K f16 MACs per point, padded to 16 per pair of
+    # harmonics); the VALU does the likelihood part, one min and per evaluated norm an add, 3/4 of a multiply, 1/4 of a
+    # quarter-rate v_log_f32 (4 slots) and 1/4 of an add: S_grid = 1 + 3 NN fp32 lane-op slots per point, NN = norms
+    # evaluated per phShift (the pruned candidates, crimp_last_toa_grid_norms); fp32 peak = 256 CUs x 4 SIMDs x 32
+    # lanes x 2.4 GHz = 7.86e13 lane-ops/s. Fit: per photon and likelihood pass, in fp64
     # operations (FMA rate, half the fp32 rate: 3.93e13/s): table sin/cos 14, per harmonic the Chebyshev step (2)
     # and h, h', h'' (7) = 9K, the model add 1, the reciprocal 5 (v_rcp_f64 + two Newton steps), ln as 1/8 of a fp64
     # log (~29) + a multiply = 4.6, 6 sums and fmin 9 -> S_full = 33 + 9K (the Newton ascent's passes); the first
@@ -155,14 +158,19 @@ def toa_leg(a, dev, world, rank):
     nn = int(N.load().crimp_last_toa_grid_norms())
     nphi = 126
     nph_tot = float(a.toa_intervals) * a.toa_photons
-    g_slots = nph_tot * nphi * (2 * K + 1 + 3 * nn)
+    g_slots = nph_tot * nphi * (1 + 3 * nn)
     g_ach = g_slots / (grid_ms * 1e-3)
-    out["toa_roofline"] = {"kernel": "k_toa_grid", "bound": "valu", "achieved": g_ach / 1e12,
+    g_mf = nph_tot * nphi * 2 * 16 * ((K + 1) // 2) / (grid_ms * 1e-3)   # f16 matrix FLOP/s issued
+    out["toa_roofline"] = {"kernel": "k_toa_grid_mf", "bound": "valu", "achieved": g_ach / 1e12,
                            "peak": PEAK_VALU_SLOTS / 1e12, "unit": "Tlane-op/s (fp32)", "frac": g_ach / PEAK_VALU_SLOTS,
-                           "norms_evaluated": nn, "slots_per_photon_phshift": 2 * K + 1 + 3 * nn,
-                           "note": "S_grid = 2K + 1 + 3 NN fp32 lane-op slots per photon x phShift (v_log_f32 at 4) x "
-                                   "1250 x 1e5 photons x 126 phShifts / brute-grid hipEvent time (k_toa_grid + "
-                                   "k_toa_grid_best); peak 256 CU x 4 SIMD x 32 lanes x 2.4 GHz"}
+                           "norms_evaluated": nn, "slots_per_photon_phshift": 1 + 3 * nn,
+                           "matrix": {"achieved": g_mf / 1e12, "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s (f16 dense)",
+                                      "frac": g_mf / 1e12 / PEAK_F16_TFLOPS},
+                           "note": "S_grid = 1 + 3 NN fp32 lane-op slots per photon x phShift (v_log_f32 at 4) beside "
+                                   "the template on v_mfma_f32_32x32x16_f16 (hi/lo f16 split, 16 MACs per pair of "
+                                   "harmonics), x 1250 x 1e5 photons x 126 phShifts / brute-grid hipEvent time "
+                                   "(k_toa_grid_mf + k_toa_grid_best); peaks 256 CU x 4 SIMD x 32 lanes x 2.4 GHz, "
+                                   "f16 dense 2.5 PFLOP/s"}
     fev = np.asarray(res["evaluations"], dtype=np.float64)
     fca = np.asarray(res["cached_evaluations"], dtype=np.float64)
     step = 2 * np.pi / f.res

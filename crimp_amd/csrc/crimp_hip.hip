@@ -816,6 +816,9 @@ constexpr int kGridProd = 4;
 constexpr int64_t kGridTarget = 16384;  // brute-grid blocks per launch (toa_grid_partials)
 static_assert(kGridNN % 2 == 0 && kGridProd == 4, "norm pairs; photons in two pairs per product");
 constexpr int kGridNNSmall = 4;  // the pruned brute grid's norms per lane (crimp_toa_fit)
+#ifndef CRIMP_GRID_MFMA
+#define CRIMP_GRID_MFMA 1  // Fourier brute grid on the f16 matrix cores (k_toa_grid_mf)
+#endif
 #ifndef CRIMP_GRID_PPL
 #define CRIMP_GRID_PPL 2
 #endif
@@ -1014,6 +1017,150 @@ __global__ __launch_bounds__(kGridBlock) __attribute__((amdgpu_waves_per_eu(4)))
                 if (a < na) lnsum[((split * nint + iv) * nnorm + a0 + a) * nphi + bphi[p]] = acc[p][a];
             if (a0 == 0) hmin[(split * nint + iv) * nphi + bphi[p]] = (double)hmn[p];
         }
+    }
+}
+
+// Brute grid of a Fourier template on the f16 matrix cores (the default for Fourier templates of <= 8 harmonics;
+// CRIMP_GRID_MFMA=0 builds the VALU kernel above for them too). The template part of every (photon, phShift)
+// point is a product of the photon's basis (cos jx, sin jx) and the phShift's coefficients (a_j, b_j):
+// h = sum_j a_j cos jx + b_j sin jx, i.e. one (32 photons x 2K) . (2K x 32 phShifts) matrix product per tile. Each
+// fp32 factor is carried as hi + lo f16 (search_fast.h split_xy; |x - hi - lo| <= 2^-22 |x|) and the four exact
+// products hi.hi, hi.lo, lo.hi, lo.lo of each term fill K = 8 per harmonic of v_mfma_f32_32x32x16_f16 (two harmonics
+// per instruction, fp32 accumulation). The VALU is left with the likelihood part: per point and evaluated norm an
+// add, 3/4 of a multiply and 1/4 of a v_log_f32 (log2 of products of 4 photons, as k_toa_grid), and the min.
+// Block: 4 waves, wave w owns the 32 phShift columns 128 bx + 32 w + (lane & 31); a 128-photon tile's A fragments
+// (per photon and harmonic 16 bytes: hi, hi, lo, lo of cos then of sin) are built once per tile in LDS by the whole
+// block. MFMA result i of lane l is photon (i & 3) + 8 (i >> 2) + 4 (l >> 5) of the 32-photon chunk, phShift column
+// l & 31, so each lane multiplies 4 consecutive photons per group; the two lane halves' sums of a column are added
+// (half 0 + half 1) at the end. fp64 folds every 32-photon chunk; deterministic, not bit-identical to k_toa_grid.
+constexpr int kGmTile = 128;  // photons per LDS tile
+template <int KF, int NN>
+__global__ __launch_bounds__(256) void k_toa_grid_mf(const double* __restrict__ x, const int64_t* __restrict__ offsets,
+                                                     const TplDev* __restrict__ T, const double* __restrict__ norm,
+                                                     int nnorm, int a0, int na, const double* __restrict__ phi, int nphi,
+                                                     int64_t chunk, int nint, double* __restrict__ lnsum,
+                                                     double* __restrict__ hmin) {
+    constexpr int NM = (KF + 1) / 2;  // MFMAs per 32-photon chunk (two harmonics each)
+    __shared__ __attribute__((aligned(16))) u32x4 afr[kGmTile][2 * NM];  // [photon][harmonic]
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hk = lane >> 5;
+    const int64_t iv = blockIdx.y, split = blockIdx.z;
+    const int bphi = blockIdx.x * kGridBlock + 32 * wv + (lane & 31);
+    // B fragments: the lane's phShift coefficients of harmonics 2m + hk + 1 (zero past K)
+    f16x8 bf[NM];
+    {
+        const double ph = phi[bphi < nphi ? bphi : nphi - 1];
+#pragma unroll
+        for (int m = 0; m < NM; ++m) {
+            const int j = 2 * m + hk;
+            float ca = 0.0f, cb = 0.0f;
+            if (j < KF) {
+                const double d = T->loc[j] - (double)(j + 1) * ph;
+                ca = (float)(T->amp[j] * cos(d));
+                cb = (float)(-T->amp[j] * sin(d));
+            }
+            uint32_t dh, dl;
+            split_xy<false>(ca, cb, dh, dl);
+            const uint32_t wc = (dh & 0xffffu) | (dl << 16), ws = (dh >> 16) | (dl & 0xffff0000u);
+            const u32x4 w = {wc, wc, ws, ws};
+            bf[m] = __builtin_bit_cast(f16x8, w);
+        }
+    }
+    f32x2 nr[NN / 2];
+#pragma unroll
+    for (int a = 0; a < NN; ++a) nr[a / 2][a % 2] = (a < na) ? (float)norm[iv * nnorm + a0 + a] : 1.0f;
+    double acc[NN];
+#pragma unroll
+    for (int a = 0; a < NN; ++a) acc[a] = 0.0;
+    float hmn = INFINITY;
+    const int64_t beg = offsets[iv] + split * chunk;
+    const int64_t end = std::min<int64_t>(offsets[iv + 1], beg + chunk);
+    for (int64_t base = beg; base < end; base += kGmTile) {
+        const int cnt = (int)std::min<int64_t>(kGmTile, end - base);
+        __syncthreads();
+        {   // A fragments: thread (photon p = tid & 127, half g = tid >> 7) builds harmonics g*4 + 1 .. g*4 + 4
+            const int p = tid & (kGmTile - 1), g = tid >> 7;
+            float c1 = 1.0f, s1 = 0.0f;
+            if (p < cnt) {
+                double rv = x[base + p];
+                rv -= rint(rv);
+                sincos_rev_poly((float)rv, s1, c1);
+            }
+            float cj = c1, sj = s1;
+#pragma unroll
+            for (int j = 0; j < 2 * NM; ++j) {
+                if (j >= 4 * g && j < 4 * g + 4) {
+                    uint32_t dh, dl;
+                    split_xy<false>(cj, sj, dh, dl);
+                    const uint32_t hc = dh & 0xffffu, hs = dh >> 16, lc = dl & 0xffffu, ls = dl >> 16;
+                    afr[p][j] = u32x4{hc | (hc << 16), lc | (lc << 16), hs | (hs << 16), ls | (ls << 16)};
+                }
+                const float cn = __builtin_fmaf(cj, c1, -sj * s1);
+                sj = __builtin_fmaf(sj, c1, cj * s1);
+                cj = cn;
+            }
+        }
+        __syncthreads();
+        for (int q0 = 0; q0 < cnt; q0 += 32) {
+            f32x16 hv = {};
+#pragma unroll
+            for (int m = 0; m < NM; ++m) {
+                const f16x8 av = __builtin_bit_cast(f16x8, afr[q0 + (lane & 31)][2 * m + hk]);
+                hv = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bf[m], hv, 0, 0, 0);
+            }
+            f32x2 pa[NN / 2];
+#pragma unroll
+            for (int b = 0; b < NN / 2; ++b) pa[b] = f32x2{0.0f, 0.0f};
+            if (q0 + 32 <= cnt) {
+#pragma unroll
+                for (int gi = 0; gi < 4; ++gi) {
+                    const float h0 = hv[4 * gi], h1 = hv[4 * gi + 1], h2 = hv[4 * gi + 2], h3 = hv[4 * gi + 3];
+                    hmn = fminf(fminf(fminf(fminf(hmn, h0), h1), h2), h3);
+#pragma unroll
+                    for (int b = 0; b < NN / 2; ++b) {
+                        f32x2 pr = nr[b] + h0;
+                        pr *= nr[b] + h1;
+                        pr *= nr[b] + h2;
+                        pr *= nr[b] + h3;
+                        pa[b] += f32x2{__builtin_amdgcn_logf(pr.x), __builtin_amdgcn_logf(pr.y)};
+                    }
+                }
+            } else {  // the tile's last, partial chunk: photons past cnt contribute a factor 1
+#pragma unroll
+                for (int gi = 0; gi < 4; ++gi) {
+                    f32x2 pr[NN / 2];
+#pragma unroll
+                    for (int b = 0; b < NN / 2; ++b) pr[b] = f32x2{1.0f, 1.0f};
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int row = q0 + r + 8 * gi + 4 * hk;
+                        if (row < cnt) {
+                            const float h = hv[4 * gi + r];
+                            hmn = fminf(hmn, h);
+#pragma unroll
+                            for (int b = 0; b < NN / 2; ++b) pr[b] *= nr[b] + h;
+                        }
+                    }
+#pragma unroll
+                    for (int b = 0; b < NN / 2; ++b)
+                        pa[b] += f32x2{__builtin_amdgcn_logf(pr[b].x), __builtin_amdgcn_logf(pr[b].y)};
+                }
+            }
+#pragma unroll
+            for (int a = 0; a < NN; ++a) acc[a] += (double)pa[a / 2][a % 2];
+        }
+    }
+    // the column's two lane halves: half 0 + half 1
+#pragma unroll
+    for (int a = 0; a < NN; ++a) {
+        const double o = __shfl_xor(acc[a], 32);
+        acc[a] = hk == 0 ? acc[a] + o : o + acc[a];
+    }
+    hmn = fminf(hmn, __shfl_xor(hmn, 32));
+    if (hk == 0 && bphi < nphi) {
+#pragma unroll
+        for (int a = 0; a < NN; ++a)
+            if (a < na) lnsum[((split * nint + iv) * nnorm + a0 + a) * nphi + bphi] = acc[a];
+        if (a0 == 0) hmin[(split * nint + iv) * nphi + bphi] = (double)hmn;
     }
 }
 
@@ -1876,7 +2023,24 @@ static int toa_grid_partials(Scratch& sc, hipStream_t s, const double* dx, const
 #define CRIMP_LG(MD, KK) do { if (nn == 2) CRIMP_LG1(MD, KK, 2, kGridPPL); \
                               else if (nn == kGridNNSmall) CRIMP_LG1(MD, KK, kGridNNSmall, kGridPPL); \
                               else CRIMP_LG1(MD, KK, kGridNN, 1); } while (0)
-        if (model == CRIMP_MODEL_FOURIER) {
+        if (model == CRIMP_MODEL_FOURIER && CRIMP_GRID_MFMA && K <= kGridKMax) {
+#define CRIMP_LM1(KK, NNV) k_toa_grid_mf<KK, NNV><<<grid, 256, 0, s>>>(dx, doff, dT, dnrm, (int)nnorm, (int)a0, na, dphi, \
+                                                                       (int)nphi, chunk, (int)nint, *pl, *ph)
+#define CRIMP_LM(KK) do { if (nn == 2) CRIMP_LM1(KK, 2); else if (nn == kGridNNSmall) CRIMP_LM1(KK, kGridNNSmall); \
+                          else CRIMP_LM1(KK, kGridNN); } while (0)
+            switch (K) {
+                case 1: CRIMP_LM(1); break;
+                case 2: CRIMP_LM(2); break;
+                case 3: CRIMP_LM(3); break;
+                case 4: CRIMP_LM(4); break;
+                case 5: CRIMP_LM(5); break;
+                case 6: CRIMP_LM(6); break;
+                case 7: CRIMP_LM(7); break;
+                default: CRIMP_LM(8); break;
+            }
+#undef CRIMP_LM
+#undef CRIMP_LM1
+        } else if (model == CRIMP_MODEL_FOURIER) {
             switch (K) {
                 case 1: CRIMP_LG(CRIMP_MODEL_FOURIER, 1); break;
                 case 2: CRIMP_LG(CRIMP_MODEL_FOURIER, 2); break;
