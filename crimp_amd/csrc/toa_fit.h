@@ -229,6 +229,9 @@ __device__ double fit_profile(const double* __restrict__ x, int64_t a, int64_t b
         step = clipd(step, -0.5 * n, 0.5 * n);
         if (bad) step = 0.5 * n;  // infeasible: model <= 0 somewhere, raise the norm
         double nn = clipd(n + step, C.lo, C.hi);
+        // converged: the next pass would move the norm by <= 1e-13 of it, so its LL equals this one's to ~1e-26
+        // relative; stop without it (toafit.profile_norm does the same)
+        if (isfinite(e.ll) && fabs(nn - n) <= 1e-13 * fmax(1.0, n)) break;
         FitEval e2 = fit_eval<MODEL, KF>(x, a, b, T, nn, phi, E, C, sh, hc, hm);
         ++nev;
         if (ncached && hc) ++*ncached;
@@ -503,6 +506,11 @@ __global__ __launch_bounds__(kFitBlock) __attribute__((amdgpu_waves_per_eu(CRIMP
     for (int it = 0; it < 60; ++it) {  // toafit.maximise
         double dn, dp;
         fit_newton_dir(n, e, dn, dp);
+        {   // converged: even the full step moves less than the stopping tolerance, so the pass that would confirm
+            // it is skipped (toafit.maximise does the same)
+            const double fn = clipd(n + dn, C.lo, C.hi), fp = clipd(p + dp, -C.pb, C.pb);
+            if (isfinite(e.ll) && fabs(fp - p) < 1e-12 && fabs(fn - n) < 1e-12 * fmax(1.0, fabs(fn))) break;
+        }
         double t = 1.0, tn = n, tp = p;
         FitEval e2 = e;
         bool ok = false;

@@ -163,6 +163,17 @@ class ToAFitter:
             if act.size == 0:
                 break
             dn, dp = self._newton_step(n[act], g[act], H[act])
+            # converged: even the full step moves less than the stopping tolerance (no confirming pass)
+            fn = np.clip(n[act] + dn, self.lo, self.hi)
+            fp = np.clip(phi[act] + dp, -self.pb, self.pb)
+            pre = np.isfinite(ll[act]) & (np.abs(fp - phi[act]) < 1e-12) & (
+                np.abs(fn - n[act]) < 1e-12 * np.maximum(1.0, np.abs(fn)))
+            if pre.any():
+                active[act[pre]] = False
+                keep = ~pre
+                act, dn, dp = act[keep], dn[keep], dp[keep]
+                if act.size == 0:
+                    break
             t = np.ones(act.size)
             pending = np.ones(act.size, dtype=bool)
             new_n, new_p = n[act].copy(), phi[act].copy()
@@ -210,21 +221,30 @@ class ToAFitter:
         iv = np.asarray(iv)
         n = np.clip(np.array(n_start, dtype=np.float64), self.lo, self.hi)
         ll, g, H = self.evaluate(iv, n, phi)
+        converged = np.zeros(n.size, dtype=bool)
         for _ in range(max_iter):
             bad = ~np.isfinite(ll)
             step = np.where(H[:, 0] < 0, -g[:, 0] / np.where(H[:, 0] < 0, H[:, 0], -1.0), 0.1 * n)
             step = np.clip(step, -0.5 * n, 0.5 * n)
             step = np.where(bad, 0.5 * n, step)  # infeasible: model <= 0 somewhere, raise the norm
             nn = np.clip(n + step, self.lo, self.hi)
-            l2, g2, H2 = self.evaluate(iv, nn, phi)
-            worse = np.isfinite(ll) & (~np.isfinite(l2) | (l2 < ll - 1e-12 * np.abs(ll)))
+            # converged: the next pass would move the norm by <= 1e-13 of it (no confirming pass)
+            done = np.isfinite(ll) & (np.abs(nn - n) <= 1e-13 * np.maximum(1.0, n)) | converged
+            converged = done
+            if np.all(done):
+                break
+            w = np.nonzero(~done)[0]
+            l2, g2, H2 = self.evaluate(iv[w], nn[w], phi[w])
+            worse = np.isfinite(ll[w]) & (~np.isfinite(l2) | (l2 < ll[w] - 1e-12 * np.abs(ll[w])))
             if np.any(worse):  # damp the few overshoots
-                nn[worse] = np.clip(n[worse] + 0.25 * step[worse], self.lo, self.hi)
-                l3, g3, H3 = self.evaluate(iv[worse], nn[worse], phi[worse])
+                ww = w[worse]
+                nn[ww] = np.clip(n[ww] + 0.25 * step[ww], self.lo, self.hi)
+                l3, g3, H3 = self.evaluate(iv[ww], nn[ww], phi[ww])
                 l2[worse], g2[worse], H2[worse] = l3, g3, H3
-            conv = np.abs(nn - n) <= 1e-13 * np.maximum(1.0, n)
-            n, ll, g, H = nn, l2, g2, H2
-            if np.all(conv):
+            conv = np.abs(nn[w] - n[w]) <= 1e-13 * np.maximum(1.0, n[w])
+            n[w], ll[w], g[w], H[w] = nn[w], l2, g2, H2
+            converged[w[conv]] = True
+            if np.all(converged):
                 break
         return n, ll
 
