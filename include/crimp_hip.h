@@ -145,7 +145,8 @@ int crimp_toa_points(const double* x, const int64_t* offsets, int64_t nint, cons
  * for every interval i, norm a, phShift b:
  *   lnsum[(i*nnorm + a)*nphi + b] = sum_photons ln(norm[i*nnorm+a] + h(x; phi[b]))
  *   hmin[i*nphi + b]              = min_photons h(x; phi[b])
- * fp32 model + logarithm, fp64 accumulation. */
+ * fp32 model + logarithm, fp64 accumulation; a Fourier template's part on the f16 matrix cores with every fp32
+ * factor split hi + lo (fp32-level products), the likelihood part on the VALU. */
 int crimp_toa_grid(const double* x, const int64_t* offsets, int64_t nint, const crimp_template* tpl,
                    const double* norm, int64_t nnorm, const double* phi, int64_t nphi, double* lnsum,
                    double* hmin, uint32_t flags, void* stream);
