@@ -2192,7 +2192,7 @@ extern "C" int crimp_toa_fit(const double* x, const int64_t* offsets, int64_t ni
                 if (rc) return rc;
                 k_toa_grid_best<<<(unsigned)nb, 256, 0, s>>>(pl, ph, dnrm + i0 * nc, dphi, doff + i0, de + i0, (int)nc,
                                                             (int)nphi, (int)nb, (int)splits, T.model, C.sum_amp,
-                                                            grid_n[0], dstart + 2 * i0);
+                                                            grid_n[0], C.lo, C.hi, dstart + 2 * i0);
                 HIPCHK(hipGetLastError());
             }
             kg.stop();

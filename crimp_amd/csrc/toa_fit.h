@@ -584,7 +584,7 @@ __global__ __launch_bounds__(256) void k_toa_grid_best(const double* __restrict_
                                                        const int64_t* __restrict__ offsets,
                                                        const double* __restrict__ expo, int nnorm, int nphi, int nint,
                                                        int splits, int model, double sum_amp, double norm_first,
-                                                       double* __restrict__ start) {
+                                                       double lo, double hi, double* __restrict__ start) {
     __shared__ double bv[4];
     __shared__ int bi[4];
     const int64_t iv = blockIdx.x;
@@ -638,8 +638,17 @@ __global__ __launch_bounds__(256) void k_toa_grid_best(const double* __restrict_
             start[2 * iv] = norm_first;
             start[2 * iv + 1] = phi[0];
         } else {
-            start[2 * iv] = norm[iv * nnorm + bidx / nphi];
-            start[2 * iv + 1] = phi[bidx % nphi];
+            // the ascent starts at the lattice phShift with the norm at the photon rate N/E (the profile optimum
+            // solves sum_i 1/(n + h_i) = E, so n* ~ N/E - <h>: within a few % where the lattice is one 26-unit norm
+            // step away), unless that is outside the bounds or makes the model non-positive at this phShift; the
+            // lattice norm otherwise. Same basin, same maximum, two fewer Newton passes (toafit.fit_host does the same)
+            const double r = N / E;
+            double hmx = INFINITY;
+            const int bj = bidx % nphi;
+            for (int sp = 0; sp < splits; ++sp) hmx = fmin(hmx, ph[((int64_t)sp * nint + iv) * nphi + bj]);
+            const bool use_rate = r >= lo && r <= hi && hmx + r > 0.0;
+            start[2 * iv] = use_rate ? r : norm[iv * nnorm + bidx / nphi];
+            start[2 * iv + 1] = phi[bj];
         }
     }
 }

@@ -127,7 +127,7 @@ class ToAFitter:
         return ll, g, H
 
     # ------------------------------------------------------------------ step 1: brute grid
-    def brute(self):
+    def brute(self, with_hmin=False):
         nphi = int(math.ceil((2 * self.pb) / (0.05 * 1.0)))
         phis = np.arange(nphi) * 0.05 + (-self.pb)                            # numpy mgrid lattice
         norms = np.arange(20) * ((self.hi - self.lo) / float(20 - 1)) + self.lo
@@ -149,6 +149,8 @@ class ToAFitter:
         flat = ll.reshape(self.nint, -1)
         idx = np.argmax(flat, axis=1)                                          # first maximum, norm-outer
         a, b = np.unravel_index(idx, (20, nphi))
+        if with_hmin:
+            return norms[a], phis[b], hmin[np.arange(self.nint), b]
         return norms[a], phis[b]
 
     # ------------------------------------------------------------------ step 2: 2-D ascent
@@ -347,7 +349,11 @@ class ToAFitter:
     def fit_host(self, brutemin=False):
         """The same fit driven from the host, one batched likelihood launch per iteration (cross-check of fit)."""
         if brutemin:
-            n0, p0 = self.brute()
+            n0, p0, hm = self.brute(with_hmin=True)
+            # the ascent's norm start: the photon rate N/E where it is inside the bounds and keeps the model positive
+            # at the lattice phShift (k_toa_grid_best does the same)
+            rate = self.N / self.E
+            n0 = np.where((rate >= self.lo) & (rate <= self.hi) & (hm + rate > 0), rate, n0)
         else:
             n0, p0 = np.full(self.nint, self.norm0), np.zeros(self.nint)
         n_hat, phi_hat, ll_max = self.maximise(n0, p0)
