@@ -592,8 +592,7 @@ __global__ __launch_bounds__(256) void k_toa_grid_best(const double* __restrict_
     const double E = expo[iv];
     double best = -INFINITY;
     int bidx = 0x7fffffff;
-    for (int idx = threadIdx.x; idx < nnorm * nphi; idx += 256) {
-        const int ai = idx / nphi, bj = idx - ai * nphi;
+    auto lattice_ll = [&](int ai, int bj) {  // the reference LL of lattice point (norm ai, phShift bj)
         double v = 0.0;
         for (int sp = 0; sp < splits; ++sp) v += pl[(((int64_t)sp * nint + iv) * nnorm + ai) * nphi + bj];
         const double ln = v * 0.69314718055994530942;  // log2 sums -> ln
@@ -608,6 +607,10 @@ __global__ __launch_bounds__(256) void k_toa_grid_best(const double* __restrict_
             ll = -F * E / kTwoPi + N * log(F * E / kTwoPi) + (ln - N * log(F));
         }
         if (!((hm + nn) > 0) || !isfinite(ll)) ll = -INFINITY;
+        return ll;
+    };
+    for (int idx = threadIdx.x; idx < nnorm * nphi; idx += 256) {
+        const double ll = lattice_ll(idx / nphi, idx % nphi);
         if (ll > best || (ll == best && idx < bidx)) {
             best = ll;
             bidx = idx;
@@ -648,7 +651,19 @@ __global__ __launch_bounds__(256) void k_toa_grid_best(const double* __restrict_
             for (int sp = 0; sp < splits; ++sp) hmx = fmin(hmx, ph[((int64_t)sp * nint + iv) * nphi + bj]);
             const bool use_rate = r >= lo && r <= hi && hmx + r > 0.0;
             start[2 * iv] = use_rate ? r : norm[iv * nnorm + bidx / nphi];
-            start[2 * iv + 1] = phi[bj];
+            // and the phShift at the vertex of the parabola through the maximum and its two lattice neighbours (at
+            // the maximum's norm; within half a lattice step), where the model stays well positive
+            double ps = phi[bj];
+            if (use_rate && hmx + r > 0.5 * r && bj >= 1 && bj + 1 < nphi) {
+                const int ai = bidx / nphi;
+                const double lm = lattice_ll(ai, bj - 1), l0 = best, lp = lattice_ll(ai, bj + 1);
+                const double den = lm - 2.0 * l0 + lp;
+                if (isfinite(lm) && isfinite(lp) && den < 0.0) {
+                    const double d = fmin(0.5, fmax(-0.5, 0.5 * (lm - lp) / den));
+                    ps = phi[bj] + d * (phi[bj + 1] - phi[bj]);
+                }
+            }
+            start[2 * iv + 1] = ps;
         }
     }
 }

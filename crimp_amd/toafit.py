@@ -146,11 +146,12 @@ class ToAFitter:
                 ll = -F * E / TWO_PI + N * np.log(F * E / TWO_PI) + (ln - N * np.log(F))
         valid = (hmin[:, None, :] + nn) > 0
         ll = np.where(valid & np.isfinite(ll), ll, -np.inf)
+        ll = ll.reshape(self.nint, 20, nphi)
         flat = ll.reshape(self.nint, -1)
         idx = np.argmax(flat, axis=1)                                          # first maximum, norm-outer
         a, b = np.unravel_index(idx, (20, nphi))
         if with_hmin:
-            return norms[a], phis[b], hmin[np.arange(self.nint), b]
+            return norms[a], phis[b], hmin[np.arange(self.nint), b], ll, a, b
         return norms[a], phis[b]
 
     # ------------------------------------------------------------------ step 2: 2-D ascent
@@ -349,11 +350,24 @@ class ToAFitter:
     def fit_host(self, brutemin=False):
         """The same fit driven from the host, one batched likelihood launch per iteration (cross-check of fit)."""
         if brutemin:
-            n0, p0, hm = self.brute(with_hmin=True)
-            # the ascent's norm start: the photon rate N/E where it is inside the bounds and keeps the model positive
-            # at the lattice phShift (k_toa_grid_best does the same)
+            n0, p0, hm, ll, a, b = self.brute(with_hmin=True)
+            # the ascent's start (k_toa_grid_best does the same): the norm at the photon rate N/E where it is inside
+            # the bounds and keeps the model positive at the lattice phShift; there, if the model stays well positive,
+            # the phShift at the vertex of the parabola through the maximum and its lattice neighbours
             rate = self.N / self.E
-            n0 = np.where((rate >= self.lo) & (rate <= self.hi) & (hm + rate > 0), rate, n0)
+            use = (rate >= self.lo) & (rate <= self.hi) & (hm + rate > 0)
+            n0 = np.where(use, rate, n0)
+            nphi = ll.shape[2]
+            phis = np.arange(nphi) * 0.05 + (-self.pb)
+            iv = np.arange(self.nint)
+            inner = use & (hm + rate > 0.5 * rate) & (b >= 1) & (b + 1 < nphi)
+            bm, bp = np.clip(b - 1, 0, nphi - 1), np.clip(b + 1, 0, nphi - 1)
+            lm, l0, lp = ll[iv, a, bm], ll[iv, a, b], ll[iv, a, bp]
+            den = lm - 2.0 * l0 + lp
+            with np.errstate(invalid="ignore", divide="ignore"):
+                d = np.clip(0.5 * (lm - lp) / den, -0.5, 0.5)
+            ok = inner & np.isfinite(lm) & np.isfinite(lp) & (den < 0)
+            p0 = np.where(ok, phis[b] + d * (phis[bp] - phis[b]), p0)
         else:
             n0, p0 = np.full(self.nint, self.norm0), np.zeros(self.nint)
         n_hat, phi_hat, ll_max = self.maximise(n0, p0)
