@@ -176,15 +176,20 @@ def toa_leg(a, dev, world, rank):
     step = 2 * np.pi / f.res
     fst = (np.rint((res["phShi_LL"] - step / 2) / step) - 1) + (np.rint((res["phShi_UL"] - step / 2) / step) - 1)
     fnw = fev - fca - fst
-    f_ops = float(np.sum(fnw * (33 + 9 * K) + fst * (27 + 5 * K) + fca * 13) * a.toa_photons)
+    # a scan profile's first pass: the moment pass (S_1..S_5, no cached passes) or, in the CRIMP_FIT_MOMENTS=0
+    # build, the pass that stores h for the cached passes
+    s_scan = (27 + 5 * K) if np.any(fca > 0) else (33 + 5 * K)
+    f_ops = float(np.sum(fnw * (33 + 9 * K) + fst * s_scan + fca * 13) * a.toa_photons)
     f_ach = f_ops / (fit_ms * 1e-3)
     out["toa_fit_roofline"] = {"kernel": "k_toa_fit", "bound": "valu", "achieved": f_ach / 1e12,
                                "peak": PEAK_F64_OPS / 1e12, "unit": "Tlane-op/s (fp64)", "frac": f_ach / PEAK_F64_OPS,
                                "newton_passes_per_interval": float(np.mean(fnw)),
                                "store_passes_per_interval": float(np.mean(fst)),
                                "cached_passes_per_interval": float(np.mean(fca)),
-                               "note": "S_full = 33 + 9K fp64 ops per photon and Newton pass, S_store = 27 + 5K for a "
-                                       "scan profile's first pass, S_cached = 13 for a pass over the cached template part; passes from the fit's own counters / "
+                               "scan_pass_ops": s_scan,
+                               "note": "S_full = 33 + 9K fp64 ops per photon and Newton pass, S_scan = 33 + 5K for a "
+                                       "scan profile's moment pass (27 + 5K for the h-storing pass of the iterative "
+                                       "profile), S_cached = 13 for a pass over its cached template part; passes from the fit's own counters / "
                                        "k_toa_fit hipEvent time; peak fp64 FMA rate 256 CU x 64 lanes x 2.4 GHz"}
     # end to end from host arrays: photon times t = (cycle + phase) / F0 around PEPOCH, intervals bracketing them
     F0, pep = 0.5, 58000.0

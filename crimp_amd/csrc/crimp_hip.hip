@@ -2209,8 +2209,10 @@ extern "C" int crimp_toa_fit(const double* x, const int64_t* offsets, int64_t ni
         if (vary_amps) {
             k_toa_fit_amp<<<(unsigned)nint, kFitBlock, 0, s>>>(dx, doff, dT, de, dstart, C, dout);
         } else {
-            double* hcache = nullptr;  // per-photon template part for the norm profiles of the 1-sigma scan
-            HIPCHK(sc.alloc(&hcache, (size_t)hoff[nint]));
+            // per-photon template part for the iterative norm profiles of the 1-sigma scan (only the
+            // CRIMP_FIT_MOMENTS=0 build caches it; the moment profile needs none)
+            double* hcache = nullptr;
+            if (!CRIMP_FIT_MOMENTS) HIPCHK(sc.alloc(&hcache, (size_t)hoff[nint]));
 #define CRIMP_LF(MD, KK) k_toa_fit<MD, KK><<<(unsigned)nint, kFitBlock, 0, s>>>(dx, doff, dT, de, dstart, C, dout, hcache)
             if (T.model == CRIMP_MODEL_FOURIER) {
 #if CRIMP_FIT_GENERIC  // A/B build: the template size read at run time

@@ -6,12 +6,15 @@
 // reduction that every thread reads back, so the workgroup iterates the reference driver itself, with
 // toafit.py's constants and stopping rules:
 //   start   the brute-grid maximum (k_toa_grid partial sums -> k_toa_grid_best) or (norm0, 0);
-//   ascent  damped 2-D Newton in (norm, phShift) with a backtracking line search (toafit.maximise);
-//   1 sigma phShift = best -/+ k*2pi/phShiftRes with lmfit's clip-to-bound semantics, the norm re-profiled by
-//           1-D Newton at every step (toafit.profile_norm); stop at the first LLmax - LL > 0.5*chi2.ppf(0.6827,1)
+//   ascent  damped 2-D Newton in (norm, phShift) with a backtracking line search, the last step below 1e-6 taken
+//           on the quadratic model without a pass (toafit.maximise, the same rule);
+//   1 sigma phShift = best -/+ k*2pi/phShiftRes with lmfit's clip-to-bound semantics, the norm re-profiled at every
+//           step -- from one pass of the moments sum (n0 + h_i)^-p (fit_profile_mom), or by 1-D Newton
+//           (toafit.profile_norm) where that series does not apply; stop at the first LLmax - LL > 0.5*chi2.ppf(0.6827,1)
 //           or once k + 1 > phShiftRes/2 (measureToAs.py:331-376, toafit.error_scan).
 // The evaluation repeats k_toa_points' per-photon arithmetic (tpl_terms), thread striding and reduction
-// order, so its sums equal the host-driven path's.
+// order, so its sums equal the host-driven path's (the moment profile is device-only: its LL agrees with the
+// iterative profile's to ~1e-10, and the scan compares it with a 0.5 threshold).
 
 constexpr int kFitBlock = kPtsBlock;
 constexpr double kHalfChi2OneSigma = 0.500021713558733;  // 0.5 * chi2.ppf(0.6827, 1)   (measureToAs.py:324)
@@ -72,6 +75,12 @@ enum : int { kHNone = 0, kHStore = 1, kHLoad = 2 };
 #define CRIMP_FIT_PROD 8
 #endif
 constexpr int kFitProd = CRIMP_FIT_PROD;  // model values per fp64 log in fit_eval
+// the photon loops load the next photon's time (or cached template part) one iteration ahead, so the load's
+// latency overlaps the current photon's arithmetic (CRIMP_FIT_PREFETCH=0: load at the top of each iteration)
+#ifndef CRIMP_FIT_PREFETCH
+#define CRIMP_FIT_PREFETCH 1
+#endif
+constexpr bool kFitPrefetch = CRIMP_FIT_PREFETCH != 0;
 
 // Reference extended LL (templatemodels.py:109-121, :213-226, :318-329) with its (norm, phShift) gradient and
 // Hessian at (n, phi), from one pass over photons x[a, b) (as toafit.ToAFitter.evaluate assembles them).
@@ -103,8 +112,11 @@ __device__ FitEval fit_eval(const double* __restrict__ x, int64_t a, int64_t b, 
         }
     };
     if (hmode == kHLoad) {
+        double hn = a + tid < b ? hc[a + tid] : 0.0;
         for (int64_t i = a + tid; i < b; i += kFitBlock) {
-            const double mv = n + hc[i];
+            const double hv = hn;
+            if (kFitPrefetch && i + kFitBlock < b) hn = hc[i + kFitBlock];
+            const double mv = n + (kFitPrefetch ? hv : hc[i]);
             const double q = lk_rcp(mv);
             lnacc(mv);
             acc[1] += q;
@@ -124,9 +136,12 @@ __device__ FitEval fit_eval(const double* __restrict__ x, int64_t a, int64_t b, 
         // the first pass of a norm profile: the profile reads only LL, dLL/dnorm and d2LL/dnorm2, so the phShift
         // derivatives h', h'' are not formed (the Fourier template: 5 instead of 9 operations per harmonic); h and
         // the sums are formed exactly as in the full pass
+        double xn = a + tid < b ? x[a + tid] : 0.0;
         for (int64_t i = a + tid; i < b; i += kFitBlock) {
             double s1, c1, h;
-            fit_sincos(model, sh, x[i], s1, c1);
+            const double xv = kFitPrefetch ? xn : x[i];
+            if (kFitPrefetch && i + kFitBlock < b) xn = x[i + kFitBlock];
+            fit_sincos(model, sh, xv, s1, c1);
             if constexpr (MODEL == CRIMP_MODEL_FOURIER && KF > 0) {
                 tpl_value_fourier<KF>(al, be, s1, c1, h);
             } else {
@@ -141,9 +156,13 @@ __device__ FitEval fit_eval(const double* __restrict__ x, int64_t a, int64_t b, 
             acc[3] -= q * q;
             mn = fmin(mn, mv);
         }
-      } else for (int64_t i = a + tid; i < b; i += kFitBlock) {
+      } else {
+       double xn = a + tid < b ? x[a + tid] : 0.0;
+       for (int64_t i = a + tid; i < b; i += kFitBlock) {
         double s1, c1, h, h1, h2;
-        fit_sincos(model, sh, x[i], s1, c1);
+        const double xv = kFitPrefetch ? xn : x[i];
+        if (kFitPrefetch && i + kFitBlock < b) xn = x[i + kFitBlock];
+        fit_sincos(model, sh, xv, s1, c1);
         if constexpr (MODEL == CRIMP_MODEL_FOURIER && KF > 0)
             tpl_terms_fourier<KF>(al, be, s1, c1, h, h1, h2);
         else
@@ -157,6 +176,7 @@ __device__ FitEval fit_eval(const double* __restrict__ x, int64_t a, int64_t b, 
         acc[4] -= h1 * q * q;
         acc[5] += h2 * q - h1 * h1 * q * q;
         mn = fmin(mn, mv);
+       }
       }
     }
     if (np) acc[0] += log(pr);
@@ -196,7 +216,7 @@ __device__ FitEval fit_eval(const double* __restrict__ x, int64_t a, int64_t b, 
 }
 
 // toafit._newton_step: Levenberg-shifted Newton direction with a trust region (0.05 rad, half the norm)
-__device__ void fit_newton_dir(double n, const FitEval& e, double& dn, double& dp) {
+__device__ void fit_newton_dir(double n, const FitEval& e, double& dn, double& dp, bool* pure = nullptr) {
     const double hnn = e.hnn, hnp = e.hnp, hpp = e.hpp;
     const double tr = hnn + hpp;
     const double det = hnn * hpp - hnp * hnp;
@@ -209,9 +229,20 @@ __device__ void fit_newton_dir(double n, const FitEval& e, double& dn, double& d
     dp = -(aa * e.gp - hnp * e.gn) / det2;
     double sc = fmin(1.0, 0.05 / fmax(fabs(dp), 1e-300));
     sc = fmin(sc, 0.5 * fabs(n) / fmax(fabs(dn), 1e-300));
+    if (pure) *pure = shift == 0.0 && sc == 1.0;  // the plain Newton step of a negative definite Hessian
     dn *= sc;
     dp *= sc;
 }
+
+// Final Newton step without a likelihood pass (toafit.maximise does the same): once the plain Newton step of a
+// negative definite Hessian is below kFitModelStep (rad, and relative in the norm) and inside the bounds, the
+// ascent takes it and reports the LL of the local quadratic model, LL + g.d + d.H.d / 2. Newton's quadratic
+// convergence leaves the point ~C d^2 (~1e-11 rad) from the maximum, and the model's LL error is third order in d
+// (~N (h' d / m)^3 ~ 1e-13 for 1e5 photons) -- instead of one more pass to find a step below 1e-12.
+#ifndef CRIMP_FIT_MODEL_STEP
+#define CRIMP_FIT_MODEL_STEP 1
+#endif
+constexpr double kFitModelStep = 1e-6;
 
 // toafit.profile_norm: max over norm in [lo, hi] of LL(norm, phi) at fixed phi (1-D Newton, concave)
 // hc: per-photon template-part cache (nullptr: recompute every pass).
@@ -248,6 +279,130 @@ __device__ double fit_profile(const double* __restrict__ x, int64_t a, int64_t b
         if (conv) break;
     }
     return e.ll;
+}
+
+// toafit.profile_norm from one photon pass (the 1-sigma scan's norm profiles). At fixed phShift the extended LL is
+// -nE + sum_i ln(n + h_i) + const, so with m_i = n0 + h_i at the start n0 and the moments S_p = sum_i m_i^-p, for
+// n = n0 + d:   sum_i ln(n + h_i) = S_0 + sum_{p>=1} (-1)^(p+1) d^p S_p / p,   dLL/dn = -E + sum_{p>=1} (-d)^(p-1) S_p.
+// One pass returns S_0 = sum ln m_i (as fit_eval forms it: one log per kFitProd values), S_1..S_5 and min m_i; the
+// root of the degree-4 derivative polynomial is the profile optimum and the series at it the profile LL. With
+// r = |d| / min m_i <= kMomR the dropped terms are <= N r^6 / 6 in the LL (1e5 photons: ~1e-12) and move the root by
+// ~r^5 of the norm, below the iterative profile's own 1e-13 stopping step; the scan needs the profile LL only for the
+// 0.5 chi2 threshold. Otherwise (start infeasible, root outside the bounds, r larger) the iterative profile runs.
+// This replaces the iterative profile's cached-template passes (store h, then ~2 passes over the cache) by one pass
+// without the h store: config 5, 4 scan profiles per interval.
+#ifndef CRIMP_FIT_MOMENTS
+#define CRIMP_FIT_MOMENTS 1
+#endif
+constexpr double kMomR = 2e-3;
+struct FitMom {
+    double s[6];  // S_0 .. S_5
+    double mn;
+};
+template <int MODEL, int KF>
+__device__ FitMom fit_moments(const double* __restrict__ x, int64_t a, int64_t b, const TplDev* __restrict__ T,
+                              double n, double phi, FitShared& sh) {
+    const int tid = threadIdx.x;
+    constexpr int model = MODEL;
+    const int K = KF > 0 ? KF : T->K;
+    __syncthreads();  // the previous evaluation's readers are done with sh
+    if (tid < K) tpl_coef(T, tid, phi, sh.coef[0][tid], sh.coef[1][tid]);
+    __syncthreads();
+    double acc[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    double mn = INFINITY;
+    double pr = 1.0;
+    int np = 0;
+    [[maybe_unused]] double al[KF > 0 ? KF : 1], be[KF > 0 ? KF : 1];
+    if constexpr (MODEL == CRIMP_MODEL_FOURIER && KF > 0) {
+#pragma unroll
+        for (int j = 0; j < KF; ++j) {
+            al[j] = sh.coef[0][j];
+            be[j] = sh.coef[1][j];
+        }
+    }
+    double xn = a + tid < b ? x[a + tid] : 0.0;
+    for (int64_t i = a + tid; i < b; i += kFitBlock) {
+        double s1, c1, h;
+        const double xv = xn;
+        if (i + kFitBlock < b) xn = x[i + kFitBlock];
+        fit_sincos(model, sh, xv, s1, c1);
+        if constexpr (MODEL == CRIMP_MODEL_FOURIER && KF > 0) {
+            tpl_value_fourier<KF>(al, be, s1, c1, h);
+        } else {
+            double h1, h2;
+            tpl_terms(T, model, K, sh.coef[0], sh.coef[1], s1, c1, h, h1, h2);
+        }
+        const double mv = n + h;
+        const double q = lk_rcp(mv);
+        pr *= mv;
+        if (++np == kFitProd) {
+            acc[0] += log(pr);
+            pr = 1.0;
+            np = 0;
+        }
+        const double q2 = q * q;
+        acc[1] += q;
+        acc[2] += q2;
+        acc[3] += q2 * q;
+        acc[4] += q2 * q2;
+        acc[5] += q2 * q2 * q;
+        mn = fmin(mn, mv);
+    }
+    if (np) acc[0] += log(pr);
+    const int w = tid >> 6, lane = tid & 63;
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+        const double v = wave_sum(acc[q]);
+        if (lane == 0) sh.red[w][q] = v;
+    }
+    const double vm = wave_min(mn);
+    if (lane == 0) sh.red[w][6] = vm;
+    __syncthreads();
+    FitMom r;
+#pragma unroll
+    for (int q = 0; q < 7; ++q) {
+        double v = sh.red[0][q];
+        for (int ww = 1; ww < kFitBlock / 64; ++ww) v = (q == 6) ? fmin(v, sh.red[ww][q]) : v + sh.red[ww][q];
+        if (q < 6) r.s[q] = v; else r.mn = v;
+    }
+    return r;
+}
+
+template <int MODEL, int KF>
+__device__ double fit_profile_mom(const double* __restrict__ x, int64_t a, int64_t b, const TplDev* __restrict__ T,
+                                  double phi, double n_start, double E, const FitCfg& C, FitShared& sh, int& nev,
+                                  int& nmom) {
+    const double n0 = clipd(n_start, C.lo, C.hi);
+    const FitMom m = fit_moments<MODEL, KF>(x, a, b, T, n0, phi, sh);
+    ++nev;
+    ++nmom;
+    const double* S = m.s;
+    if (m.mn > 0 && isfinite(S[0]) && S[2] > 0) {
+        // Newton on g(d) = -E + S1 - d S2 + d^2 S3 - d^3 S4 + d^4 S5 (strictly decreasing near 0: g' ~ -S2)
+        double d = 0.0;
+        bool ok = false;
+        for (int it = 0; it < 12; ++it) {
+            const double g = -E + S[1] + d * (-S[2] + d * (S[3] + d * (-S[4] + d * S[5])));
+            const double gp = -S[2] + d * (2.0 * S[3] + d * (-3.0 * S[4] + d * 4.0 * S[5]));
+            if (!(gp < 0)) break;
+            const double st = -g / gp;
+            d += st;
+            if (!(fabs(d) <= kMomR * m.mn)) break;
+            if (fabs(st) <= 1e-15 * n0) {
+                ok = true;
+                break;
+            }
+        }
+        const double nn = n0 + d;
+        if (ok && nn >= C.lo && nn <= C.hi) {
+            const double s0 = S[0] + d * (S[1] + d * (-S[2] / 2 + d * (S[3] / 3 + d * (-S[4] / 4 + d * (S[5] / 5)))));
+            const double N = (double)(b - a);
+            if (MODEL == CRIMP_MODEL_FOURIER) return -nn * E + N * log(nn * E) + (s0 - N * log(nn));
+            const double F = kTwoPi * nn + C.sum_amp;
+            return -F * E / kTwoPi + N * log(F * E / kTwoPi) + (s0 - N * log(F));
+        }
+    }
+    return fit_profile<MODEL, KF>(x, a, b, T, phi, n_start, E, C, sh, nev);  // iterative, recomputing h
 }
 
 // ---------------------------------------------------------------- varyAmps (measureToAs.py:305-312)
@@ -499,17 +654,27 @@ __global__ __launch_bounds__(kFitBlock) __attribute__((amdgpu_waves_per_eu(CRIMP
     const int64_t iv = blockIdx.x;
     const int64_t a = offsets[iv], b = offsets[iv + 1];
     const double E = expo[iv];
-    int nev = 0, ncached = 0;
+    int nev = 0, ncached = 0, nmom = 0;
     double n = start[2 * iv], p = start[2 * iv + 1];
     FitEval e = fit_eval<MODEL, KF>(x, a, b, T, n, p, E, C, sh);
     ++nev;
     for (int it = 0; it < 60; ++it) {  // toafit.maximise
         double dn, dp;
-        fit_newton_dir(n, e, dn, dp);
+        bool pure = false;
+        fit_newton_dir(n, e, dn, dp, &pure);
         {   // converged: even the full step moves less than the stopping tolerance, so the pass that would confirm
             // it is skipped (toafit.maximise does the same)
             const double fn = clipd(n + dn, C.lo, C.hi), fp = clipd(p + dp, -C.pb, C.pb);
             if (isfinite(e.ll) && fabs(fp - p) < 1e-12 && fabs(fn - n) < 1e-12 * fmax(1.0, fabs(fn))) break;
+            if (CRIMP_FIT_MODEL_STEP && pure && isfinite(e.ll) && fn == n + dn && fp == p + dp &&
+                fabs(dp) < kFitModelStep && fabs(dn) < kFitModelStep * fmax(1.0, fabs(n))) {
+#pragma clang fp contract(off)
+                const double q = e.hnn * dn * dn + 2.0 * e.hnp * dn * dp + e.hpp * dp * dp;
+                e.ll = e.ll + (e.gn * dn + e.gp * dp + 0.5 * q);
+                n = fn;
+                p = fp;
+                break;
+            }
         }
         double t = 1.0, tn = n, tp = p;
         FitEval e2 = e;
@@ -553,7 +718,9 @@ __global__ __launch_bounds__(kFitBlock) __attribute__((amdgpu_waves_per_eu(CRIMP
             } else {
                 ph = clipd(target, -C.pb, C.pb);
             }
-            const double llk = fit_profile<MODEL, KF>(x, a, b, T, ph, nhat, E, C, sh, nev, hcache, &ncached);
+            const double llk = CRIMP_FIT_MOMENTS
+                                   ? fit_profile_mom<MODEL, KF>(x, a, b, T, ph, nhat, E, C, sh, nev, nmom)
+                                   : fit_profile<MODEL, KF>(x, a, b, T, ph, nhat, E, C, sh, nev, hcache, &ncached);
             const double diff = llmax - llk;
             if (diff > kHalfChi2OneSigma || (double)(k + 1) > C.kcap) {
                 kk = k + 1;

@@ -34,6 +34,7 @@ from ._native import _is_torch
 
 CHI2_1SIG_1DOF = 0.500021713558733  # 0.5 * scipy.stats.chi2.ppf(0.6827, 1)   (measureToAs.py:324)
 TWO_PI = 2.0 * math.pi
+MODEL_STEP = 1e-6  # ascent: final plain Newton step below this (rad; relative in the norm) taken by the quadratic model
 
 
 def _vals(tmpl, prefix, K):
@@ -165,12 +166,24 @@ class ToAFitter:
             act = np.nonzero(active)[0]
             if act.size == 0:
                 break
-            dn, dp = self._newton_step(n[act], g[act], H[act])
+            dn, dp, pure = self._newton_step(n[act], g[act], H[act], with_pure=True)
             # converged: even the full step moves less than the stopping tolerance (no confirming pass)
             fn = np.clip(n[act] + dn, self.lo, self.hi)
             fp = np.clip(phi[act] + dp, -self.pb, self.pb)
             pre = np.isfinite(ll[act]) & (np.abs(fp - phi[act]) < 1e-12) & (
                 np.abs(fn - n[act]) < 1e-12 * np.maximum(1.0, np.abs(fn)))
+            # final step by the local quadratic model (k_toa_fit's kFitModelStep): the plain Newton step of a
+            # negative definite Hessian below MODEL_STEP, inside the bounds, is taken without a likelihood pass
+            ia = act
+            mod = ~pre & pure & np.isfinite(ll[ia]) & (fn == n[ia] + dn) & (fp == phi[ia] + dp) & (
+                np.abs(dp) < MODEL_STEP) & (np.abs(dn) < MODEL_STEP * np.maximum(1.0, np.abs(n[ia])))
+            if mod.any():
+                im = ia[mod]
+                Hm, gm, dnm, dpm = H[im], g[im], dn[mod], dp[mod]
+                q = Hm[:, 0] * dnm * dnm + 2.0 * Hm[:, 1] * dnm * dpm + Hm[:, 2] * dpm * dpm
+                ll[im] = ll[im] + (gm[:, 0] * dnm + gm[:, 1] * dpm + 0.5 * q)
+                n[im], phi[im] = fn[mod], fp[mod]
+            pre |= mod
             if pre.any():
                 active[act[pre]] = False
                 keep = ~pre
@@ -203,7 +216,7 @@ class ToAFitter:
             active[act[done]] = False
         return n, phi, ll
 
-    def _newton_step(self, n, g, H):
+    def _newton_step(self, n, g, H, with_pure=False):
         hnn, hnp, hpp = H[:, 0], H[:, 1], H[:, 2]
         # shift the Hessian to be negative definite (Levenberg damping), then solve
         tr = hnn + hpp
@@ -217,6 +230,8 @@ class ToAFitter:
         # trust region: at most 0.05 rad in phShift and half the norm per step
         sc = np.minimum(1.0, 0.05 / np.maximum(np.abs(dp), 1e-300))
         sc = np.minimum(sc, 0.5 * np.abs(n) / np.maximum(np.abs(dn), 1e-300))
+        if with_pure:
+            return dn * sc, dp * sc, (shift == 0.0) & (sc == 1.0)
         return dn * sc, dp * sc
 
     def profile_norm(self, iv, phi, n_start, max_iter=30):
