@@ -174,22 +174,31 @@ def toa_leg(a, dev, world, rank):
     fev = np.asarray(res["evaluations"], dtype=np.float64)
     fca = np.asarray(res["cached_evaluations"], dtype=np.float64)
     step = 2 * np.pi / f.res
-    fst = (np.rint((res["phShi_LL"] - step / 2) / step) - 1) + (np.rint((res["phShi_UL"] - step / 2) / step) - 1)
+    kl = np.rint((res["phShi_LL"] - step / 2) / step) - 1  # scan profiles per side
+    ku = np.rint((res["phShi_UL"] - step / 2) / step) - 1
+    fst = kl + ku
+    fjo = 2 * np.minimum(kl, ku)  # profiles evaluated two per joint pass (both sides active)
     fnw = fev - fca - fst
     # a scan profile's first pass: the moment pass (S_1..S_5, no cached passes) or, in the CRIMP_FIT_MOMENTS=0
     # build, the pass that stores h for the cached passes
-    s_scan = (27 + 5 * K) if np.any(fca > 0) else (33 + 5 * K)
-    f_ops = float(np.sum(fnw * (33 + 9 * K) + fst * s_scan + fca * 13) * a.toa_photons)
+    # (CRIMP_FIT_MOMENTS=0 build) or, for a step of both sides in one joint pass, the shared sin/cos and recurrence
+    # (14 + 2K) once and each side's template and moment work (3K + 19) per profile: 26 + 4K per profile
+    if np.any(fca > 0):
+        s_scan, fjo = 27 + 5 * K, 0 * fjo
+    else:
+        s_scan = 33 + 5 * K
+    f_ops = float(np.sum(fnw * (33 + 9 * K) + (fst - fjo) * s_scan + fjo * (26 + 4 * K) + fca * 13) * a.toa_photons)
     f_ach = f_ops / (fit_ms * 1e-3)
     out["toa_fit_roofline"] = {"kernel": "k_toa_fit", "bound": "valu", "achieved": f_ach / 1e12,
                                "peak": PEAK_F64_OPS / 1e12, "unit": "Tlane-op/s (fp64)", "frac": f_ach / PEAK_F64_OPS,
                                "newton_passes_per_interval": float(np.mean(fnw)),
-                               "store_passes_per_interval": float(np.mean(fst)),
+                               "scan_profiles_per_interval": float(np.mean(fst)),
+                               "joint_pass_profiles_per_interval": float(np.mean(fjo)),
                                "cached_passes_per_interval": float(np.mean(fca)),
                                "scan_pass_ops": s_scan,
                                "note": "S_full = 33 + 9K fp64 ops per photon and Newton pass, S_scan = 33 + 5K for a "
-                                       "scan profile's moment pass (27 + 5K for the h-storing pass of the iterative "
-                                       "profile), S_cached = 13 for a pass over its cached template part; passes from the fit's own counters / "
+                                       "scan profile's moment pass, 26 + 4K per profile of a joint two-side moment pass "
+                                       "(27 + 5K for the h-storing pass of the iterative profile), S_cached = 13 for a pass over its cached template part; passes from the fit's own counters / "
                                        "k_toa_fit hipEvent time; peak fp64 FMA rate 256 CU x 64 lanes x 2.4 GHz"}
     # end to end from host arrays: photon times t = (cycle + phase) / F0 around PEPOCH, intervals bracketing them
     F0, pep = 0.5, 58000.0
@@ -428,6 +437,28 @@ def pmc_traffic(photons, trials, nharm):
     return rec.get("bytes_per_search"), rec.get("source")
 
 
+def pmc_clock():
+    """The search kernel's clock and clock-normalised matrix-pipe occupancy from the tree's SQ counter pass
+    (tools/pmc_round.sh -> profiles/r03/pmc_search/): clock = GRBM_GUI_ACTIVE / 8 XCDs / the launch's duration in
+    the same session's kernel trace; busy = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x those cycles)."""
+    d = os.path.join(ROOT, "profiles", "r03", "pmc_search")
+    try:
+        cnt = {}
+        for line in open(os.path.join(d, "summary_k_search_exact.txt")):
+            f = line.split()
+            if len(f) >= 2 and f[0].endswith("/disp"):
+                cnt[f[0][:-5]] = float(f[1])
+        ns = None
+        for line in open(os.path.join(d, "trace_kernel_stats.csv")):
+            if line.startswith('"void k_search_exact<false>'):
+                ns = float(line.rsplit('",', 1)[1].split(",")[2])
+        cyc = cnt["GRBM_GUI_ACTIVE"] / 8.0
+        return {"clock_ghz": cyc / ns, "matrix_pipe_busy_at_clock": cnt["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024.0 * cyc),
+                "source": "profiles/r03/pmc_search (rocprofv3 --pmc over tools/run_search.py, config 3, the same kernel)"}
+    except (OSError, KeyError, ValueError, IndexError, TypeError, ZeroDivisionError):
+        return None
+
+
 def main():
     a = parse()
     import torch
@@ -529,7 +560,7 @@ def main():
                        "search_path": "exact (default precision)", "fp64_fixup_trials_per_step": float(np.mean(fixups))},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_I8_TOPS, "unit": "TFLOP/s",
                          "frac": achieved / PEAK_I8_TOPS, "traffic": traffic,
-                         "kernel_ms": kern_ms, "step_ms": step_ms,
+                         "kernel_ms": kern_ms, "step_ms": step_ms, "pmc": pmc_clock(),
                          "note": "int8 matrix ops issued: 128 per photon*trial*harmonic (8 v_mfma_i32_32x32x32_i8 + 4 "
                                  "2:4-sparse v_smfmac_i32_32x32x64_i8 per 4 photons x 2048 trials) / mean duration of "
                                  "the harmonic-sum kernels (hipEvents in libcrimp_hip on their stream); peak = that "

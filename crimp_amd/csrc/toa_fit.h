@@ -28,6 +28,7 @@ struct FitCfg {
     double sum_amp;  // sum_j amp_j: cauchy / von Mises normalisation F = 2 pi norm + sum_amp
     double amp_lo, amp_hi;  // ampShift bounds when varied: [0.01, 100] fourier (:308), [0, inf) cauchy (:461),
                             // [0, 500] von Mises (:605)
+    double mom_r;           // fit_profile_mom's largest |d| / min m (kMomR; test hook CRIMP_FIT_MOM_R, 0: iterative)
 };
 
 struct FitEval {
@@ -37,6 +38,8 @@ struct FitEval {
 struct FitShared {
     double red[kFitBlock / 64][8];
     double coef[2][CRIMP_MAX_COMP];
+    double coef2[2][CRIMP_MAX_COMP];       // the second phShift of a joint moment pass (fit_moments2)
+    double red2[kFitBlock / 64][8];
 #if CRIMP_FIT_TABLE
     double2 tab[kSinTab];  // photon_sincos_tab (filled once per workgroup)
 #endif
@@ -242,12 +245,15 @@ __device__ void fit_newton_dir(double n, const FitEval& e, double& dn, double& d
 #ifndef CRIMP_FIT_MODEL_STEP
 #define CRIMP_FIT_MODEL_STEP 1
 #endif
-constexpr double kFitModelStep = 1e-6;
+#ifndef CRIMP_FIT_MODEL_STEP_TOL
+#define CRIMP_FIT_MODEL_STEP_TOL 1e-6
+#endif
+constexpr double kFitModelStep = CRIMP_FIT_MODEL_STEP_TOL;
 
 // toafit.profile_norm: max over norm in [lo, hi] of LL(norm, phi) at fixed phi (1-D Newton, concave)
 // hc: per-photon template-part cache (nullptr: recompute every pass).
 template <int MODEL, int KF>
-__device__ double fit_profile(const double* __restrict__ x, int64_t a, int64_t b, const TplDev* __restrict__ T,
+__device__ __noinline__ double fit_profile(const double* __restrict__ x, int64_t a, int64_t b, const TplDev* __restrict__ T,
                               double phi, double n_start, double E, const FitCfg& C, FitShared& sh, int& nev,
                               double* __restrict__ hc = nullptr, int* ncached = nullptr) {
     double n = clipd(n_start, C.lo, C.hi);
@@ -295,6 +301,10 @@ __device__ double fit_profile(const double* __restrict__ x, int64_t a, int64_t b
 #define CRIMP_FIT_MOMENTS 1
 #endif
 constexpr double kMomR = 2e-3;
+// the scan's two sides in one moment pass per step (fit_moments2; CRIMP_FIT_JOINT=0: one pass per side and step)
+#ifndef CRIMP_FIT_JOINT
+#define CRIMP_FIT_JOINT 1
+#endif
 struct FitMom {
     double s[6];  // S_0 .. S_5
     double mn;
@@ -368,41 +378,157 @@ __device__ FitMom fit_moments(const double* __restrict__ x, int64_t a, int64_t b
     return r;
 }
 
+// the profile optimum and LL from one phShift's moments (fit_profile_mom); false where the series does not apply
+template <int MODEL>
+__device__ bool mom_solve(const FitMom& m, double n0, double E, double N, const FitCfg& C, double& ll) {
+    const double* S = m.s;
+    if (!(m.mn > 0 && isfinite(S[0]) && S[2] > 0)) return false;
+    // Newton on g(d) = -E + S1 - d S2 + d^2 S3 - d^3 S4 + d^4 S5 (strictly decreasing near 0: g' ~ -S2)
+    double d = 0.0;
+    bool ok = false;
+    for (int it = 0; it < 12; ++it) {
+        const double g = -E + S[1] + d * (-S[2] + d * (S[3] + d * (-S[4] + d * S[5])));
+        const double gp = -S[2] + d * (2.0 * S[3] + d * (-3.0 * S[4] + d * 4.0 * S[5]));
+        if (!(gp < 0)) break;
+        const double st = -g / gp;
+        d += st;
+        if (!(fabs(d) <= C.mom_r * m.mn)) break;
+        if (fabs(st) <= 1e-15 * n0) {
+            ok = true;
+            break;
+        }
+    }
+    const double nn = n0 + d;
+    if (!(ok && nn >= C.lo && nn <= C.hi)) return false;
+    const double s0 = S[0] + d * (S[1] + d * (-S[2] / 2 + d * (S[3] / 3 + d * (-S[4] / 4 + d * (S[5] / 5)))));
+    if (MODEL == CRIMP_MODEL_FOURIER) {
+        ll = -nn * E + N * log(nn * E) + (s0 - N * log(nn));
+    } else {
+        const double F = kTwoPi * nn + C.sum_amp;
+        ll = -F * E / kTwoPi + N * log(F * E / kTwoPi) + (s0 - N * log(F));
+    }
+    return true;
+}
+
 template <int MODEL, int KF>
 __device__ double fit_profile_mom(const double* __restrict__ x, int64_t a, int64_t b, const TplDev* __restrict__ T,
-                                  double phi, double n_start, double E, const FitCfg& C, FitShared& sh, int& nev,
-                                  int& nmom) {
+                                  double phi, double n_start, double E, const FitCfg& C, FitShared& sh, int& nev) {
     const double n0 = clipd(n_start, C.lo, C.hi);
     const FitMom m = fit_moments<MODEL, KF>(x, a, b, T, n0, phi, sh);
     ++nev;
-    ++nmom;
-    const double* S = m.s;
-    if (m.mn > 0 && isfinite(S[0]) && S[2] > 0) {
-        // Newton on g(d) = -E + S1 - d S2 + d^2 S3 - d^3 S4 + d^4 S5 (strictly decreasing near 0: g' ~ -S2)
-        double d = 0.0;
-        bool ok = false;
-        for (int it = 0; it < 12; ++it) {
-            const double g = -E + S[1] + d * (-S[2] + d * (S[3] + d * (-S[4] + d * S[5])));
-            const double gp = -S[2] + d * (2.0 * S[3] + d * (-3.0 * S[4] + d * 4.0 * S[5]));
-            if (!(gp < 0)) break;
-            const double st = -g / gp;
-            d += st;
-            if (!(fabs(d) <= kMomR * m.mn)) break;
-            if (fabs(st) <= 1e-15 * n0) {
-                ok = true;
-                break;
+    double ll;
+    if (mom_solve<MODEL>(m, n0, E, (double)(b - a), C, ll)) return ll;
+    return fit_profile<MODEL, KF>(x, a, b, T, phi, n_start, E, C, sh, nev);  // iterative, recomputing h
+}
+
+// Two phShifts' moments in one pass (the 1-sigma scan's step k on both sides, Fourier templates of compile-time
+// size): the photon's sin/cos and harmonic recurrence are formed once, and each phShift's sums repeat
+// fit_moments' per-photon operations, striding and reduction order, so they equal two fit_moments passes.
+template <int KF>
+__device__ __noinline__ void fit_moments2(const double* __restrict__ x, int64_t a, int64_t b,
+                                          const TplDev* __restrict__ T, double n, double phi0, double phi1,
+                                          FitShared& sh, FitMom& m0, FitMom& m1) {
+    static_assert(KF > 0, "compile-time template size");
+    const int tid = threadIdx.x;
+    __syncthreads();  // the previous evaluation's readers are done with sh
+    if (tid < KF) tpl_coef(T, tid, phi0, sh.coef[0][tid], sh.coef[1][tid]);
+    else if (tid >= 64 && tid < 64 + KF) tpl_coef(T, tid - 64, phi1, sh.coef2[0][tid - 64], sh.coef2[1][tid - 64]);
+    __syncthreads();
+    double al0[KF], be0[KF], al1[KF], be1[KF];
+#pragma unroll
+    for (int j = 0; j < KF; ++j) {
+        al0[j] = sh.coef[0][j];
+        be0[j] = sh.coef[1][j];
+        al1[j] = sh.coef2[0][j];
+        be1[j] = sh.coef2[1][j];
+    }
+    double acc0[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0}, acc1[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    double mn0 = INFINITY, mn1 = INFINITY, pr0 = 1.0, pr1 = 1.0;
+    int np = 0;
+    double xn = a + tid < b ? x[a + tid] : 0.0;
+    for (int64_t i = a + tid; i < b; i += kFitBlock) {
+        double s1, c1;
+        const double xv = xn;
+        if (i + kFitBlock < b) xn = x[i + kFitBlock];
+        fit_sincos(CRIMP_MODEL_FOURIER, sh, xv, s1, c1);
+        // tpl_value_fourier for both coefficient rows on one recurrence (the same h, operation by operation)
+        double h0 = 0.0, h1 = 0.0;
+        {
+            const double tc = c1 + c1;
+            double cj = c1, sj = s1, cp = 1.0, sp = 0.0;
+#pragma unroll
+            for (int j = 0; j < KF; ++j) {
+                h0 += fma(al0[j], cj, be0[j] * sj);
+                h1 += fma(al1[j], cj, be1[j] * sj);
+                if (j + 1 < KF) {
+                    const double cn = fma(tc, cj, -cp), sn = fma(tc, sj, -sp);
+                    cp = cj;
+                    sp = sj;
+                    cj = cn;
+                    sj = sn;
+                }
             }
         }
-        const double nn = n0 + d;
-        if (ok && nn >= C.lo && nn <= C.hi) {
-            const double s0 = S[0] + d * (S[1] + d * (-S[2] / 2 + d * (S[3] / 3 + d * (-S[4] / 4 + d * (S[5] / 5)))));
-            const double N = (double)(b - a);
-            if (MODEL == CRIMP_MODEL_FOURIER) return -nn * E + N * log(nn * E) + (s0 - N * log(nn));
-            const double F = kTwoPi * nn + C.sum_amp;
-            return -F * E / kTwoPi + N * log(F * E / kTwoPi) + (s0 - N * log(F));
+        const double mv0 = n + h0, mv1 = n + h1;
+        const double q0 = lk_rcp(mv0), q1 = lk_rcp(mv1);
+        pr0 *= mv0;
+        pr1 *= mv1;
+        if (++np == kFitProd) {
+            acc0[0] += log(pr0);
+            acc1[0] += log(pr1);
+            pr0 = 1.0;
+            pr1 = 1.0;
+            np = 0;
+        }
+        const double r0 = q0 * q0, r1 = q1 * q1;
+        acc0[1] += q0;
+        acc0[2] += r0;
+        acc0[3] += r0 * q0;
+        acc0[4] += r0 * r0;
+        acc0[5] += r0 * r0 * q0;
+        acc1[1] += q1;
+        acc1[2] += r1;
+        acc1[3] += r1 * q1;
+        acc1[4] += r1 * r1;
+        acc1[5] += r1 * r1 * q1;
+        mn0 = fmin(mn0, mv0);
+        mn1 = fmin(mn1, mv1);
+    }
+    if (np) {
+        acc0[0] += log(pr0);
+        acc1[0] += log(pr1);
+    }
+    const int w = tid >> 6, lane = tid & 63;
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+        const double v0 = wave_sum(acc0[q]);
+        const double v1 = wave_sum(acc1[q]);
+        if (lane == 0) {
+            sh.red[w][q] = v0;
+            sh.red2[w][q] = v1;
         }
     }
-    return fit_profile<MODEL, KF>(x, a, b, T, phi, n_start, E, C, sh, nev);  // iterative, recomputing h
+    const double vm0 = wave_min(mn0), vm1 = wave_min(mn1);
+    if (lane == 0) {
+        sh.red[w][6] = vm0;
+        sh.red2[w][6] = vm1;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 7; ++q) {
+        double v0 = sh.red[0][q], v1 = sh.red2[0][q];
+        for (int ww = 1; ww < kFitBlock / 64; ++ww) {
+            v0 = (q == 6) ? fmin(v0, sh.red[ww][q]) : v0 + sh.red[ww][q];
+            v1 = (q == 6) ? fmin(v1, sh.red2[ww][q]) : v1 + sh.red2[ww][q];
+        }
+        if (q < 6) {
+            m0.s[q] = v0;
+            m1.s[q] = v1;
+        } else {
+            m0.mn = v0;
+            m1.mn = v1;
+        }
+    }
 }
 
 // ---------------------------------------------------------------- varyAmps (measureToAs.py:305-312)
@@ -654,7 +780,7 @@ __global__ __launch_bounds__(kFitBlock) __attribute__((amdgpu_waves_per_eu(CRIMP
     const int64_t iv = blockIdx.x;
     const int64_t a = offsets[iv], b = offsets[iv + 1];
     const double E = expo[iv];
-    int nev = 0, ncached = 0, nmom = 0;
+    int nev = 0, ncached = 0;
     double n = start[2 * iv], p = start[2 * iv + 1];
     FitEval e = fit_eval<MODEL, KF>(x, a, b, T, n, p, E, C, sh);
     ++nev;
@@ -698,37 +824,62 @@ __global__ __launch_bounds__(kFitBlock) __attribute__((amdgpu_waves_per_eu(CRIMP
         if (mvp < 1e-12 && mvn < 1e-12 * fmax(1.0, fabs(tn))) break;
     }
     const double nhat = n, phat = p, llmax = e.ll;
+    // toafit.error_scan, measureToAs.py:331-376: both sides step k = 1, 2, ... in lockstep (each side's sequence of
+    // phShifts, profiles and stopping rule is its own, so the order of evaluation cannot change a bound); with the
+    // moment profile of a compile-time Fourier template a step of both sides is one joint pass (fit_moments2)
     double sig[2];
-    for (int s = 0; s < 2; ++s) {  // toafit.error_scan, measureToAs.py:331-376
-        const int side = s == 0 ? -1 : 1;
-        bool past = false;
-        int kk = 0;
-        for (int k = 1;; ++k) {
+    int kk[2] = {0, 0};
+    bool past[2] = {false, false};
+    for (int k = 1; kk[0] == 0 || kk[1] == 0; ++k) {
+        double ph[2] = {0.0, 0.0};
+        for (int s = 0; s < 2; ++s) {
+            if (kk[s]) continue;
+            const int side = s == 0 ? -1 : 1;
             const double target = phat + (double)(side * k) * C.step;
-            double ph;
             if (MODEL == CRIMP_MODEL_FOURIER) {
                 // the first step past +-pi is clipped to the bound; later ones move the bound (:332-334, :357-359)
                 const bool beyond = side < 0 ? (target <= -M_PI) : (target >= M_PI);
-                if (beyond && !past) {
-                    ph = side < 0 ? -M_PI : M_PI;
-                    past = true;
+                if (beyond && !past[s]) {
+                    ph[s] = side < 0 ? -M_PI : M_PI;
+                    past[s] = true;
                 } else {
-                    ph = target;
+                    ph[s] = target;
                 }
             } else {
-                ph = clipd(target, -C.pb, C.pb);
-            }
-            const double llk = CRIMP_FIT_MOMENTS
-                                   ? fit_profile_mom<MODEL, KF>(x, a, b, T, ph, nhat, E, C, sh, nev, nmom)
-                                   : fit_profile<MODEL, KF>(x, a, b, T, ph, nhat, E, C, sh, nev, hcache, &ncached);
-            const double diff = llmax - llk;
-            if (diff > kHalfChi2OneSigma || (double)(k + 1) > C.kcap) {
-                kk = k + 1;
-                break;
+                ph[s] = clipd(target, -C.pb, C.pb);
             }
         }
-        sig[s] = sigma_bound(kk, C.step);
+        double llk[2] = {0.0, 0.0};
+        bool have[2] = {kk[0] != 0, kk[1] != 0};
+        bool iter[2] = {!CRIMP_FIT_MOMENTS, !CRIMP_FIT_MOMENTS};  // the iterative profile (no moment pass first)
+        if constexpr (CRIMP_FIT_MOMENTS && CRIMP_FIT_JOINT && MODEL == CRIMP_MODEL_FOURIER && KF > 0) {
+            if (!have[0] && !have[1]) {
+                const double n0 = clipd(nhat, C.lo, C.hi);
+                FitMom m[2];
+                fit_moments2<KF>(x, a, b, T, n0, ph[0], ph[1], sh, m[0], m[1]);
+                nev += 2;
+                for (int s = 0; s < 2; ++s) {
+                    have[s] = mom_solve<MODEL>(m[s], n0, E, (double)(b - a), C, llk[s]);
+                    iter[s] = true;
+                }
+            }
+        }
+        for (int s = 0; s < 2; ++s) {
+            if (have[s]) continue;
+            if (!iter[s])
+                llk[s] = fit_profile_mom<MODEL, KF>(x, a, b, T, ph[s], nhat, E, C, sh, nev);
+            else
+                llk[s] = fit_profile<MODEL, KF>(x, a, b, T, ph[s], nhat, E, C, sh, nev,
+                                                CRIMP_FIT_MOMENTS ? nullptr : hcache, &ncached);
+        }
+        for (int s = 0; s < 2; ++s) {
+            if (kk[s]) continue;
+            const double diff = llmax - llk[s];
+            if (diff > kHalfChi2OneSigma || (double)(k + 1) > C.kcap) kk[s] = k + 1;
+        }
     }
+    sig[0] = sigma_bound(kk[0], C.step);
+    sig[1] = sigma_bound(kk[1], C.step);
     if (threadIdx.x == 0) {
         double* o = out + iv * 8;
         o[0] = nhat;
