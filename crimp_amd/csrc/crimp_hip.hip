@@ -1171,6 +1171,7 @@ __global__ __launch_bounds__(256) void k_toa_grid_mf(const double* __restrict__ 
 // into ns blocks per interval cannot change a count. (One 256-thread block per interval with one shared histogram:
 // 0.6 ms for config 5's 1250 x 1e5 photons, ~1.7 TB/s.)
 constexpr int kBinWaves = 4;
+constexpr int kBinRegs = 16;
 __global__ __launch_bounds__(64 * kBinWaves) void k_binphases(const double* __restrict__ x,
                                                               const int64_t* __restrict__ offsets,
                                                               const double* __restrict__ edges, int nb,
@@ -1183,6 +1184,12 @@ __global__ __launch_bounds__(64 * kBinWaves) void k_binphases(const double* __re
     const double first = edges[0], last = edges[nb];
     const double denom = last - first;
     const int64_t stride = (int64_t)blockDim.x * gridDim.y;
+    // up to kBinRegs bins (measuretoas' default 15): per-thread counters in registers (one compare-add per bin and
+    // photon, no LDS atomics in the photon loop), added to the wave's LDS histogram once at the end
+    uint32_t rc[kBinRegs];
+#pragma unroll
+    for (int b = 0; b < kBinRegs; ++b) rc[b] = 0;
+    const bool regs = nb <= kBinRegs;
     for (int64_t i = offsets[iv] + (int64_t)blockIdx.y * blockDim.x + tid; i < offsets[iv + 1]; i += stride) {
         const double v = x[i];
         if (!(v >= first && v <= last)) continue;
@@ -1190,7 +1197,17 @@ __global__ __launch_bounds__(64 * kBinWaves) void k_binphases(const double* __re
         if (idx == nb) idx -= 1;
         if (v < edges[idx]) idx -= 1;
         if (v >= edges[idx + 1] && idx != nb - 1) idx += 1;
-        atomicAdd(&cnt[w][idx], 1u);
+        if (regs) {
+#pragma unroll
+            for (int b = 0; b < kBinRegs; ++b) rc[b] += idx == b ? 1u : 0u;
+        } else {
+            atomicAdd(&cnt[w][idx], 1u);
+        }
+    }
+    if (regs) {
+#pragma unroll
+        for (int b = 0; b < kBinRegs; ++b)
+            if (rc[b]) atomicAdd(&cnt[w][b], rc[b]);
     }
     __syncthreads();
     for (int b = tid; b < nb; b += blockDim.x) {

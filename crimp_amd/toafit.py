@@ -339,7 +339,12 @@ class ToAFitter:
         a = amp_shift
         for j in range(self.K):
             if self.model == "fourier":
-                y = y + t.amp[j] * a * np.cos((j + 1) * 2 * np.pi * xx + t.loc[j] - (j + 1) * phi)
+                # cos(A - B) with A = (j+1) 2 pi xx + loc_j, B = (j+1) phi by angle subtraction: the cos/sin run on
+                # the bin centres and on the intervals' phShifts (no (intervals x bins) cos), the terms differ from
+                # np.cos(A - B) by ~1e-16
+                ang = (j + 1) * 2 * np.pi * xx + t.loc[j]
+                bph = (j + 1) * phi
+                y = y + t.amp[j] * a * (np.cos(ang) * np.cos(bph) + np.sin(ang) * np.sin(bph))
             elif self.model == "cauchy":
                 y = y + ((t.amp[j] * a) / (2 * np.pi)) * (np.sinh(t.wid[j]) / (np.cosh(t.wid[j]) - np.cos(xx - t.loc[j] - phi)))
             else:
