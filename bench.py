@@ -20,9 +20,10 @@ Also reported:
 * ToA (config 5 per GPU): the device fit of 1250 intervals x 1e5 photons, and the end-to-end ``measure_intervals``
   (interval selection, calcphase, fits, per-interval H-test) from host MJD arrays, with the oracle's fits on all
   allowed host cores as its CPU baseline (a sample, extrapolated) and the fits' VALU roofline;
-* ``config4``: 1e8 photons, 2-D H_20, the first 131072 trials of this rank's shard of the 1e7-trial grid;
+* ``config4``: 1e8 photons, 2-D H_20 on a sub-grid of the 1e7-trial grid (131072 trials per GPU), sharded_search;
 * ``config2``: ``measureToAs`` on the bundled events, ToAs 35-41, FITS -> table (the reference's published rate).
-The multi-GPU search step is ``sharding.sharded_search(gather="best")``, the path tests/test_distributed_*.py test.
+The multi-GPU paths are the tested ones (tests/test_distributed_*.py): the search step and the config-4 leg run
+``sharding.sharded_search(gather="best")``, the ToA leg ``sharding.sharded_toa_fit`` (records all_gathered).
 """
 import argparse
 import json
@@ -60,12 +61,13 @@ def parse():
     p.add_argument("--toa-intervals", type=int, default=1250, help="ToA intervals per GPU (config 5: 1e4 over 8)")
     p.add_argument("--toa-photons", type=int, default=100_000)
     p.add_argument("--no-toa", action="store_true", help="skip the ToA legs")
+    p.add_argument("--full-c5", type=int, default=10_000, help="N=1: intervals of the whole-config-5 fit (0: skip)")
     p.add_argument("--calcphase-photons", type=int, default=100_000_000)
     p.add_argument("--no-calcphase", action="store_true", help="skip the calcphase (HBM-bound) leg")
     p.add_argument("--no-config2", action="store_true", help="skip the config-2 measureToAs leg")
     p.add_argument("--no-config4", action="store_true", help="skip the config-4 (1e8 photons, H_20) leg")
     p.add_argument("--c4-photons", type=int, default=100_000_000)
-    p.add_argument("--c4-trials", type=int, default=131072, help="config-4 trials timed per GPU")
+    p.add_argument("--c4-trials", type=int, default=131072, help="config-4 trials timed per GPU (even)")
     return p.parse_args()
 
 
@@ -108,20 +110,34 @@ def toa_leg(a, dev, world, rank):
     from crimp_amd.toafit import ToAFitter
     from crimp_amd import _native as N
     from crimp_amd.measureToAs import measure_intervals
+    from crimp_amd.sharding import interval_shard, sharded_toa_fit
     tm = _tmpl()
+    # one global interval set of world x toa_intervals intervals (weak scaling); rank r's block [r n, (r+1) n) is
+    # drawn with seed 2 + r, so every rank generates only the photons it fits (sharding.interval_shard)
+    nint_g = a.toa_intervals * world
+    off_g = np.arange(nint_g + 1, dtype=np.int64) * a.toa_photons
+    E_g = np.full(nint_g, a.toa_photons / T2259["norm"]["value"])
     x, off, E, shifts = template_intervals_torch(a.toa_intervals, a.toa_photons, T2259["norm"]["value"],
                                                  T2259["amp"], T2259["ph"], seed=2 + rank, device=dev)
+    first, count, pa, pb = interval_shard(off_g, world, rank)
+    assert (first, count) == (rank * a.toa_intervals, a.toa_intervals)
+
+    def rank_photons(lo, hi):  # sharded_toa_fit's loader: this rank's block only
+        assert (lo, hi) == (pa, pb)
+        return x
+
     for _ in range(max(a.warmup, 0)):  # untimed: code-object load, scratch-pool growth
-        ToAFitter(x, off, E, tm).fit(brutemin=True)
+        res = ToAFitter(x, off, E, tm).fit(brutemin=True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     reps = max(1, min(a.steps, 3))
     t1 = time.perf_counter()
-    for _ in range(reps):
-        res = ToAFitter(x, off, E, tm).fit(brutemin=True)
+    for _ in range(reps):  # the tested multi-GPU path: each rank fits its block, one all_gather of the records
+        allrec = sharded_toa_fit(rank_photons, off_g, E_g, tm, brutemin=True)
     torch.cuda.synchronize()
     el = (time.perf_counter() - t1) / reps
+    assert allrec["phShi"].size == nint_g and np.array_equal(allrec["phShi"][first:first + count], res["phShi"])
     # kernel split of one fit (hipEvents around the brute-grid and the fit kernels inside crimp_toa_fit)
     from crimp_amd import ops
     f = ToAFitter(x, off, E, tm)
@@ -133,8 +149,9 @@ def toa_leg(a, dev, world, rank):
         dist.all_reduce(elt, op=dist.ReduceOp.MAX)
     d = np.angle(np.exp(1j * (res["phShi"] - shifts)))  # recovered vs true shift, wrapped
     out = {"toa_fits_per_s": a.toa_intervals * world / float(elt.item()),
-           "toa_config": "config5: %d intervals/GPU x %d photons, Fourier K=6 (1e2259), brute+MLE+1-sigma scan"
-                         % (a.toa_intervals, a.toa_photons),
+           "toa_config": "config5: %d intervals/GPU x %d photons, Fourier K=6 (1e2259), brute+MLE+1-sigma scan+redChi2; "
+                         "sharding.sharded_toa_fit over %d ranks (all_gather of the records in the timed region)"
+                         % (a.toa_intervals, a.toa_photons, world),
            "toa_seconds": float(elt.item()),
            "toa_mean_likelihood_evaluations": float(np.mean(res["evaluations"])),
            "toa_shift_recovery_rms_cycles": float(np.sqrt(np.mean(d ** 2)) / (2 * np.pi)),
@@ -156,17 +173,22 @@ def toa_leg(a, dev, world, rank):
     # side's sigma is kk step + step / 2.
     K = len(T2259["amp"])
     nn = int(N.load().crimp_last_toa_grid_norms())
+    gmode = int(N.load().crimp_last_toa_grid_fast())   # bit 0: no min h, bit 1: log2 per eight model values
     nphi = 126
     nph_tot = float(a.toa_intervals) * a.toa_photons
-    g_slots = nph_tot * nphi * (1 + 3 * nn)
+    # per point: the min (1, unless bit 0) and per norm an add, (P-1)/P multiply, 1/P of a 4-slot v_log_f32 and 1/P add
+    P = 8 if gmode & 2 else 4
+    s_grid = (0 if gmode & 1 else 1) + nn * (1 + (P - 1) / P + 5.0 / P)
+    g_slots = nph_tot * nphi * s_grid
     g_ach = g_slots / (grid_ms * 1e-3)
     g_mf = nph_tot * nphi * 2 * 16 * ((K + 1) // 2) / (grid_ms * 1e-3)   # f16 matrix FLOP/s issued
     out["toa_roofline"] = {"kernel": "k_toa_grid_mf", "bound": "valu", "achieved": g_ach / 1e12,
                            "peak": PEAK_VALU_SLOTS / 1e12, "unit": "Tlane-op/s (fp32)", "frac": g_ach / PEAK_VALU_SLOTS,
-                           "norms_evaluated": nn, "slots_per_photon_phshift": 1 + 3 * nn,
+                           "norms_evaluated": nn, "slots_per_photon_phshift": s_grid, "grid_mode": gmode,
                            "matrix": {"achieved": g_mf / 1e12, "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s (f16 dense)",
                                       "frac": g_mf / 1e12 / PEAK_F16_TFLOPS},
-                           "note": "S_grid = 1 + 3 NN fp32 lane-op slots per photon x phShift (v_log_f32 at 4) beside "
+                           "note": "S_grid = [min] + NN (1 + (P-1)/P + 5/P) fp32 lane-op slots per photon x phShift "
+                                   "(log2 of products of P = 4 or 8 model values, v_log_f32 at 4) beside "
                                    "the template on v_mfma_f32_32x32x16_f16 (hi/lo f16 split, 16 MACs per pair of "
                                    "harmonics), x 1250 x 1e5 photons x 126 phShifts / brute-grid hipEvent time "
                                    "(k_toa_grid_mf + k_toa_grid_best); peaks 256 CU x 4 SIMD x 32 lanes x 2.4 GHz, "
@@ -227,6 +249,27 @@ def toa_leg(a, dev, world, rank):
         np.angle(np.exp(1j * (r2["phShi"] - res["phShi"]))))) / (2 * np.pi))
     if not a.no_cpu and rank == 0 and world == 1:  # CPU baselines: rank 0 at N=1 only
         out["toa_cpu_baseline"] = toa_cpu_baseline(x, off, E, tm, a.cpu_seconds)
+    if world == 1 and a.full_c5 > 0:  # the whole of config 5 (1e4 intervals x 1e5 photons, 8 GB) on one GPU
+        del x, off, r2, mjd, allrec
+        torch.cuda.empty_cache()
+        t1 = time.perf_counter()
+        xf, offf, Ef, _ = template_intervals_torch(a.full_c5, a.toa_photons, T2259["norm"]["value"], T2259["amp"],
+                                                   T2259["ph"], seed=12, device=dev)
+        torch.cuda.synchronize()
+        gen = time.perf_counter() - t1
+        ToAFitter(xf, offf, Ef, tm).fit(brutemin=True)   # untimed: scratch-pool growth to the larger sizes
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        rf = ToAFitter(xf, offf, Ef, tm).fit(brutemin=True)
+        torch.cuda.synchronize()
+        elf = time.perf_counter() - t1
+        out["toa_full_config5"] = {"fits_per_s": a.full_c5 / elf, "seconds": elf, "intervals": a.full_c5,
+                                   "photons_per_interval": a.toa_photons, "generation_s": gen,
+                                   "median_sigma_cycles": float(np.median(rf["phShi_LL"]) / (2 * np.pi)),
+                                   "note": "BASELINE config 5 whole (not per GPU) on one GPU: brute+MLE+1-sigma "
+                                           "scan+redChi2, phases resident in HBM"}
+        del xf, offf, rf
+        torch.cuda.empty_cache()
     return out
 
 
@@ -311,57 +354,57 @@ def config2_leg(a):
 
 
 def config4_leg(a, dev, world, rank):
-    """BASELINE config 4 on this rank's shard: 1e8 photons (T = 1e7 s, p = 0.05, fdot = -1e-12, seed 1), 2-D H_20
-    over 1e5 f (step 1/(10 T)) x 100 log10|fdot| rows linspace(-13.5, -11.5, 100) = 1e7 trials split over the ranks
-    (sharding.shard_range, fd-outer flat index); the first ``c4_trials`` trials of the rank's shard are timed
-    (the whole 1.25e6-trial shard of one of 8 GPUs takes ~14x longer). Default (exact) path; one untimed search,
-    then one timed; evals/s summed over ranks / max-over-ranks time."""
+    """BASELINE config 4, sharded: 1e8 photons (T = 1e7 s, p = 0.05, fdot = -1e-12, seed 1), 2-D H_20 on the grid of 1e5
+    f (step 1/(10 T)) x 100 log10|fdot| rows linspace(-13.5, -11.5, 100) = 1e7 trials. The whole grid takes ~107 s per
+    GPU at N = 8 (~14 min at N = 1), so the timed search is its sub-grid of the first ``c4_trials`` / 2 frequencies x
+    the first 2 N fdot rows -- ``c4_trials`` trials per GPU -- through sharding.sharded_search(gather="best"), the
+    tested multi-GPU path (each rank its contiguous fd-outer slice, one all_gather of the per-rank best). Default
+    (exact) path; one untimed search, then one timed; evals/s summed over ranks / max-over-ranks time."""
     import torch
     import torch.distributed as dist
-    from crimp_amd import ops
     from crimp_amd import _native as N
-    from crimp_amd.sharding import shard_range
+    from crimp_amd.sharding import shard_range, sharded_search
     from crimp_amd.synth import pulsed_events
     n, span, f0, fdot, M = a.c4_photons, 1.0e7, 7.123456789, -1.0e-12, 100_000
+    nf = a.c4_trials // 2
     t1 = time.perf_counter()
     t_h = pulsed_events(n, span, f0, pulsed_frac=0.05, fdot=fdot, seed=1)
     gen_s = time.perf_counter() - t1
     t = torch.as_tensor(t_h, device=dev)
-    t0 = (t_h[0] + t_h[-1]) / 2
     del t_h
-    f = torch.as_tensor(f0 + (np.arange(M) - M // 2) / (10.0 * span), device=dev)
-    fd = torch.as_tensor(np.linspace(-13.5, -11.5, 100), device=dev)
-    first, count = shard_range(100 * M, world, rank)
-    count = min(count, a.c4_trials)
-    ops.search(t, t0, f, 20, 1, log10_negfdot=fd, first=first, count=count)   # untimed
+    f = torch.as_tensor((f0 + (np.arange(M) - M // 2) / (10.0 * span))[:nf], device=dev)
+    fd = torch.as_tensor(np.linspace(-13.5, -11.5, 100)[:2 * world], device=dev)
+    first, count = shard_range(2 * world * nf, world, rank)
+    sharded_search(t, f, 20, 1, freq_dot=fd, gather="best")   # untimed
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
-    h = ops.search(t, t0, f, 20, 1, log10_negfdot=fd, first=first, count=count, flags=N.FLAG_TIME_KERNELS)
+    best_pow, best_idx = sharded_search(t, f, 20, 1, freq_dot=fd, gather="best", flags=N.FLAG_TIME_KERNELS)
     torch.cuda.synchronize()
     el = time.perf_counter() - t1
     kms = N.load().crimp_last_kernel_ms()
     nfix = N.load().crimp_last_fixups()
-    best = int(torch.argmax(h).item())
     elt = torch.tensor([el], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(elt, op=dist.ReduceOp.MAX)
     el = float(elt.item())
     ops_launch = OPS_PER_EVAL_HARM * 20 * float(n) * count
     ach = ops_launch / (kms * 1e-3) / 1e12
-    del t, f, fd, h
+    del t, f, fd
     torch.cuda.empty_cache()
+    row, col = divmod(best_idx, nf)
     return {"evals_per_s": float(n) * count * world / el, "unit": "photon*trial evals/s (H_20)", "seconds": el,
             "kernel_ms": kms, "trials_per_gpu_timed": count, "photons": n, "first_flat_trial": first,
-            "fp64_fixup_trials": nfix, "best_flat_trial_in_timed_range": first + best,
+            "fp64_fixup_trials": nfix, "best_power": best_pow, "best_trial": {"fdot_row": row, "f_index": col},
             "photon_generation_s": gen_s,
             "roofline": {"bound": "mfma", "achieved": ach, "peak": PEAK_I8_TOPS, "unit": "TFLOP/s",
                          "frac": ach / PEAK_I8_TOPS,
                          "note": "128 int8 matrix ops per photon*trial*harmonic x 20 harmonics / k_search_exact "
                                  "hipEvent time (the harmonic launches of the search)"},
-            "workload": "config4: %.3g photons, H_20, 2-D grid 1e5 f x 100 fdot = 1e7 trials sharded over %d rank(s); "
-                        "first %d trials of the rank's shard timed" % (n, world, count)}
+            "workload": "config4 sub-grid: %.3g photons, H_20, first %d f x first %d fdot rows of the 1e5 x 100 grid "
+                        "(%d trials per GPU), sharding.sharded_search(gather='best') over %d rank(s)"
+                        % (n, nf, 2 * world, count, world)}
 
 
 def calcphase_leg(a, dev):

@@ -56,9 +56,9 @@ class Template(ctypes.Structure):
 
 
 EXPORTS = ("crimp_version", "crimp_last_error", "crimp_last_kernel_ms", "crimp_last_kernel_times", "crimp_last_fixups",
-           "crimp_last_toa_grid_norms", "crimp_release_scratch",
+           "crimp_last_toa_grid_norms", "crimp_last_toa_grid_fast", "crimp_release_scratch",
            "crimp_device_count", "crimp_calcphase", "crimp_search", "crimp_search_sets", "crimp_toa_points",
-           "crimp_toa_grid", "crimp_toa_fit", "crimp_toa_shape_points", "crimp_binphases")
+           "crimp_toa_grid", "crimp_toa_fit", "crimp_toa_redchi2", "crimp_toa_shape_points", "crimp_binphases")
 
 _lib = None
 _lock = threading.Lock()
@@ -83,6 +83,7 @@ def load(require_device=True):
             L.crimp_last_kernel_ms.restype = ctypes.c_double
             L.crimp_last_fixups.restype = ctypes.c_int64
             L.crimp_last_toa_grid_norms.restype = ctypes.c_int64
+            L.crimp_last_toa_grid_fast.restype = ctypes.c_int64
             L.crimp_last_kernel_times.argtypes = [ctypes.POINTER(ctypes.c_double), i32]
             L.crimp_device_count.argtypes = [ctypes.POINTER(i32)]
             L.crimp_calcphase.argtypes = [P, i64, ctypes.POINTER(TimingModel), i32, P, P, u32, P]
@@ -93,9 +94,10 @@ def load(require_device=True):
             L.crimp_toa_fit.argtypes = [P, P, i64, ctypes.POINTER(Template), P, ctypes.c_double, i32, i32, P, u32, P]
             L.crimp_toa_shape_points.argtypes = [P, P, i64, ctypes.POINTER(Template), P, P, P, P, i64, P, u32, P]
             L.crimp_binphases.argtypes = [P, P, i64, P, i32, P, u32, P]
+            L.crimp_toa_redchi2.argtypes = [P, P, i64, ctypes.POINTER(Template), P, P, P, P, i32, i32, P, u32, P]
             for name in EXPORTS:
                 if name not in ("crimp_last_error", "crimp_last_kernel_ms", "crimp_last_fixups",
-                                "crimp_last_toa_grid_norms"):
+                                "crimp_last_toa_grid_norms", "crimp_last_toa_grid_fast"):
                     getattr(L, name).restype = ctypes.c_int
             _lib = L
         if require_device and not _dev_ok:

@@ -36,6 +36,7 @@ static std::vector<double> g_kernel_times;
 // trials of the last crimp_search recomputed by the fp64 fix-up (exact path)
 static int64_t g_last_fixups = 0;
 static int64_t g_last_grid_norms = 0;  // brute-grid norms evaluated per phShift by the last crimp_toa_fit
+static int64_t g_last_grid_fast = 0;   // the last crimp_toa_fit's brute-grid mode (kGridNoMin | kGridProd8 bits)
 struct KernelTimer {
     hipEvent_t a = nullptr, b = nullptr;
     hipStream_t s;
@@ -1033,18 +1034,29 @@ __global__ __launch_bounds__(kGridBlock) __attribute__((amdgpu_waves_per_eu(4)))
 // block. MFMA result i of lane l is photon (i & 3) + 8 (i >> 2) + 4 (l >> 5) of the 32-photon chunk, phShift column
 // l & 31, so each lane multiplies 4 consecutive photons per group; the two lane halves' sums of a column are added
 // (half 0 + half 1) at the end. fp64 folds every 32-photon chunk; deterministic, not bit-identical to k_toa_grid.
+// Scale: the coefficients and the norms enter multiplied by s = 2^se (grid_mf_scale: the largest amplitude brought into
+// [1, 4096] when it lies outside), so that faint templates keep the split's 2^-22 relative accuracy (a lo part below
+// 2^-14 would be an f16 subnormal) and bright ones cannot overflow f16; every factor norm + h is then s (norm + h)
+// exactly, so the log2 sums lose se per photon (subtracted exactly at the end) and min h is hmn / s. se = 0 (the
+// amplitudes already in range, e.g. the bundled template) is the unscaled kernel, bit for bit.
 constexpr int kGmTile = 128;  // photons per LDS tile
-template <int KF, int NN>
+static_assert(kGridBlock == 32 * 4, "k_toa_grid_mf: 4 waves of 32 phShift columns cover a block's kGridBlock columns");
+// HMIN: track min h per phShift (the public crimp_toa_grid; the device fit skips it when the template's lower bound
+// already keeps every evaluated norm + h positive, k_toa_grid_best then takes that bound). PROD: model values per log2
+// (4, or 8 when the host has checked that a product of eight factors stays a normal fp32, grid_prod8_ok): the min is
+// ~29 % and the logs ~15 % of the likelihood part's VALU.
+template <int KF, int NN, bool HMIN = true, int PROD = 4>
 __global__ __launch_bounds__(256) void k_toa_grid_mf(const double* __restrict__ x, const int64_t* __restrict__ offsets,
                                                      const TplDev* __restrict__ T, const double* __restrict__ norm,
                                                      int nnorm, int a0, int na, const double* __restrict__ phi, int nphi,
-                                                     int64_t chunk, int nint, double* __restrict__ lnsum,
+                                                     int64_t chunk, int nint, int se, double* __restrict__ lnsum,
                                                      double* __restrict__ hmin) {
     constexpr int NM = (KF + 1) / 2;  // MFMAs per 32-photon chunk (two harmonics each)
     __shared__ __attribute__((aligned(16))) u32x4 afr[kGmTile][2 * NM];  // [photon][harmonic]
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hk = lane >> 5;
     const int64_t iv = blockIdx.y, split = blockIdx.z;
     const int bphi = blockIdx.x * kGridBlock + 32 * wv + (lane & 31);
+    const double sc = ldexp(1.0, se);
     // B fragments: the lane's phShift coefficients of harmonics 2m + hk + 1 (zero past K)
     f16x8 bf[NM];
     {
@@ -1055,8 +1067,8 @@ __global__ __launch_bounds__(256) void k_toa_grid_mf(const double* __restrict__ 
             float ca = 0.0f, cb = 0.0f;
             if (j < KF) {
                 const double d = T->loc[j] - (double)(j + 1) * ph;
-                ca = (float)(T->amp[j] * cos(d));
-                cb = (float)(-T->amp[j] * sin(d));
+                ca = (float)(T->amp[j] * cos(d) * sc);
+                cb = (float)(-T->amp[j] * sin(d) * sc);
             }
             uint32_t dh, dl;
             split_xy<false>(ca, cb, dh, dl);
@@ -1067,7 +1079,7 @@ __global__ __launch_bounds__(256) void k_toa_grid_mf(const double* __restrict__ 
     }
     f32x2 nr[NN / 2];
 #pragma unroll
-    for (int a = 0; a < NN; ++a) nr[a / 2][a % 2] = (a < na) ? (float)norm[iv * nnorm + a0 + a] : 1.0f;
+    for (int a = 0; a < NN; ++a) nr[a / 2][a % 2] = (a < na) ? (float)(norm[iv * nnorm + a0 + a] * sc) : 1.0f;
     double acc[NN];
 #pragma unroll
     for (int a = 0; a < NN; ++a) acc[a] = 0.0;
@@ -1112,15 +1124,16 @@ __global__ __launch_bounds__(256) void k_toa_grid_mf(const double* __restrict__ 
             for (int b = 0; b < NN / 2; ++b) pa[b] = f32x2{0.0f, 0.0f};
             if (q0 + 32 <= cnt) {
 #pragma unroll
-                for (int gi = 0; gi < 4; ++gi) {
-                    const float h0 = hv[4 * gi], h1 = hv[4 * gi + 1], h2 = hv[4 * gi + 2], h3 = hv[4 * gi + 3];
-                    hmn = fminf(fminf(fminf(fminf(hmn, h0), h1), h2), h3);
+                for (int gi = 0; gi < 16 / PROD; ++gi) {
+                    if constexpr (HMIN) {
+#pragma unroll
+                        for (int r = 0; r < PROD; ++r) hmn = fminf(hmn, hv[PROD * gi + r]);
+                    }
 #pragma unroll
                     for (int b = 0; b < NN / 2; ++b) {
-                        f32x2 pr = nr[b] + h0;
-                        pr *= nr[b] + h1;
-                        pr *= nr[b] + h2;
-                        pr *= nr[b] + h3;
+                        f32x2 pr = nr[b] + hv[PROD * gi];
+#pragma unroll
+                        for (int r = 1; r < PROD; ++r) pr *= nr[b] + hv[PROD * gi + r];
                         pa[b] += f32x2{__builtin_amdgcn_logf(pr.x), __builtin_amdgcn_logf(pr.y)};
                     }
                 }
@@ -1135,7 +1148,7 @@ __global__ __launch_bounds__(256) void k_toa_grid_mf(const double* __restrict__ 
                         const int row = q0 + r + 8 * gi + 4 * hk;
                         if (row < cnt) {
                             const float h = hv[4 * gi + r];
-                            hmn = fminf(hmn, h);
+                            if constexpr (HMIN) hmn = fminf(hmn, h);
 #pragma unroll
                             for (int b = 0; b < NN / 2; ++b) pr[b] *= nr[b] + h;
                         }
@@ -1156,11 +1169,16 @@ __global__ __launch_bounds__(256) void k_toa_grid_mf(const double* __restrict__ 
         acc[a] = hk == 0 ? acc[a] + o : o + acc[a];
     }
     hmn = fminf(hmn, __shfl_xor(hmn, 32));
+    if (se != 0) {  // every photon's factor carried s = 2^se: log2 s per photon of the split, exactly
+        const double drop = (double)se * (double)(end > beg ? end - beg : 0);
+#pragma unroll
+        for (int a = 0; a < NN; ++a) acc[a] -= drop;
+    }
     if (hk == 0 && bphi < nphi) {
 #pragma unroll
         for (int a = 0; a < NN; ++a)
             if (a < na) lnsum[((split * nint + iv) * nnorm + a0 + a) * nphi + bphi] = acc[a];
-        if (a0 == 0) hmin[(split * nint + iv) * nphi + bphi] = (double)hmn;
+        if (HMIN && a0 == 0) hmin[(split * nint + iv) * nphi + bphi] = ldexp((double)hmn, -se);
     }
 }
 
@@ -1368,6 +1386,7 @@ extern "C" int crimp_version(void) { return CRIMP_VERSION; }
 
 extern "C" int64_t crimp_last_fixups(void) { return g_last_fixups; }
 extern "C" int64_t crimp_last_toa_grid_norms(void) { return g_last_grid_norms; }
+extern "C" int64_t crimp_last_toa_grid_fast(void) { return g_last_grid_fast; }
 
 extern "C" int crimp_release_scratch(void) {
     std::lock_guard<std::mutex> lk(g_mutex);
@@ -1937,6 +1956,33 @@ static int make_tpl(const crimp_template* tpl, TplDev* T) {
 
 // Bounds hmin <= h <= hmax of the template part h = model - norm over every phase and phShift
 // (templatemodels.py:64-82, :166-185, :271-290 with TplDev's folded amplitudes)
+// A lower bound of the template part h over every phase and phShift, from the template's own shape: min over u of
+// h(u) (h(x; phShift) is h shifted in phase for every model, so its minimum does not depend on phShift) sampled on
+// 2^16 points per turn, less the largest change between neighbouring samples (a smooth h cannot dip further between
+// two samples than it moves across one step). Tighter than tpl_bounds' -sum|amp_j| for Fourier templates.
+static double tpl_hmin_scan(const TplDev& T) {
+    const int M = 1 << 16;
+    double mn = INFINITY, dmax = 0.0, prev = 0.0, first = 0.0;
+    for (int i = 0; i <= M; ++i) {
+        const double u = 2.0 * M_PI * (double)(i % M) / (double)M;
+        double h = 0.0;
+        for (int j = 0; j < T.K; ++j) {
+            if (T.model == CRIMP_MODEL_FOURIER)
+                h += T.amp[j] * std::cos((double)(j + 1) * u + T.loc[j]);
+            else if (T.model == CRIMP_MODEL_CAUCHY)
+                h += T.amp[j] / (T.ch[j] - std::cos(u - T.loc[j]));
+            else
+                h += T.amp[j] * std::exp(T.kap[j] * std::cos(u - T.loc[j]));
+        }
+        if (i == 0) first = h;
+        if (i > 0) dmax = std::max(dmax, std::fabs(h - prev));
+        mn = std::min(mn, h);
+        prev = h;
+    }
+    (void)first;
+    return mn - dmax - 1e-12 * (std::fabs(mn) + dmax);
+}
+
 static void tpl_bounds(const TplDev& T, double* hmin, double* hmax) {
     double lo = 0.0, hi = 0.0;
     for (int j = 0; j < T.K; ++j) {
@@ -2026,11 +2072,36 @@ extern "C" int crimp_toa_points(const double* x, const int64_t* offsets, int64_t
     return finish(s, flags);
 }
 
+// k_toa_grid_mf's power-of-two coefficient scale: 0 when the largest |amp_j| is in [1, 4096], otherwise the exponent
+// that brings it there; *ok = false where even that is out of reach (the exponent is clamped to [-64, 20], so that
+// s x 500 stays far from fp32 overflow in the kernel's products of four factors): those go to the VALU kernel.
+static int grid_mf_scale(const TplDev& T, bool* ok) {
+    double m = 0.0;
+    for (int j = 0; j < T.K; ++j) m = std::max(m, std::fabs(T.amp[j]));
+    *ok = std::isfinite(m) && m > 0.0;
+    if (!*ok) return 0;
+    int e = 0;
+    while (std::ldexp(m, e) < 1.0 && e < 20) ++e;
+    while (std::ldexp(m, e) > 4096.0 && e > -64) --e;
+    const double ms = std::ldexp(m, e);
+    *ok = ms >= 1.0 && ms <= 4096.0;
+    return e;
+}
+
 // Per-split brute-grid partial sums (k_toa_grid) for nint <= 65535 intervals of at most maxn photons:
 // pl[((split*nint + i)*nnorm + a)*nphi + b] (log2 sums), ph[(split*nint + i)*nphi + b] (min h).
+// mode (crimp_toa_fit's brute grid, Fourier templates on k_toa_grid_mf only): bit 0 (kGridNoMin) -- no per-phShift
+// min h (*ph = nullptr: the host's template bound certifies every candidate norm + h > 0); bit 1 (kGridProd8) -- log2 of
+// products of eight model values (the host certified that every factor of a valid lattice point stays inside
+// [2^-15, 2^15] after the coefficient scale, or k_toa_grid_best checks it where the min decides validity)
+constexpr int kGridNoMin = 1, kGridProd8 = 2;
 static int toa_grid_partials(Scratch& sc, hipStream_t s, const double* dx, const int64_t* doff, const TplDev* dT,
-                             int model, int K, const double* dnrm, int64_t nnorm, const double* dphi, int64_t nphi, int64_t nint,
-                             int64_t maxn, double** pl, double** ph, int64_t* splits_out) {
+                             const TplDev& T, const double* dnrm, int64_t nnorm, const double* dphi, int64_t nphi,
+                             int64_t nint, int64_t maxn, double** pl, double** ph, int64_t* splits_out,
+                             int mode = 0, int* mode_out = nullptr) {
+    const int model = T.model, K = T.K;
+    bool mf_ok = false;
+    const int se = grid_mf_scale(T, &mf_ok);
     const int64_t pblocks = cdiv(nphi, kGridBlock);
     // photon splits: aim at kGridTarget blocks (2 waves each; 4 waves/SIMD fit, 2048 resident blocks), so
     // that the last round of waves is a small part of the launch (config 5: 1250 intervals x 14 splits = 8.5
@@ -2043,7 +2114,13 @@ static int toa_grid_partials(Scratch& sc, hipStream_t s, const double* dx, const
     chunk = cdiv(chunk, kGridBlock) * kGridBlock;
     splits = cdiv(std::max<int64_t>(maxn, 1), chunk);
     HIPCHK(sc.alloc(pl, (size_t)(splits * nint * nnorm * nphi)));
-    HIPCHK(sc.alloc(ph, (size_t)(splits * nint * nphi)));
+    const bool mf = model == CRIMP_MODEL_FOURIER && CRIMP_GRID_MFMA && K <= kGridKMax && mf_ok;
+    if (!mf) mode = 0;
+    if (mode_out) *mode_out = mode;
+    if (mode & kGridNoMin)
+        *ph = nullptr;
+    else
+        HIPCHK(sc.alloc(ph, (size_t)(splits * nint * nphi)));
     dim3 grid((unsigned)pblocks, (unsigned)nint, (unsigned)splits);
     // norms per lane: 2 or kGridNNSmall for a pruned grid (crimp_toa_fit), otherwise kGridNN per launch
     const int nn = nnorm <= 2 ? 2 : nnorm <= kGridNNSmall ? kGridNNSmall : kGridNN;
@@ -2054,9 +2131,14 @@ static int toa_grid_partials(Scratch& sc, hipStream_t s, const double* dx, const
 #define CRIMP_LG(MD, KK) do { if (nn == 2) CRIMP_LG1(MD, KK, 2, kGridPPL); \
                               else if (nn == kGridNNSmall) CRIMP_LG1(MD, KK, kGridNNSmall, kGridPPL); \
                               else CRIMP_LG1(MD, KK, kGridNN, 1); } while (0)
-        if (model == CRIMP_MODEL_FOURIER && CRIMP_GRID_MFMA && K <= kGridKMax) {
-#define CRIMP_LM1(KK, NNV) k_toa_grid_mf<KK, NNV><<<grid, 256, 0, s>>>(dx, doff, dT, dnrm, (int)nnorm, (int)a0, na, dphi, \
-                                                                       (int)nphi, chunk, (int)nint, *pl, *ph)
+        if (mf) {
+#define CRIMP_LM2(KK, NNV, HM, PR) k_toa_grid_mf<KK, NNV, HM, PR><<<grid, 256, 0, s>>>(dx, doff, dT, dnrm, (int)nnorm, \
+                                                        (int)a0, na, dphi, (int)nphi, chunk, (int)nint, se, *pl, *ph)
+#define CRIMP_LM1(KK, NNV) do { \
+        if (mode == (kGridNoMin | kGridProd8)) CRIMP_LM2(KK, NNV, false, 8); \
+        else if (mode == kGridProd8) CRIMP_LM2(KK, NNV, true, 8); \
+        else if (mode == kGridNoMin) CRIMP_LM2(KK, NNV, false, 4); \
+        else CRIMP_LM2(KK, NNV, true, 4); } while (0)
 #define CRIMP_LM(KK) do { if (nn == 2) CRIMP_LM1(KK, 2); else if (nn == kGridNNSmall) CRIMP_LM1(KK, kGridNNSmall); \
                           else CRIMP_LM1(KK, kGridNN); } while (0)
             switch (K) {
@@ -2071,6 +2153,7 @@ static int toa_grid_partials(Scratch& sc, hipStream_t s, const double* dx, const
             }
 #undef CRIMP_LM
 #undef CRIMP_LM1
+#undef CRIMP_LM2
         } else if (model == CRIMP_MODEL_FOURIER) {
             switch (K) {
                 case 1: CRIMP_LG(CRIMP_MODEL_FOURIER, 1); break;
@@ -2116,6 +2199,7 @@ extern "C" int crimp_toa_fit(const double* x, const int64_t* offsets, int64_t ni
     const bool dev = flags & CRIMP_FLAG_DEVICE_PTRS;
     hipStream_t s = as_stream(stream);
     g_last_grid_norms = 0;
+    g_last_grid_fast = 0;
     std::vector<int64_t> hoff((size_t)nint + 1);
     if (dev) {
         HIPCHK(d2h(s, hoff.data(), offsets, (nint + 1) * sizeof(int64_t)));
@@ -2212,21 +2296,67 @@ extern "C" int crimp_toa_fit(const double* x, const int64_t* offsets, int64_t ni
             HIPCHK(sc.alloc(&dnrm, (size_t)(nint * nc)));
             HIPCHK(h2d(dphi, hphi.data(), nphi * sizeof(double)));
             HIPCHK(h2d(dnrm, hnrm.data(), nint * nc * sizeof(double)));
+            // test hook: start the ascent at the brute lattice point itself (not at the rate norm + parabola vertex)
+            const int lattice_start = getenv("CRIMP_TOA_LATTICE_START") != nullptr;
+            // Fast brute grid (k_toa_grid_mf, Fourier): without the per-phShift min h when a lower bound hb of h keeps
+            // every candidate lattice point valid (norm + h > 0) and decides k_toa_grid_best's start rule as the min
+            // would (hb + N/E > N/E / 2 for every interval); with log2 of products of eight model values when every
+            // factor s (norm + h) of a valid point stays in [2^-15, 2^15], so that a product of eight is a normal fp32:
+            // certified here from hb and the template's upper bound for the norms above -hb, and checked by
+            // k_toa_grid_best (from the min) for the others -- a lattice point there that could have underflowed sends
+            // the grid back to the four-factor kernel (test hook CRIMP_TOA_GRID_SLOW: always the full kernel).
+            const double hb = tpl_hmin_scan(T);
+            int mode = 0;
+            bool mf_ok = false;
+            const double gsc = std::ldexp(1.0, grid_mf_scale(T, &mf_ok));
+            if (getenv("CRIMP_TOA_GRID_SLOW") == nullptr && std::isfinite(hb)) {
+                bool nomin = true, prod8 = true;
+                for (const double nv : hnrm) {
+                    nomin = nomin && nv + hb > 0.0;
+                    prod8 = prod8 && (nv + hhi) * gsc <= std::ldexp(1.0, 15) &&
+                            (nv + hb <= 0.0 || (nv + hb) * gsc >= std::ldexp(1.0, -15));
+                }
+                for (int64_t i = 0; i < nint && nomin; ++i) {
+                    const double r = (double)(hoff[i + 1] - hoff[i]) / hexp[(size_t)i];
+                    nomin = hb + r > 0.5 * r;
+                }
+                mode = (nomin ? kGridNoMin : 0) | (prod8 ? kGridProd8 : 0);
+            }
+            int* dunsafe = nullptr;  // k_toa_grid_best: a valid lattice point whose min factor is below 2^-15 / s
+            HIPCHK(sc.alloc(&dunsafe, 1));
+            HIPCHK(hipMemsetAsync(dunsafe, 0, sizeof(int), s));
             KernelTimer kg(s, flags & CRIMP_FLAG_TIME_KERNELS);  // brute grid: k_toa_grid + k_toa_grid_best
             kg.start();
-            for (int64_t i0 = 0; i0 < nint; i0 += 65535) {
-                const int64_t nb = std::min<int64_t>(65535, nint - i0);
-                int64_t maxn = 0;
-                for (int64_t i = i0; i < i0 + nb; ++i) maxn = std::max(maxn, hoff[i + 1] - hoff[i]);
-                double *pl = nullptr, *ph = nullptr;
-                int64_t splits = 0;
-                rc = toa_grid_partials(sc, s, dx, doff + i0, dT, T.model, T.K, dnrm + i0 * nc, nc, dphi, nphi, nb, maxn, &pl, &ph,
-                                       &splits);
-                if (rc) return rc;
-                k_toa_grid_best<<<(unsigned)nb, 256, 0, s>>>(pl, ph, dnrm + i0 * nc, dphi, doff + i0, de + i0, (int)nc,
-                                                            (int)nphi, (int)nb, (int)splits, T.model, C.sum_amp,
-                                                            grid_n[0], C.lo, C.hi, dstart + 2 * i0);
-                HIPCHK(hipGetLastError());
+            auto brute = [&](int md) -> int {
+                for (int64_t i0 = 0; i0 < nint; i0 += 65535) {
+                    const int64_t nb = std::min<int64_t>(65535, nint - i0);
+                    int64_t maxn = 0;
+                    for (int64_t i = i0; i < i0 + nb; ++i) maxn = std::max(maxn, hoff[i + 1] - hoff[i]);
+                    double *pl = nullptr, *ph = nullptr;
+                    int64_t splits = 0;
+                    int ran = 0;
+                    const int r2 = toa_grid_partials(sc, s, dx, doff + i0, dT, T, dnrm + i0 * nc, nc, dphi, nphi, nb,
+                                                     maxn, &pl, &ph, &splits, md, &ran);
+                    if (r2) return r2;
+                    g_last_grid_fast = ran;
+                    k_toa_grid_best<<<(unsigned)nb, 256, 0, s>>>(pl, ph, dnrm + i0 * nc, dphi, doff + i0, de + i0, (int)nc,
+                                                                (int)nphi, (int)nb, (int)splits, T.model, C.sum_amp,
+                                                                grid_n[0], C.lo, C.hi, lattice_start, hb,
+                                                                (ran & kGridProd8) ? gsc : 0.0, dunsafe, dstart + 2 * i0);
+                    HIPCHK(hipGetLastError());
+                }
+                return CRIMP_OK;
+            };
+            rc = brute(mode);
+            if (rc) return rc;
+            if ((mode & kGridProd8) && !(mode & kGridNoMin)) {  // the runtime half of the eight-factor certificate
+                int unsafe = 0;
+                HIPCHK(d2h(s, &unsafe, dunsafe, sizeof(int)));
+                HIPCHK(hipStreamSynchronize(s));
+                if (unsafe) {
+                    rc = brute(mode & ~kGridProd8);
+                    if (rc) return rc;
+                }
             }
             kg.stop();
         } else {  // Nelder-Mead starts from the template (norm0, phShift 0) (measureToAs.py:301)
@@ -2323,7 +2453,7 @@ extern "C" int crimp_toa_grid(const double* x, const int64_t* offsets, int64_t n
         HIPCHK(h2d(dT, &T, sizeof(T)));
         double *pl = nullptr, *ph = nullptr;
         int64_t splits = 0;
-        rc = toa_grid_partials(sc, s, dx, doff, dT, T.model, T.K, dnrm, nnorm, dphi, nphi, nint, maxn, &pl, &ph, &splits);
+        rc = toa_grid_partials(sc, s, dx, doff, dT, T, dnrm, nnorm, dphi, nphi, nint, maxn, &pl, &ph, &splits);
         if (rc) return rc;
         // combine splits on the host in a fixed order (deterministic)
         std::vector<double> hl((size_t)(splits * nint * nnorm * nphi)), hh((size_t)(splits * nint * nphi));
@@ -2425,6 +2555,123 @@ extern "C" int crimp_toa_shape_points(const double* x, const int64_t* offsets, i
         HIPCHK(hipGetLastError());
         HIPCHK(copy_back(s, out, dout, (size_t)npts * kShapeSums, dev));
         HIPCHK(hipStreamSynchronize(s));
+    }
+    return finish(s, flags);
+}
+
+// redChi2 of every fitted interval on the device (measureToAs.py:385-393 and the Cauchy / von Mises copies):
+// binphases' histogram (np.histogram semantics, as k_binphases) and, against it, the best-fit template curve at the
+// bin centres; chi2 = sum_b (model_b - rate_b)^2 / err_b^2 with rate = cts / (E / nbins), err = sqrt(cts) / (E /
+// nbins) (numpy's division: an empty bin gives inf, or nan where the model is 0 too), redChi2 = chi2 / (nbins -
+// nfree). One block per interval; rec = the fit records (norm [0], phShift [1], ampShift [6]).
+__global__ __launch_bounds__(256) void k_toa_redchi2(const double* __restrict__ x, const int64_t* __restrict__ offsets,
+                                                     const TplDev* __restrict__ T, const double* __restrict__ expo,
+                                                     const double* __restrict__ rec, const double* __restrict__ edges,
+                                                     const double* __restrict__ centers, int nb, int nfree,
+                                                     double* __restrict__ out) {
+    __shared__ unsigned int cnt[256];
+    __shared__ double term[256];
+    const int64_t iv = blockIdx.x;
+    const int tid = threadIdx.x;
+    for (int b = tid; b < 256; b += blockDim.x) cnt[b] = 0;
+    __syncthreads();
+    const double first = edges[0], last = edges[nb];
+    const double denom = last - first;
+    uint32_t rc[kBinRegs];
+#pragma unroll
+    for (int b = 0; b < kBinRegs; ++b) rc[b] = 0;
+    const bool regs = nb <= kBinRegs;
+    for (int64_t i = offsets[iv] + tid; i < offsets[iv + 1]; i += blockDim.x) {
+        const double v = x[i];
+        if (!(v >= first && v <= last)) continue;
+        int64_t idx = (int64_t)(((v - first) / denom) * (double)nb);
+        if (idx == nb) idx -= 1;
+        if (v < edges[idx]) idx -= 1;
+        if (v >= edges[idx + 1] && idx != nb - 1) idx += 1;
+        if (regs) {
+#pragma unroll
+            for (int b = 0; b < kBinRegs; ++b) rc[b] += idx == b ? 1u : 0u;
+        } else {
+            atomicAdd(&cnt[idx], 1u);
+        }
+    }
+    if (regs) {
+#pragma unroll
+        for (int b = 0; b < kBinRegs; ++b)
+            if (rc[b]) atomicAdd(&cnt[b], rc[b]);
+    }
+    __syncthreads();
+    if (tid < nb) {
+        const double n = rec[iv * 8], ph = rec[iv * 8 + 1], A = rec[iv * 8 + 6];
+        const double xx = centers[tid];
+        double y = n;  // toafit.ToAFitter.curve: fourseries / wrapcauchy / vonmises (templatemodels.py:64-82, :166-185,
+                       // :271-290); Fourier by angle subtraction as the host formed it
+        for (int j = 0; j < T->K; ++j) {
+            if (T->model == CRIMP_MODEL_FOURIER) {
+                const double ang = (double)(j + 1) * 2.0 * M_PI * xx + T->loc[j], bph = (double)(j + 1) * ph;
+                y = y + T->amp[j] * A * (cos(ang) * cos(bph) + sin(ang) * sin(bph));
+            } else if (T->model == CRIMP_MODEL_CAUCHY) {
+                y = y + T->amp[j] * A / (T->ch[j] - cos(xx - T->loc[j] - ph));
+            } else {
+                y = y + T->amp[j] * A * exp(T->kap[j] * cos(xx - T->loc[j] - ph));
+            }
+        }
+        const double w = expo[iv] / (double)nb, c = (double)cnt[tid];
+        const double rate = c / w, err = sqrt(c) / w;
+        term[tid] = ((y - rate) * (y - rate)) / (err * err);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        double chi2 = 0.0;
+        for (int b = 0; b < nb; ++b) chi2 += term[b];
+        out[iv] = chi2 / (double)(nb - nfree);
+    }
+}
+
+extern "C" int crimp_toa_redchi2(const double* x, const int64_t* offsets, int64_t nint, const crimp_template* tpl,
+                                 const double* exposure, const double* records, const double* edges,
+                                 const double* centers, int32_t nbins, int32_t nfree, double* out, uint32_t flags,
+                                 void* stream) {
+    ARGCHK(nint >= 1 && nbins >= 1 && nbins <= 256, "bad sizes (nbins must be 1..256)");
+    ARGCHK(x != nullptr && offsets != nullptr && exposure != nullptr && records != nullptr && edges != nullptr &&
+               centers != nullptr && out != nullptr, "null argument");
+    ARGCHK(nint <= 2147483647LL, "too many intervals");
+    TplDev T;
+    int rc = make_tpl(tpl, &T);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(g_mutex);
+    if (flags & CRIMP_FLAG_TIME_KERNELS) {
+        g_kernel_times.clear();
+        g_last_kernel_ms = -1.0;
+    }
+    const bool dev = flags & CRIMP_FLAG_DEVICE_PTRS;
+    hipStream_t s = as_stream(stream);
+    int64_t ntot = 0;
+    if (dev) {
+        HIPCHK(d2h(s, &ntot, offsets + nint, sizeof(int64_t)));
+        HIPCHK(hipStreamSynchronize(s));
+    } else {
+        ntot = offsets[nint];
+    }
+    {
+        Scratch sc(s);
+        const double *dx = nullptr, *de = nullptr, *dc = nullptr, *dexp = nullptr, *drec = nullptr;
+        const int64_t* doff = nullptr;
+        double* dout = nullptr;
+        TplDev* dT = nullptr;
+        HIPCHK(stage_in(sc, x, (size_t)ntot, dev, &dx));
+        HIPCHK(stage_in(sc, offsets, (size_t)nint + 1, dev, &doff));
+        HIPCHK(stage_in(sc, exposure, (size_t)nint, dev, &dexp));
+        HIPCHK(stage_in(sc, records, (size_t)nint * 8, dev, &drec));
+        HIPCHK(stage_in(sc, edges, (size_t)nbins + 1, dev, &de));
+        HIPCHK(stage_in(sc, centers, (size_t)nbins, dev, &dc));
+        HIPCHK(stage_out(sc, out, (size_t)nint, dev, &dout));
+        HIPCHK(sc.alloc(&dT, 1));
+        HIPCHK(h2d(dT, &T, sizeof(T)));
+        k_toa_redchi2<<<(unsigned)nint, 256, 0, s>>>(dx, doff, dT, dexp, drec, de, dc, nbins, nfree, dout);
+        HIPCHK(hipGetLastError());
+        HIPCHK(copy_back(s, out, dout, (size_t)nint, dev));
+        HIPCHK(hipStreamSynchronize(s));  // the template copy above reads host T
     }
     return finish(s, flags);
 }

@@ -71,11 +71,24 @@ struct ExArg {
     uint32_t idx;  // table index
     float y;       // residual in table steps, |y| <= 1/2
 };
+// Floating-point contraction is spelled out here (contract off, explicit fma) so that the digits -- and the exact
+// integer sums -- are a function of the source alone: with hipcc's default contraction the choice between
+// fma(a, b, -kf) and rint(a b) - kf depended on the schedule, and a build without the ex_ready fences returned
+// different (equally accurate) sums (profiles/r04/ab_fences.log).
 __device__ __forceinline__ ExArg ex_begin(double t) {
+#pragma clang fp contract(off)
     const double M = 6755399441055744.0;  // 1.5 * 2^52: low mantissa bits of t + M = rint(t) (|t| < 2^51)
     const double tm = t + M;
     const double kf = tm - M;
     return ExArg{(uint32_t)__double2loint(tm) & (kExTab - 1), (float)(t - kf)};  // t - kf is exact
+}
+// the same for the phase t = a * b taken from the exact product: index from fma(a, b, M), residual fma(a, b, -kf)
+__device__ __forceinline__ ExArg ex_begin_prod(double a, double b) {
+#pragma clang fp contract(off)
+    const double M = 6755399441055744.0;
+    const double tm = __builtin_fma(a, b, M);
+    const double kf = tm - M;
+    return ExArg{(uint32_t)__double2loint(tm) & (kExTab - 1), (float)__builtin_fma(a, b, -kf)};
 }
 // -> digit dwords of cos (dc) and sin (ds), in two halves (ex_end_a: the rotation terms, ex_end_b: the digits)
 struct ExRot { float ts, tc; };
@@ -137,17 +150,57 @@ __device__ __forceinline__ uint32_t ex_neg_digits(uint32_t d) {
 // waits (s_waitcnt) for the asm operands.
 // The wave's 16 int32 accumulator tiles live in AGPRs for the whole kernel, outside the compiler's register
 // model: tile m (level m >> 2, fragment (m >> 1) & 1, Re/Im m & 1) is a[16m : 16m + 15]. Only these asm helpers
-// touch AGPRs (the kernel has no spills, so hipcc never allocates them; ex_acc_zero's clobber makes the code
-// object reserve all 256), so the accumulators never move; tools/isa_hazards.py checks both on the built code.
+// touch AGPRs, so the accumulators never move. Every MFMA statement lists all 256 AGPRs as clobbers (and
+// ex_acc_zero's clobber makes the code object reserve them): hipcc may then keep no value of its own in an AGPR
+// across any MFMA, so under register pressure it spills to scratch -- visible, and rejected by the no-scratch test
+// -- instead of allocating AGPRs. Without the clobbers (CRIMP_EX_AGPR_CLOBBERS=0) the build without the ex_open
+// fences parks the 64-bit photon-time address of fetch_dt in a0:a1, tile 0's MFMAs overwrite it and the next
+// global_load faults (profiles/r03/ab_search_no_open_fences_rejected_fault.log; tools/agpr_check.py flags it on the
+// CPU). The cost is one s_nop 0 per chunk's MFMA sequence. tools/isa_hazards.py and tools/agpr_check.py check
+// the built code.
+#ifndef CRIMP_EX_AGPR_CLOBBERS
+#define CRIMP_EX_AGPR_CLOBBERS 1
+#endif
+// every AGPR, as a clobber of each MFMA statement (below)
+#define EX_ALL_AGPRS \
+    "a0", "a1", "a2", "a3", "a4", "a5", "a6", "a7", "a8", "a9", "a10", "a11", "a12", "a13", "a14", "a15", \
+    "a16", "a17", "a18", "a19", "a20", "a21", "a22", "a23", "a24", "a25", "a26", "a27", "a28", "a29", "a30", "a31", \
+    "a32", "a33", "a34", "a35", "a36", "a37", "a38", "a39", "a40", "a41", "a42", "a43", "a44", "a45", "a46", "a47", \
+    "a48", "a49", "a50", "a51", "a52", "a53", "a54", "a55", "a56", "a57", "a58", "a59", "a60", "a61", "a62", "a63", \
+    "a64", "a65", "a66", "a67", "a68", "a69", "a70", "a71", "a72", "a73", "a74", "a75", "a76", "a77", "a78", "a79", \
+    "a80", "a81", "a82", "a83", "a84", "a85", "a86", "a87", "a88", "a89", "a90", "a91", "a92", "a93", "a94", "a95", \
+    "a96", "a97", "a98", "a99", "a100", "a101", "a102", "a103", "a104", "a105", "a106", "a107", "a108", "a109", "a110", "a111", \
+    "a112", "a113", "a114", "a115", "a116", "a117", "a118", "a119", "a120", "a121", "a122", "a123", "a124", "a125", "a126", "a127", \
+    "a128", "a129", "a130", "a131", "a132", "a133", "a134", "a135", "a136", "a137", "a138", "a139", "a140", "a141", "a142", "a143", \
+    "a144", "a145", "a146", "a147", "a148", "a149", "a150", "a151", "a152", "a153", "a154", "a155", "a156", "a157", "a158", "a159", \
+    "a160", "a161", "a162", "a163", "a164", "a165", "a166", "a167", "a168", "a169", "a170", "a171", "a172", "a173", "a174", "a175", \
+    "a176", "a177", "a178", "a179", "a180", "a181", "a182", "a183", "a184", "a185", "a186", "a187", "a188", "a189", "a190", "a191", \
+    "a192", "a193", "a194", "a195", "a196", "a197", "a198", "a199", "a200", "a201", "a202", "a203", "a204", "a205", "a206", "a207", \
+    "a208", "a209", "a210", "a211", "a212", "a213", "a214", "a215", "a216", "a217", "a218", "a219", "a220", "a221", "a222", "a223", \
+    "a224", "a225", "a226", "a227", "a228", "a229", "a230", "a231", "a232", "a233", "a234", "a235", "a236", "a237", "a238", "a239", \
+    "a240", "a241", "a242", "a243", "a244", "a245", "a246", "a247", "a248", "a249", "a250", "a251", "a252", "a253", "a254", "a255"
+// CRIMP_EX_PRE_NOP=N (A/B only): every MFMA statement starts with s_nop N, N + 1 wait states after whatever
+// hipcc issued before it
+#ifdef CRIMP_EX_PRE_NOP
+#define EX_STR2(x) #x
+#define EX_STR(x) EX_STR2(x)
+#define EX_PRE "s_nop " EX_STR(CRIMP_EX_PRE_NOP) "\n\t"
+#else
+#define EX_PRE ""
+#endif
+#if !CRIMP_EX_AGPR_CLOBBERS
+#undef EX_ALL_AGPRS
+#define EX_ALL_AGPRS
+#endif
 template <int M>
 __device__ __forceinline__ void ex_mfma(const i32x4& a, const i32x4& b) {
-    asm volatile("v_mfma_i32_32x32x32_i8 a[%c2:%c3], %0, %1, a[%c2:%c3]" ::"v"(a), "v"(b), "i"(16 * M),
-                 "i"(16 * M + 15));
+    asm volatile(EX_PRE "v_mfma_i32_32x32x32_i8 a[%c2:%c3], %0, %1, a[%c2:%c3]" ::"v"(a), "v"(b), "i"(16 * M),
+                 "i"(16 * M + 15) : EX_ALL_AGPRS);
 }
 template <int M>
 __device__ __forceinline__ void ex_smfma(const i32x4& a, const i32x8& b, int idx) {
-    asm volatile("v_smfmac_i32_32x32x64_i8 a[%c3:%c4], %0, %1, %2" ::"v"(a), "v"(b), "v"(idx), "i"(16 * M),
-                 "i"(16 * M + 15));
+    asm volatile(EX_PRE "v_smfmac_i32_32x32x64_i8 a[%c3:%c4], %0, %1, %2" ::"v"(a), "v"(b), "v"(idx), "i"(16 * M),
+                 "i"(16 * M + 15) : EX_ALL_AGPRS);
 }
 template <int R>
 __device__ __forceinline__ int ex_acc_read(std::integral_constant<int, R>) {
@@ -172,17 +225,46 @@ __device__ __forceinline__ void ex_acc_zero() {
     asm volatile("v_accvgpr_write_b32 a255, 0" ::: "a255");
     ex_static_for<255>([&](auto r) { asm volatile("v_accvgpr_write_b32 a%c0, 0" ::"i"(decltype(r)::value)); });
 }
+// A/B switches of the fence analysis: CRIMP_EX_OPEN=0 / CRIMP_EX_READY=0 build the kernel without
+// the ex_open / ex_ready fences. Without ex_ready, hipcc computes an MFMA's operands right before it (2 wait
+// states after the writing VALU, where the fenced build leaves >= 16): tools/isa_hazards.py rejects that build.
+#ifndef CRIMP_EX_OPEN
+#define CRIMP_EX_OPEN 1
+#endif
+#ifndef CRIMP_EX_READY
+#define CRIMP_EX_READY 1
+#endif
 __device__ __forceinline__ void ex_keep(const i32x4& x) { asm volatile("" ::"v"(x)); }
 __device__ __forceinline__ void ex_keep(const i32x8& x) { asm volatile("" ::"v"(x)); }
+#if CRIMP_EX_READY
 __device__ __forceinline__ void ex_ready(const i32x4& x) { asm volatile("" ::"v"(x)); }
 __device__ __forceinline__ void ex_ready(uint32_t x, float y) { asm volatile("" ::"v"(x), "v"(y)); }
 __device__ __forceinline__ void ex_ready(uint32_t x, uint32_t y) { asm volatile("" ::"v"(x), "v"(y)); }
+__device__ __forceinline__ void ex_ready(float x, float y) { asm volatile("" ::"v"(x), "v"(y)); }
+__device__ __forceinline__ void ex_ready(uint32_t x) { asm volatile("" ::"v"(x)); }
+#else
+__device__ __forceinline__ void ex_ready(const i32x4&) {}
+__device__ __forceinline__ void ex_ready(uint32_t, float) {}
+__device__ __forceinline__ void ex_ready(uint32_t, uint32_t) {}
+__device__ __forceinline__ void ex_ready(float, float) {}
+__device__ __forceinline__ void ex_ready(uint32_t) {}
+#endif
+#if CRIMP_EX_OPEN == 2  // A/B: a scheduling barrier instead of the opaque redefinition (no VGPR output, no pad)
+__device__ __forceinline__ void ex_open(double&) { __builtin_amdgcn_sched_barrier(0); }
+__device__ __forceinline__ void ex_open(i32x4&) { __builtin_amdgcn_sched_barrier(0); }
+__device__ __forceinline__ void ex_open(float&) { __builtin_amdgcn_sched_barrier(0); }
+__device__ __forceinline__ void ex_open(uint32_t&, uint32_t&) { __builtin_amdgcn_sched_barrier(0); }
+#elif CRIMP_EX_OPEN
 __device__ __forceinline__ void ex_open(double& x) { asm volatile("" : "+v"(x)); }
 __device__ __forceinline__ void ex_open(i32x4& x) { asm volatile("" : "+v"(x)); }
 __device__ __forceinline__ void ex_open(float& x) { asm volatile("" : "+v"(x)); }
-__device__ __forceinline__ void ex_ready(float x, float y) { asm volatile("" ::"v"(x), "v"(y)); }
-__device__ __forceinline__ void ex_ready(uint32_t x) { asm volatile("" ::"v"(x)); }
 __device__ __forceinline__ void ex_open(uint32_t& x, uint32_t& y) { asm volatile("" : "+v"(x), "+v"(y)); }
+#else
+__device__ __forceinline__ void ex_open(double&) {}
+__device__ __forceinline__ void ex_open(i32x4&) {}
+__device__ __forceinline__ void ex_open(float&) {}
+__device__ __forceinline__ void ex_open(uint32_t&, uint32_t&) {}
+#endif
 
 // level-4 operand: every digit dword shifted right by one byte (logical: the top byte becomes 0)
 typedef unsigned ex_u32x4 __attribute__((ext_vector_type(4)));
@@ -253,7 +335,7 @@ __global__ __launch_bounds__(kExBlock, 1) void k_search_exact(
     auto v_read = [&](int cj, int s, VItem& it) { it.d = sdt[(cj & (kExDtSlots - 1)) * kExChunk + pp + 4 * s]; };
     // a photon past the split (pp + 4 s >= nlive: wave-uniform) reads the zero entry, so its V digits are 0
     auto v_begin = [&](VItem& it, int s, int nlive) {
-        it.g = ex_begin(gbv * it.d);
+        it.g = ex_begin_prod(gbv, it.d);
         it.g.idx = ppu + 4 * s < nlive ? it.g.idx : (uint32_t)kExTab;
     };
     auto v_table = [&](VItem& it) { it.e = tab[it.g.idx]; };
@@ -322,7 +404,10 @@ __global__ __launch_bounds__(kExBlock, 1) void k_search_exact(
         read_dt(c, 2 * p + 1, D.d[1]);
     };
     // the phase in table units; the 2-D grid's dt^2 is formed here as d * d, bit-identical to the dt2 array
-    auto begin1 = [&](double d) -> ExArg { return ex_begin(TWOD ? fma(fa, d, c2 * (d * d)) : fa * d); };
+    auto begin1 = [&](double d) -> ExArg {
+#pragma clang fp contract(off)
+        return TWOD ? ex_begin(__builtin_fma(fa, d, c2 * (d * d))) : ex_begin_prod(fa, d);
+    };
     // B fragments of pair p of chunk c (p = kExQuads / 2 is pair 0 of chunk c+1)
     auto read_b = [&](int c, int p, ExOps& o) {
 #pragma unroll

@@ -17,6 +17,8 @@
 // iterative profile's to ~1e-10, and the scan compares it with a 0.5 threshold).
 
 constexpr int kFitBlock = kPtsBlock;
+// fit_moments2 fills the second phShift's coefficients from threads 64 .. 64 + K - 1 (the first wave fills the first's)
+static_assert(kFitBlock >= 64 + CRIMP_MAX_COMP, "fit_moments2: the block must cover threads 64 .. 64 + CRIMP_MAX_COMP");
 constexpr double kHalfChi2OneSigma = 0.500021713558733;  // 0.5 * chi2.ppf(0.6827, 1)   (measureToAs.py:324)
 constexpr double kTwoPi = 6.283185307179586476925286766559;
 
@@ -218,8 +220,25 @@ __device__ FitEval fit_eval(const double* __restrict__ x, int64_t a, int64_t b, 
     return r;
 }
 
-// toafit._newton_step: Levenberg-shifted Newton direction with a trust region (0.05 rad, half the norm)
-__device__ void fit_newton_dir(double n, const FitEval& e, double& dn, double& dp, bool* pure = nullptr) {
+// toafit._newton_step: Levenberg-shifted Newton direction with a trust region (0.05 rad, half the norm). Projected:
+// a coordinate on its bound whose gradient points out of the box is held there and the other takes its own 1-D Newton
+// step, so that when phShift stops on -+bound (a maximum beyond it) the norm is still maximised exactly -- the
+// reference's lmfit fit, and the oracle's bounded search, profile it there; a joint step whose phShift part is clipped
+// away would leave the norm wherever the clipped line search stalls (redChi2 off by ~1e-5).
+__device__ void fit_newton_dir(double n, double p, const FitCfg& C, const FitEval& e, double& dn, double& dp,
+                               bool* pure = nullptr) {
+    const bool pfix = (p <= -C.pb && e.gp < 0.0) || (p >= C.pb && e.gp > 0.0);
+    const bool nfix = (n <= C.lo && e.gn < 0.0) || (n >= C.hi && e.gn > 0.0);
+    if (pfix || nfix) {
+        dn = nfix ? 0.0 : (e.hnn < 0.0 ? -e.gn / e.hnn : (e.gn > 0.0 ? 0.1 : -0.1) * fabs(n));
+        dp = pfix ? 0.0 : (e.hpp < 0.0 ? -e.gp / e.hpp : (e.gp > 0.0 ? 0.05 : -0.05));
+        double sc = fmin(1.0, 0.05 / fmax(fabs(dp), 1e-300));
+        sc = fmin(sc, 0.5 * fabs(n) / fmax(fabs(dn), 1e-300));
+        if (pure) *pure = sc == 1.0 && (nfix || e.hnn < 0.0) && (pfix || e.hpp < 0.0);
+        dn *= sc;
+        dp *= sc;
+        return;
+    }
     const double hnn = e.hnn, hnp = e.hnp, hpp = e.hpp;
     const double tr = hnn + hpp;
     const double det = hnn * hpp - hnp * hnp;
@@ -673,7 +692,10 @@ __device__ FitEval3 fit_ascent3(const double* __restrict__ x, int64_t a, int64_t
     ++nev;
     for (int it = 0; it < max_iter; ++it) {
         double d[3];
-        fit_newton_dir3(v, e, mask, d);
+        int m = mask;  // projected: a coordinate on its bound with the gradient pointing out is held (fit_newton_dir)
+        for (int i = 0; i < 3; ++i)
+            if ((v[i] <= lo[i] && e.g[i] < 0.0) || (v[i] >= hi[i] && e.g[i] > 0.0)) m &= ~(1 << i);
+        fit_newton_dir3(v, e, m, d);
         double t = 1.0, tv[3] = {v[0], v[1], v[2]};
         FitEval3 e2 = e;
         bool ok = false;
@@ -787,7 +809,7 @@ __global__ __launch_bounds__(kFitBlock) __attribute__((amdgpu_waves_per_eu(CRIMP
     for (int it = 0; it < 60; ++it) {  // toafit.maximise
         double dn, dp;
         bool pure = false;
-        fit_newton_dir(n, e, dn, dp, &pure);
+        fit_newton_dir(n, p, C, e, dn, dp, &pure);
         {   // converged: even the full step moves less than the stopping tolerance, so the pass that would confirm
             // it is skipped (toafit.maximise does the same)
             const double fn = clipd(n + dn, C.lo, C.hi), fp = clipd(p + dp, -C.pb, C.pb);
@@ -902,7 +924,9 @@ __global__ __launch_bounds__(256) void k_toa_grid_best(const double* __restrict_
                                                        const int64_t* __restrict__ offsets,
                                                        const double* __restrict__ expo, int nnorm, int nphi, int nint,
                                                        int splits, int model, double sum_amp, double norm_first,
-                                                       double lo, double hi, double* __restrict__ start) {
+                                                       double lo, double hi, int plain, double hconst,
+                                                       double prod8_scale, int* __restrict__ unsafe,
+                                                       double* __restrict__ start) {
     __shared__ double bv[4];
     __shared__ int bi[4];
     const int64_t iv = blockIdx.x;
@@ -914,8 +938,9 @@ __global__ __launch_bounds__(256) void k_toa_grid_best(const double* __restrict_
         double v = 0.0;
         for (int sp = 0; sp < splits; ++sp) v += pl[(((int64_t)sp * nint + iv) * nnorm + ai) * nphi + bj];
         const double ln = v * 0.69314718055994530942;  // log2 sums -> ln
-        double hm = INFINITY;
-        for (int sp = 0; sp < splits; ++sp) hm = fmin(hm, ph[((int64_t)sp * nint + iv) * nphi + bj]);
+        double hm = ph ? INFINITY : hconst;  // no per-phShift min: the host's lower bound of h (crimp_toa_fit)
+        if (ph)
+            for (int sp = 0; sp < splits; ++sp) hm = fmin(hm, ph[((int64_t)sp * nint + iv) * nphi + bj]);
         const double nn = norm[iv * nnorm + ai];
         double ll;
         if (model == CRIMP_MODEL_FOURIER) {
@@ -924,7 +949,11 @@ __global__ __launch_bounds__(256) void k_toa_grid_best(const double* __restrict_
             const double F = kTwoPi * nn + sum_amp;
             ll = -F * E / kTwoPi + N * log(F * E / kTwoPi) + (ln - N * log(F));
         }
-        if (!((hm + nn) > 0) || !isfinite(ll)) ll = -INFINITY;
+        if (!((hm + nn) > 0) || !isfinite(ll)) {
+            ll = -INFINITY;
+        } else if (prod8_scale > 0.0 && (hm + nn) * prod8_scale < 0x1p-15) {
+            atomicOr(unsafe, 1);  // a product of eight factors could have underflowed: the host reruns with four
+        }
         return ll;
     };
     for (int idx = threadIdx.x; idx < nnorm * nphi; idx += 256) {
@@ -963,11 +992,13 @@ __global__ __launch_bounds__(256) void k_toa_grid_best(const double* __restrict_
             // solves sum_i 1/(n + h_i) = E, so n* ~ N/E - <h>: within a few % where the lattice is one 26-unit norm
             // step away), unless that is outside the bounds or makes the model non-positive at this phShift; the
             // lattice norm otherwise. Same basin, same maximum, two fewer Newton passes (toafit.fit_host does the same)
+            // (plain: the test hook CRIMP_TOA_LATTICE_START, the lattice point itself, as lmfit hands it on)
             const double r = N / E;
-            double hmx = INFINITY;
+            double hmx = ph ? INFINITY : hconst;
             const int bj = bidx % nphi;
-            for (int sp = 0; sp < splits; ++sp) hmx = fmin(hmx, ph[((int64_t)sp * nint + iv) * nphi + bj]);
-            const bool use_rate = r >= lo && r <= hi && hmx + r > 0.0;
+            if (ph)
+                for (int sp = 0; sp < splits; ++sp) hmx = fmin(hmx, ph[((int64_t)sp * nint + iv) * nphi + bj]);
+            const bool use_rate = !plain && r >= lo && r <= hi && hmx + r > 0.0;
             start[2 * iv] = use_rate ? r : norm[iv * nnorm + bidx / nphi];
             // and the phShift at the vertex of the parabola through the maximum and its two lattice neighbours (at
             // the maximum's norm; within half a lattice step), where the model stays well positive

@@ -26,7 +26,7 @@ from ._native import STAT_H
 from .readPPtemplate import readPPtemplate
 from .readtimingmodel import ReadTimingModel
 from .timfile import phshiftTotimfile
-from .toafit import ToAFitter
+from .toafit import ToAFitter, warn_capped
 from .toafit_vary import VaryParamFitter
 
 logger = get_logger(__name__)
@@ -93,7 +93,7 @@ def defineinitialfitparam(tempModPP, readvaryparam=False):
 
 
 def _single(model, tempModPP, phases, exposureInt, phShiftRes, nbrBins, varyAmps, brutemin, readvaryparam,
-            plotLLs, plotPPs):
+            plotLLs, plotPPs, outFile=''):
     if str(tempModPP["model"]).lower() != model:
         raise ValueError("template model %s used with measureToA_%s" % (tempModPP["model"], model))
     x = np.ascontiguousarray(np.ravel(phases), dtype=np.float64)
@@ -103,6 +103,7 @@ def _single(model, tempModPP, phases, exposureInt, phShiftRes, nbrBins, varyAmps
     else:
         fit = ToAFitter(x, np.array([0, x.size]), np.array([float(exposureInt)]), tempModPP, phShiftRes, nbrBins)
         r = fit.fit(brutemin=brutemin, vary_amps=bool(varyAmps))
+    warn_capped(r, phShiftRes, [outFile], logger)                 # measureToAs.py:348-350, :373-375
     if plotLLs or plotPPs:
         logger.warning("plotPPs/plotLLs are diagnostic plots and are not produced by this build")
     return {"phShi": float(r["phShi"][0]), "phShi_LL": float(r["phShi_LL"][0]), "phShi_UL": float(r["phShi_UL"][0]),
@@ -113,21 +114,21 @@ def measureToA_fourier(tempModPP, cycleFoldedPhases, exposureInt, outFile='', ph
                        varyAmps=False, brutemin=False, plotPPs=False, plotLLs=False, readvaryparam=False):
     """Fourier-template ToA (measureToAs.py:254-403); phases in cycles [0,1)."""
     return _single("fourier", tempModPP, cycleFoldedPhases, exposureInt, phShiftRes, nbrBins, varyAmps, brutemin,
-                   readvaryparam, plotLLs, plotPPs)
+                   readvaryparam, plotLLs, plotPPs, outFile)
 
 
 def measureToA_cauchy(tempModPP, cycleFoldedPhases, exposureInt, outFile='', phShiftRes=1000, nbrBins=15,
                       varyAmps=False, brutemin=False, plotPPs=False, plotLLs=False, readvaryparam=False):
     """Wrapped-Cauchy ToA (measureToAs.py:406-548); phases in radians [0,2pi)."""
     return _single("cauchy", tempModPP, cycleFoldedPhases, exposureInt, phShiftRes, nbrBins, varyAmps, brutemin,
-                   readvaryparam, plotLLs, plotPPs)
+                   readvaryparam, plotLLs, plotPPs, outFile)
 
 
 def measureToA_vonmises(tempModPP, cycleFoldedPhases, exposureInt, outFile='', phShiftRes=1000, nbrBins=15,
                         varyAmps=False, brutemin=False, plotPPs=False, plotLLs=False, readvaryparam=False):
     """von Mises ToA (measureToAs.py:551-693); phases in radians [0,2pi)."""
     return _single("vonmises", tempModPP, cycleFoldedPhases, exposureInt, phShiftRes, nbrBins, varyAmps, brutemin,
-                   readvaryparam, plotLLs, plotPPs)
+                   readvaryparam, plotLLs, plotPPs, outFile)
 
 
 HEADER = ('ToA \t ToA_mid \t ToA_start \t ToA_end \t ToA_lenInt \t ToA_exp \t nbr_events \t count_rate \t phShift'
@@ -216,10 +217,38 @@ def measure_intervals(TIMEMJD, timMod, tempModPP, starts, ends, exposures, phShi
     return res
 
 
+def _interval_counts(T, starts, ends):
+    """Photons of every interval [start, end] (inclusive, measureToAs.py:173-174) without selecting them."""
+    T = np.asarray(T, dtype=np.float64)
+    if T.size < 2 or np.all(T[1:] >= T[:-1]):
+        return np.maximum(np.searchsorted(T, ends, side="right") - np.searchsorted(T, starts, side="left"), 0)
+    return np.array([np.count_nonzero((T >= a) & (T <= b)) for a, b in zip(starts, ends)], dtype=np.int64)
+
+
+def _batches(counts, budget):
+    """Consecutive runs of intervals holding at most ``budget`` photons each (at least one interval per run)."""
+    out, lo, acc = [], 0, 0
+    for i, c in enumerate(counts):
+        if i > lo and acc + c > budget:
+            out.append((lo, i))
+            lo, acc = i, 0
+        acc += int(c)
+    if lo < len(counts):
+        out.append((lo, len(counts)))
+    return out
+
+
 def measureToAs(evtFile, timMod, tempModPP, toagtifile, eneLow=0.5, eneHigh=10., toaStart=0, toaEnd=None,
                 phShiftRes=1000, nbrBins=15, varyAmps=False, readvaryparam=False, brutemin=False, plotPPs=False,
                 plotLLs=False, toaFile='ToAs', timFile=None):
-    """ToAs of every interval of ``toagtifile`` (measureToAs.py:64-251)."""
+    """ToAs of every interval of ``toagtifile`` (measureToAs.py:64-251).
+
+    The reference writes each ToA's row as soon as it is measured (:160-162, :222-226). Here the intervals are
+    fitted in batches of at most CRIMP_TOA_BATCH_PHOTONS photons (default 2^27) and each batch's rows are written
+    and flushed when the batch finishes. An interval without photons ends the reference's loop with an IndexError
+    at :182 after the rows before it were written; the same happens here: the intervals before it are measured and
+    written, then the IndexError is raised."""
+    import os
     import pandas as pd
     logger.info("\n Running measureToAs with input parameters: evtFile: %s timMod: %s tempModPP: %s toagtifile: %s"
                 " eneLow: %s eneHigh: %s toaStart: %s toaEnd: %s phShiftRes: %s brutemin: %s toaFile: %s",
@@ -232,25 +261,45 @@ def measureToAs(evtFile, timMod, tempModPP, toagtifile, eneLow=0.5, eneHigh=10.,
     lenInt, expo = iv['ToA_lenInt'].to_numpy(), iv['ToA_exposure'].to_numpy()
     events, rate = iv['Events'].to_numpy(), iv['ct_rate'].to_numpy()
     toaEnd = np.size(en) if toaEnd is None else toaEnd + 1  # :147-150 (inclusive end)
-    rng = list(range(toaStart, toaEnd))
+    rng = np.arange(toaStart, toaEnd)
     tmpl = readPPtemplate(tempModPP)
+    tm = timMod if isinstance(timMod, dict) else ReadTimingModel(str(timMod)).readfulltimingmodel()[0]
     logger.info('\n Using best fit model of template {} to measure ToAs'.format(tmpl["model"]))
-    for ii in rng:
-        print('ToA {}'.format(ii))
-    res = measure_intervals(TIMEMJD, timMod, tmpl, st[rng], en[rng], expo[rng], phShiftRes, nbrBins, varyAmps,
-                            brutemin, readvaryparam)
+    counts = _interval_counts(TIMEMJD, st[rng], en[rng])
+    empty = np.nonzero(counts <= 0)[0]
+    nfit = int(empty[0]) if empty.size else rng.size      # the reference's loop ends at the first empty interval
+    T = _device_times(TIMEMJD) if nfit else None
+    T = TIMEMJD if T is None else T
+    budget = int(os.environ.get("CRIMP_TOA_BATCH_PHOTONS", 1 << 27))
+    allres = []
     with open(toaFile + '.txt', "w+") as f:
         f.write(HEADER)
-        for k, ii in enumerate(rng):
-            f.write(str(ii) + '\t' + str(res["ToA_mid"][k]) + '\t' + str(st[ii]) + '\t' + str(en[ii]) + '\t' +
-                    str(lenInt[ii]) + '\t' + str(expo[ii]) + '\t' + str(events[ii]) + '\t' + str(rate[ii]) + '\t' +
-                    str(res["phShi"][k]) + '\t' + str(res["phShi_LL"][k]) + '\t' + str(res["phShi_UL"][k]) + '\t' +
-                    str(res["htestPow"][k]) + '\t' + str(res["reducedChi2"][k]) + '\n')
+        f.flush()
+        for b0, b1 in _batches(counts[:nfit], budget):
+            sel = rng[b0:b1]
+            for ii in sel:
+                print('ToA {}'.format(ii))
+            res = measure_intervals(T, tm, tmpl, st[sel], en[sel], expo[sel], phShiftRes, nbrBins, varyAmps,
+                                    brutemin, readvaryparam)
+            warn_capped(res, phShiftRes, ['ToA' + str(ii) for ii in sel], logger)
+            for k, ii in enumerate(sel):
+                f.write(str(ii) + '\t' + str(res["ToA_mid"][k]) + '\t' + str(st[ii]) + '\t' + str(en[ii]) + '\t' +
+                        str(lenInt[ii]) + '\t' + str(expo[ii]) + '\t' + str(events[ii]) + '\t' + str(rate[ii]) + '\t' +
+                        str(res["phShi"][k]) + '\t' + str(res["phShi_LL"][k]) + '\t' + str(res["phShi_UL"][k]) + '\t' +
+                        str(res["htestPow"][k]) + '\t' + str(res["reducedChi2"][k]) + '\n')
+            f.flush()
+            allres.append(res)
+        if nfit < rng.size:
+            print('ToA {}'.format(rng[nfit]))
+            raise IndexError("index -1 is out of bounds for axis 0 with size 0 (ToA {} holds no photons, "
+                             "measureToAs.py:182)".format(rng[nfit]))
     logger.info('\n Wrote ToA properties to {}.txt'.format(toaFile))
     if timFile is not None:  # measureToAs.py:238-240
         phshiftTotimfile(toaFile + '.txt', timMod, timFile, tempModPP=tempModPP)
         logger.info('\n Wrote timfile {}.tim'.format(timFile))
-    _plot_residuals(res, toaFile)
+    if allres:
+        _plot_residuals({k: np.concatenate([r[k] for r in allres]) for k in ("ToA_mid", "phShi", "phShi_LL", "phShi_UL")},
+                        toaFile)
     return pd.read_csv(toaFile + '.txt', sep=r'\s+', comment='#')
 
 

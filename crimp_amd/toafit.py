@@ -18,8 +18,9 @@ iterates:
    bound behaviour, norm re-profiled (1-D Newton) at every step, stop at the first
    LLmax - LL > 0.5*chi2.ppf(0.6827, 1); sigma = (k+1)*step + step/2, capped at
    phShiftRes/2 steps (:330-376);
-4. redChi2 from the ``binphases`` profile (device histogram, numpy.histogram
-   edge semantics) against the best-fit curve, dof = nbrBins - 2 (:385-393).
+4. redChi2 from the ``binphases`` profile (numpy.histogram edge semantics) against
+   the best-fit curve, dof = nbrBins - 2 (:385-393), on the device from the fit
+   records (``crimp_toa_redchi2``).
 
 ``varyAmps`` (a free ampShift, :305-312) runs on the device too (``k_toa_fit_amp``: (norm, ampShift)
 re-profiled at every scan step); ``readvaryparam`` (free template parameters, :727-801) is driven from
@@ -35,6 +36,22 @@ from ._native import _is_torch
 CHI2_1SIG_1DOF = 0.500021713558733  # 0.5 * scipy.stats.chi2.ppf(0.6827, 1)   (measureToAs.py:324)
 TWO_PI = 2.0 * math.pi
 MODEL_STEP = 1e-6  # ascent: final plain Newton step below this (rad; relative in the norm) taken by the quadratic model
+
+
+def scan_capped(sigma, ph_shift_res):
+    """True where a 1-sigma bound came from the phShiftRes/2 cap rather than the chi2 crossing: the reference loop
+    stops once its counter kk exceeds phShiftRes/2 and logs 'Could not estimate lower/upper-bound uncertainty'
+    (measureToAs.py:348-350, :373-375); the bound is kk*step + step/2, so kk is read back from it."""
+    step = TWO_PI / int(ph_shift_res)
+    kk = np.rint((np.asarray(sigma, dtype=np.float64) - step / 2) / step)
+    return kk > int(ph_shift_res) / 2
+
+
+def warn_capped(res, ph_shift_res, names, log):
+    """The reference's warnings for every interval whose scan hit the cap (one call per fit batch)."""
+    for side, key in (("lower", "phShi_LL"), ("upper", "phShi_UL")):
+        for i in np.nonzero(scan_capped(res[key], ph_shift_res))[0]:
+            log.warning('Could not estimate {}-bound uncertainty on {}'.format(side, names[i]))
 
 
 def _vals(tmpl, prefix, K):
@@ -166,7 +183,7 @@ class ToAFitter:
             act = np.nonzero(active)[0]
             if act.size == 0:
                 break
-            dn, dp, pure = self._newton_step(n[act], g[act], H[act], with_pure=True)
+            dn, dp, pure = self._newton_step(n[act], g[act], H[act], with_pure=True, phi=phi[act])
             # converged: even the full step moves less than the stopping tolerance (no confirming pass)
             fn = np.clip(n[act] + dn, self.lo, self.hi)
             fp = np.clip(phi[act] + dp, -self.pb, self.pb)
@@ -216,8 +233,16 @@ class ToAFitter:
             active[act[done]] = False
         return n, phi, ll
 
-    def _newton_step(self, n, g, H, with_pure=False):
+    def _newton_step(self, n, g, H, with_pure=False, phi=None):
+        """Levenberg-shifted Newton step with a trust region; projected (k_toa_fit's fit_newton_dir): a coordinate on
+        its bound whose gradient points out is held and the other takes its own 1-D Newton step."""
         hnn, hnp, hpp = H[:, 0], H[:, 1], H[:, 2]
+        if phi is not None:
+            pfix = ((phi <= -self.pb) & (g[:, 1] < 0)) | ((phi >= self.pb) & (g[:, 1] > 0))
+            nfix = ((n <= self.lo) & (g[:, 0] < 0)) | ((n >= self.hi) & (g[:, 0] > 0))
+            proj = pfix | nfix
+        else:
+            proj = np.zeros(n.size, dtype=bool)
         # shift the Hessian to be negative definite (Levenberg damping), then solve
         tr = hnn + hpp
         det = hnn * hpp - hnp * hnp
@@ -228,10 +253,18 @@ class ToAFitter:
         dn = -(c * g[:, 0] - hnp * g[:, 1]) / det2
         dp = -(a * g[:, 1] - hnp * g[:, 0]) / det2
         # trust region: at most 0.05 rad in phShift and half the norm per step
+        pure = shift == 0.0
+        if proj.any():
+            with np.errstate(divide="ignore", invalid="ignore"):
+                dn1 = np.where(hnn < 0, -g[:, 0] / np.where(hnn < 0, hnn, -1.0), np.where(g[:, 0] > 0, 0.1, -0.1) * np.abs(n))
+                dp1 = np.where(hpp < 0, -g[:, 1] / np.where(hpp < 0, hpp, -1.0), np.where(g[:, 1] > 0, 0.05, -0.05))
+            dn = np.where(proj, np.where(nfix, 0.0, dn1), dn)
+            dp = np.where(proj, np.where(pfix, 0.0, dp1), dp)
+            pure = np.where(proj, (nfix | (hnn < 0)) & (pfix | (hpp < 0)), pure)
         sc = np.minimum(1.0, 0.05 / np.maximum(np.abs(dp), 1e-300))
         sc = np.minimum(sc, 0.5 * np.abs(n) / np.maximum(np.abs(dn), 1e-300))
         if with_pure:
-            return dn * sc, dp * sc, (shift == 0.0) & (sc == 1.0)
+            return dn * sc, dp * sc, pure & (sc == 1.0)
         return dn * sc, dp * sc
 
     def profile_norm(self, iv, phi, n_start, max_iter=30):
@@ -316,21 +349,26 @@ class ToAFitter:
         return out[-1], out[1]
 
     # ------------------------------------------------------------------ step 4: redChi2
-    def reduced_chi2(self, n_hat, phi_hat, nfree=2, amp_shift=None):
+    def _bins(self):
+        """numpy.linspace edges and the bin centres of binphases (binphases.py:9-39, measureToAs.py:385-387)."""
         upper = 1.0 if self.model == "fourier" else TWO_PI
         edges = np.linspace(0, upper, self.nbins + 1, endpoint=True)
-        cts = ops.binphases_counts(self.x, self.offsets, self._arr(edges, np.float64))
-        if _is_torch(cts):
-            cts = cts.cpu().numpy()
-        cts = np.asarray(cts, dtype=np.float64)
         pp = np.linspace(0, upper, self.nbins, endpoint=False) + (upper / self.nbins) / 2
-        rate = cts / (self.E[:, None] / self.nbins)
-        err = np.sqrt(cts) / (self.E[:, None] / self.nbins)
-        amp = np.ones_like(n_hat) if amp_shift is None else np.asarray(amp_shift, dtype=np.float64)
-        model = self.curve(n_hat[:, None], phi_hat[:, None], pp[None, :], amp[:, None])
-        with np.errstate(divide="ignore", invalid="ignore"):
-            chi2 = np.sum(np.divide((model - rate) ** 2, err ** 2), axis=1)
-        return np.divide(chi2, self.nbins - nfree)
+        return edges, pp
+
+    def reduced_chi2(self, n_hat, phi_hat, nfree=2, amp_shift=None, records=None):
+        """redChi2 per interval (measureToAs.py:385-393) on the device (crimp_toa_redchi2: the binned profile against
+        the best-fit curve). ``records``: crimp_toa_fit's [nint, 8] records where they are at hand (device-resident,
+        no host round trip); else built from the arguments."""
+        edges, pp = self._bins()
+        if records is None:
+            rec = np.zeros((self.nint, 8))
+            rec[:, 0], rec[:, 1] = n_hat, phi_hat
+            rec[:, 6] = 1.0 if amp_shift is None else np.asarray(amp_shift, dtype=np.float64)
+            records = self._arr(rec, np.float64)
+        rc = ops.toa_redchi2(self.x, self.offsets, self.tpl, self._arr(self.E, np.float64), records,
+                             self._arr(edges, np.float64), self._arr(pp, np.float64), nfree)
+        return rc.cpu().numpy() if _is_torch(rc) else np.asarray(rc)
 
     def curve(self, n, phi, xx, amp_shift=1.0):
         """fourseries / wrapcauchy / vonmises at xx (templatemodels.py:64-82, :166-185, :271-290)."""
@@ -356,13 +394,11 @@ class ToAFitter:
         """Every interval's fit in one device call (crimp_toa_fit: one workgroup per interval runs steps 1-3),
         then the redChi2 of step 4. ``vary_amps``: ampShift free (Fourier [0.01, 100], Cauchy [0, inf), von Mises [0, 500]) after the (norm, phShift) fit,
         re-profiled with the norm in the 1-sigma scan, one more free parameter in redChi2 (:305-312)."""
-        r = ops.toa_fit(self.x, self.offsets, self.tpl, self._arr(self.E, np.float64), self.norm0, self.res, brutemin,
-                        vary_amps)
-        if _is_torch(r):
-            r = r.cpu().numpy()
-        r = np.asarray(r)
+        rd = ops.toa_fit(self.x, self.offsets, self.tpl, self._arr(self.E, np.float64), self.norm0, self.res, brutemin,
+                         vary_amps)
+        rchi2 = self.reduced_chi2(None, None, nfree=3 if vary_amps else 2, records=rd)
+        r = np.asarray(rd.cpu().numpy() if _is_torch(rd) else rd)
         n_hat, phi_hat, amp = r[:, 0].copy(), r[:, 1].copy(), r[:, 6].copy()
-        rchi2 = self.reduced_chi2(n_hat, phi_hat, nfree=3 if vary_amps else 2, amp_shift=amp)
         return {"phShi": phi_hat, "phShi_LL": r[:, 3].copy(), "phShi_UL": r[:, 4].copy(), "reducedChi2": rchi2,
                 "norm": n_hat, "LLmax": r[:, 2].copy(), "evaluations": r[:, 5].copy(), "ampShift": amp,
                 "cached_evaluations": r[:, 7].copy()}

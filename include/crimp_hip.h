@@ -101,6 +101,11 @@ int64_t crimp_last_fixups(void);
  * lmfit's 20-norm lattice, padded to 2, 4 or 20; 0 without a brute grid). Measurement hook for bench.py's
  * algorithmic work count, not in the reference. */
 int64_t crimp_last_toa_grid_norms(void);
+/* The form of the last crimp_toa_fit's brute grid (Fourier templates): bit 0 -- no per-phShift min of the template
+ * part (the template's bound certified every candidate lattice point valid), bit 1 -- log2 of products of eight model
+ * values instead of four (every factor certified inside [2^-15, 2^15]); 0 = the full kernel. Measurement hook for
+ * bench.py, not in the reference. */
+int64_t crimp_last_toa_grid_fast(void);
 /* Frees the library's idle cached device scratch on every device (not in the reference). */
 int crimp_release_scratch(void);
 int crimp_device_count(int32_t* count);
@@ -161,7 +166,7 @@ int crimp_toa_grid(const double* x, const int64_t* offsets, int64_t nint, const 
  * 2pi/res with the other free parameters re-profiled at each step. One workgroup per interval runs the
  * whole fit on the device (csrc/toa_fit.h).
  * out[i*8 + 0..6] = { norm, phShift, LLmax, phShift_LL, phShift_UL, likelihood evaluations, ampShift }.
- * The reduced chi2 (:385-393) is left to the caller (crimp_binphases + the template curve). */
+ * The reduced chi2 (:385-393) is crimp_toa_redchi2 on these records. */
 int crimp_toa_fit(const double* x, const int64_t* offsets, int64_t nint, const crimp_template* tpl,
                   const double* exposure, double norm0, int32_t ph_shift_res, int32_t options, double* out,
                   uint32_t flags, void* stream);
@@ -178,6 +183,15 @@ int crimp_toa_fit(const double* x, const int64_t* offsets, int64_t nint, const c
 int crimp_toa_shape_points(const double* x, const int64_t* offsets, int64_t nint, const crimp_template* tpls,
                            const double* aux, const int64_t* pt_interval, const double* pt_norm,
                            const double* pt_phi, int64_t npts, double* out, uint32_t flags, void* stream);
+
+/* redChi2 of every fitted interval   [measureToAs.py:385-393 (Fourier), :530-538, :675-683; binphases.py:9-39]:
+ * the binned profile (np.histogram with edges[nbins+1] = numpy.linspace(0, upper, nbins+1), upper 1 (Fourier, cycles)
+ * or 2 pi) against the template curve at centers[nbins] with the interval's fitted norm, phShift and ampShift from
+ * records[i*8 + 0, 1, 6] (crimp_toa_fit's records): out[i] = sum_b (model_b - rate_b)^2 / err_b^2 / (nbins - nfree),
+ * rate = cts / (E_i / nbins), err = sqrt(cts) / (E_i / nbins). fp64. */
+int crimp_toa_redchi2(const double* x, const int64_t* offsets, int64_t nint, const crimp_template* tpl,
+                      const double* exposure, const double* records, const double* edges, const double* centers,
+                      int32_t nbins, int32_t nfree, double* out, uint32_t flags, void* stream);
 
 /* binphases(phases, nbrBins) counts per interval   [binphases.py:9-39]:
  * np.histogram(x, bins=edges) semantics with edges[nbins+1] (numpy.linspace). counts[i*nbins+b]. */

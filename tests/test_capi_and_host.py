@@ -63,6 +63,38 @@ def test_exact_kernel_accumulators_untouched_by_compiler():
         assert bad == [], (name, bad[:4])
 
 
+def test_agpr_check_flags_the_unclobbered_build():
+    """The fault of round 3's no-ex_open build: without the AGPR clobbers on the MFMA statements, hipcc keeps a
+    value of its own in an accumulator AGPR (the photon-time address, overwritten by tile 0's MFMAs ->
+    hipErrorIllegalAddress). tools/agpr_check.py must see that in the build without clobbers and fences; the shipped
+    build (clobbers on) has none (test above), and the clobbered no-fence build ran bit-identically on the GPU
+    (profiles/r04/ab_fences.log)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("agpr_check", os.path.join(ROOT, "tools", "agpr_check.py"))
+    A = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(A)
+    bad = A.compiler_agpr_accesses(defines=("-DCRIMP_EX_AGPR_CLOBBERS=0", "-DCRIMP_EX_OPEN=0"))
+    assert any(v for v in bad.values()), bad
+    ok = A.compiler_agpr_accesses(defines=("-DCRIMP_EX_OPEN=0",))
+    assert all(v == [] for v in ok.values()), ok
+
+
+def test_isa_hazards_rejects_the_unfenced_build(tmp_path):
+    """Without the ex_open fences hipcc rewrites MFMA A operands 32-64 issue cycles after the MFMA; on the GPU that
+    build returned rows 16..31 of every 2-D tile differently from run to run (profiles/r04/ab_fences.log). The
+    checker must reject it, as it accepts the shipped kernel (test_mfma_hazard_rules_hold_in_default_kernel)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("isa_hazards", os.path.join(ROOT, "tools", "isa_hazards.py"))
+    H = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(H)
+    co = H.compile_device_object(str(tmp_path / "noopen.co"), ("-DCRIMP_EX_OPEN=0",))
+    funcs = {k: v for k, v in H.disassemble(co).items() if "k_search_exact" in k}
+    assert len(funcs) == 2
+    for name, insts in funcs.items():
+        bad = H.check_function(insts)
+        assert any("rewrites A" in v[2] and v[3] < H.ISSUE_MIN for v in bad), name
+
+
 def test_hot_path_fails_loudly_without_gpu():
     import torch
     if torch.cuda.is_available():
@@ -207,6 +239,64 @@ def test_error_scan_phase_sequence_clip_semantics():
     seq = fit._scan_phases(np.array([1.5 * np.pi - step]), 1, ks)
     np.testing.assert_array_equal(seq[0], np.minimum(1.5 * np.pi - step + ks * step, 1.5 * np.pi))
     del tm
+
+
+def test_scan_cap_detection_and_warning_text(caplog):
+    """The reference's loop leaves kk = k + 1 and logs 'Could not estimate ...' once kk > phShiftRes/2
+    (measureToAs.py:348-350, :373-375); toafit.scan_capped reads kk back from the bound kk*step + step/2."""
+    import logging
+    from crimp_amd.toafit import scan_capped, warn_capped
+    for res in (20, 21, 1000):
+        step = 2 * np.pi / res
+        kk = np.arange(2, res // 2 + 3)
+        sig = kk * step + step / 2
+        np.testing.assert_array_equal(scan_capped(sig, res), kk > res / 2)
+    res = 20
+    step = 2 * np.pi / res
+    r = {"phShi_LL": np.array([11 * step + step / 2, 3 * step + step / 2]),
+         "phShi_UL": np.array([4 * step + step / 2, 11 * step + step / 2])}
+    with caplog.at_level(logging.WARNING):
+        warn_capped(r, res, ["ToA5", "ToA6"], logging.getLogger("crimp_amd.measureToAs"))
+    assert [rec.getMessage() for rec in caplog.records] == ["Could not estimate lower-bound uncertainty on ToA5",
+                                                            "Could not estimate upper-bound uncertainty on ToA6"]
+
+
+def test_toa_batches_and_interval_counts():
+    """measureToAs' batching of intervals by photon budget and its photon counts (inclusive bounds, the
+    reference's mask for unsorted times, measureToAs.py:173-174)."""
+    from crimp_amd.measureToAs import _batches, _interval_counts
+    assert _batches([5, 5, 5, 5], 10) == [(0, 2), (2, 4)]
+    assert _batches([50, 1, 1], 10) == [(0, 1), (1, 3)]
+    assert _batches([1, 1, 1], 1) == [(0, 1), (1, 2), (2, 3)]
+    assert _batches([], 10) == []
+    rng = np.random.default_rng(3)
+    t = np.sort(rng.uniform(0.0, 100.0, 3000))
+    st, en = np.array([1.0, t[10], 60.0, 200.0]), np.array([2.0, t[20], 60.0, 300.0])
+    want = [np.count_nonzero((t >= a) & (t <= b)) for a, b in zip(st, en)]
+    assert _interval_counts(t, st, en).tolist() == want
+    assert _interval_counts(rng.permutation(t), st, en).tolist() == want
+    assert want[1] == 11 and want[3] == 0
+
+
+def test_measuretoas_empty_first_interval_writes_header_then_raises(tmp_path):
+    """An empty first interval: the reference has written only the header when TIME_toa[-1] raises at
+    measureToAs.py:182; so does the drop-in (no device call is made before it)."""
+    from crimp_amd.eventfile import write_events_fits
+    from crimp_amd.measureToAs import HEADER, measureToAs
+    ev = gold("events_1e2259.npz")
+    p = str(tmp_path / "ev.fits")
+    write_events_fits(p, ev["TIME"], ev["PI"], int(ev["MJDREFI"]), float(ev["MJDREFF"]))
+    lines = open(gpath("timIntToAs_1e2259.txt")).read().splitlines()
+    cols = lines[36].split("\t")
+    cols[1], cols[2] = "70000.0", "70000.5"
+    lines[36] = "\t".join(cols)
+    ivf = str(tmp_path / "iv.txt")
+    open(ivf, "w").write("\n".join(lines) + "\n")
+    out = str(tmp_path / "ToAs")
+    with pytest.raises(IndexError):
+        measureToAs(p, gpath("1e2259.par"), gpath("1e2259_template.txt"), ivf, eneLow=1, eneHigh=5, toaStart=35,
+                    toaEnd=41, toaFile=out)
+    assert open(out + ".txt").read() == HEADER
 
 
 def test_tim_writer_matches_reference_tim(tmp_path):

@@ -194,12 +194,41 @@ def test_pruned_brute_grid_equals_full_grid(gpu):
         xs = [_sample_template(tm, 20_000, s, rng) for s in (0.3, -2.0, 3.5, 1.0)]
         rate = tc["norm"] + (tc["amp_1"] + tc["amp_2"]) / (2 * np.pi)
         cases.append((np.concatenate(xs), np.arange(5, dtype=np.int64) * 20_000, np.full(4, 20_000 / rate), tm))
-    for xx, oo, ee, tm in cases:
-        a = ToAFitter(xx, oo, ee, tm).fit(brutemin=True)
-        os.environ["CRIMP_TOA_FULL_GRID"] = "1"
-        try:
-            b = ToAFitter(xx, oo, ee, tm).fit(brutemin=True)
-        finally:
-            del os.environ["CRIMP_TOA_FULL_GRID"]
-        for k in ("phShi", "phShi_LL", "phShi_UL", "reducedChi2", "norm", "LLmax"):
-            np.testing.assert_array_equal(a[k], b[k], err_msg="%s %s" % (tm["model"], k))
+    os.environ["CRIMP_TOA_GRID_SLOW"] = "1"  # the same grid kernel for both (the fast form: the test below)
+    try:
+        for xx, oo, ee, tm in cases:
+            a = ToAFitter(xx, oo, ee, tm).fit(brutemin=True)
+            os.environ["CRIMP_TOA_FULL_GRID"] = "1"
+            try:
+                b = ToAFitter(xx, oo, ee, tm).fit(brutemin=True)
+            finally:
+                del os.environ["CRIMP_TOA_FULL_GRID"]
+            for k in ("phShi", "phShi_LL", "phShi_UL", "reducedChi2", "norm", "LLmax"):
+                np.testing.assert_array_equal(a[k], b[k], err_msg="%s %s" % (tm["model"], k))
+    finally:
+        del os.environ["CRIMP_TOA_GRID_SLOW"]
+
+
+def test_fast_brute_grid_equals_full_kernel(gpu, monkeypatch):
+    """The device fit's fast brute grid (k_toa_grid_mf with log2 of products of eight model values, and without the
+    per-phShift min h where the template's bound makes every candidate point valid; crimp_toa_fit certifies both)
+    against the full kernel (CRIMP_TOA_GRID_SLOW): config-5-style Fourier intervals, every interval. The lattice LL
+    values differ only by fp32 rounding, so the lattice point is the same and the fits reach the same maximum (the
+    parabola-vertex start moves by rounding only): phShift within 1e-9 cycles, identical 1-sigma bounds, LLmax within
+    1e-12 relative. (Config 5's lower candidate norm, norm0/100, can be invalid, so its grid keeps the min: mode 2.)"""
+    from crimp_amd import _native as N
+    from crimp_amd.synth import template_intervals_torch
+    from crimp_amd.toafit import ToAFitter
+    from bench import T2259, _tmpl
+    x, off, E, _ = template_intervals_torch(400, 100_000, T2259["norm"]["value"], T2259["amp"], T2259["ph"], seed=6,
+                                            device=gpu)
+    monkeypatch.delenv("CRIMP_TOA_GRID_SLOW", raising=False)
+    a = ToAFitter(x, off, E, _tmpl()).fit(brutemin=True)
+    assert N.load().crimp_last_toa_grid_fast() == 2
+    monkeypatch.setenv("CRIMP_TOA_GRID_SLOW", "1")
+    b = ToAFitter(x, off, E, _tmpl()).fit(brutemin=True)
+    assert N.load().crimp_last_toa_grid_fast() == 0
+    np.testing.assert_allclose(a["phShi"], b["phShi"], rtol=0, atol=2 * np.pi * 1e-9)
+    np.testing.assert_array_equal(a["phShi_LL"], b["phShi_LL"])
+    np.testing.assert_array_equal(a["phShi_UL"], b["phShi_UL"])
+    np.testing.assert_allclose(a["LLmax"], b["LLmax"], rtol=1e-12)

@@ -462,6 +462,36 @@ def test_measuretoas_end_to_end(gpu, tmp_path):
     assert lines[0] == open(gpath("ToAs_2259.txt")).read().splitlines()[0]
 
 
+def test_measuretoas_rows_before_empty_interval(gpu, tmp_path, monkeypatch):
+    """An interval without photons at position k: the reference's loop has written rows < k when
+    TIME_toa[-1] raises (measureToAs.py:160-162, :182, :222-226). The drop-in writes them too (here in batches of
+    one interval, CRIMP_TOA_BATCH_PHOTONS=1, so every row is flushed as soon as its fit is known), then raises the
+    IndexError; the rows equal the full run's."""
+    from crimp_amd.eventfile import write_events_fits
+    from crimp_amd.measureToAs import measureToAs
+    ev = gold("events_1e2259.npz")
+    p = str(tmp_path / "ev.fits")
+    write_events_fits(p, ev["TIME"], ev["PI"], int(ev["MJDREFI"]), float(ev["MJDREFF"]))
+    full = str(tmp_path / "full")
+    measureToAs(p, gpath("1e2259.par"), gpath("1e2259_template.txt"), gpath("timIntToAs_1e2259.txt"),
+                eneLow=1, eneHigh=5, toaStart=35, toaEnd=41, brutemin=True, toaFile=full)
+    lines = open(gpath("timIntToAs_1e2259.txt")).read().splitlines()
+    k = 38
+    cols = lines[k + 1].split("\t")
+    cols[1], cols[2] = "70000.0", "70000.5"  # interval 38 now covers no photon
+    lines[k + 1] = "\t".join(cols)
+    ivf = str(tmp_path / "iv.txt")
+    open(ivf, "w").write("\n".join(lines) + "\n")
+    monkeypatch.setenv("CRIMP_TOA_BATCH_PHOTONS", "1")
+    part = str(tmp_path / "part")
+    with pytest.raises(IndexError):
+        measureToAs(p, gpath("1e2259.par"), gpath("1e2259_template.txt"), ivf, eneLow=1, eneHigh=5, toaStart=35,
+                    toaEnd=41, brutemin=True, toaFile=part)
+    got = open(part + ".txt").read().splitlines()
+    want = open(full + ".txt").read().splitlines()
+    assert got == want[:1 + (k - 35)]          # header + ToAs 35, 36, 37
+
+
 def _vary_template(base, free):
     t = {k: (dict(v) if isinstance(v, dict) else v) for k, v in base.items()}
     for k, v in t.items():

@@ -2,7 +2,7 @@
 (crimp_amd/csrc/search_exact.h, ex_mfma): any AGPR access hipcc generates itself -- a VGPR spilled to an AGPR under
 register pressure, which resource-usage reports do not count as a spill -- would overwrite them. Compiles the
 device code to assembly and lists such accesses (outside inline-asm blocks) in the k_search_exact kernels.
-usage: python tools/agpr_check.py   (exit status 1 if any)"""
+usage: python tools/agpr_check.py [-DNAME=VALUE ...]   (exit status 1 if any)"""
 import os
 import re
 import subprocess
@@ -13,11 +13,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "crimp_amd", "csrc")
 
 
-def compiler_agpr_accesses(kernel="k_search_exact"):
+def compiler_agpr_accesses(kernel="k_search_exact", defines=()):
+    """{kernel symbol: [compiler-generated lines naming an AGPR]} of the device code built with ``defines``
+    (e.g. ("-DCRIMP_EX_AGPR_CLOBBERS=0", "-DCRIMP_EX_OPEN=0"): round 3's faulting build)."""
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "k.s")
         subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-w", "--cuda-device-only",
-                        "-S", "-o", out, "crimp_hip.hip"], cwd=SRC, check=True, capture_output=True)
+                        "-S", *defines, "-o", out, "crimp_hip.hip"], cwd=SRC, check=True, capture_output=True)
         text = open(out).read()
     found = {}
     for m in re.finditer(r"^(_Z\w*%s\w*):" % kernel, text, re.M):
@@ -36,7 +38,7 @@ def compiler_agpr_accesses(kernel="k_search_exact"):
 
 
 if __name__ == "__main__":
-    res = compiler_agpr_accesses()
+    res = compiler_agpr_accesses(defines=tuple(sys.argv[1:]))
     n = 0
     for name, bad in res.items():
         print("%s: %d compiler AGPR accesses %s" % (name, len(bad), bad[:4]))
