@@ -19,6 +19,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <functional>
 #include <vector>
 
 #include "../../include/crimp_hip.h"
@@ -1049,8 +1050,8 @@ template <int KF, int NN, bool HMIN = true, int PROD = 4>
 __global__ __launch_bounds__(256) void k_toa_grid_mf(const double* __restrict__ x, const int64_t* __restrict__ offsets,
                                                      const TplDev* __restrict__ T, const double* __restrict__ norm,
                                                      int nnorm, int a0, int na, const double* __restrict__ phi, int nphi,
-                                                     int64_t chunk, int nint, int se, double* __restrict__ lnsum,
-                                                     double* __restrict__ hmin) {
+                                                     int64_t chunk, int nint, int se, int a_first,
+                                                     double* __restrict__ lnsum, double* __restrict__ hmin) {
     constexpr int NM = (KF + 1) / 2;  // MFMAs per 32-photon chunk (two harmonics each)
     __shared__ __attribute__((aligned(16))) u32x4 afr[kGmTile][2 * NM];  // [photon][harmonic]
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hk = lane >> 5;
@@ -1077,9 +1078,17 @@ __global__ __launch_bounds__(256) void k_toa_grid_mf(const double* __restrict__ 
             bf[m] = __builtin_bit_cast(f16x8, w);
         }
     }
-    f32x2 nr[NN / 2];
+    // PROD 4: the norms in pairs (f32x2 over two norms); PROD 8: one norm at a time over photon pairs (f32x2 over two
+    // photons), so that an odd number of norms (a single one after k_toa_grid_best's lazy norms) costs no dead lane
+    constexpr int NP = NN > 1 ? NN / 2 : 1;
+    f32x2 nr[NP];
+    float nrs[NN];
 #pragma unroll
-    for (int a = 0; a < NN; ++a) nr[a / 2][a % 2] = (a < na) ? (float)(norm[iv * nnorm + a0 + a] * sc) : 1.0f;
+    for (int a = 0; a < NN; ++a) {
+        nrs[a] = (a < na) ? (float)(norm[iv * nnorm + a0 + a] * sc) : 1.0f;
+        nr[a / 2][a % 2] = nrs[a];
+    }
+    if (NN == 1) nr[0][1] = 1.0f;
     double acc[NN];
 #pragma unroll
     for (int a = 0; a < NN; ++a) acc[a] = 0.0;
@@ -1119,30 +1128,80 @@ __global__ __launch_bounds__(256) void k_toa_grid_mf(const double* __restrict__ 
                 const f16x8 av = __builtin_bit_cast(f16x8, afr[q0 + (lane & 31)][2 * m + hk]);
                 hv = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bf[m], hv, 0, 0, 0);
             }
-            f32x2 pa[NN / 2];
+            if constexpr (PROD == 8) {
+                // photon pairs: per norm, the 16 factors norm + h of the lane's chunk as 8 f32x2, multiplied down a tree
+                // to two products of eight (even and odd photons), one v_log_f32 each
+                f32x2 pl[NN];
 #pragma unroll
-            for (int b = 0; b < NN / 2; ++b) pa[b] = f32x2{0.0f, 0.0f};
-            if (q0 + 32 <= cnt) {
-#pragma unroll
-                for (int gi = 0; gi < 16 / PROD; ++gi) {
+                for (int b = 0; b < NN; ++b) pl[b] = f32x2{0.0f, 0.0f};
+                if (q0 + 32 <= cnt) {
                     if constexpr (HMIN) {
 #pragma unroll
-                        for (int r = 0; r < PROD; ++r) hmn = fminf(hmn, hv[PROD * gi + r]);
+                        for (int r = 0; r < 16; ++r) hmn = fminf(hmn, hv[r]);
                     }
 #pragma unroll
-                    for (int b = 0; b < NN / 2; ++b) {
-                        f32x2 pr = nr[b] + hv[PROD * gi];
+                    for (int b = 0; b < NN; ++b) {
+                        const f32x2 n2 = f32x2{nrs[b], nrs[b]};
+                        f32x2 f[8];
 #pragma unroll
-                        for (int r = 1; r < PROD; ++r) pr *= nr[b] + hv[PROD * gi + r];
+                        for (int k = 0; k < 8; ++k) f[k] = f32x2{hv[2 * k], hv[2 * k + 1]} + n2;
+                        f[0] *= f[1];
+                        f[2] *= f[3];
+                        f[4] *= f[5];
+                        f[6] *= f[7];
+                        f[0] *= f[2];
+                        f[4] *= f[6];
+                        f[0] *= f[4];
+                        pl[b] += f32x2{__builtin_amdgcn_logf(f[0].x), __builtin_amdgcn_logf(f[0].y)};
+                    }
+                } else {  // the tile's last, partial chunk: photons past cnt contribute a factor 1 (products of four)
+#pragma unroll
+                    for (int gi = 0; gi < 4; ++gi) {
+                        float pr[NN];
+#pragma unroll
+                        for (int b = 0; b < NN; ++b) pr[b] = 1.0f;
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const int row = q0 + r + 8 * gi + 4 * hk;
+                            if (row < cnt) {
+                                const float h = hv[4 * gi + r];
+                                if constexpr (HMIN) hmn = fminf(hmn, h);
+#pragma unroll
+                                for (int b = 0; b < NN; ++b) pr[b] *= nrs[b] + h;
+                            }
+                        }
+#pragma unroll
+                        for (int b = 0; b < NN; ++b) pl[b].x += __builtin_amdgcn_logf(pr[b]);
+                    }
+                }
+#pragma unroll
+                for (int a = 0; a < NN; ++a) acc[a] += (double)pl[a].x + (double)pl[a].y;
+                continue;
+            }
+            f32x2 pa[NP];
+#pragma unroll
+            for (int b = 0; b < NP; ++b) pa[b] = f32x2{0.0f, 0.0f};
+            if (q0 + 32 <= cnt) {
+#pragma unroll
+                for (int gi = 0; gi < 4; ++gi) {
+                    if constexpr (HMIN) {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) hmn = fminf(hmn, hv[4 * gi + r]);
+                    }
+#pragma unroll
+                    for (int b = 0; b < NP; ++b) {
+                        f32x2 pr = nr[b] + hv[4 * gi];
+#pragma unroll
+                        for (int r = 1; r < 4; ++r) pr *= nr[b] + hv[4 * gi + r];
                         pa[b] += f32x2{__builtin_amdgcn_logf(pr.x), __builtin_amdgcn_logf(pr.y)};
                     }
                 }
             } else {  // the tile's last, partial chunk: photons past cnt contribute a factor 1
 #pragma unroll
                 for (int gi = 0; gi < 4; ++gi) {
-                    f32x2 pr[NN / 2];
+                    f32x2 pr[NP];
 #pragma unroll
-                    for (int b = 0; b < NN / 2; ++b) pr[b] = f32x2{1.0f, 1.0f};
+                    for (int b = 0; b < NP; ++b) pr[b] = f32x2{1.0f, 1.0f};
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         const int row = q0 + r + 8 * gi + 4 * hk;
@@ -1150,11 +1209,11 @@ __global__ __launch_bounds__(256) void k_toa_grid_mf(const double* __restrict__ 
                             const float h = hv[4 * gi + r];
                             if constexpr (HMIN) hmn = fminf(hmn, h);
 #pragma unroll
-                            for (int b = 0; b < NN / 2; ++b) pr[b] *= nr[b] + h;
+                            for (int b = 0; b < NP; ++b) pr[b] *= nr[b] + h;
                         }
                     }
 #pragma unroll
-                    for (int b = 0; b < NN / 2; ++b)
+                    for (int b = 0; b < NP; ++b)
                         pa[b] += f32x2{__builtin_amdgcn_logf(pr[b].x), __builtin_amdgcn_logf(pr[b].y)};
                 }
             }
@@ -1178,7 +1237,8 @@ __global__ __launch_bounds__(256) void k_toa_grid_mf(const double* __restrict__ 
 #pragma unroll
         for (int a = 0; a < NN; ++a)
             if (a < na) lnsum[((split * nint + iv) * nnorm + a0 + a) * nphi + bphi] = acc[a];
-        if (HMIN && a0 == 0) hmin[(split * nint + iv) * nphi + bphi] = ldexp((double)hmn, -se);
+        // the first evaluated norm block writes the min (a_first: past toa_grid_partials' lazy norms)
+        if (HMIN && a0 == a_first) hmin[(split * nint + iv) * nphi + bphi] = ldexp((double)hmn, -se);
     }
 }
 
@@ -1373,6 +1433,14 @@ __global__ __launch_bounds__(kFixBlock) void k_search_f64_few(
 
 // ============================================================== 6. C-ABI
 static hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+// A second stream per device for crimp_toa_fit's overlapped halves (created once, kept for the process)
+static hipStream_t aux_stream() {
+    static hipStream_t st[64] = {};
+    int d = 0;
+    if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= 64) return nullptr;
+    if (!st[d] && hipStreamCreateWithFlags(&st[d], hipStreamNonBlocking) != hipSuccess) st[d] = nullptr;
+    return st[d];
+}
 
 extern "C" double crimp_last_kernel_ms(void) { return g_last_kernel_ms; }
 
@@ -1960,7 +2028,18 @@ static int make_tpl(const crimp_template* tpl, TplDev* T) {
 // h(u) (h(x; phShift) is h shifted in phase for every model, so its minimum does not depend on phShift) sampled on
 // 2^16 points per turn, less the largest change between neighbouring samples (a smooth h cannot dip further between
 // two samples than it moves across one step). Tighter than tpl_bounds' -sum|amp_j| for Fourier templates.
-static double tpl_hmin_scan(const TplDev& T) {
+static double tpl_hmin_scan_uncached(const TplDev& T);
+static double tpl_hmin_scan(const TplDev& T) {  // cached for the last template (a fit batch reuses one template)
+    static TplDev last;
+    static double val = 0.0;
+    static bool have = false;
+    if (have && std::memcmp(&last, &T, sizeof(T)) == 0) return val;
+    val = tpl_hmin_scan_uncached(T);
+    std::memcpy(&last, &T, sizeof(T));
+    have = true;
+    return val;
+}
+static double tpl_hmin_scan_uncached(const TplDev& T) {
     const int M = 1 << 16;
     double mn = INFINITY, dmax = 0.0, prev = 0.0, first = 0.0;
     for (int i = 0; i <= M; ++i) {
@@ -2095,10 +2174,12 @@ static int grid_mf_scale(const TplDev& T, bool* ok) {
 // products of eight model values (the host certified that every factor of a valid lattice point stays inside
 // [2^-15, 2^15] after the coefficient scale, or k_toa_grid_best checks it where the min decides validity)
 constexpr int kGridNoMin = 1, kGridProd8 = 2;
+// a_first: the lazy norms [0, a_first) of every interval are not evaluated (their lnsum entries are left unwritten;
+// k_toa_grid_best knows them invalid from the min, or has the grid rerun in full)
 static int toa_grid_partials(Scratch& sc, hipStream_t s, const double* dx, const int64_t* doff, const TplDev* dT,
                              const TplDev& T, const double* dnrm, int64_t nnorm, const double* dphi, int64_t nphi,
                              int64_t nint, int64_t maxn, double** pl, double** ph, int64_t* splits_out,
-                             int mode = 0, int* mode_out = nullptr) {
+                             int mode = 0, int* mode_out = nullptr, int64_t a_first = 0) {
     const int model = T.model, K = T.K;
     bool mf_ok = false;
     const int se = grid_mf_scale(T, &mf_ok);
@@ -2116,15 +2197,19 @@ static int toa_grid_partials(Scratch& sc, hipStream_t s, const double* dx, const
     HIPCHK(sc.alloc(pl, (size_t)(splits * nint * nnorm * nphi)));
     const bool mf = model == CRIMP_MODEL_FOURIER && CRIMP_GRID_MFMA && K <= kGridKMax && mf_ok;
     if (!mf) mode = 0;
+    if (!(mode & kGridProd8)) a_first = 0;  // lazy norms only on the eight-factor kernel (its caller checks them)
     if (mode_out) *mode_out = mode;
     if (mode & kGridNoMin)
         *ph = nullptr;
     else
         HIPCHK(sc.alloc(ph, (size_t)(splits * nint * nphi)));
     dim3 grid((unsigned)pblocks, (unsigned)nint, (unsigned)splits);
-    // norms per lane: 2 or kGridNNSmall for a pruned grid (crimp_toa_fit), otherwise kGridNN per launch
-    const int nn = nnorm <= 2 ? 2 : nnorm <= kGridNNSmall ? kGridNNSmall : kGridNN;
-    for (int64_t a0 = 0; a0 < nnorm; a0 += nn) {
+    // norms per lane: 2 or kGridNNSmall for a pruned grid (crimp_toa_fit; 1 left after its lazy norms, on the eight-
+    // factor kernel), otherwise kGridNN per launch
+    const int64_t neval = nnorm - a_first;
+    const int nn = (neval == 1 && mf && (mode & kGridProd8)) ? 1 : neval <= 2 ? 2 : neval <= kGridNNSmall ? kGridNNSmall
+                                                                                                       : kGridNN;
+    for (int64_t a0 = a_first; a0 < nnorm; a0 += nn) {
         const int na = (int)std::min<int64_t>(nn, nnorm - a0);
 #define CRIMP_LG1(MD, KK, NNV, PP) k_toa_grid<kGridKMax, MD, KK, NNV, PP><<<grid, kGridBlock / PP, 0, s>>>(dx, doff, dT, dnrm, \
                                                           (int)nnorm, (int)a0, na, dphi, (int)nphi, chunk, (int)nint, *pl, *ph)
@@ -2133,13 +2218,15 @@ static int toa_grid_partials(Scratch& sc, hipStream_t s, const double* dx, const
                               else CRIMP_LG1(MD, KK, kGridNN, 1); } while (0)
         if (mf) {
 #define CRIMP_LM2(KK, NNV, HM, PR) k_toa_grid_mf<KK, NNV, HM, PR><<<grid, 256, 0, s>>>(dx, doff, dT, dnrm, (int)nnorm, \
-                                                        (int)a0, na, dphi, (int)nphi, chunk, (int)nint, se, *pl, *ph)
+                                                        (int)a0, na, dphi, (int)nphi, chunk, (int)nint, se, (int)a_first, \
+                                                        *pl, *ph)
 #define CRIMP_LM1(KK, NNV) do { \
         if (mode == (kGridNoMin | kGridProd8)) CRIMP_LM2(KK, NNV, false, 8); \
         else if (mode == kGridProd8) CRIMP_LM2(KK, NNV, true, 8); \
         else if (mode == kGridNoMin) CRIMP_LM2(KK, NNV, false, 4); \
         else CRIMP_LM2(KK, NNV, true, 4); } while (0)
-#define CRIMP_LM(KK) do { if (nn == 2) CRIMP_LM1(KK, 2); else if (nn == kGridNNSmall) CRIMP_LM1(KK, kGridNNSmall); \
+#define CRIMP_LM(KK) do { if (nn == 1) CRIMP_LM2(KK, 1, true, 8); \
+                          else if (nn == 2) CRIMP_LM1(KK, 2); else if (nn == kGridNNSmall) CRIMP_LM1(KK, kGridNNSmall); \
                           else CRIMP_LM1(KK, kGridNN); } while (0)
             switch (K) {
                 case 1: CRIMP_LM(1); break;
@@ -2237,14 +2324,21 @@ extern "C" int crimp_toa_fit(const double* x, const int64_t* offsets, int64_t ni
         HIPCHK(sc.alloc(&dT, 1));
         HIPCHK(h2d(dT, &T, sizeof(T)));
         HIPCHK(sc.alloc(&dstart, (size_t)(2 * nint)));
-        std::vector<double> hphi, hnrm, hstart;
+        std::vector<double> hphi, hnrm, hstart, grid_n;
+        // the brute grid's state, used by the launches below the setup (run_brute)
+        int64_t nphi = 0, nc = 0, nlazy = 0;
+        double hb = 0.0, gsc = 1.0;
+        int grid_mode = 0, lattice_start = 0;
+        double *dphi = nullptr, *dnrm = nullptr;
+        int* dunsafe = nullptr;
+        std::function<int(int, hipStream_t, int64_t, int64_t)> run_brute;
         if (brutemin) {
             // lmfit brute lattices (measureToAs.py:292-295): scipy mgrid phShift = k*0.05 - bound, 20 norms
-            const int64_t nphi = (int64_t)std::ceil((2.0 * C.pb) / (0.05 * 1.0));
+            nphi = (int64_t)std::ceil((2.0 * C.pb) / (0.05 * 1.0));
             const int64_t nn = 20;
             hphi.resize((size_t)nphi);
             for (int64_t k = 0; k < nphi; ++k) hphi[(size_t)k] = (double)k * 0.05 + (-C.pb);
-            std::vector<double> grid_n((size_t)nn);
+            grid_n.resize((size_t)nn);
             for (int64_t a = 0; a < nn; ++a) grid_n[(size_t)a] = (double)a * ((C.hi - C.lo) / (double)(nn - 1)) + C.lo;
             // Pruned norm axis. At fixed phShift the extended LL is -nE + sum_i ln(n + h_i) + const (every model:
             // templatemodels.py:109-121, :213-226, :318-329), strictly concave in n, with its maximum n* where
@@ -2285,19 +2379,18 @@ extern "C" int crimp_toa_fit(const double* x, const int64_t* offsets, int64_t ni
             }
             // compacted per-interval norms: the candidates in grid order, padded by repeating the last (a repeat
             // comes later in norm-outer order, so it never wins a tie)
-            const int64_t nc = ncand <= 2 ? 2 : ncand <= kGridNNSmall ? kGridNNSmall : ncand;
+            nc = ncand <= 2 ? 2 : ncand <= kGridNNSmall ? kGridNNSmall : ncand;
             g_last_grid_norms = nc;
             hnrm.resize((size_t)(nint * nc));
             for (int64_t i = 0; i < nint; ++i)
                 for (int64_t c = 0; c < nc; ++c)
                     hnrm[(size_t)(i * nc + c)] = grid_n[(size_t)(alo[(size_t)i] + std::min(c, acnt[(size_t)i] - 1))];
-            double *dphi = nullptr, *dnrm = nullptr;
             HIPCHK(sc.alloc(&dphi, (size_t)nphi));
             HIPCHK(sc.alloc(&dnrm, (size_t)(nint * nc)));
             HIPCHK(h2d(dphi, hphi.data(), nphi * sizeof(double)));
             HIPCHK(h2d(dnrm, hnrm.data(), nint * nc * sizeof(double)));
             // test hook: start the ascent at the brute lattice point itself (not at the rate norm + parabola vertex)
-            const int lattice_start = getenv("CRIMP_TOA_LATTICE_START") != nullptr;
+            lattice_start = getenv("CRIMP_TOA_LATTICE_START") != nullptr;
             // Fast brute grid (k_toa_grid_mf, Fourier): without the per-phShift min h when a lower bound hb of h keeps
             // every candidate lattice point valid (norm + h > 0) and decides k_toa_grid_best's start rule as the min
             // would (hb + N/E > N/E / 2 for every interval); with log2 of products of eight model values when every
@@ -2305,10 +2398,10 @@ extern "C" int crimp_toa_fit(const double* x, const int64_t* offsets, int64_t ni
             // certified here from hb and the template's upper bound for the norms above -hb, and checked by
             // k_toa_grid_best (from the min) for the others -- a lattice point there that could have underflowed sends
             // the grid back to the four-factor kernel (test hook CRIMP_TOA_GRID_SLOW: always the full kernel).
-            const double hb = tpl_hmin_scan(T);
+            hb = tpl_hmin_scan(T);
             int mode = 0;
             bool mf_ok = false;
-            const double gsc = std::ldexp(1.0, grid_mf_scale(T, &mf_ok));
+            gsc = std::ldexp(1.0, grid_mf_scale(T, &mf_ok));
             if (getenv("CRIMP_TOA_GRID_SLOW") == nullptr && std::isfinite(hb)) {
                 bool nomin = true, prod8 = true;
                 for (const double nv : hnrm) {
@@ -2322,43 +2415,48 @@ extern "C" int crimp_toa_fit(const double* x, const int64_t* offsets, int64_t ni
                 }
                 mode = (nomin ? kGridNoMin : 0) | (prod8 ? kGridProd8 : 0);
             }
-            int* dunsafe = nullptr;  // k_toa_grid_best: a valid lattice point whose min factor is below 2^-15 / s
+            // Lazy norms: the leading candidate norms of every interval with norm + hb <= 0 are left out of the grid.
+            // Their lattice points are valid only where the per-phShift min h exceeds -norm; k_toa_grid_best marks the
+            // rest -inf, as the full grid does, and a valid one sends the grid back to the full evaluation. (Config 5:
+            // lmfit's lowest grid norm, norm0/100, is a candidate of every interval and invalid everywhere.)
+            if ((mode & kGridProd8) && !(mode & kGridNoMin)) {
+                nlazy = nc;
+                for (int64_t i = 0; i < nint && nlazy > 0; ++i) {
+                    int64_t z = 0;
+                    while (z < nc && hnrm[(size_t)(i * nc + z)] + hb <= 0.0) ++z;
+                    nlazy = std::min(nlazy, z);
+                }
+                if (nlazy >= nc) nlazy = 0;  // every candidate lazy: evaluate them all
+            }
+            // dunsafe -- k_toa_grid_best: a valid lattice point whose min factor is below 2^-15 / s, or of a lazy norm
             HIPCHK(sc.alloc(&dunsafe, 1));
             HIPCHK(hipMemsetAsync(dunsafe, 0, sizeof(int), s));
-            KernelTimer kg(s, flags & CRIMP_FLAG_TIME_KERNELS);  // brute grid: k_toa_grid + k_toa_grid_best
-            kg.start();
-            auto brute = [&](int md) -> int {
-                for (int64_t i0 = 0; i0 < nint; i0 += 65535) {
-                    const int64_t nb = std::min<int64_t>(65535, nint - i0);
+            // brute grid of intervals [i0, i0 + n) on stream st (k_toa_grid_mf / k_toa_grid + k_toa_grid_best)
+            auto brute = [&](int md, hipStream_t st, int64_t b0, int64_t bn) -> int {
+                for (int64_t i0 = b0; i0 < b0 + bn; i0 += 65535) {
+                    const int64_t nb = std::min<int64_t>(65535, b0 + bn - i0);
                     int64_t maxn = 0;
                     for (int64_t i = i0; i < i0 + nb; ++i) maxn = std::max(maxn, hoff[i + 1] - hoff[i]);
                     double *pl = nullptr, *ph = nullptr;
                     int64_t splits = 0;
                     int ran = 0;
-                    const int r2 = toa_grid_partials(sc, s, dx, doff + i0, dT, T, dnrm + i0 * nc, nc, dphi, nphi, nb,
-                                                     maxn, &pl, &ph, &splits, md, &ran);
+                    const int64_t lz = (md & kGridProd8) ? nlazy : 0;
+                    const int r2 = toa_grid_partials(sc, st, dx, doff + i0, dT, T, dnrm + i0 * nc, nc, dphi, nphi, nb,
+                                                     maxn, &pl, &ph, &splits, md, &ran, lz);
                     if (r2) return r2;
                     g_last_grid_fast = ran;
-                    k_toa_grid_best<<<(unsigned)nb, 256, 0, s>>>(pl, ph, dnrm + i0 * nc, dphi, doff + i0, de + i0, (int)nc,
-                                                                (int)nphi, (int)nb, (int)splits, T.model, C.sum_amp,
-                                                                grid_n[0], C.lo, C.hi, lattice_start, hb,
-                                                                (ran & kGridProd8) ? gsc : 0.0, dunsafe, dstart + 2 * i0);
+                    k_toa_grid_best<<<(unsigned)nb, 256, 0, st>>>(pl, ph, dnrm + i0 * nc, dphi, doff + i0, de + i0, (int)nc,
+                                                                 (int)nphi, (int)nb, (int)splits, T.model, C.sum_amp,
+                                                                 grid_n[0], C.lo, C.hi, lattice_start, hb,
+                                                                 (ran & kGridProd8) ? gsc : 0.0,
+                                                                 (ran & kGridProd8) ? (int)lz : 0, dunsafe,
+                                                                 dstart + 2 * i0);
                     HIPCHK(hipGetLastError());
                 }
                 return CRIMP_OK;
             };
-            rc = brute(mode);
-            if (rc) return rc;
-            if ((mode & kGridProd8) && !(mode & kGridNoMin)) {  // the runtime half of the eight-factor certificate
-                int unsafe = 0;
-                HIPCHK(d2h(s, &unsafe, dunsafe, sizeof(int)));
-                HIPCHK(hipStreamSynchronize(s));
-                if (unsafe) {
-                    rc = brute(mode & ~kGridProd8);
-                    if (rc) return rc;
-                }
-            }
-            kg.stop();
+            grid_mode = mode;
+            run_brute = brute;
         } else {  // Nelder-Mead starts from the template (norm0, phShift 0) (measureToAs.py:301)
             hstart.resize((size_t)(2 * nint));
             for (int64_t i = 0; i < nint; ++i) {
@@ -2367,16 +2465,18 @@ extern "C" int crimp_toa_fit(const double* x, const int64_t* offsets, int64_t ni
             }
             HIPCHK(h2d(dstart, hstart.data(), 2 * nint * sizeof(double)));
         }
-        KernelTimer kf(s, flags & CRIMP_FLAG_TIME_KERNELS);  // the fit kernel
-        kf.start();
-        if (vary_amps) {
-            k_toa_fit_amp<<<(unsigned)nint, kFitBlock, 0, s>>>(dx, doff, dT, de, dstart, C, dout);
-        } else {
-            // per-photon template part for the iterative norm profiles of the 1-sigma scan (only the
-            // CRIMP_FIT_MOMENTS=0 build caches it; the moment profile needs none)
-            double* hcache = nullptr;
-            if (!CRIMP_FIT_MOMENTS) HIPCHK(sc.alloc(&hcache, (size_t)hoff[nint]));
-#define CRIMP_LF(MD, KK) k_toa_fit<MD, KK><<<(unsigned)nint, kFitBlock, 0, s>>>(dx, doff, dT, de, dstart, C, dout, hcache)
+        // the fit kernel over intervals [f0, f0 + fn) on stream st
+        double* hcache = nullptr;  // per-photon template part for the iterative norm profiles of the 1-sigma scan (only
+                                   // the CRIMP_FIT_MOMENTS=0 build caches it; the moment profile needs none)
+        if (!vary_amps && !CRIMP_FIT_MOMENTS) HIPCHK(sc.alloc(&hcache, (size_t)hoff[nint]));
+        auto fit = [&](hipStream_t st, int64_t f0, int64_t fn) {
+            if (vary_amps) {
+                k_toa_fit_amp<<<(unsigned)fn, kFitBlock, 0, st>>>(dx, doff + f0, dT, de + f0, dstart + 2 * f0, C,
+                                                                  dout + 8 * f0);
+                return;
+            }
+#define CRIMP_LF(MD, KK) k_toa_fit<MD, KK><<<(unsigned)fn, kFitBlock, 0, st>>>(dx, doff + f0, dT, de + f0, dstart + 2 * f0, \
+                                                                             C, dout + 8 * f0, hcache)
             if (T.model == CRIMP_MODEL_FOURIER) {
 #if CRIMP_FIT_GENERIC  // A/B build: the template size read at run time
                 CRIMP_LF(CRIMP_MODEL_FOURIER, 0);
@@ -2399,9 +2499,66 @@ extern "C" int crimp_toa_fit(const double* x, const int64_t* offsets, int64_t ni
                 CRIMP_LF(CRIMP_MODEL_VONMISES, 0);
             }
 #undef CRIMP_LF
+        };
+        // Brute grid, then fits. Timed calls (CRIMP_FLAG_TIME_KERNELS) and small batches run the two in sequence on the
+        // caller's stream; otherwise the intervals go in two halves on two streams -- the second half's grid runs
+        // beside the first half's fits and fills the last, partly empty round of their workgroups (every interval's
+        // fit is independent of its batch, so the records are those of the sequential order)
+        auto all = [&](int md) -> int {
+            const bool timed = flags & CRIMP_FLAG_TIME_KERNELS;
+            const bool overlap = run_brute && !timed && nint >= 2 * 512 && getenv("CRIMP_TOA_NO_OVERLAP") == nullptr;
+            if (!overlap) {
+                KernelTimer kg(s, timed);  // brute grid: k_toa_grid(_mf) + k_toa_grid_best
+                kg.start();
+                if (run_brute) {
+                    const int r2 = run_brute(md, s, 0, nint);
+                    if (r2) return r2;
+                }
+                if (run_brute) kg.stop();
+                KernelTimer kf(s, timed);  // the fit kernel
+                kf.start();
+                fit(s, 0, nint);
+                HIPCHK(hipGetLastError());
+                kf.stop();
+                return CRIMP_OK;
+            }
+            hipStream_t s1 = aux_stream();
+            if (!s1) return set_err(CRIMP_ERR_HIP, "cannot create the auxiliary stream");
+            hipEvent_t e0 = nullptr, e1 = nullptr;
+            HIPCHK(hipEventCreateWithFlags(&e0, hipEventDisableTiming));
+            HIPCHK(hipEventCreateWithFlags(&e1, hipEventDisableTiming));
+            const int64_t h = nint / 2;
+            int r2 = run_brute(md, s, 0, h);
+            if (!r2) {
+                HIPCHK(hipEventRecord(e0, s));
+                fit(s, 0, h);
+                HIPCHK(hipGetLastError());
+                HIPCHK(hipStreamWaitEvent(s1, e0, 0));
+                r2 = run_brute(md, s1, h, nint - h);
+            }
+            if (!r2) {
+                fit(s1, h, nint - h);
+                HIPCHK(hipGetLastError());
+                HIPCHK(hipEventRecord(e1, s1));
+                HIPCHK(hipStreamWaitEvent(s, e1, 0));
+            }
+            (void)hipEventDestroy(e0);  // destruction waits for nothing; the events complete in stream order
+            (void)hipEventDestroy(e1);
+            return r2;
+        };
+        rc = all(grid_mode);
+        if (rc) return rc;
+        if (run_brute && (grid_mode & kGridProd8) && !(grid_mode & kGridNoMin)) {
+            // the runtime half of the certificates (eight factors, lazy norms): a flagged lattice point reruns the
+            // grid and the fits with the full four-factor kernel
+            int unsafe = 0;
+            HIPCHK(d2h(s, &unsafe, dunsafe, sizeof(int)));
+            HIPCHK(hipStreamSynchronize(s));
+            if (unsafe) {
+                rc = all(grid_mode & ~kGridProd8);
+                if (rc) return rc;
+            }
         }
-        HIPCHK(hipGetLastError());
-        kf.stop();
         HIPCHK(copy_back(s, out, dout, (size_t)nint * 8, dev));
         HIPCHK(hipStreamSynchronize(s));
     }

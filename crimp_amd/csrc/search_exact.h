@@ -231,6 +231,13 @@ __device__ __forceinline__ void ex_acc_zero() {
 #ifndef CRIMP_EX_OPEN
 #define CRIMP_EX_OPEN 1
 #endif
+// CRIMP_EX_EARLY_OPEN=1: every ex_open that pins a piece to its MFMA gap is issued before the MFMA that opens the gap
+// instead of after it, and the ones whose input was computed in the same gap are dropped: hipcc pads one wait state
+// (s_nop 0) between an asm statement's outputs and the next VALU reading them, and with the MFMA between the two
+// there is no such VALU
+#ifndef CRIMP_EX_EARLY_OPEN
+#define CRIMP_EX_EARLY_OPEN 0
+#endif
 #ifndef CRIMP_EX_READY
 #define CRIMP_EX_READY 1
 #endif
@@ -428,50 +435,51 @@ __global__ __launch_bounds__(kExBlock, 1) void k_search_exact(
     // Pieces of the pipeline, each pinned to one MFMA gap (ex_open on its input at the start, ex_ready on its output
     // at the end). U photon i of a pair = photon i & 1 of the lane's two in quad i >> 1 -> digit dwords
     // a[quad][Ur, Ui of photon 0, then of photon 1].
+    constexpr bool kEarly = CRIMP_EX_EARLY_OPEN;
     auto u_a = [&](ExPend& P, int i) -> ExRot {
-        ex_open(P.g[i].y);
+        if constexpr (!kEarly) ex_open(P.g[i].y);
         const ExRot r = ex_end_a(P.e[i], P.g[i].y);
         ex_ready(r.ts, r.tc);
         return r;
     };
     auto u_s = [&](ExPend& P, int i, ExRot& r, uint32_t (&a)[2][4]) {
-        ex_open(r.ts);
+        if constexpr (!kEarly) ex_open(r.ts);
         a[i >> 1][2 * (i & 1) + 1] = ex_end_s(P.e[i], P.g[i].y, r.ts);
         ex_ready(a[i >> 1][2 * (i & 1) + 1]);
     };
     auto u_c = [&](ExPend& P, int i, ExRot& r, uint32_t (&a)[2][4]) {
-        ex_open(r.tc);
+        if constexpr (!kEarly) ex_open(r.tc);
         a[i >> 1][2 * (i & 1)] = ex_end_c(P.e[i], P.g[i].y, r.tc);
         ex_ready(a[i >> 1][2 * (i & 1)]);
     };
     auto item_begin = [&](VItem& it, int s, int nlive) {
-        ex_open(it.d);
+        if constexpr (!kEarly) ex_open(it.d);
         v_begin(it, s, nlive);
         ex_ready(it.g.idx, it.g.y);
     };
     auto item_a = [&](VItem& it) {
-        ex_open(it.g.y);
+        if constexpr (!kEarly) ex_open(it.g.y);
         it.r = ex_end_a(it.e, it.g.y);
         ex_ready(it.r.ts, it.r.tc);
     };
     auto item_s = [&](VItem& it) {
-        ex_open(it.r.ts);
+        if constexpr (!kEarly) ex_open(it.r.ts);
         it.dsn = ex_end_s(it.e, it.g.y, it.r.ts);
         ex_ready(it.dsn);
     };
     auto item_c = [&](VItem& it) {
-        ex_open(it.r.tc);
+        if constexpr (!kEarly) ex_open(it.r.tc);
         it.dc = ex_end_c(it.e, it.g.y, it.r.tc);
         ex_ready(it.dc);
     };
     auto item_post = [&](VItem& it) {
-        ex_open(it.dc, it.dsn);
+        if constexpr (!kEarly) ex_open(it.dc, it.dsn);
         v_post(it);
         ex_ready(it.rc, it.rs);
         ex_ready(it.rn);
     };
     auto u_begin = [&](double& d) -> ExArg {
-        ex_open(d);
+        if constexpr (!kEarly) ex_open(d);
         const ExArg g = begin1(d);
         ex_ready(g.idx, g.y);
         return g;
@@ -492,68 +500,105 @@ __global__ __launch_bounds__(kExBlock, 1) void k_search_exact(
         ExArg g[4];
         uint32_t a[2][4];
         ExRot r[4];
+        // (kEarly: each piece's input opened before the MFMA that starts its gap; EO = early open)
+#define EO(...) do { if constexpr (kEarly) ex_open(__VA_ARGS__); } while (0)
+        EO(D.d[0].x);
         ex_mfma<0>(X.A3[0], EX_LO(X.b[0][0]));
         g[0] = u_begin(D.d[0].x);                                // gap 0
+        EO(D.d[0].y);
         ex_mfma<1>(X.A3[0], EX_LO(X.b[0][1]));
-        ex_keep(Y.A6);  // read by the previous group's last MFMAs
-        ex_keep(Y.b[1][0]);
-        ex_keep(Y.b[1][1]);
+        // operands are kept allocated two MFMAs past their last reader (three with the early opens, whose missing
+        // pads shorten the gaps: tools/isa_hazards.py's 64-issue-cycle rule)
+#define EK(...) do { if constexpr (!kEarly) ex_keep(__VA_ARGS__); } while (0)
+#define EK3(...) do { if constexpr (kEarly) ex_keep(__VA_ARGS__); } while (0)
+        EK(Y.A6);  // read by the previous group's last MFMAs
+        EK(Y.b[1][0]);
+        EK(Y.b[1][1]);
         g[1] = u_begin(D.d[0].y);                                // gap 1
+        EO(D.d[1].x);
         ex_mfma<2>(X.A3[0], EX_LO(X.b[1][0]));
+        EK3(Y.A6);
+        EK3(Y.b[1][0]);
+        EK3(Y.b[1][1]);
         if (sync) __syncthreads();  // the chunk's barrier: after the previous group's V writes, before this read
         read_b(c, p + 1, Y);                                     // gap 2: consumed in the next group
         g[2] = u_begin(D.d[1].x);
+        EO(D.d[1].y);
         ex_mfma<3>(X.A3[0], EX_LO(X.b[1][1]));
         g[3] = u_begin(D.d[1].y);                                // gap 3
         read_dt_pair(c, p + 3, D);                               //        consumed in the next group
+        EO(I0.d);
         ex_mfma<0>(X.A3[1], EX_HI(X.b[0][0]));
         item_begin(I0, is, inl);                                 // gap 4
         ex_mfma<1>(X.A3[1], EX_HI(X.b[0][1]));
-        ex_keep(X.A3[0]);
+        EK(X.A3[0]);
         v_table(I0);                                             // gap 5
-        ex_open(X.A3[0]);
+        if constexpr (!kEarly) ex_open(X.A3[0]);
         const i32x4 A40 = ex_shr8(X.A3[0]);
         ex_ready(A40);
+        EO(I1.d);
         ex_mfma<2>(X.A3[1], EX_HI(X.b[1][0]));
+        EK3(X.A3[0]);
         item_begin(I1, is + 1, inl);                             // gap 6
         ex_mfma<3>(X.A3[1], EX_HI(X.b[1][1]));
         v_table(I1);                                             // gap 7
-        ex_open(X.A3[1]);
+        if constexpr (!kEarly) ex_open(X.A3[1]);
         const i32x4 A41 = ex_shr8(X.A3[1]);
         ex_ready(A41);
+        EO(P.g[0].y);
         ex_mfma<4>(A40, EX_LO(X.b[0][0]));
         r[0] = u_a(P, 0);                                        // gap 8
         u_s(P, 0, r[0], a);
+        EO(r[0].tc);
+        EO(I0.g.y);
         ex_mfma<5>(A40, EX_LO(X.b[0][1]));
-        ex_keep(X.A3[1]);
+        EK(X.A3[1]);
         u_c(P, 0, r[0], a);                                      // gap 9
         item_a(I0);
+        EO(P.g[1].y);
         ex_mfma<6>(A40, EX_LO(X.b[1][0]));
+        EK3(X.A3[1]);
         r[1] = u_a(P, 1);                                        // gap 10
         u_s(P, 1, r[1], a);
+        EO(r[1].tc);
+        EO(I1.g.y);
         ex_mfma<7>(A40, EX_LO(X.b[1][1]));
         u_c(P, 1, r[1], a);                                      // gap 11
         item_a(I1);
+        EO(P.g[2].y);
         ex_mfma<4>(A41, EX_HI(X.b[0][0]));
         r[2] = u_a(P, 2);                                        // gap 12
         u_s(P, 2, r[2], a);
+        EO(r[2].tc);
+        EO(I0.r.ts);
         ex_mfma<5>(A41, EX_HI(X.b[0][1]));
-        ex_keep(A40);
+        EK(A40);
         u_c(P, 2, r[2], a);                                      // gap 13
         item_s(I0);
+        EO(P.g[3].y);
         ex_mfma<6>(A41, EX_HI(X.b[1][0]));
+        EK3(A40);
         r[3] = u_a(P, 3);                                        // gap 14
         u_s(P, 3, r[3], a);
+        EO(r[3].tc);
+        EO(I0.r.tc);
         ex_mfma<7>(A41, EX_HI(X.b[1][1]));
         u_c(P, 3, r[3], a);                                      // gap 15
         item_c(I0);
         // the next pair's operands: dense digits, compressed level-5/6 bytes (lane-swapped below)
         uint32_t c5[2][2], c6[2][2];
+        EO(a[0][0], a[0][1]);
+        EO(a[0][2], a[0][3]);
+        EO(a[1][0], a[1][1]);
+        EO(a[1][2], a[1][3]);
+        EO(I1.r.ts);
         ex_smfma<8>(X.A5, X.b[0][0], kIdx);
 #pragma unroll
         for (int qd = 0; qd < 2; ++qd) {                         // gap 16
-            ex_open(a[qd][0], a[qd][1]);
-            ex_open(a[qd][2], a[qd][3]);
+            if constexpr (!kEarly) {
+                ex_open(a[qd][0], a[qd][1]);
+                ex_open(a[qd][2], a[qd][3]);
+            }
             Y.A3[qd] = i32x4{(int)a[qd][0], (int)a[qd][1], (int)a[qd][2], (int)a[qd][3]};
 #pragma unroll
             for (int w = 0; w < 2; ++w)
@@ -563,8 +608,9 @@ __global__ __launch_bounds__(kExBlock, 1) void k_search_exact(
         ex_ready(Y.A3[0]);
         ex_ready(Y.A3[1]);
         item_s(I1);
+        EO(I1.r.tc);
         ex_smfma<9>(X.A5, X.b[0][1], kIdx);
-        ex_keep(A41);
+        EK(A41);
 #pragma unroll
         for (int qd = 0; qd < 2; ++qd) {                         // gap 17
 #pragma unroll
@@ -580,6 +626,7 @@ __global__ __launch_bounds__(kExBlock, 1) void k_search_exact(
         }
 
         ex_smfma<10>(X.A5, X.b[1][0], kIdx);
+        EK3(A41);
         {                                                        // gap 18
             uint32_t s5[2][2], s6[2][2];
 #pragma unroll
@@ -596,18 +643,24 @@ __global__ __launch_bounds__(kExBlock, 1) void k_search_exact(
         }
         ex_ready(Y.A5);
         ex_ready(Y.A6);
+        EO(I0.dc, I0.dsn);
         ex_smfma<11>(X.A5, X.b[1][1], kIdx);
         item_post(I0);                                           // gap 19
+        EO(I1.dc, I1.dsn);
         ex_smfma<12>(X.A6, X.b[0][0], kIdx);
         item_post(I1);                                           // gap 20
         ex_smfma<13>(X.A6, X.b[0][1], kIdx);
-        ex_keep(X.A5);
+        EK(X.A5);
         v_write(I0, icj, is);                                    // gap 21
         v_write(I1, icj, is + 1);
         ex_smfma<14>(X.A6, X.b[1][0], kIdx);
+        EK3(X.A5);
         v_read(ncj, ns, I0);                                     // gap 22: the next group's items
         v_read(ncj, ns + 1, I1);
         ex_smfma<15>(X.A6, X.b[1][1], kIdx);
+#undef EO
+#undef EK
+#undef EK3
         ex_keep(X.b[0][0]);
         ex_keep(X.b[0][1]);
     };

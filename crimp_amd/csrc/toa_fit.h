@@ -925,7 +925,7 @@ __global__ __launch_bounds__(256) void k_toa_grid_best(const double* __restrict_
                                                        const double* __restrict__ expo, int nnorm, int nphi, int nint,
                                                        int splits, int model, double sum_amp, double norm_first,
                                                        double lo, double hi, int plain, double hconst,
-                                                       double prod8_scale, int* __restrict__ unsafe,
+                                                       double prod8_scale, int nlazy, int* __restrict__ unsafe,
                                                        double* __restrict__ start) {
     __shared__ double bv[4];
     __shared__ int bi[4];
@@ -934,7 +934,13 @@ __global__ __launch_bounds__(256) void k_toa_grid_best(const double* __restrict_
     const double E = expo[iv];
     double best = -INFINITY;
     int bidx = 0x7fffffff;
-    auto lattice_ll = [&](int ai, int bj) {  // the reference LL of lattice point (norm ai, phShift bj)
+    auto lattice_ll = [&](int ai, int bj) -> double {  // the reference LL of lattice point (norm ai, phShift bj)
+        if (ai < nlazy) {  // a lazy norm (not evaluated): -inf where the min h invalidates it, else the grid reruns
+            double hm = INFINITY;
+            for (int sp = 0; sp < splits; ++sp) hm = fmin(hm, ph[((int64_t)sp * nint + iv) * nphi + bj]);
+            if ((hm + norm[iv * nnorm + ai]) > 0) atomicOr(unsafe, 1);
+            return (double)-INFINITY;
+        }
         double v = 0.0;
         for (int sp = 0; sp < splits; ++sp) v += pl[(((int64_t)sp * nint + iv) * nnorm + ai) * nphi + bj];
         const double ln = v * 0.69314718055994530942;  // log2 sums -> ln

@@ -73,7 +73,7 @@ def sharded_search(time, freq, nharm=2, stat=0, freq_dot=None, gather="all", com
     else:
         t0 = (time[0] + time[-1]) / 2  # periodsearch.py:54, shared by every shard
         nf = int(np.size(freq))
-    nfd = 0 if freq_dot is None else int(np.size(freq_dot))
+    nfd = 0 if freq_dot is None else int(freq_dot.numel() if isinstance(freq_dot, torch.Tensor) else np.size(freq_dot))
     total = (nfd if nfd else 1) * nf
     first, count = shard_range(total, world, rank)
     local = compute(time, t0, freq, nharm, stat, freq_dot, first, count)

@@ -50,36 +50,37 @@ def test_mfma_hazard_rules_hold_in_default_kernel():
     assert checked == 2
 
 
-def test_exact_kernel_accumulators_untouched_by_compiler():
-    """The exact kernel's accumulators live in AGPRs outside hipcc's register model (search_exact.h, ex_mfma):
-    the compiled kernels may not touch an AGPR themselves (a VGPR spilled to an AGPR would overwrite them)."""
+def _agpr_check():
     import importlib.util
     spec = importlib.util.spec_from_file_location("agpr_check", os.path.join(ROOT, "tools", "agpr_check.py"))
     A = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(A)
-    res = A.compiler_agpr_accesses()
+    return A
+
+
+def test_exact_kernel_accumulators_untouched_by_compiler(device_builds):
+    """The exact kernel's accumulators live in AGPRs outside hipcc's register model (search_exact.h, ex_mfma):
+    the compiled kernels may not touch an AGPR themselves (a VGPR spilled to an AGPR would overwrite them)."""
+    res = _agpr_check().compiler_agpr_accesses(asm_path=device_builds["default"])
     assert len(res) == 2
     for name, bad in res.items():
         assert bad == [], (name, bad[:4])
 
 
-def test_agpr_check_flags_the_unclobbered_build():
+def test_agpr_check_flags_the_unclobbered_build(device_builds):
     """The fault of round 3's no-ex_open build: without the AGPR clobbers on the MFMA statements, hipcc keeps a
     value of its own in an accumulator AGPR (the photon-time address, overwritten by tile 0's MFMAs ->
     hipErrorIllegalAddress). tools/agpr_check.py must see that in the build without clobbers and fences; the shipped
     build (clobbers on) has none (test above), and the clobbered no-fence build ran bit-identically on the GPU
     (profiles/r04/ab_fences.log)."""
-    import importlib.util
-    spec = importlib.util.spec_from_file_location("agpr_check", os.path.join(ROOT, "tools", "agpr_check.py"))
-    A = importlib.util.module_from_spec(spec)
-    spec.loader.exec_module(A)
-    bad = A.compiler_agpr_accesses(defines=("-DCRIMP_EX_AGPR_CLOBBERS=0", "-DCRIMP_EX_OPEN=0"))
+    A = _agpr_check()
+    bad = A.compiler_agpr_accesses(asm_path=device_builds["noclob_noopen"])
     assert any(v for v in bad.values()), bad
-    ok = A.compiler_agpr_accesses(defines=("-DCRIMP_EX_OPEN=0",))
+    ok = A.compiler_agpr_accesses(asm_path=device_builds["noopen"])
     assert all(v == [] for v in ok.values()), ok
 
 
-def test_isa_hazards_rejects_the_unfenced_build(tmp_path):
+def test_isa_hazards_rejects_the_unfenced_build(device_builds):
     """Without the ex_open fences hipcc rewrites MFMA A operands 32-64 issue cycles after the MFMA; on the GPU that
     build returned rows 16..31 of every 2-D tile differently from run to run (profiles/r04/ab_fences.log). The
     checker must reject it, as it accepts the shipped kernel (test_mfma_hazard_rules_hold_in_default_kernel)."""
@@ -87,8 +88,7 @@ def test_isa_hazards_rejects_the_unfenced_build(tmp_path):
     spec = importlib.util.spec_from_file_location("isa_hazards", os.path.join(ROOT, "tools", "isa_hazards.py"))
     H = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(H)
-    co = H.compile_device_object(str(tmp_path / "noopen.co"), ("-DCRIMP_EX_OPEN=0",))
-    funcs = {k: v for k, v in H.disassemble(co).items() if "k_search_exact" in k}
+    funcs = {k: v for k, v in H.disassemble(device_builds["noopen_co"]).items() if "k_search_exact" in k}
     assert len(funcs) == 2
     for name, insts in funcs.items():
         bad = H.check_function(insts)

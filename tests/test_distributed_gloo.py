@@ -49,6 +49,10 @@ def _worker(rank, world, port, out_path):
     fd = np.array([-12.0, -9.0, -8.5])
     full = sharded_search(t, f, 2, 0, freq_dot=fd, gather="all", compute=_oracle_slice)
     best = sharded_search(t, f, 3, 1, freq_dot=fd, gather="best", compute=_oracle_slice)
+    import torch  # the same through tensors (bench.py's config-4 leg passes device tensors, freq_dot included)
+    best_t = sharded_search(torch.as_tensor(t), torch.as_tensor(f), 3, 1, freq_dot=torch.as_tensor(fd), gather="best",
+                            compute=_oracle_slice)
+    assert best_t == best
     amps, phs = [2.0, 1.0], [0.3, -1.0]
     x, off, E, _ = template_intervals(5, 1500, 10.0, amps, phs, seed=3)
     tmpl = {"model": "fourier", "norm": {"value": 10.0}, "amp_1": {"value": 2.0}, "ph_1": {"value": 0.3},

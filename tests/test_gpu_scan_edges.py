@@ -204,3 +204,24 @@ def test_ascent_start_reaches_the_lattice_points_maximum(gpu, model, monkeypatch
     np.testing.assert_allclose(a["phShi"], b["phShi"], rtol=0, atol=2 * math.pi * 1e-9)
     np.testing.assert_allclose(a["LLmax"], b["LLmax"], rtol=1e-12)
     assert np.array_equal(a["phShi_LL"], b["phShi_LL"]) and np.array_equal(a["phShi_UL"], b["phShi_UL"])
+
+
+def test_projected_ascent_on_the_bound_device_equals_host(gpu):
+    """A maximum beyond -pi: the ascent stops on the bound and holds phShift there while the norm takes its own
+    Newton steps (projected Newton, k_toa_fit's fit_newton_dir and toafit._newton_step); the device driver and the
+    host-driven iterations agree (phShift exactly -pi, norm and LLmax to 1e-12, identical 1-sigma bounds), and the
+    norm is the profile maximum there (dLL/dnorm ~ 0), which is what the redChi2 against the oracle needs."""
+    from crimp_amd.toafit import ToAFitter
+    case = [c for c in CASES if c[1] == "beyond-bound"][0]
+    model, name, n, shift, seed, res, bm, window, capped = case
+    tm = _template(model, name)
+    x, E = _sample(tm, n, shift, seed)
+    f = ToAFitter(x, np.array([0, x.size]), np.array([E]), tm, ph_shift_res=res)
+    d = f.fit(brutemin=True)
+    h = f.fit_host(brutemin=True)
+    assert d["phShi"][0] == -math.pi and h["phShi"][0] == -math.pi
+    np.testing.assert_allclose(d["norm"], h["norm"], rtol=1e-12)
+    np.testing.assert_allclose(d["LLmax"], h["LLmax"], rtol=1e-12)
+    assert d["phShi_LL"][0] == h["phShi_LL"][0] and d["phShi_UL"][0] == h["phShi_UL"][0]
+    ll, g, H = f.evaluate(np.array([0]), d["norm"], d["phShi"])
+    assert abs(g[0, 0]) <= 1e-6 * abs(E)        # dLL/dnorm = -E + sum 1/m vanishes at the profiled norm

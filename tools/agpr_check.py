@@ -13,14 +13,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "crimp_amd", "csrc")
 
 
-def compiler_agpr_accesses(kernel="k_search_exact", defines=()):
-    """{kernel symbol: [compiler-generated lines naming an AGPR]} of the device code built with ``defines``
-    (e.g. ("-DCRIMP_EX_AGPR_CLOBBERS=0", "-DCRIMP_EX_OPEN=0"): round 3's faulting build)."""
-    with tempfile.TemporaryDirectory() as d:
-        out = os.path.join(d, "k.s")
-        subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-w", "--cuda-device-only",
-                        "-S", *defines, "-o", out, "crimp_hip.hip"], cwd=SRC, check=True, capture_output=True)
-        text = open(out).read()
+def compile_cmd(out, defines=(), asm=True):
+    """hipcc command building the library's gfx950 device code with ``defines``: assembly (asm) or a bare code object"""
+    return ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-w", "--cuda-device-only"] + (
+        ["-S"] if asm else ["--no-gpu-bundle-output", "-c"]) + list(defines) + ["-o", out, "crimp_hip.hip"]
+
+
+def accesses(text, kernel="k_search_exact"):
+    """{kernel symbol: [compiler-generated lines naming an AGPR]} of a device assembly listing."""
     found = {}
     for m in re.finditer(r"^(_Z\w*%s\w*):" % kernel, text, re.M):
         name = m.group(1)
@@ -35,6 +35,18 @@ def compiler_agpr_accesses(kernel="k_search_exact", defines=()):
                 bad.append(line.strip())
         found[name] = bad
     return found
+
+
+def compiler_agpr_accesses(kernel="k_search_exact", defines=(), asm_path=None):
+    """{kernel symbol: [compiler-generated lines naming an AGPR]} of the device code built with ``defines``
+    (e.g. ("-DCRIMP_EX_AGPR_CLOBBERS=0", "-DCRIMP_EX_OPEN=0"): round 3's faulting build), or of an
+    already built listing ``asm_path``."""
+    if asm_path is not None:
+        return accesses(open(asm_path).read(), kernel)
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "k.s")
+        subprocess.run(compile_cmd(out, defines), cwd=SRC, check=True, capture_output=True)
+        return accesses(open(out).read(), kernel)
 
 
 if __name__ == "__main__":

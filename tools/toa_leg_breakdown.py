@@ -1,5 +1,5 @@
 """Where the bench's ToA leg spends its time (config 5 per GPU: 1250 intervals x 1e5 photons, brute + MLE + 1-sigma
-scan + redChi2): ToAFitter construction, the crimp_toa_fit call, and the redChi2 step (k_binphases + host chi^2),
+scan + redChi2): ToAFitter construction, the crimp_toa_fit call, and the device redChi2 step (crimp_toa_redchi2),
 each bracketed by torch.cuda.synchronize(), mean of REPS after one warm-up.
 usage: python tools/toa_leg_breakdown.py"""
 import os
@@ -21,7 +21,7 @@ x, off, E, _ = template_intervals_torch(nint, nper, bench.T2259["norm"]["value"]
                                         bench.T2259["ph"], seed=2, device="cuda")
 ToAFitter(x, off, E, tm).fit(brutemin=True)
 torch.cuda.synchronize()
-t = {"construct": [], "toa_fit": [], "to_host": [], "redchi2": [], "whole_fit": []}
+t = {"construct": [], "toa_fit": [], "redchi2": [], "whole_fit": []}
 for _ in range(reps):
     t0 = time.perf_counter()
     f = ToAFitter(x, off, E, tm)
@@ -30,15 +30,14 @@ for _ in range(reps):
     r = ops.toa_fit(f.x, f.offsets, f.tpl, f._arr(f.E, np.float64), f.norm0, f.res, True, False)
     torch.cuda.synchronize()
     t2 = time.perf_counter()
-    r = r.cpu().numpy()
     t3 = time.perf_counter()
-    f.reduced_chi2(r[:, 0].copy(), r[:, 1].copy())
+    f.reduced_chi2(None, None, records=r)
     torch.cuda.synchronize()
     t4 = time.perf_counter()
     ToAFitter(x, off, E, tm).fit(brutemin=True)
     torch.cuda.synchronize()
     t5 = time.perf_counter()
-    for k, v in zip(t, (t1 - t0, t2 - t1, t3 - t2, t4 - t3, t5 - t4)):
+    for k, v in zip(t, (t1 - t0, t2 - t1, t4 - t3, t5 - t4)):
         t[k].append(v * 1e3)
 for k, v in t.items():
     print("%-10s %8.3f ms (min %.3f)" % (k, np.mean(v), np.min(v)), flush=True)
