@@ -14,7 +14,7 @@ Also reported:
   the peak of this instruction mix is 2/3 x 5.0 + 1/3 x 10.0 = 6.67 POP/s (the i8 dense peak, 2x BF16's 2.5 PF,
   and the 2:4-sparse peak, 2x dense) and ``frac`` is the matrix pipe's occupancy at the nominal 2.4 GHz; kernel
   time from hipEvents around the harmonic-sum kernels on their stream; ``traffic`` from the same tree's rocprofv3
-  PMC pass (profiles/r03/pmc_traffic.json, tools/pmc_round.sh) when it was taken on this workload;
+  PMC pass (profiles/r04/pmc_traffic.json, tools/pmc_round.sh) when it was taken on this workload;
 * ``cpu_baseline``: the oracle (oracle/liborc.so, fp64, OpenMP over trials) on a bounded sample;
 * ``fast_path``: the opt-in fp32 sin/cos path (precision="fast") on the same workload, for comparison;
 * ToA (config 5 per GPU): the device fit of 1250 intervals x 1e5 photons, and the end-to-end ``measure_intervals``
@@ -44,7 +44,7 @@ PEAK_HBM_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E ~8 TB/s
 PEAK_VALU_SLOTS = 256 * 4 * 32 * 2.4e9   # fp32 lane-ops/s: 256 CUs x 4 SIMD-32 x 2.4 GHz
 PEAK_F64_OPS = 256 * 64 * 2.4e9          # fp64 FMA-rate lane-ops/s: half the fp32 rate (78.6 TFLOP/s fp64 vector)
 PEAK_F16_TFLOPS = 2500.0                 # MI355X_MICROARCH.md: dense F16/BF16 MFMA ~2.5 PFLOP/s
-PMC_FILE = os.path.join(ROOT, "profiles", "r03", "pmc_traffic.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r04", "pmc_traffic.json")
 
 
 def parse():
@@ -242,11 +242,23 @@ def toa_leg(a, dev, world, rank):
     e2e = time.perf_counter() - t1
     out["toa_e2e_fits_per_s"] = a.toa_intervals / e2e
     out["toa_e2e_seconds"] = e2e
-    out["toa_e2e_note"] = ("measure_intervals from host MJD arrays (%d photons): upload, interval selection, calcphase, "
-                           "brute+MLE+1-sigma fits, redChi2, per-interval H_5 (measureToAs.py:168-226 minus file I/O)"
-                           % mjd.size)
+    out["toa_e2e_note"] = ("measure_intervals from a host MJD array (%d photons, pageable numpy; toa_e2e_pinned_*: "
+                           "from a page-locked torch tensor): upload, interval selection, calcphase, brute+MLE+1-sigma "
+                           "fits, redChi2, per-interval H_5 (measureToAs.py:168-226 minus file I/O)" % mjd.size)
     out["toa_e2e_max_shift_diff_vs_device_fit_cycles"] = float(np.max(np.abs(
         np.angle(np.exp(1j * (r2["phShi"] - res["phShi"]))))) / (2 * np.pi))
+    # the same from a page-locked host tensor (an event reader's pinned staging buffer): the upload is one DMA
+    pin = torch.from_numpy(mjd).pin_memory()
+    measure_intervals(pin, par, tm, starts, ends, E, brutemin=True)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    r3 = measure_intervals(pin, par, tm, starts, ends, E, brutemin=True)
+    torch.cuda.synchronize()
+    e2p = time.perf_counter() - t1
+    assert np.array_equal(r3["phShi"], r2["phShi"])
+    out["toa_e2e_pinned_fits_per_s"] = a.toa_intervals / e2p
+    out["toa_e2e_pinned_seconds"] = e2p
+    del pin, r3
     if not a.no_cpu and rank == 0 and world == 1:  # CPU baselines: rank 0 at N=1 only
         out["toa_cpu_baseline"] = toa_cpu_baseline(x, off, E, tm, a.cpu_seconds)
     if world == 1 and a.full_c5 > 0:  # the whole of config 5 (1e4 intervals x 1e5 photons, 8 GB) on one GPU
@@ -470,7 +482,7 @@ def cpu_baseline(t, f0, df, nharm, budget_s):
 
 def pmc_traffic(photons, trials, nharm):
     """HBM bytes per search of this workload from the tree's own rocprofv3 PMC pass (tools/pmc_exact.sh ->
-    profiles/r03/pmc_traffic.json), or None if that pass was not taken on this workload."""
+    profiles/r04/pmc_traffic.json), or None if that pass was not taken on this workload."""
     try:
         rec = json.load(open(PMC_FILE))
     except (OSError, ValueError):
@@ -482,9 +494,9 @@ def pmc_traffic(photons, trials, nharm):
 
 def pmc_clock():
     """The search kernel's clock and clock-normalised matrix-pipe occupancy from the tree's SQ counter pass
-    (tools/pmc_round.sh -> profiles/r03/pmc_search/): clock = GRBM_GUI_ACTIVE / 8 XCDs / the launch's duration in
+    (tools/pmc_round.sh -> profiles/r04/pmc_search/): clock = GRBM_GUI_ACTIVE / 8 XCDs / the launch's duration in
     the same session's kernel trace; busy = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x those cycles)."""
-    d = os.path.join(ROOT, "profiles", "r03", "pmc_search")
+    d = os.path.join(ROOT, "profiles", "r04", "pmc_search")
     try:
         cnt = {}
         for line in open(os.path.join(d, "summary_k_search_exact.txt")):
@@ -497,7 +509,7 @@ def pmc_clock():
                 ns = float(line.rsplit('",', 1)[1].split(",")[2])
         cyc = cnt["GRBM_GUI_ACTIVE"] / 8.0
         return {"clock_ghz": cyc / ns, "matrix_pipe_busy_at_clock": cnt["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024.0 * cyc),
-                "source": "profiles/r03/pmc_search (rocprofv3 --pmc over tools/run_search.py, config 3, the same kernel)"}
+                "source": "profiles/r04/pmc_search (rocprofv3 --pmc over tools/run_search.py, config 3, the same kernel)"}
     except (OSError, KeyError, ValueError, IndexError, TypeError, ZeroDivisionError):
         return None
 

@@ -1040,7 +1040,20 @@ __global__ __launch_bounds__(kGridBlock) __attribute__((amdgpu_waves_per_eu(4)))
 // 2^-14 would be an f16 subnormal) and bright ones cannot overflow f16; every factor norm + h is then s (norm + h)
 // exactly, so the log2 sums lose se per photon (subtracted exactly at the end) and min h is hmn / s. se = 0 (the
 // amplitudes already in range, e.g. the bundled template) is the unscaled kernel, bit for bit.
-constexpr int kGmTile = 128;  // photons per LDS tile
+// Tile: CRIMP_GM_TILE photons per LDS tile, built by the block's 256 threads -- 256: one thread per photon computes all
+// of its harmonics (one sin/cos and one recurrence per photon); 128 (round 3): two threads per photon, each storing
+// half of the harmonics but running the recurrence up to its own. Each photon row has one spare 16-byte slot
+// (kGmPad): the 16 lanes of a b128 read pass take 16 consecutive rows, whose start banks are then 16 distinct
+// multiples of 4 (row strides of 3, 5, 7, 9 slots for K <= 2, 4, 6, 8; without the pad 2, 4, 6, 8 slots put 2-8 rows
+// on the same banks).
+#ifndef CRIMP_GM_TILE
+#define CRIMP_GM_TILE 256
+#endif
+#ifndef CRIMP_GM_PAD
+#define CRIMP_GM_PAD 1
+#endif
+constexpr int kGmTile = CRIMP_GM_TILE, kGmPad = CRIMP_GM_PAD;
+static_assert(kGmTile == 128 || kGmTile == 256, "k_toa_grid_mf: one or two of the block's 256 threads per photon");
 static_assert(kGridBlock == 32 * 4, "k_toa_grid_mf: 4 waves of 32 phShift columns cover a block's kGridBlock columns");
 // HMIN: track min h per phShift (the public crimp_toa_grid; the device fit skips it when the template's lower bound
 // already keeps every evaluated norm + h positive, k_toa_grid_best then takes that bound). PROD: model values per log2
@@ -1053,7 +1066,7 @@ __global__ __launch_bounds__(256) void k_toa_grid_mf(const double* __restrict__ 
                                                      int64_t chunk, int nint, int se, int a_first,
                                                      double* __restrict__ lnsum, double* __restrict__ hmin) {
     constexpr int NM = (KF + 1) / 2;  // MFMAs per 32-photon chunk (two harmonics each)
-    __shared__ __attribute__((aligned(16))) u32x4 afr[kGmTile][2 * NM];  // [photon][harmonic]
+    __shared__ __attribute__((aligned(16))) u32x4 afr[kGmTile][2 * NM + kGmPad];  // [photon][harmonic]
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hk = lane >> 5;
     const int64_t iv = blockIdx.y, split = blockIdx.z;
     const int bphi = blockIdx.x * kGridBlock + 32 * wv + (lane & 31);
@@ -1098,8 +1111,9 @@ __global__ __launch_bounds__(256) void k_toa_grid_mf(const double* __restrict__ 
     for (int64_t base = beg; base < end; base += kGmTile) {
         const int cnt = (int)std::min<int64_t>(kGmTile, end - base);
         __syncthreads();
-        {   // A fragments: thread (photon p = tid & 127, half g = tid >> 7) builds harmonics g*4 + 1 .. g*4 + 4
-            const int p = tid & (kGmTile - 1), g = tid >> 7;
+        {   // A fragments: thread (photon p = tid % kGmTile, part g = tid / kGmTile) builds harmonics [g JP, (g+1) JP)
+            constexpr int JP = kGmTile == 256 ? 2 * NM : 4;
+            const int p = tid & (kGmTile - 1), g = kGmTile == 256 ? 0 : tid >> 7;
             float c1 = 1.0f, s1 = 0.0f;
             if (p < cnt) {
                 double rv = x[base + p];
@@ -1109,11 +1123,12 @@ __global__ __launch_bounds__(256) void k_toa_grid_mf(const double* __restrict__ 
             float cj = c1, sj = s1;
 #pragma unroll
             for (int j = 0; j < 2 * NM; ++j) {
-                if (j >= 4 * g && j < 4 * g + 4) {
+                if (j >= JP * g && j < JP * g + JP) {
                     uint32_t dh, dl;
                     split_xy<false>(cj, sj, dh, dl);
-                    const uint32_t hc = dh & 0xffffu, hs = dh >> 16, lc = dl & 0xffffu, ls = dl >> 16;
-                    afr[p][j] = u32x4{hc | (hc << 16), lc | (lc << 16), hs | (hs << 16), ls | (ls << 16)};
+                    // {hi, hi}, {lo, lo} of cos (low halves of dh, dl), then of sin (high halves): one v_perm each
+                    afr[p][j] = u32x4{__builtin_amdgcn_perm(dh, dh, 0x01000100u), __builtin_amdgcn_perm(dl, dl, 0x01000100u),
+                                      __builtin_amdgcn_perm(dh, dh, 0x03020302u), __builtin_amdgcn_perm(dl, dl, 0x03020302u)};
                 }
                 const float cn = __builtin_fmaf(cj, c1, -sj * s1);
                 sj = __builtin_fmaf(sj, c1, cj * s1);
@@ -1255,37 +1270,68 @@ __global__ __launch_bounds__(64 * kBinWaves) void k_binphases(const double* __re
                                                               const double* __restrict__ edges, int nb,
                                                               unsigned long long* __restrict__ counts) {
     __shared__ unsigned int cnt[kBinWaves][256];
+    __shared__ double se[257];
     const int64_t iv = blockIdx.x;
     const int tid = threadIdx.x, w = tid >> 6;
     for (int b = tid; b < kBinWaves * 256; b += blockDim.x) cnt[b >> 8][b & 255] = 0;
+    for (int b = tid; b <= nb; b += blockDim.x) se[b] = edges[b];
     __syncthreads();
-    const double first = edges[0], last = edges[nb];
-    const double denom = last - first;
+    const double first = se[0], last = se[nb];
+    const double scale = (double)nb / (last - first);
+    // np.histogram's bin: the estimate floor((v - first) / (last - first) * nb), then its two corrections against the
+    // edges (v below its left edge: one down; at or above its right edge, unless the last bin: one up). Any estimate
+    // within one bin of the true one ends on the same bin, so the product with the reciprocal (a few ulps from numpy's
+    // quotient) gives numpy's counts without an fp64 division per photon.
+    auto bin = [&](double v) -> int {
+        int idx = (int)((v - first) * scale);
+        idx = idx < nb ? idx : nb - 1;
+        if (v < se[idx]) idx -= 1;
+        if (idx != nb - 1 && v >= se[idx + 1]) idx += 1;
+        return idx;
+    };
     const int64_t stride = (int64_t)blockDim.x * gridDim.y;
-    // up to kBinRegs bins (measuretoas' default 15): per-thread counters in registers (one compare-add per bin and
-    // photon, no LDS atomics in the photon loop), added to the wave's LDS histogram once at the end
-    uint32_t rc[kBinRegs];
+    const int64_t beg = offsets[iv] + (int64_t)blockIdx.y * blockDim.x + tid, end = offsets[iv + 1];
+    if (nb <= kBinRegs) {
+        // up to kBinRegs bins (measuretoas' default 15): per-thread 8-bit counters, bins 0-7 in lo and 8-15 in hi
+        // (one shift and a 64-bit add per photon), moved to 32-bit registers every 32 iterations of two photons (a
+        // byte holds 64 at most), added to the wave's LDS histogram once at the end
+        uint32_t rc[kBinRegs];
 #pragma unroll
-    for (int b = 0; b < kBinRegs; ++b) rc[b] = 0;
-    const bool regs = nb <= kBinRegs;
-    for (int64_t i = offsets[iv] + (int64_t)blockIdx.y * blockDim.x + tid; i < offsets[iv + 1]; i += stride) {
-        const double v = x[i];
-        if (!(v >= first && v <= last)) continue;
-        int64_t idx = (int64_t)(((v - first) / denom) * (double)nb);
-        if (idx == nb) idx -= 1;
-        if (v < edges[idx]) idx -= 1;
-        if (v >= edges[idx + 1] && idx != nb - 1) idx += 1;
-        if (regs) {
+        for (int b = 0; b < kBinRegs; ++b) rc[b] = 0;
+        uint64_t lo = 0, hi = 0;
+        int pend = 0;
+        auto count = [&](double v) {
+            if (!(v >= first && v <= last)) return;
+            const int idx = bin(v);
+            const uint64_t one = 1ull << (8 * (idx & 7));
+            lo += idx < 8 ? one : 0ull;
+            hi += idx < 8 ? 0ull : one;
+        };
+        auto flush = [&]() {
 #pragma unroll
-            for (int b = 0; b < kBinRegs; ++b) rc[b] += idx == b ? 1u : 0u;
-        } else {
-            atomicAdd(&cnt[w][idx], 1u);
+            for (int b = 0; b < 8; ++b) {
+                rc[b] += (uint32_t)(lo >> (8 * b)) & 0xffu;
+                rc[b + 8] += (uint32_t)(hi >> (8 * b)) & 0xffu;
+            }
+            lo = hi = 0;
+            pend = 0;
+        };
+        for (int64_t i = beg; i < end; i += 2 * stride) {
+            const double v0 = x[i];
+            const double v1 = i + stride < end ? x[i + stride] : NAN;
+            count(v0);
+            count(v1);
+            if (++pend == 32) flush();
         }
-    }
-    if (regs) {
+        flush();
 #pragma unroll
         for (int b = 0; b < kBinRegs; ++b)
             if (rc[b]) atomicAdd(&cnt[w][b], rc[b]);
+    } else {
+        for (int64_t i = beg; i < end; i += stride) {
+            const double v = x[i];
+            if (v >= first && v <= last) atomicAdd(&cnt[w][bin(v)], 1u);
+        }
     }
     __syncthreads();
     for (int b = tid; b < nb; b += blockDim.x) {
@@ -1294,6 +1340,12 @@ __global__ __launch_bounds__(64 * kBinWaves) void k_binphases(const double* __re
         for (int k = 0; k < kBinWaves; ++k) c += cnt[k][b];
         if (c) atomicAdd(&counts[iv * nb + b], c);
     }
+}
+
+// photon splits per interval for k_binphases: about 8 blocks per CU over the whole call, at least 4096 photons per block
+static int64_t bin_splits(int64_t ntot, int64_t nint) {
+    const int64_t per = (ntot + nint - 1) / nint;
+    return std::max<int64_t>(1, std::min<int64_t>({(2048 + nint - 1) / nint, (per + 4095) / 4096, 65535}));
 }
 
 // Many independent one-trial searches (measureToAs.py:210-212: PeriodSearch(TIME_toa*86400, [f(ToA_mid)], 5).htest()
@@ -2445,6 +2497,7 @@ extern "C" int crimp_toa_fit(const double* x, const int64_t* offsets, int64_t ni
                                                      maxn, &pl, &ph, &splits, md, &ran, lz);
                     if (r2) return r2;
                     g_last_grid_fast = ran;
+                    g_last_grid_norms = nc - ((ran & kGridProd8) ? lz : 0);  // the lazy norms are not evaluated
                     k_toa_grid_best<<<(unsigned)nb, 256, 0, st>>>(pl, ph, dnrm + i0 * nc, dphi, doff + i0, de + i0, (int)nc,
                                                                  (int)nphi, (int)nb, (int)splits, T.model, C.sum_amp,
                                                                  grid_n[0], C.lo, C.hi, lattice_start, hb,
@@ -2500,13 +2553,14 @@ extern "C" int crimp_toa_fit(const double* x, const int64_t* offsets, int64_t ni
             }
 #undef CRIMP_LF
         };
-        // Brute grid, then fits. Timed calls (CRIMP_FLAG_TIME_KERNELS) and small batches run the two in sequence on the
-        // caller's stream; otherwise the intervals go in two halves on two streams -- the second half's grid runs
-        // beside the first half's fits and fills the last, partly empty round of their workgroups (every interval's
-        // fit is independent of its batch, so the records are those of the sequential order)
+        // Brute grid, then fits, in sequence on the caller's stream. CRIMP_TOA_OVERLAP=1 (A/B build switch, read per
+        // call) runs the intervals in two halves on two streams instead, the second half's grid beside the first half's
+        // fits (every interval's fit is independent of its batch, so the records are those of the sequential order):
+        // measured slower on config 5 (6.1 vs 5.7 ms per 1250 intervals, profiles/r04/toa_breakdown.log) -- each half's
+        // fit runs 1.2 rounds of the resident workgroups and its grid half as many blocks, so the tails grow, not shrink
         auto all = [&](int md) -> int {
             const bool timed = flags & CRIMP_FLAG_TIME_KERNELS;
-            const bool overlap = run_brute && !timed && nint >= 2 * 512 && getenv("CRIMP_TOA_NO_OVERLAP") == nullptr;
+            const bool overlap = run_brute && !timed && nint >= 2 * 512 && getenv("CRIMP_TOA_OVERLAP") != nullptr;
             if (!overlap) {
                 KernelTimer kg(s, timed);  // brute grid: k_toa_grid(_mf) + k_toa_grid_best
                 kg.start();
@@ -2716,69 +2770,39 @@ extern "C" int crimp_toa_shape_points(const double* x, const int64_t* offsets, i
     return finish(s, flags);
 }
 
-// redChi2 of every fitted interval on the device (measureToAs.py:385-393 and the Cauchy / von Mises copies):
-// binphases' histogram (np.histogram semantics, as k_binphases) and, against it, the best-fit template curve at the
-// bin centres; chi2 = sum_b (model_b - rate_b)^2 / err_b^2 with rate = cts / (E / nbins), err = sqrt(cts) / (E /
-// nbins) (numpy's division: an empty bin gives inf, or nan where the model is 0 too), redChi2 = chi2 / (nbins -
-// nfree). One block per interval; rec = the fit records (norm [0], phShift [1], ampShift [6]).
-__global__ __launch_bounds__(256) void k_toa_redchi2(const double* __restrict__ x, const int64_t* __restrict__ offsets,
-                                                     const TplDev* __restrict__ T, const double* __restrict__ expo,
-                                                     const double* __restrict__ rec, const double* __restrict__ edges,
-                                                     const double* __restrict__ centers, int nb, int nfree,
-                                                     double* __restrict__ out) {
-    __shared__ unsigned int cnt[256];
+// redChi2 of every fitted interval on the device (measureToAs.py:385-393 and the Cauchy / von Mises copies): against
+// binphases' histogram (k_binphases, np.histogram semantics) the best-fit template curve at the bin centres;
+// chi2 = sum_b (model_b - rate_b)^2 / err_b^2 with rate = cts / (E / nbins), err = sqrt(cts) / (E / nbins) (numpy's
+// division: an empty bin gives inf, or nan where the model is 0 too), summed in bin order, redChi2 = chi2 / (nbins -
+// nfree). One 64-thread block per interval; rec = the fit records (norm [0], phShift [1], ampShift [6]).
+__global__ __launch_bounds__(64) void k_toa_chi2(const unsigned long long* __restrict__ counts, const TplDev T,
+                                                 const double* __restrict__ expo, const double* __restrict__ rec,
+                                                 const double* __restrict__ centers, int nb, int nfree,
+                                                 double* __restrict__ out) {
     __shared__ double term[256];
     const int64_t iv = blockIdx.x;
-    const int tid = threadIdx.x;
-    for (int b = tid; b < 256; b += blockDim.x) cnt[b] = 0;
-    __syncthreads();
-    const double first = edges[0], last = edges[nb];
-    const double denom = last - first;
-    uint32_t rc[kBinRegs];
-#pragma unroll
-    for (int b = 0; b < kBinRegs; ++b) rc[b] = 0;
-    const bool regs = nb <= kBinRegs;
-    for (int64_t i = offsets[iv] + tid; i < offsets[iv + 1]; i += blockDim.x) {
-        const double v = x[i];
-        if (!(v >= first && v <= last)) continue;
-        int64_t idx = (int64_t)(((v - first) / denom) * (double)nb);
-        if (idx == nb) idx -= 1;
-        if (v < edges[idx]) idx -= 1;
-        if (v >= edges[idx + 1] && idx != nb - 1) idx += 1;
-        if (regs) {
-#pragma unroll
-            for (int b = 0; b < kBinRegs; ++b) rc[b] += idx == b ? 1u : 0u;
-        } else {
-            atomicAdd(&cnt[idx], 1u);
-        }
-    }
-    if (regs) {
-#pragma unroll
-        for (int b = 0; b < kBinRegs; ++b)
-            if (rc[b]) atomicAdd(&cnt[b], rc[b]);
-    }
-    __syncthreads();
-    if (tid < nb) {
-        const double n = rec[iv * 8], ph = rec[iv * 8 + 1], A = rec[iv * 8 + 6];
-        const double xx = centers[tid];
+    const double n = rec[iv * 8], ph = rec[iv * 8 + 1], A = rec[iv * 8 + 6];
+    const double w = expo[iv] / (double)nb;
+    for (int b = threadIdx.x; b < nb; b += 64) {
+        const double xx = centers[b];
         double y = n;  // toafit.ToAFitter.curve: fourseries / wrapcauchy / vonmises (templatemodels.py:64-82, :166-185,
                        // :271-290); Fourier by angle subtraction as the host formed it
-        for (int j = 0; j < T->K; ++j) {
-            if (T->model == CRIMP_MODEL_FOURIER) {
-                const double ang = (double)(j + 1) * 2.0 * M_PI * xx + T->loc[j], bph = (double)(j + 1) * ph;
-                y = y + T->amp[j] * A * (cos(ang) * cos(bph) + sin(ang) * sin(bph));
-            } else if (T->model == CRIMP_MODEL_CAUCHY) {
-                y = y + T->amp[j] * A / (T->ch[j] - cos(xx - T->loc[j] - ph));
+        for (int j = 0; j < T.K; ++j) {
+            if (T.model == CRIMP_MODEL_FOURIER) {
+                const double ang = (double)(j + 1) * 2.0 * M_PI * xx + T.loc[j], bph = (double)(j + 1) * ph;
+                y = y + T.amp[j] * A * (cos(ang) * cos(bph) + sin(ang) * sin(bph));
+            } else if (T.model == CRIMP_MODEL_CAUCHY) {
+                y = y + T.amp[j] * A / (T.ch[j] - cos(xx - T.loc[j] - ph));
             } else {
-                y = y + T->amp[j] * A * exp(T->kap[j] * cos(xx - T->loc[j] - ph));
+                y = y + T.amp[j] * A * exp(T.kap[j] * cos(xx - T.loc[j] - ph));
             }
         }
-        const double w = expo[iv] / (double)nb, c = (double)cnt[tid];
+        const double c = (double)counts[iv * nb + b];
         const double rate = c / w, err = sqrt(c) / w;
-        term[tid] = ((y - rate) * (y - rate)) / (err * err);
+        term[b] = ((y - rate) * (y - rate)) / (err * err);
     }
     __syncthreads();
-    if (tid == 0) {
+    if (threadIdx.x == 0) {
         double chi2 = 0.0;
         for (int b = 0; b < nb; ++b) chi2 += term[b];
         out[iv] = chi2 / (double)(nb - nfree);
@@ -2815,7 +2839,7 @@ extern "C" int crimp_toa_redchi2(const double* x, const int64_t* offsets, int64_
         const double *dx = nullptr, *de = nullptr, *dc = nullptr, *dexp = nullptr, *drec = nullptr;
         const int64_t* doff = nullptr;
         double* dout = nullptr;
-        TplDev* dT = nullptr;
+        unsigned long long* dcnt = nullptr;
         HIPCHK(stage_in(sc, x, (size_t)ntot, dev, &dx));
         HIPCHK(stage_in(sc, offsets, (size_t)nint + 1, dev, &doff));
         HIPCHK(stage_in(sc, exposure, (size_t)nint, dev, &dexp));
@@ -2823,12 +2847,16 @@ extern "C" int crimp_toa_redchi2(const double* x, const int64_t* offsets, int64_
         HIPCHK(stage_in(sc, edges, (size_t)nbins + 1, dev, &de));
         HIPCHK(stage_in(sc, centers, (size_t)nbins, dev, &dc));
         HIPCHK(stage_out(sc, out, (size_t)nint, dev, &dout));
-        HIPCHK(sc.alloc(&dT, 1));
-        HIPCHK(h2d(dT, &T, sizeof(T)));
-        k_toa_redchi2<<<(unsigned)nint, 256, 0, s>>>(dx, doff, dT, dexp, drec, de, dc, nbins, nfree, dout);
+        HIPCHK(sc.alloc(&dcnt, (size_t)(nint * nbins)));
+        HIPCHK(hipMemsetAsync(dcnt, 0, (size_t)(nint * nbins) * sizeof(unsigned long long), s));
+        const int64_t ns = bin_splits(ntot, nint);
+        KernelTimer kt(s, flags & CRIMP_FLAG_TIME_KERNELS);
+        kt.start();
+        k_binphases<<<dim3((unsigned)nint, (unsigned)ns), 64 * kBinWaves, 0, s>>>(dx, doff, de, nbins, dcnt);
+        k_toa_chi2<<<(unsigned)nint, 64, 0, s>>>(dcnt, T, dexp, drec, dc, nbins, nfree, dout);
         HIPCHK(hipGetLastError());
+        kt.stop();
         HIPCHK(copy_back(s, out, dout, (size_t)nint, dev));
-        HIPCHK(hipStreamSynchronize(s));  // the template copy above reads host T
     }
     return finish(s, flags);
 }
@@ -2861,9 +2889,7 @@ extern "C" int crimp_binphases(const double* x, const int64_t* offsets, int64_t 
         HIPCHK(stage_in(sc, offsets, (size_t)nint + 1, dev, &doff));
         HIPCHK(stage_in(sc, edges, (size_t)nbins + 1, dev, &de));
         HIPCHK(stage_out(sc, counts, (size_t)(nint * nbins), dev, &dc));
-        // photon splits per interval: about 8 blocks per CU over the whole call, at least 4096 photons per block
-        const int64_t per = (ntot + nint - 1) / nint;
-        const int64_t ns = std::max<int64_t>(1, std::min<int64_t>({(2048 + nint - 1) / nint, (per + 4095) / 4096, 65535}));
+        const int64_t ns = bin_splits(ntot, nint);
         HIPCHK(hipMemsetAsync(dc, 0, (size_t)(nint * nbins) * sizeof(int64_t), s));
         k_binphases<<<dim3((unsigned)nint, (unsigned)ns), 64 * kBinWaves, 0, s>>>(
             dx, doff, de, nbins, reinterpret_cast<unsigned long long*>(dc));

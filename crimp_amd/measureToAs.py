@@ -152,11 +152,17 @@ def select_intervals(TIMEMJD, starts, ends):
 
 
 def _device_times(TIMEMJD):
-    """The photon times as one fp64 CUDA tensor (uploaded once), or None without a GPU."""
+    """The photon times as one fp64 CUDA tensor (uploaded once), or None without a GPU. A host torch tensor in
+    page-locked memory (``pin_memory()``, e.g. an event reader's staging buffer) goes up by DMA straight from it."""
     from ._native import _is_torch
     import torch
     if _is_torch(TIMEMJD):
-        return TIMEMJD.reshape(-1).to(torch.float64).contiguous() if TIMEMJD.is_cuda else None
+        if TIMEMJD.is_cuda:
+            return TIMEMJD.reshape(-1).to(torch.float64).contiguous()
+        if not torch.cuda.is_available():
+            return None
+        src = TIMEMJD.reshape(-1).to(torch.float64).contiguous()
+        return src.to("cuda", non_blocking=src.is_pinned())
     if not torch.cuda.is_available():
         return None
     return torch.as_tensor(np.ascontiguousarray(TIMEMJD, dtype=np.float64), device="cuda")
@@ -183,10 +189,15 @@ def measure_intervals(TIMEMJD, timMod, tempModPP, starts, ends, exposures, phShi
         offs = np.concatenate([[0], np.cumsum(n)]).astype(np.int64)
         if np.any(n <= 0):  # measureToAs.py:182 reads TIME_toa[-1] of every interval
             raise IndexError("index -1 is out of bounds for axis 0 with size 0 (a ToA interval holds no photons)")
-        rel = torch.arange(int(offs[-1]), device=T.device, dtype=torch.int64)
-        seg = torch.repeat_interleave(torch.arange(n.size, device=T.device), torch.as_tensor(n, device=T.device))
         offs_d = torch.as_tensor(offs, device=T.device)
-        allt = T[lo[seg] + (rel - offs_d[seg])]
+        if n.size == 1 or bool((lo[1:] == hi[:-1]).all()):
+            # consecutive intervals with no photon between them (ToA intervals tiling an observation): their
+            # concatenation is a slice of the time array, no copy
+            allt = T[int(lo[0]):int(lo[0]) + int(offs[-1])]
+        else:
+            rel = torch.arange(int(offs[-1]), device=T.device, dtype=torch.int64)
+            seg = torch.repeat_interleave(torch.arange(n.size, device=T.device), torch.as_tensor(n, device=T.device))
+            allt = T[lo[seg] + (rel - offs_d[seg])]
         first, last = allt[offs_d[:-1]], allt[offs_d[1:] - 1]
     else:
         allt, offs = select_intervals(TIMEMJD if T is None else T.cpu().numpy(), starts, ends)

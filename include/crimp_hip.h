@@ -98,7 +98,8 @@ int crimp_last_kernel_times(double* ms, int32_t cap);
 /* Trials of the last crimp_search (default precision) whose power was recomputed by the fp64 fix-up. */
 int64_t crimp_last_fixups(void);
 /* Brute-grid norms evaluated per phShift by the last crimp_toa_fit with CRIMP_TOA_BRUTE (the pruned candidates of
- * lmfit's 20-norm lattice, padded to 2, 4 or 20; 0 without a brute grid). Measurement hook for bench.py's
+ * lmfit's 20-norm lattice, padded to 2, 4 or 20, less the lazy norms the eight-factor grid leaves out; 0 without a
+ * brute grid). Measurement hook for bench.py's
  * algorithmic work count, not in the reference. */
 int64_t crimp_last_toa_grid_norms(void);
 /* The form of the last crimp_toa_fit's brute grid (Fourier templates): bit 0 -- no per-phShift min of the template

@@ -289,16 +289,20 @@ def test_binphases_device_counts(gpu):
 
 def test_binphases_split_blocks_ragged(gpu):
     """Photon splits per interval (several blocks add into one interval's counts): ragged intervals from 1 to 3e5
-    photons, values outside the edges and on them, 1 and 256 bins, host and device inputs -- np.histogram exactly."""
+    photons, values outside the edges and on them, 1 to 256 bins (16 and 17: both sides of the packed per-thread
+    counters), [0, 1] and [0, 2 pi] (the Cauchy / von Mises phases), host and device inputs -- np.histogram exactly."""
     import torch
     from crimp_amd import ops
     rng = np.random.default_rng(17)
     sizes = np.array([1, 7, 300000, 4096, 4097, 123457, 2, 65536])
-    x = rng.uniform(-0.1, 1.1, sizes.sum())
-    x[::97] = np.round(x[::97] * 16) / 16  # on bin edges
+    u = rng.uniform(-0.1, 1.1, sizes.sum())
     off = np.concatenate([[0], np.cumsum(sizes)])
-    for nb in (1, 15, 256):
-        edges = np.linspace(0, 1, nb + 1)
+    for nb, upper in ((1, 1.0), (15, 1.0), (16, 1.0), (17, 1.0), (15, 2 * np.pi), (256, 1.0)):
+        edges = np.linspace(0, upper, nb + 1)
+        x = u * upper
+        x[::97] = edges[rng.integers(0, nb + 1, x[::97].size)]  # on bin edges, the last one included
+        e = edges[rng.integers(0, nb + 1, x[1::89].size)]  # one ulp either side of an edge
+        x[1::89] = np.nextafter(e, np.where(rng.random(e.size) < 0.5, -np.inf, np.inf))
         ref = np.stack([np.histogram(x[off[i]:off[i + 1]], bins=edges)[0] for i in range(sizes.size)])
         assert np.array_equal(ops.binphases_counts(x, off, edges), ref)
         got = ops.binphases_counts(torch.tensor(x, device="cuda"), torch.tensor(off, device="cuda"),
@@ -460,6 +464,36 @@ def test_measuretoas_end_to_end(gpu, tmp_path):
     np.testing.assert_allclose(tab["Hpower"].to_numpy(), g["h5"], rtol=1e-6)
     lines = open(out + ".txt").read().splitlines()
     assert lines[0] == open(gpath("ToAs_2259.txt")).read().splitlines()[0]
+
+
+def test_measure_intervals_slice_gather_and_pinned_source(gpu):
+    """measure_intervals: consecutive intervals (their photons one slice of the time array, no gather), a page-locked
+    torch source (DMA from it), and the same intervals with photons left between two of them (the gather path) give
+    identical records for every interval the change does not touch (each interval's fit and H test are independent
+    of its batch)."""
+    import torch
+    from bench import T2259, _tmpl
+    from crimp_amd.measureToAs import measure_intervals
+    from crimp_amd.synth import template_intervals_torch
+    x, off, E, _ = template_intervals_torch(6, 20000, T2259["norm"]["value"], T2259["amp"], T2259["ph"], seed=4,
+                                            device=gpu)
+    F0, pep = 0.5, 58000.0
+    mjd = (pep + ((torch.arange(x.numel(), device=gpu, dtype=torch.float64) + x) / F0) / 86400.0).cpu().numpy()
+    offh = off.cpu().numpy()
+    starts, ends = mjd[offh[:-1]] - 1e-9, mjd[offh[1:] - 1] + 1e-9
+    par = {"PEPOCH": pep, "F0": F0}
+    tm = _tmpl()
+    a = measure_intervals(mjd, par, tm, starts, ends, E, brutemin=True)
+    b = measure_intervals(torch.from_numpy(mjd).pin_memory(), par, tm, starts, ends, E, brutemin=True)
+    ends2 = ends.copy()
+    ends2[2] = mjd[offh[3] - 11] + 1e-9  # interval 2 loses its last 10 photons: they sit between intervals 2 and 3
+    c = measure_intervals(mjd, par, tm, starts, ends2, E, brutemin=True)
+    keep = np.array([0, 1, 3, 4, 5])
+    for k in a:
+        va, vb, vc = (np.asarray(r[k]) for r in (a, b, c))
+        np.testing.assert_array_equal(va, vb, err_msg=k)
+        np.testing.assert_array_equal(va[keep], vc[keep], err_msg=k)
+    assert not np.array_equal(np.asarray(a["phShi"])[2], np.asarray(c["phShi"])[2])
 
 
 def test_measuretoas_rows_before_empty_interval(gpu, tmp_path, monkeypatch):
