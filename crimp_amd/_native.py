@@ -58,7 +58,7 @@ class Template(ctypes.Structure):
 EXPORTS = ("crimp_version", "crimp_last_error", "crimp_last_kernel_ms", "crimp_last_kernel_times", "crimp_last_fixups",
            "crimp_last_toa_grid_norms", "crimp_last_toa_grid_fast", "crimp_release_scratch",
            "crimp_device_count", "crimp_calcphase", "crimp_search", "crimp_search_sets", "crimp_toa_points",
-           "crimp_toa_grid", "crimp_toa_fit", "crimp_toa_redchi2", "crimp_toa_shape_points", "crimp_binphases")
+           "crimp_toa_grid", "crimp_toa_fit", "crimp_toa_redchi2", "crimp_toa_fit_redchi2", "crimp_toa_shape_points", "crimp_binphases")
 
 _lib = None
 _lock = threading.Lock()
@@ -95,6 +95,8 @@ def load(require_device=True):
             L.crimp_toa_shape_points.argtypes = [P, P, i64, ctypes.POINTER(Template), P, P, P, P, i64, P, u32, P]
             L.crimp_binphases.argtypes = [P, P, i64, P, i32, P, u32, P]
             L.crimp_toa_redchi2.argtypes = [P, P, i64, ctypes.POINTER(Template), P, P, P, P, i32, i32, P, u32, P]
+            L.crimp_toa_fit_redchi2.argtypes = [P, P, i64, ctypes.POINTER(Template), P, ctypes.c_double, i32, i32, P, P,
+                                                i32, i32, P, P, u32, P]
             for name in EXPORTS:
                 if name not in ("crimp_last_error", "crimp_last_kernel_ms", "crimp_last_fixups",
                                 "crimp_last_toa_grid_norms", "crimp_last_toa_grid_fast"):

@@ -2317,9 +2317,28 @@ static int toa_grid_partials(Scratch& sc, hipStream_t s, const double* dx, const
     return CRIMP_OK;
 }
 
-extern "C" int crimp_toa_fit(const double* x, const int64_t* offsets, int64_t nint, const crimp_template* tpl,
-                             const double* exposure, double norm0, int32_t ph_shift_res, int32_t options, double* out,
-                             uint32_t flags, void* stream) {
+// crimp_toa_fit_redchi2's binned part: np.histogram edges and bin centres (binphases), free parameters, output
+struct RedChi2Req {
+    const double *edges, *centers;
+    int32_t nbins, nfree;
+    double* out;
+};
+
+struct EventGuard {  // an event destroyed on every return path (destruction waits for nothing)
+    hipEvent_t e = nullptr;
+    ~EventGuard() {
+        if (e) (void)hipEventDestroy(e);
+    }
+};
+
+__global__ __launch_bounds__(64) void k_toa_chi2(const unsigned long long* __restrict__ counts, const TplDev T,
+                                                 const double* __restrict__ expo, const double* __restrict__ rec,
+                                                 const double* __restrict__ centers, int nb, int nfree,
+                                                 double* __restrict__ out);
+
+static int toa_fit_impl(const double* x, const int64_t* offsets, int64_t nint, const crimp_template* tpl,
+                        const double* exposure, double norm0, int32_t ph_shift_res, int32_t options, double* out,
+                        uint32_t flags, void* stream, const RedChi2Req* rq) {
     ARGCHK(nint >= 1, "bad sizes");
     ARGCHK(ph_shift_res >= 1, "phShiftRes must be >= 1");
     ARGCHK(norm0 > 0.0, "template norm must be positive");
@@ -2371,6 +2390,33 @@ extern "C" int crimp_toa_fit(const double* x, const int64_t* offsets, int64_t ni
         HIPCHK(stage_in(sc, offsets, (size_t)nint + 1, dev, &doff));
         HIPCHK(stage_in(sc, exposure, (size_t)nint, dev, &de));
         HIPCHK(stage_out(sc, out, (size_t)nint * 8, dev, &dout));
+        // redChi2's histogram (crimp_toa_fit_redchi2) needs only the photons: it runs on the auxiliary stream beside
+        // the brute grid and the fits, in the partly empty last round of the fit's workgroups (timed calls: after the
+        // fits on this stream, so that the kernel times stay those of the grid and the fit alone)
+        const double *dedg = nullptr, *dcen = nullptr;
+        double* dred = nullptr;
+        unsigned long long* dcnt = nullptr;
+        EventGuard ebin;
+        if (rq) {
+            HIPCHK(stage_in(sc, rq->edges, (size_t)rq->nbins + 1, dev, &dedg));
+            HIPCHK(stage_in(sc, rq->centers, (size_t)rq->nbins, dev, &dcen));
+            HIPCHK(stage_out(sc, rq->out, (size_t)nint, dev, &dred));
+            HIPCHK(sc.alloc(&dcnt, (size_t)(nint * rq->nbins)));
+            HIPCHK(hipMemsetAsync(dcnt, 0, (size_t)(nint * rq->nbins) * sizeof(unsigned long long), s));
+            if (!(flags & CRIMP_FLAG_TIME_KERNELS)) {
+                hipStream_t s1 = aux_stream();
+                if (!s1) return set_err(CRIMP_ERR_HIP, "cannot create the auxiliary stream");
+                EventGuard e0;
+                HIPCHK(hipEventCreateWithFlags(&e0.e, hipEventDisableTiming));
+                HIPCHK(hipEventRecord(e0.e, s));
+                HIPCHK(hipStreamWaitEvent(s1, e0.e, 0));
+                k_binphases<<<dim3((unsigned)nint, (unsigned)bin_splits(hoff[nint], nint)), 64 * kBinWaves, 0, s1>>>(
+                    dx, doff, dedg, rq->nbins, dcnt);
+                HIPCHK(hipGetLastError());
+                HIPCHK(hipEventCreateWithFlags(&ebin.e, hipEventDisableTiming));
+                HIPCHK(hipEventRecord(ebin.e, s1));
+            }
+        }
         TplDev* dT = nullptr;
         double* dstart = nullptr;
         HIPCHK(sc.alloc(&dT, 1));
@@ -2613,10 +2659,37 @@ extern "C" int crimp_toa_fit(const double* x, const int64_t* offsets, int64_t ni
                 if (rc) return rc;
             }
         }
+        if (rq) {  // redChi2 from the final records
+            if (ebin.e) {
+                HIPCHK(hipStreamWaitEvent(s, ebin.e, 0));
+            } else {
+                k_binphases<<<dim3((unsigned)nint, (unsigned)bin_splits(hoff[nint], nint)), 64 * kBinWaves, 0, s>>>(
+                    dx, doff, dedg, rq->nbins, dcnt);
+            }
+            k_toa_chi2<<<(unsigned)nint, 64, 0, s>>>(dcnt, T, de, dout, dcen, rq->nbins, rq->nfree, dred);
+            HIPCHK(hipGetLastError());
+            HIPCHK(copy_back(s, rq->out, dred, (size_t)nint, dev));
+        }
         HIPCHK(copy_back(s, out, dout, (size_t)nint * 8, dev));
         HIPCHK(hipStreamSynchronize(s));
     }
     return finish(s, flags);
+}
+
+extern "C" int crimp_toa_fit(const double* x, const int64_t* offsets, int64_t nint, const crimp_template* tpl,
+                             const double* exposure, double norm0, int32_t ph_shift_res, int32_t options, double* out,
+                             uint32_t flags, void* stream) {
+    return toa_fit_impl(x, offsets, nint, tpl, exposure, norm0, ph_shift_res, options, out, flags, stream, nullptr);
+}
+
+extern "C" int crimp_toa_fit_redchi2(const double* x, const int64_t* offsets, int64_t nint, const crimp_template* tpl,
+                                     const double* exposure, double norm0, int32_t ph_shift_res, int32_t options,
+                                     const double* edges, const double* centers, int32_t nbins, int32_t nfree,
+                                     double* out, double* redchi2, uint32_t flags, void* stream) {
+    ARGCHK(nbins >= 1 && nbins <= 256, "bad sizes (nbins must be 1..256)");
+    ARGCHK(edges != nullptr && centers != nullptr && redchi2 != nullptr, "null argument");
+    const RedChi2Req rq{edges, centers, nbins, nfree, redchi2};
+    return toa_fit_impl(x, offsets, nint, tpl, exposure, norm0, ph_shift_res, options, out, flags, stream, &rq);
 }
 
 extern "C" int crimp_toa_grid(const double* x, const int64_t* offsets, int64_t nint, const crimp_template* tpl,

@@ -181,6 +181,11 @@ def measure_intervals(TIMEMJD, timMod, tempModPP, starts, ends, exposures, phShi
     tm = timMod if isinstance(timMod, dict) else ReadTimingModel(str(timMod)).readfulltimingmodel()[0]
     starts = np.asarray(starts, dtype=np.float64)
     ends = np.asarray(ends, dtype=np.float64)
+    if not readvaryparam:
+        res = _measure_pipelined(TIMEMJD, tm, tmpl, model, starts, ends, exposures, phShiftRes, nbrBins, varyAmps,
+                                 brutemin)
+        if res is not None:
+            return res
     T = _device_times(TIMEMJD)
     if T is not None and (T.numel() < 2 or bool((T[1:] >= T[:-1]).all())):
         lo = torch.searchsorted(T, torch.as_tensor(starts, device=T.device), right=False)
@@ -226,6 +231,132 @@ def measure_intervals(TIMEMJD, timMod, tempModPP, starts, ends, exposures, phShi
     res["ToA_mid"] = mids
     res["htestPow"] = np.asarray(hp)
     return res
+
+
+def _fit_block(allt, offs, mids, tm, tmpl, model, E, phShiftRes, nbrBins, varyAmps, brutemin):
+    """Fold, fit and H-test one block of intervals whose photons (device tensor ``allt``, seconds MJD) are concatenated
+    at ``offs`` (measureToAs.py:186-226 for every interval of the block)."""
+    import torch
+    _, folded = calcphase(allt, tm)
+    if model in ("cauchy", "vonmises"):
+        folded = folded * (2 * np.pi)                  # :195, :200
+    res = ToAFitter(folded, offs, E, tmpl, phShiftRes, nbrBins).fit(brutemin=brutemin, vary_amps=bool(varyAmps))
+    freqs = np.atleast_1d(ephemTmjd(mids, tm)["freqAtTmjd"])          # :210
+    hp = ops.search_sets(allt * 86400, torch.as_tensor(offs, device=allt.device),
+                         torch.as_tensor(freqs, dtype=torch.float64, device=allt.device), 5, STAT_H).cpu().numpy()
+    res["ToA_mid"] = mids
+    res["htestPow"] = np.asarray(hp)
+    return res
+
+
+def _measure_pipelined(TIMEMJD, tm, tmpl, model, starts, ends, exposures, phShiftRes, nbrBins, varyAmps, brutemin):
+    """measure_intervals for host photon times of at least CRIMP_E2E_MIN_PHOTONS (default 2^24): the intervals are cut
+    into CRIMP_E2E_BLOCKS (default 4) consecutive blocks of shrinking size (_shrinking_blocks); a second host thread
+    uploads block k + 1
+    on its own stream (a pageable copy blocks only that thread; torch releases the GIL) while this thread folds, fits
+    and H-tests block k on the device, so the PCIe upload hides the device work. Interval selection is the host's
+    binary search on the times (measureToAs.py:173-174 for sorted times); every block is checked on the device to be
+    sorted (and to continue the previous one), and the whole call is redone by the one-shot path below when one is
+    not, or when an interval is empty (its IndexError). Every interval's fit and H test are independent of its block
+    (the brute grid's kernel choice is per call: records within the fast-vs-full grid tolerance of the one-shot
+    path's, test_measure_intervals_blocks_equal_one_shot). Returns None where it does not apply."""
+    import os
+    import queue
+    import threading
+    import torch
+    from ._native import _is_torch
+    if not torch.cuda.is_available() or (_is_torch(TIMEMJD) and TIMEMJD.is_cuda):
+        return None
+    src = TIMEMJD.reshape(-1).to(torch.float64).contiguous() if _is_torch(TIMEMJD) else \
+        torch.from_numpy(np.ascontiguousarray(TIMEMJD, dtype=np.float64).reshape(-1))
+    if src.numel() < int(os.environ.get("CRIMP_E2E_MIN_PHOTONS", 1 << 24)) or starts.size < 2:
+        return None
+    t = src.numpy()
+    lo = np.searchsorted(t, starts, side="left")
+    hi = np.maximum(np.searchsorted(t, ends, side="right"), lo)
+    n = hi - lo
+    if np.any(n <= 0):
+        return None
+    blocks = _shrinking_blocks(n, int(os.environ.get("CRIMP_E2E_BLOCKS", 4)))
+    if len(blocks) < 2:
+        return None
+    E = np.asarray(exposures, dtype=np.float64)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    up = torch.cuda.Stream(device=dev)
+    pinned = src.is_pinned()
+    q = queue.Queue(maxsize=2)
+
+    def uploader():
+        try:
+            for b0, b1 in blocks:
+                a, b = int(lo[b0]), int(np.max(hi[b0:b1]))
+                with torch.cuda.stream(up):
+                    d = src[a:b].to(dev, non_blocking=pinned)
+                    ev = torch.cuda.Event()
+                    ev.record(up)
+                q.put((d, ev, a))
+        except BaseException as e:  # handed to the main thread
+            q.put(e)
+
+    th = threading.Thread(target=uploader, daemon=True)
+    # this thread holds the GIL between its device calls; a short switch interval lets the uploader start its next
+    # copy within ~0.1 ms instead of up to 5 ms (restored below)
+    switch = sys.getswitchinterval()
+    sys.setswitchinterval(1e-4)
+    th.start()
+    cur = torch.cuda.current_stream(dev)
+    ok = torch.ones((), dtype=torch.bool, device=dev)
+    prev_last = None
+    parts = []
+    try:
+        for b0, b1 in blocks:
+            item = q.get()
+            if isinstance(item, BaseException):
+                raise item
+            d, ev, a = item
+            cur.wait_event(ev)
+            d.record_stream(cur)
+            if d.numel() > 1:
+                ok &= (d[1:] >= d[:-1]).all()
+            if prev_last is not None:
+                ok &= d[0] >= prev_last
+            prev_last = d[-1]
+            nb = n[b0:b1]
+            offs = np.concatenate([[0], np.cumsum(nb)]).astype(np.int64)
+            rel_lo = lo[b0:b1] - a
+            if np.all(rel_lo[1:] == rel_lo[:-1] + nb[:-1]):   # consecutive intervals: one slice, no copy
+                allt = d[int(rel_lo[0]):int(rel_lo[0]) + int(offs[-1])]
+            else:
+                seg = torch.repeat_interleave(torch.arange(nb.size, device=dev), torch.as_tensor(nb, device=dev))
+                rel = torch.arange(int(offs[-1]), device=dev, dtype=torch.int64)
+                offs_d = torch.as_tensor(offs, device=dev)
+                allt = d[torch.as_tensor(rel_lo, device=dev)[seg] + (rel - offs_d[seg])]
+            first = t[lo[b0:b1]]
+            last = t[lo[b0:b1] + nb - 1]
+            mids = ((last - first) / 2) + first                 # measureToAs.py:182
+            parts.append(_fit_block(allt, offs, mids, tm, tmpl, model, E[b0:b1], phShiftRes, nbrBins, varyAmps,
+                                    brutemin))
+    finally:  # on an error here, keep taking the uploader's blocks until it has finished
+        while th.is_alive():
+            try:
+                q.get(timeout=0.05)
+            except queue.Empty:
+                pass
+        th.join()
+        sys.setswitchinterval(switch)
+    if not bool(ok):
+        return None
+    return {k: np.concatenate([np.atleast_1d(np.asarray(p[k])) for p in parts]) for k in parts[0]}
+
+
+def _shrinking_blocks(counts, nblocks):
+    """Consecutive runs of intervals for the pipelined upload: photon shares nblocks, nblocks - 1, ..., 1 (out of
+    their sum), so that the last block -- whose device work follows the whole upload -- is the smallest."""
+    w = np.arange(nblocks, 0, -1, dtype=np.float64)
+    cuts = np.cumsum(w)[:-1] / w.sum() * float(np.sum(counts))
+    at = np.searchsorted(np.cumsum(counts), cuts, side="left") + 1
+    edges = np.unique(np.concatenate([[0], np.clip(at, 1, len(counts) - 1), [len(counts)]]))
+    return [(int(a), int(b)) for a, b in zip(edges[:-1], edges[1:])]
 
 
 def _interval_counts(T, starts, ends):

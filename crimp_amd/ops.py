@@ -248,6 +248,29 @@ def toa_fit(x, offsets, tpl, exposure, norm0, ph_shift_res=1000, brutemin=False,
     return out.reshape(nint, 8)
 
 
+def toa_fit_redchi2(x, offsets, tpl, exposure, norm0, ph_shift_res, brutemin, vary_amps, edges, centers, nfree,
+                    flags=0):
+    """toa_fit and toa_redchi2 in one call (crimp_toa_fit_redchi2): ([nint, 8] records, [nint] redChi2)."""
+    options = (TOA_BRUTE if brutemin else 0) | (TOA_VARY_AMPS if vary_amps else 0)
+    L = N.load()
+    b = N.Buffers()
+    xp = b.arg(x, np.float64)
+    op = b.arg(offsets, np.int64)
+    ep = b.arg(exposure, np.float64)
+    eg = b.arg(edges, np.float64)
+    cg = b.arg(centers, np.float64)
+    nint = int((offsets.numel() if N._is_torch(offsets) else np.size(offsets)) - 1)
+    nb = int((centers.numel() if N._is_torch(centers) else np.size(centers)))
+    out = _empty_like_input(x, nint * 8, b)
+    red = _empty_like_input(x, nint, b)
+    outp = b.arg(out, np.float64, writable=True)
+    redp = b.arg(red, np.float64, writable=True)
+    with b.device_guard():
+        N.check(L.crimp_toa_fit_redchi2(xp, op, nint, ctypes.byref(tpl), ep, float(norm0), int(ph_shift_res), options,
+                                        eg, cg, nb, int(nfree), outp, redp, b.flags(flags), b.stream()))
+    return out.reshape(nint, 8), red
+
+
 def toa_redchi2(x, offsets, tpl, exposure, records, edges, centers, nfree):
     """redChi2 of every interval from its fit record (crimp_toa_redchi2: histogram + template curve + chi2 on the
     device, measureToAs.py:385-393); ``records`` [nint, 8] as toa_fit returns them."""

@@ -391,12 +391,14 @@ class ToAFitter:
 
     # ------------------------------------------------------------------ drivers
     def fit(self, brutemin=False, vary_amps=False):
-        """Every interval's fit in one device call (crimp_toa_fit: one workgroup per interval runs steps 1-3),
-        then the redChi2 of step 4. ``vary_amps``: ampShift free (Fourier [0.01, 100], Cauchy [0, inf), von Mises [0, 500]) after the (norm, phShift) fit,
+        """Every interval's fit and redChi2 in one device call (crimp_toa_fit_redchi2: one workgroup per interval runs
+        steps 1-3, the histogram of step 4 beside them). ``vary_amps``: ampShift free (Fourier [0.01, 100], Cauchy [0, inf), von Mises [0, 500]) after the (norm, phShift) fit,
         re-profiled with the norm in the 1-sigma scan, one more free parameter in redChi2 (:305-312)."""
-        rd = ops.toa_fit(self.x, self.offsets, self.tpl, self._arr(self.E, np.float64), self.norm0, self.res, brutemin,
-                         vary_amps)
-        rchi2 = self.reduced_chi2(None, None, nfree=3 if vary_amps else 2, records=rd)
+        edges, pp = self._bins()
+        rd, rc = ops.toa_fit_redchi2(self.x, self.offsets, self.tpl, self._arr(self.E, np.float64), self.norm0,
+                                     self.res, brutemin, vary_amps, self._arr(edges, np.float64),
+                                     self._arr(pp, np.float64), 3 if vary_amps else 2)
+        rchi2 = rc.cpu().numpy() if _is_torch(rc) else np.asarray(rc)
         r = np.asarray(rd.cpu().numpy() if _is_torch(rd) else rd)
         n_hat, phi_hat, amp = r[:, 0].copy(), r[:, 1].copy(), r[:, 6].copy()
         return {"phShi": phi_hat, "phShi_LL": r[:, 3].copy(), "phShi_UL": r[:, 4].copy(), "reducedChi2": rchi2,

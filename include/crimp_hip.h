@@ -167,7 +167,7 @@ int crimp_toa_grid(const double* x, const int64_t* offsets, int64_t nint, const 
  * 2pi/res with the other free parameters re-profiled at each step. One workgroup per interval runs the
  * whole fit on the device (csrc/toa_fit.h).
  * out[i*8 + 0..6] = { norm, phShift, LLmax, phShift_LL, phShift_UL, likelihood evaluations, ampShift }.
- * The reduced chi2 (:385-393) is crimp_toa_redchi2 on these records. */
+ * The reduced chi2 (:385-393) is crimp_toa_redchi2 on these records (or crimp_toa_fit_redchi2: both at once). */
 int crimp_toa_fit(const double* x, const int64_t* offsets, int64_t nint, const crimp_template* tpl,
                   const double* exposure, double norm0, int32_t ph_shift_res, int32_t options, double* out,
                   uint32_t flags, void* stream);
@@ -193,6 +193,14 @@ int crimp_toa_shape_points(const double* x, const int64_t* offsets, int64_t nint
 int crimp_toa_redchi2(const double* x, const int64_t* offsets, int64_t nint, const crimp_template* tpl,
                       const double* exposure, const double* records, const double* edges, const double* centers,
                       int32_t nbins, int32_t nfree, double* out, uint32_t flags, void* stream);
+
+/* crimp_toa_fit and crimp_toa_redchi2 in one call (the whole measureToA_* of every interval, :254-393): the same
+ * records in out[i*8 + 0..6] and the same redchi2[i]. The histogram needs only the photons, so it runs on a second
+ * stream beside the brute grid and the fits (with CRIMP_FLAG_TIME_KERNELS: after them). */
+int crimp_toa_fit_redchi2(const double* x, const int64_t* offsets, int64_t nint, const crimp_template* tpl,
+                          const double* exposure, double norm0, int32_t ph_shift_res, int32_t options,
+                          const double* edges, const double* centers, int32_t nbins, int32_t nfree, double* out,
+                          double* redchi2, uint32_t flags, void* stream);
 
 /* binphases(phases, nbrBins) counts per interval   [binphases.py:9-39]:
  * np.histogram(x, bins=edges) semantics with edges[nbins+1] (numpy.linspace). counts[i*nbins+b]. */

@@ -278,6 +278,20 @@ def test_toa_batches_and_interval_counts():
     assert want[1] == 11 and want[3] == 0
 
 
+def test_shrinking_pipeline_blocks():
+    """measure_intervals' pipelined blocks: consecutive, covering every interval once, none empty, photon shares
+    non-increasing (4 : 3 : 2 : 1 of the total where the interval sizes allow)."""
+    from crimp_amd.measureToAs import _shrinking_blocks
+    assert _shrinking_blocks(np.full(1250, 100000), 4) == [(0, 500), (500, 875), (875, 1125), (1125, 1250)]
+    assert _shrinking_blocks(np.full(2, 7), 4) == [(0, 1), (1, 2)]
+    rng = np.random.default_rng(5)
+    for _ in range(50):
+        c = rng.integers(1, 1000, rng.integers(2, 40))
+        b = _shrinking_blocks(c, int(rng.integers(2, 6)))
+        assert b[0][0] == 0 and b[-1][1] == c.size and all(x[1] == y[0] for x, y in zip(b, b[1:]))
+        assert all(x[1] > x[0] for x in b)
+
+
 def test_measuretoas_empty_first_interval_writes_header_then_raises(tmp_path):
     """An empty first interval: the reference has written only the header when TIME_toa[-1] raises at
     measureToAs.py:182; so does the drop-in (no device call is made before it)."""

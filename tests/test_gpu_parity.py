@@ -337,6 +337,46 @@ def test_toa_fits_match_reference_and_oracle(gpu):
         assert r["reducedChi2"][i] == pytest.approx(o["reducedChi2"], rel=1e-6)
 
 
+@pytest.mark.parametrize("model", ["fourier", "cauchy"])
+def test_toa_fit_redchi2_fused_equals_separate(gpu, model):
+    """crimp_toa_fit_redchi2 (histogram on a second stream beside the grid and the fits; timed: after them) returns
+    exactly crimp_toa_fit's records and crimp_toa_redchi2's values, host and device buffers, with and without the
+    brute start and varyAmps."""
+    import torch
+    from crimp_amd import ops, _native as N
+    from crimp_amd.toafit import ToAFitter
+    from crimp_amd.readPPtemplate import readPPtemplate
+    g, iv, _ = _golden_rows()
+    if model == "fourier":
+        tm, x, off = readPPtemplate(gpath("1e2259_template.txt")), g["folded"], g["offsets"]
+        E = iv["ToA_exposure"].to_numpy()[g["ids"]]
+    else:  # the Cauchy template and phases of the LL goldens, split into two intervals
+        tc = json.load(open(gpath("cauchy_vm_theta.json")))
+        tm = {"model": "cauchy", "norm": {"value": 5.0, "vary": True}}
+        for j in (1, 2):
+            for nm in ("amp", "cen", "wid"):
+                tm["%s_%d" % (nm, j)] = {"value": tc["%s_%d" % (nm, j)], "vary": True}
+        x = gold("templatemodels.npz")["x"]
+        off = np.array([0, x.size // 2, x.size], dtype=np.int64)
+        E = np.array([125.0, 125.0])
+    for dev in (False, True):
+        xs = torch.tensor(x, device=gpu) if dev else x
+        os_ = torch.tensor(off, device=gpu) if dev else off
+        f = ToAFitter(xs, os_, E, tm)
+        edges, pp = f._bins()
+        for brute, va in ((True, False), (False, False), (True, True)):
+            for flags in (0, N.FLAG_TIME_KERNELS):
+                rec, red = ops.toa_fit_redchi2(f.x, f.offsets, f.tpl, f._arr(f.E, np.float64), f.norm0, f.res, brute,
+                                               va, f._arr(edges, np.float64), f._arr(pp, np.float64), 3 if va else 2,
+                                               flags=flags)
+                rec2 = ops.toa_fit(f.x, f.offsets, f.tpl, f._arr(f.E, np.float64), f.norm0, f.res, brute, va)
+                red2 = ops.toa_redchi2(f.x, f.offsets, f.tpl, f._arr(f.E, np.float64), rec2,
+                                       f._arr(edges, np.float64), f._arr(pp, np.float64), 3 if va else 2)
+                h = [np.asarray(v.cpu().numpy() if hasattr(v, "cpu") else v) for v in (rec, red, rec2, red2)]
+                np.testing.assert_array_equal(h[0], h[2])
+                np.testing.assert_array_equal(h[1], h[3])
+
+
 def test_device_toa_driver_equals_host_driver(gpu):
     """crimp_toa_fit (one workgroup per interval runs the whole fit) against the host-driven iterations."""
     from crimp_amd.toafit import ToAFitter
@@ -494,6 +534,44 @@ def test_measure_intervals_slice_gather_and_pinned_source(gpu):
         np.testing.assert_array_equal(va, vb, err_msg=k)
         np.testing.assert_array_equal(va[keep], vc[keep], err_msg=k)
     assert not np.array_equal(np.asarray(a["phShi"])[2], np.asarray(c["phShi"])[2])
+
+
+def test_measure_intervals_blocks_equal_one_shot(gpu, monkeypatch):
+    """The pipelined measure_intervals (host times cut into shrinking blocks, block k + 1 uploaded by a second thread
+    while block k is fitted) against the one-shot call: consecutive intervals, a gap
+    (gather inside a block), a page-locked source, and unsorted times (detected on the device: the call falls back
+    to the one-shot path's host mask). The brute grid's kernel choice is per call, so phShift is held to the
+    fast-vs-full grid tolerance (1e-9 rad) and everything else to equality."""
+    import torch
+    from bench import T2259, _tmpl
+    from crimp_amd.measureToAs import measure_intervals
+    from crimp_amd.synth import template_intervals_torch
+    x, off, E, _ = template_intervals_torch(6, 20000, T2259["norm"]["value"], T2259["amp"], T2259["ph"], seed=5,
+                                            device=gpu)
+    F0, pep = 0.5, 58000.0
+    mjd = (pep + ((torch.arange(x.numel(), device=gpu, dtype=torch.float64) + x) / F0) / 86400.0).cpu().numpy()
+    offh = off.cpu().numpy()
+    starts, ends = mjd[offh[:-1]] - 1e-9, mjd[offh[1:] - 1] + 1e-9
+    ends_gap = ends.copy()
+    ends_gap[2] = mjd[offh[3] - 11] + 1e-9
+    par = {"PEPOCH": pep, "F0": F0}
+    tm = _tmpl()
+
+    def same(a, b):
+        for k in a:
+            va, vb = np.asarray(a[k]), np.asarray(b[k])
+            if k == "phShi":
+                np.testing.assert_allclose(va, vb, rtol=0, atol=1e-9)
+            else:
+                np.testing.assert_array_equal(va, vb, err_msg=k)
+
+    unsorted = mjd.copy()
+    unsorted[offh[4] + 5], unsorted[offh[4] + 6] = mjd[offh[4] + 6], mjd[offh[4] + 5]
+    for src, en in ((mjd, ends), (mjd, ends_gap), (torch.from_numpy(mjd).pin_memory(), ends), (unsorted, ends)):
+        monkeypatch.setenv("CRIMP_E2E_MIN_PHOTONS", str(1 << 40))
+        one = measure_intervals(src, par, tm, starts, en, E, brutemin=True)
+        monkeypatch.setenv("CRIMP_E2E_MIN_PHOTONS", "1000")  # blocks of 3, 2 and 1 intervals
+        same(one, measure_intervals(src, par, tm, starts, en, E, brutemin=True))
 
 
 def test_measuretoas_rows_before_empty_interval(gpu, tmp_path, monkeypatch):

@@ -82,7 +82,14 @@ for k, v in acc.items():
     print("%-13s %8.3f ms (min %.3f)" % (k, np.mean(v), np.min(v)), flush=True)
 print("%-13s %8.3f ms" % ("sum", tot), flush=True)
 pin = torch.from_numpy(mjd).pin_memory()
-for name, src in (("numpy", mjd), ("pinned", pin)):
+runs = [("numpy", mjd, b) for b in os.environ.get("BLOCKS", "1,2,3,4,6,8").split(",")] + [("pinned", pin, "4")]
+for name, src, nbk in runs:
+    if nbk == "1":
+        os.environ["CRIMP_E2E_MIN_PHOTONS"] = str(1 << 62)  # one shot
+    else:
+        os.environ.pop("CRIMP_E2E_MIN_PHOTONS", None)
+        os.environ["CRIMP_E2E_BLOCKS"] = nbk
+    name = "%s/%s blocks" % (name, nbk)
     measure_intervals(src, par, tm, starts, ends, E, brutemin=True)
     ts = []
     for _ in range(reps):
@@ -91,5 +98,5 @@ for name, src in (("numpy", mjd), ("pinned", pin)):
         measure_intervals(src, par, tm, starts, ends, E, brutemin=True)
         torch.cuda.synchronize()
         ts.append(time.perf_counter() - t0)
-    print("measure_intervals from %-6s %8.3f ms (min %.3f), %.4g fits/s" % (name, np.mean(ts) * 1e3, np.min(ts) * 1e3,
+    print("measure_intervals from %-16s %8.3f ms (min %.3f), %.4g fits/s" % (name, np.mean(ts) * 1e3, np.min(ts) * 1e3,
                                                                           nint / np.mean(ts)), flush=True)
