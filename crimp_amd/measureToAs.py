@@ -249,6 +249,9 @@ def _fit_block(allt, offs, mids, tm, tmpl, model, E, phShiftRes, nbrBins, varyAm
     return res
 
 
+_UPLOAD_STREAMS = {}
+
+
 def _measure_pipelined(TIMEMJD, tm, tmpl, model, starts, ends, exposures, phShiftRes, nbrBins, varyAmps, brutemin):
     """measure_intervals for host photon times of at least CRIMP_E2E_MIN_PHOTONS (default 2^24): the intervals are cut
     into CRIMP_E2E_BLOCKS (default 4) consecutive blocks of shrinking size (_shrinking_blocks); a second host thread
@@ -282,7 +285,9 @@ def _measure_pipelined(TIMEMJD, tm, tmpl, model, starts, ends, exposures, phShif
         return None
     E = np.asarray(exposures, dtype=np.float64)
     dev = torch.device("cuda", torch.cuda.current_device())
-    up = torch.cuda.Stream(device=dev)
+    up = _UPLOAD_STREAMS.get(dev.index)
+    if up is None:  # one per device for the process: the caching allocator pools blocks per stream
+        up = _UPLOAD_STREAMS[dev.index] = torch.cuda.Stream(device=dev)
     pinned = src.is_pinned()
     q = queue.Queue(maxsize=2)
 
