@@ -1052,6 +1052,13 @@ __global__ __launch_bounds__(kGridBlock) __attribute__((amdgpu_waves_per_eu(4)))
 #ifndef CRIMP_GM_PAD
 #define CRIMP_GM_PAD 1
 #endif
+// CRIMP_GM_CIN: with one evaluated norm on the eight-factor kernel, the MFMA accumulators start at s norm instead of 0,
+// so the matrix cores return the factors s (norm + h) themselves (no add per point; the min h is then
+// min(s (norm + h)) - s norm, exact in fp64). The factor is the MFMA's fp32 sum with the norm inside instead of
+// fl(norm + fl(h)): rounding-level changes of the lattice LL, held to the full kernel's brute argmax by the tests.
+#ifndef CRIMP_GM_CIN
+#define CRIMP_GM_CIN 1
+#endif
 constexpr int kGmTile = CRIMP_GM_TILE, kGmPad = CRIMP_GM_PAD;
 static_assert(kGmTile == 128 || kGmTile == 256, "k_toa_grid_mf: one or two of the block's 256 threads per photon");
 static_assert(kGridBlock == 32 * 4, "k_toa_grid_mf: 4 waves of 32 phShift columns cover a block's kGridBlock columns");
@@ -1094,6 +1101,7 @@ __global__ __launch_bounds__(256) void k_toa_grid_mf(const double* __restrict__ 
     // PROD 4: the norms in pairs (f32x2 over two norms); PROD 8: one norm at a time over photon pairs (f32x2 over two
     // photons), so that an odd number of norms (a single one after k_toa_grid_best's lazy norms) costs no dead lane
     constexpr int NP = NN > 1 ? NN / 2 : 1;
+    constexpr bool CIN = CRIMP_GM_CIN && PROD == 8 && NN == 1;
     f32x2 nr[NP];
     float nrs[NN];
 #pragma unroll
@@ -1138,6 +1146,10 @@ __global__ __launch_bounds__(256) void k_toa_grid_mf(const double* __restrict__ 
         __syncthreads();
         for (int q0 = 0; q0 < cnt; q0 += 32) {
             f32x16 hv = {};
+            if constexpr (CIN) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) hv[r] = nrs[0];
+            }
 #pragma unroll
             for (int m = 0; m < NM; ++m) {
                 const f16x8 av = __builtin_bit_cast(f16x8, afr[q0 + (lane & 31)][2 * m + hk]);
@@ -1159,7 +1171,10 @@ __global__ __launch_bounds__(256) void k_toa_grid_mf(const double* __restrict__ 
                         const f32x2 n2 = f32x2{nrs[b], nrs[b]};
                         f32x2 f[8];
 #pragma unroll
-                        for (int k = 0; k < 8; ++k) f[k] = f32x2{hv[2 * k], hv[2 * k + 1]} + n2;
+                        for (int k = 0; k < 8; ++k) {
+                            f[k] = f32x2{hv[2 * k], hv[2 * k + 1]};
+                            if constexpr (!CIN) f[k] += n2;
+                        }
                         f[0] *= f[1];
                         f[2] *= f[3];
                         f[4] *= f[5];
@@ -1182,7 +1197,7 @@ __global__ __launch_bounds__(256) void k_toa_grid_mf(const double* __restrict__ 
                                 const float h = hv[4 * gi + r];
                                 if constexpr (HMIN) hmn = fminf(hmn, h);
 #pragma unroll
-                                for (int b = 0; b < NN; ++b) pr[b] *= nrs[b] + h;
+                                for (int b = 0; b < NN; ++b) pr[b] *= CIN ? h : nrs[b] + h;
                             }
                         }
 #pragma unroll
@@ -1253,7 +1268,8 @@ __global__ __launch_bounds__(256) void k_toa_grid_mf(const double* __restrict__ 
         for (int a = 0; a < NN; ++a)
             if (a < na) lnsum[((split * nint + iv) * nnorm + a0 + a) * nphi + bphi] = acc[a];
         // the first evaluated norm block writes the min (a_first: past toa_grid_partials' lazy norms)
-        if (HMIN && a0 == a_first) hmin[(split * nint + iv) * nphi + bphi] = ldexp((double)hmn, -se);
+        if (HMIN && a0 == a_first)
+            hmin[(split * nint + iv) * nphi + bphi] = ldexp(CIN ? (double)hmn - (double)nrs[0] : (double)hmn, -se);
     }
 }
 

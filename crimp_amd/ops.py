@@ -249,8 +249,9 @@ def toa_fit(x, offsets, tpl, exposure, norm0, ph_shift_res=1000, brutemin=False,
 
 
 def toa_fit_redchi2(x, offsets, tpl, exposure, norm0, ph_shift_res, brutemin, vary_amps, edges, centers, nfree,
-                    flags=0):
-    """toa_fit and toa_redchi2 in one call (crimp_toa_fit_redchi2): ([nint, 8] records, [nint] redChi2)."""
+                    flags=0, packed=False):
+    """toa_fit and toa_redchi2 in one call (crimp_toa_fit_redchi2): ([nint, 8] records, [nint] redChi2), views of
+    one buffer; ``packed``: that buffer itself ([9 nint]: the records, then redChi2), for a single readback."""
     options = (TOA_BRUTE if brutemin else 0) | (TOA_VARY_AMPS if vary_amps else 0)
     L = N.load()
     b = N.Buffers()
@@ -261,14 +262,14 @@ def toa_fit_redchi2(x, offsets, tpl, exposure, norm0, ph_shift_res, brutemin, va
     cg = b.arg(centers, np.float64)
     nint = int((offsets.numel() if N._is_torch(offsets) else np.size(offsets)) - 1)
     nb = int((centers.numel() if N._is_torch(centers) else np.size(centers)))
-    out = _empty_like_input(x, nint * 8, b)
-    red = _empty_like_input(x, nint, b)
+    buf = _empty_like_input(x, nint * 9, b)
+    out, red = buf[:nint * 8], buf[nint * 8:]
     outp = b.arg(out, np.float64, writable=True)
     redp = b.arg(red, np.float64, writable=True)
     with b.device_guard():
         N.check(L.crimp_toa_fit_redchi2(xp, op, nint, ctypes.byref(tpl), ep, float(norm0), int(ph_shift_res), options,
                                         eg, cg, nb, int(nfree), outp, redp, b.flags(flags), b.stream()))
-    return out.reshape(nint, 8), red
+    return buf if packed else (out.reshape(nint, 8), red)
 
 
 def toa_redchi2(x, offsets, tpl, exposure, records, edges, centers, nfree):

@@ -395,11 +395,12 @@ class ToAFitter:
         steps 1-3, the histogram of step 4 beside them). ``vary_amps``: ampShift free (Fourier [0.01, 100], Cauchy [0, inf), von Mises [0, 500]) after the (norm, phShift) fit,
         re-profiled with the norm in the 1-sigma scan, one more free parameter in redChi2 (:305-312)."""
         edges, pp = self._bins()
-        rd, rc = ops.toa_fit_redchi2(self.x, self.offsets, self.tpl, self._arr(self.E, np.float64), self.norm0,
-                                     self.res, brutemin, vary_amps, self._arr(edges, np.float64),
-                                     self._arr(pp, np.float64), 3 if vary_amps else 2)
-        rchi2 = rc.cpu().numpy() if _is_torch(rc) else np.asarray(rc)
-        r = np.asarray(rd.cpu().numpy() if _is_torch(rd) else rd)
+        n = self.nint
+        small = self._arr(np.concatenate([self.E, edges, pp]), np.float64)  # one upload
+        buf = ops.toa_fit_redchi2(self.x, self.offsets, self.tpl, small[:n], self.norm0, self.res, brutemin, vary_amps,
+                                  small[n:n + edges.size], small[n + edges.size:], 3 if vary_amps else 2, packed=True)
+        buf = np.asarray(buf.cpu().numpy() if _is_torch(buf) else buf)           # one readback
+        r, rchi2 = buf[:8 * n].reshape(n, 8), buf[8 * n:].copy()
         n_hat, phi_hat, amp = r[:, 0].copy(), r[:, 1].copy(), r[:, 6].copy()
         return {"phShi": phi_hat, "phShi_LL": r[:, 3].copy(), "phShi_UL": r[:, 4].copy(), "reducedChi2": rchi2,
                 "norm": n_hat, "LLmax": r[:, 2].copy(), "evaluations": r[:, 5].copy(), "ampShift": amp,
