@@ -142,8 +142,9 @@ def toa_leg(a, dev, world, rank):
     # kernel split of one fit (hipEvents around the brute-grid and the fit kernels inside crimp_toa_fit)
     from crimp_amd import ops
     f = ToAFitter(x, off, E, tm)
-    ops.toa_fit(f.x, f.offsets, f.tpl, f._arr(f.E, np.float64), f.norm0, f.res, True, False,
-                flags=N.FLAG_TIME_KERNELS)
+    edges, pp = f._bins()
+    ops.toa_fit_redchi2(f.x, f.offsets, f.tpl, f._arr(f.E, np.float64), f.norm0, f.res, True, False,
+                        f._arr(edges, np.float64), f._arr(pp, np.float64), 2, flags=N.FLAG_TIME_KERNELS)
     grid_ms, fit_ms = N.last_kernel_times()[:2]
     elt = torch.tensor([el], dtype=torch.float64, device=dev)
     if world > 1:
@@ -174,12 +175,14 @@ def toa_leg(a, dev, world, rank):
     # side's sigma is kk step + step / 2.
     K = len(T2259["amp"])
     nn = int(N.load().crimp_last_toa_grid_norms())
-    gmode = int(N.load().crimp_last_toa_grid_fast())   # bit 0: no min h, bit 1: log2 per eight model values
+    gmode = int(N.load().crimp_last_toa_grid_fast())   # bits: 1 no min h, 2 log2 per eight model values, 4 certificate
     nphi = 126
     nph_tot = float(a.toa_intervals) * a.toa_photons
-    # per point: the min (1, unless bit 0) and per norm an add, (P-1)/P multiply, 1/P of a 4-slot v_log_f32 and 1/P add
+    # per point: the min (1, unless bit 0) and per norm an add, (P-1)/P multiply, 1/P of a 4-slot v_log_f32 and 1/P add;
+    # with one evaluated norm on the eight-factor kernel the add is done by the MFMA (accumulators start at the norm)
     P = 8 if gmode & 2 else 4
-    s_grid = (0 if gmode & 1 else 1) + nn * (1 + (P - 1) / P + 5.0 / P)
+    cin = bool(gmode & 2) and nn == 1
+    s_grid = (0 if gmode & 5 else 1) + nn * ((0 if cin else 1) + (P - 1) / P + 5.0 / P)
     g_slots = nph_tot * nphi * s_grid
     g_ach = g_slots / (grid_ms * 1e-3)
     g_mf = nph_tot * nphi * 2 * 16 * ((K + 1) // 2) / (grid_ms * 1e-3)   # f16 matrix FLOP/s issued
@@ -188,8 +191,9 @@ def toa_leg(a, dev, world, rank):
                            "norms_evaluated": nn, "slots_per_photon_phshift": s_grid, "grid_mode": gmode,
                            "matrix": {"achieved": g_mf / 1e12, "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s (f16 dense)",
                                       "frac": g_mf / 1e12 / PEAK_F16_TFLOPS},
-                           "note": "S_grid = [min] + NN (1 + (P-1)/P + 5/P) fp32 lane-op slots per photon x phShift "
-                                   "(log2 of products of P = 4 or 8 model values, v_log_f32 at 4) beside "
+                           "note": "S_grid = [min] + NN ([1] + (P-1)/P + 5/P) fp32 lane-op slots per photon x phShift "
+                                   "(log2 of products of P = 4 or 8 model values, v_log_f32 at 4; the add of the norm "
+                                   "not counted where the MFMA accumulators start at it: P = 8, NN = 1) beside "
                                    "the template on v_mfma_f32_32x32x16_f16 (hi/lo f16 split, 16 MACs per pair of "
                                    "harmonics), x 1250 x 1e5 photons x 126 phShifts / brute-grid hipEvent time "
                                    "(k_toa_grid_mf + k_toa_grid_best); peaks 256 CU x 4 SIMD x 32 lanes x 2.4 GHz, "

@@ -2130,6 +2130,45 @@ static double tpl_hmin_scan_uncached(const TplDev& T) {
     return mn - dmax - 1e-12 * (std::fabs(mn) + dmax);
 }
 
+// Lazy-norm certificate (crimp_toa_fit_redchi2): per phShift phi_k of the brute lattice and histogram bin b = [e_b,
+// e_{b+1}], an upper bound of the Fourier template part over every photon bin b can hold at phi_k,
+// max_{x in bin} h0(x - phi_k / 2 pi) with h0(u) = sum_j amp_j cos(2 pi (j+1) u + loc_j) (k_toa_grid_mf's h): the
+// largest of 8192 samples per cycle over the covering sample range plus the Lipschitz bound L / 8192,
+// L = sum_j 2 pi (j+1) |amp_j|. out[k * nb + b]. Cached for the last (template, lattice, edges).
+static const std::vector<double>& tpl_bin_max(const TplDev& T, const std::vector<double>& phi, const double* edges,
+                                              int nb) {
+    static TplDev last;
+    static std::vector<double> lphi, ledg, val;
+    static bool have = false;
+    std::vector<double> edg(edges, edges + nb + 1);
+    if (have && std::memcmp(&last, &T, sizeof(T)) == 0 && lphi == phi && ledg == edg) return val;
+    constexpr int G = 8192;
+    std::vector<double> hs(G);
+    double L = 0.0;
+    for (int j = 0; j < T.K; ++j) L += 2.0 * M_PI * (double)(j + 1) * std::fabs(T.amp[j]);
+    for (int g = 0; g < G; ++g) {
+        double h = 0.0;
+        for (int j = 0; j < T.K; ++j) h += T.amp[j] * std::cos(2.0 * M_PI * (double)(j + 1) * ((double)g / G) + T.loc[j]);
+        hs[(size_t)g] = h;
+    }
+    val.assign(phi.size() * (size_t)nb, 0.0);
+    for (size_t k = 0; k < phi.size(); ++k) {
+        const double sh = phi[k] / (2.0 * M_PI);
+        for (int b = 0; b < nb; ++b) {
+            const int64_t g0 = (int64_t)std::floor((edg[(size_t)b] - sh) * G) - 1;
+            const int64_t g1 = (int64_t)std::ceil((edg[(size_t)b + 1] - sh) * G) + 1;
+            double mx = -INFINITY;
+            for (int64_t g = g0; g <= g1; ++g) mx = std::max(mx, hs[(size_t)(((g % G) + G) % G)]);
+            val[k * (size_t)nb + (size_t)b] = mx + L / G;
+        }
+    }
+    std::memcpy(&last, &T, sizeof(T));
+    lphi = phi;
+    ledg = edg;
+    have = true;
+    return val;
+}
+
 static void tpl_bounds(const TplDev& T, double* hmin, double* hmax) {
     double lo = 0.0, hi = 0.0;
     for (int j = 0; j < T.K; ++j) {
@@ -2241,7 +2280,9 @@ static int grid_mf_scale(const TplDev& T, bool* ok) {
 // min h (*ph = nullptr: the host's template bound certifies every candidate norm + h > 0); bit 1 (kGridProd8) -- log2 of
 // products of eight model values (the host certified that every factor of a valid lattice point stays inside
 // [2^-15, 2^15] after the coefficient scale, or k_toa_grid_best checks it where the min decides validity)
-constexpr int kGridNoMin = 1, kGridProd8 = 2;
+// bit 2 (kGridCert) -- no per-phShift min either: the lazy norms' points are shown invalid by the phase histogram
+// (k_toa_grid_best with lzmask; crimp_toa_fit_redchi2's histogram, tpl_bin_max)
+constexpr int kGridNoMin = 1, kGridProd8 = 2, kGridCert = 4;
 // a_first: the lazy norms [0, a_first) of every interval are not evaluated (their lnsum entries are left unwritten;
 // k_toa_grid_best knows them invalid from the min, or has the grid rerun in full)
 static int toa_grid_partials(Scratch& sc, hipStream_t s, const double* dx, const int64_t* doff, const TplDev* dT,
@@ -2266,8 +2307,10 @@ static int toa_grid_partials(Scratch& sc, hipStream_t s, const double* dx, const
     const bool mf = model == CRIMP_MODEL_FOURIER && CRIMP_GRID_MFMA && K <= kGridKMax && mf_ok;
     if (!mf) mode = 0;
     if (!(mode & kGridProd8)) a_first = 0;  // lazy norms only on the eight-factor kernel (its caller checks them)
+    if (!(mode & kGridProd8)) mode &= ~kGridCert;
     if (mode_out) *mode_out = mode;
-    if (mode & kGridNoMin)
+    const bool hm = !(mode & (kGridNoMin | kGridCert)), p8 = mode & kGridProd8;
+    if (!hm)
         *ph = nullptr;
     else
         HIPCHK(sc.alloc(ph, (size_t)(splits * nint * nphi)));
@@ -2289,11 +2332,11 @@ static int toa_grid_partials(Scratch& sc, hipStream_t s, const double* dx, const
                                                         (int)a0, na, dphi, (int)nphi, chunk, (int)nint, se, (int)a_first, \
                                                         *pl, *ph)
 #define CRIMP_LM1(KK, NNV) do { \
-        if (mode == (kGridNoMin | kGridProd8)) CRIMP_LM2(KK, NNV, false, 8); \
-        else if (mode == kGridProd8) CRIMP_LM2(KK, NNV, true, 8); \
-        else if (mode == kGridNoMin) CRIMP_LM2(KK, NNV, false, 4); \
+        if (!hm && p8) CRIMP_LM2(KK, NNV, false, 8); \
+        else if (p8) CRIMP_LM2(KK, NNV, true, 8); \
+        else if (!hm) CRIMP_LM2(KK, NNV, false, 4); \
         else CRIMP_LM2(KK, NNV, true, 4); } while (0)
-#define CRIMP_LM(KK) do { if (nn == 1) CRIMP_LM2(KK, 1, true, 8); \
+#define CRIMP_LM(KK) do { if (nn == 1) { if (hm) CRIMP_LM2(KK, 1, true, 8); else CRIMP_LM2(KK, 1, false, 8); } \
                           else if (nn == 2) CRIMP_LM1(KK, 2); else if (nn == kGridNNSmall) CRIMP_LM1(KK, kGridNNSmall); \
                           else CRIMP_LM1(KK, kGridNN); } while (0)
             switch (K) {
@@ -2407,8 +2450,9 @@ static int toa_fit_impl(const double* x, const int64_t* offsets, int64_t nint, c
         HIPCHK(stage_in(sc, exposure, (size_t)nint, dev, &de));
         HIPCHK(stage_out(sc, out, (size_t)nint * 8, dev, &dout));
         // redChi2's histogram (crimp_toa_fit_redchi2) needs only the photons: it runs on the auxiliary stream beside
-        // the brute grid and the fits, in the partly empty last round of the fit's workgroups (timed calls: after the
-        // fits on this stream, so that the kernel times stay those of the grid and the fit alone)
+        // the brute grid and the fits, in the partly empty last round of the fit's workgroups (timed calls: on this
+        // stream before the grid's timer starts, so that the kernel times stay those of the grid and the fit alone).
+        // The brute grid's lazy-norm certificate reads it too (kGridCert).
         const double *dedg = nullptr, *dcen = nullptr;
         double* dred = nullptr;
         unsigned long long* dcnt = nullptr;
@@ -2431,6 +2475,10 @@ static int toa_fit_impl(const double* x, const int64_t* offsets, int64_t nint, c
                 HIPCHK(hipGetLastError());
                 HIPCHK(hipEventCreateWithFlags(&ebin.e, hipEventDisableTiming));
                 HIPCHK(hipEventRecord(ebin.e, s1));
+            } else {
+                k_binphases<<<dim3((unsigned)nint, (unsigned)bin_splits(hoff[nint], nint)), 64 * kBinWaves, 0, s>>>(
+                    dx, doff, dedg, rq->nbins, dcnt);
+                HIPCHK(hipGetLastError());
             }
         }
         TplDev* dT = nullptr;
@@ -2445,6 +2493,8 @@ static int toa_fit_impl(const double* x, const int64_t* offsets, int64_t nint, c
         int grid_mode = 0, lattice_start = 0;
         double *dphi = nullptr, *dnrm = nullptr;
         int* dunsafe = nullptr;
+        uint64_t* dlzmask = nullptr;
+        int* dlzrow = nullptr;
         std::function<int(int, hipStream_t, int64_t, int64_t)> run_brute;
         if (brutemin) {
             // lmfit brute lattices (measureToAs.py:292-295): scipy mgrid phShift = k*0.05 - bound, 20 norms
@@ -2542,6 +2592,56 @@ static int toa_fit_impl(const double* x, const int64_t* offsets, int64_t nint, c
                 }
                 if (nlazy >= nc) nlazy = 0;  // every candidate lazy: evaluate them all
             }
+            // Lazy-norm certificate (crimp_toa_fit_redchi2, whose histogram is at hand; CRIMP_TOA_NO_CERT: off): a lazy
+            // point (norm n0, phi_k) is invalid when some photon has h <= -n0; it does where a bin b holds photons and
+            // the template's bound over that bin at phi_k (tpl_bin_max) is <= -n0 - 1e-3 (the margin covers the
+            // kernel's fp32 h). With the start rule decided by hb too (as kGridNoMin), the grid then needs no min h:
+            // k_toa_grid_best marks those points -inf from the counts, and one it cannot show invalid reruns the grid
+            // with the min (the flag below). Used only when every (lazy norm, phi_k) has such a bin.
+            if (rq && nlazy > 0 && mode == kGridProd8 && rq->nbins <= 64 && getenv("CRIMP_TOA_NO_CERT") == nullptr) {
+                bool srule = true;
+                for (int64_t i = 0; i < nint && srule; ++i) {
+                    const double r = (double)(hoff[i + 1] - hoff[i]) / hexp[(size_t)i];
+                    srule = hb + r > 0.5 * r;
+                }
+                if (srule) {
+                    const int nb = rq->nbins;
+                    std::vector<double> hedg((size_t)nb + 1);
+                    if (dev) {
+                        HIPCHK(d2h(s, hedg.data(), rq->edges, (size_t)(nb + 1) * sizeof(double)));
+                    } else {
+                        std::memcpy(hedg.data(), rq->edges, (size_t)(nb + 1) * sizeof(double));
+                    }
+                    const std::vector<double>& bm = tpl_bin_max(T, hphi, hedg.data(), nb);
+                    std::vector<double> vals;  // the distinct lazy norms (lattice values)
+                    std::vector<int> hrow((size_t)(nint * nlazy));
+                    for (int64_t i = 0; i < nint; ++i)
+                        for (int64_t z = 0; z < nlazy; ++z) {
+                            const double v = hnrm[(size_t)(i * nc + z)];
+                            size_t r = 0;
+                            while (r < vals.size() && vals[r] != v) ++r;
+                            if (r == vals.size()) vals.push_back(v);
+                            hrow[(size_t)(i * nlazy + z)] = (int)r;
+                        }
+                    std::vector<uint64_t> hmask(vals.size() * (size_t)nphi, 0);
+                    bool all_k = true;
+                    for (size_t r = 0; r < vals.size(); ++r)
+                        for (int64_t k = 0; k < nphi; ++k) {
+                            uint64_t m = 0;
+                            for (int b = 0; b < nb; ++b)
+                                if (bm[(size_t)k * nb + b] + 1e-3 <= -vals[r]) m |= 1ull << b;
+                            hmask[r * (size_t)nphi + (size_t)k] = m;
+                            all_k = all_k && m != 0;
+                        }
+                    if (all_k) {
+                        HIPCHK(sc.alloc(&dlzmask, hmask.size()));
+                        HIPCHK(sc.alloc(&dlzrow, hrow.size()));
+                        HIPCHK(h2d(dlzmask, hmask.data(), hmask.size() * sizeof(uint64_t)));
+                        HIPCHK(h2d(dlzrow, hrow.data(), hrow.size() * sizeof(int)));
+                        mode |= kGridCert;
+                    }
+                }
+            }
             // dunsafe -- k_toa_grid_best: a valid lattice point whose min factor is below 2^-15 / s, or of a lazy norm
             HIPCHK(sc.alloc(&dunsafe, 1));
             HIPCHK(hipMemsetAsync(dunsafe, 0, sizeof(int), s));
@@ -2560,11 +2660,15 @@ static int toa_fit_impl(const double* x, const int64_t* offsets, int64_t nint, c
                     if (r2) return r2;
                     g_last_grid_fast = ran;
                     g_last_grid_norms = nc - ((ran & kGridProd8) ? lz : 0);  // the lazy norms are not evaluated
+                    const bool cert = ran & kGridCert;
+                    if (cert && ebin.e) HIPCHK(hipStreamWaitEvent(st, ebin.e, 0));  // the histogram's counts
                     k_toa_grid_best<<<(unsigned)nb, 256, 0, st>>>(pl, ph, dnrm + i0 * nc, dphi, doff + i0, de + i0, (int)nc,
                                                                  (int)nphi, (int)nb, (int)splits, T.model, C.sum_amp,
                                                                  grid_n[0], C.lo, C.hi, lattice_start, hb,
                                                                  (ran & kGridProd8) ? gsc : 0.0,
                                                                  (ran & kGridProd8) ? (int)lz : 0, dunsafe,
+                                                                 cert ? dlzmask : nullptr, cert ? dlzrow + i0 * lz : nullptr,
+                                                                 cert ? dcnt + i0 * rq->nbins : nullptr, cert ? rq->nbins : 0,
                                                                  dstart + 2 * i0);
                     HIPCHK(hipGetLastError());
                 }
@@ -2671,17 +2775,12 @@ static int toa_fit_impl(const double* x, const int64_t* offsets, int64_t nint, c
             HIPCHK(d2h(s, &unsafe, dunsafe, sizeof(int)));
             HIPCHK(hipStreamSynchronize(s));
             if (unsafe) {
-                rc = all(grid_mode & ~kGridProd8);
+                rc = all(grid_mode & ~(kGridProd8 | kGridCert));
                 if (rc) return rc;
             }
         }
         if (rq) {  // redChi2 from the final records
-            if (ebin.e) {
-                HIPCHK(hipStreamWaitEvent(s, ebin.e, 0));
-            } else {
-                k_binphases<<<dim3((unsigned)nint, (unsigned)bin_splits(hoff[nint], nint)), 64 * kBinWaves, 0, s>>>(
-                    dx, doff, dedg, rq->nbins, dcnt);
-            }
+            if (ebin.e) HIPCHK(hipStreamWaitEvent(s, ebin.e, 0));
             k_toa_chi2<<<(unsigned)nint, 64, 0, s>>>(dcnt, T, de, dout, dcen, rq->nbins, rq->nfree, dred);
             HIPCHK(hipGetLastError());
             HIPCHK(copy_back(s, rq->out, dred, (size_t)nint, dev));

@@ -926,6 +926,9 @@ __global__ __launch_bounds__(256) void k_toa_grid_best(const double* __restrict_
                                                        int splits, int model, double sum_amp, double norm_first,
                                                        double lo, double hi, int plain, double hconst,
                                                        double prod8_scale, int nlazy, int* __restrict__ unsafe,
+                                                       const uint64_t* __restrict__ lzmask,
+                                                       const int* __restrict__ lzrow,
+                                                       const unsigned long long* __restrict__ cnt, int nbins,
                                                        double* __restrict__ start) {
     __shared__ double bv[4];
     __shared__ int bi[4];
@@ -936,6 +939,13 @@ __global__ __launch_bounds__(256) void k_toa_grid_best(const double* __restrict_
     int bidx = 0x7fffffff;
     auto lattice_ll = [&](int ai, int bj) -> double {  // the reference LL of lattice point (norm ai, phShift bj)
         if (ai < nlazy) {  // a lazy norm (not evaluated): -inf where the min h invalidates it, else the grid reruns
+            if (lzmask) {  // kGridCert: a photon-holding bin whose template bound at this phShift is <= -norm
+                const uint64_t m = lzmask[(int64_t)lzrow[iv * nlazy + ai] * nphi + bj];
+                bool inv = false;
+                for (int b = 0; b < nbins; ++b) inv = inv || (((m >> b) & 1ull) != 0 && cnt[iv * nbins + b] > 0);
+                if (!inv) atomicOr(unsafe, 1);
+                return (double)-INFINITY;
+            }
             double hm = INFINITY;
             for (int sp = 0; sp < splits; ++sp) hm = fmin(hm, ph[((int64_t)sp * nint + iv) * nphi + bj]);
             if ((hm + norm[iv * nnorm + ai]) > 0) atomicOr(unsafe, 1);

@@ -215,7 +215,8 @@ def test_fast_brute_grid_equals_full_kernel(gpu, monkeypatch):
     against the full kernel (CRIMP_TOA_GRID_SLOW): config-5-style Fourier intervals, every interval. The lattice LL
     values differ only by fp32 rounding, so the lattice point is the same and the fits reach the same maximum (the
     parabola-vertex start moves by rounding only): phShift within 1e-9 cycles, identical 1-sigma bounds, LLmax within
-    1e-12 relative. (Config 5's lower candidate norm, norm0/100, can be invalid, so its grid keeps the min: mode 2.)"""
+    1e-12 relative. (Config 5's lower candidate norm, norm0/100, is lazy and shown invalid by the phase histogram:
+    mode 6.)"""
     from crimp_amd import _native as N
     from crimp_amd.synth import template_intervals_torch
     from crimp_amd.toafit import ToAFitter
@@ -224,7 +225,7 @@ def test_fast_brute_grid_equals_full_kernel(gpu, monkeypatch):
                                             device=gpu)
     monkeypatch.delenv("CRIMP_TOA_GRID_SLOW", raising=False)
     a = ToAFitter(x, off, E, _tmpl()).fit(brutemin=True)
-    assert N.load().crimp_last_toa_grid_fast() == 2
+    assert N.load().crimp_last_toa_grid_fast() == 6  # eight factors, lazy norms by the histogram certificate
     monkeypatch.setenv("CRIMP_TOA_GRID_SLOW", "1")
     b = ToAFitter(x, off, E, _tmpl()).fit(brutemin=True)
     assert N.load().crimp_last_toa_grid_fast() == 0
@@ -232,3 +233,34 @@ def test_fast_brute_grid_equals_full_kernel(gpu, monkeypatch):
     np.testing.assert_array_equal(a["phShi_LL"], b["phShi_LL"])
     np.testing.assert_array_equal(a["phShi_UL"], b["phShi_UL"])
     np.testing.assert_allclose(a["LLmax"], b["LLmax"], rtol=1e-12)
+
+
+def test_lazy_norm_certificate_equals_min_path(gpu, monkeypatch):
+    """The brute grid's lazy-norm certificate (kGridCert: the lazy points shown invalid by photon-holding histogram
+    bins whose template bound is below -norm, no per-phShift min h) against the same kernel with the min
+    (CRIMP_TOA_NO_CERT): identical records and redChi2 for config-5-style intervals, host and device inputs; and no
+    certificate where no norm is lazy (a weak template: every candidate norm valid everywhere)."""
+    from crimp_amd import _native as N
+    from crimp_amd.synth import template_intervals_torch
+    from crimp_amd.toafit import ToAFitter
+    from bench import T2259, _tmpl
+    x, off, E, _ = template_intervals_torch(300, 50_000, T2259["norm"]["value"], T2259["amp"], T2259["ph"], seed=8,
+                                            device=gpu)
+    for xs, os_ in ((x, off), (x.cpu().numpy(), off.cpu().numpy())):
+        monkeypatch.delenv("CRIMP_TOA_NO_CERT", raising=False)
+        a = ToAFitter(xs, os_, E, _tmpl()).fit(brutemin=True)
+        assert N.load().crimp_last_toa_grid_fast() == 6
+        monkeypatch.setenv("CRIMP_TOA_NO_CERT", "1")
+        b = ToAFitter(xs, os_, E, _tmpl()).fit(brutemin=True)
+        assert N.load().crimp_last_toa_grid_fast() == 2
+        for k in a:
+            np.testing.assert_array_equal(np.asarray(a[k]), np.asarray(b[k]), err_msg=k)
+    monkeypatch.delenv("CRIMP_TOA_NO_CERT", raising=False)
+    weak = _tmpl()
+    for k in weak:
+        if k.startswith("amp_"):
+            weak[k] = {"value": weak[k]["value"] * 0.01}
+    xw, offw, Ew, _ = template_intervals_torch(20, 20_000, T2259["norm"]["value"], [a_ * 0.01 for a_ in T2259["amp"]],
+                                               T2259["ph"], seed=9, device=gpu)
+    ToAFitter(xw, offw, Ew, weak).fit(brutemin=True)
+    assert N.load().crimp_last_toa_grid_fast() & 4 == 0

@@ -22,7 +22,7 @@ res = ToAFitter(x, off, E, tm).fit(brutemin=True); torch.cuda.synchronize()
 g, k = [], []
 for _ in range(int(os.environ.get("REPS", 3))):
     f = ToAFitter(x, off, E, tm)
-    ops.toa_fit(f.x, f.offsets, f.tpl, f._arr(f.E, np.float64), f.norm0, f.res, True, False, flags=N.FLAG_TIME_KERNELS)
+    ops.toa_fit_redchi2(f.x, f.offsets, f.tpl, f._arr(f.E, np.float64), f.norm0, f.res, True, False, f._arr(f._bins()[0], np.float64), f._arr(f._bins()[1], np.float64), 2, flags=N.FLAG_TIME_KERNELS)
     gm, km = N.last_kernel_times()[:2]; g.append(gm); k.append(km)
 h = hashlib.sha1()
 for key in sorted(res):

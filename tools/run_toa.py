@@ -29,7 +29,7 @@ for rep in range(3):
     torch.cuda.synchronize()
     el = time.perf_counter() - t1
     f = ToAFitter(x, off, E, tm)
-    ops.toa_fit(f.x, f.offsets, f.tpl, f._arr(f.E, np.float64), f.norm0, f.res, True, False, flags=N.FLAG_TIME_KERNELS)
+    ops.toa_fit_redchi2(f.x, f.offsets, f.tpl, f._arr(f.E, np.float64), f.norm0, f.res, True, False, f._arr(f._bins()[0], np.float64), f._arr(f._bins()[1], np.float64), 2, flags=N.FLAG_TIME_KERNELS)
     g_ms, f_ms = N.last_kernel_times()[:2]
     print("lib %s: %d x %d photons: %.1f ms (grid %.2f ms, fit %.2f ms), %.4g fits/s, phShi[0:3] %s" % (
         os.path.basename(N.LIB_PATH), nint, nph, el * 1e3, g_ms, f_ms, nint / el, r["phShi"][:3]), flush=True)
