@@ -1059,6 +1059,16 @@ __global__ __launch_bounds__(kGridBlock) __attribute__((amdgpu_waves_per_eu(4)))
 #ifndef CRIMP_GM_CIN
 #define CRIMP_GM_CIN 1
 #endif
+// CRIMP_GM_PREF: each thread loads its photon of the next tile right after building the current one, so the global
+// load's latency passes under the current tile's chunks instead of stalling every wave of the block at the build.
+// CRIMP_GM_PIPE: a wave issues the next chunk's MFMAs before the VALU work on the current chunk's results, so its
+// matrix instructions run under its own likelihood arithmetic.
+#ifndef CRIMP_GM_PREF
+#define CRIMP_GM_PREF 1
+#endif
+#ifndef CRIMP_GM_PIPE
+#define CRIMP_GM_PIPE 1
+#endif
 constexpr int kGmTile = CRIMP_GM_TILE, kGmPad = CRIMP_GM_PAD;
 static_assert(kGmTile == 128 || kGmTile == 256, "k_toa_grid_mf: one or two of the block's 256 threads per photon");
 static_assert(kGridBlock == 32 * 4, "k_toa_grid_mf: 4 waves of 32 phShift columns cover a block's kGridBlock columns");
@@ -1116,18 +1126,21 @@ __global__ __launch_bounds__(256) void k_toa_grid_mf(const double* __restrict__ 
     float hmn = INFINITY;
     const int64_t beg = offsets[iv] + split * chunk;
     const int64_t end = std::min<int64_t>(offsets[iv + 1], beg + chunk);
+    const int pt = tid & (kGmTile - 1);  // this thread's photon of a tile
+    double xpre = (CRIMP_GM_PREF && beg + pt < end) ? x[beg + pt] : 0.0;
     for (int64_t base = beg; base < end; base += kGmTile) {
         const int cnt = (int)std::min<int64_t>(kGmTile, end - base);
         __syncthreads();
         {   // A fragments: thread (photon p = tid % kGmTile, part g = tid / kGmTile) builds harmonics [g JP, (g+1) JP)
             constexpr int JP = kGmTile == 256 ? 2 * NM : 4;
-            const int p = tid & (kGmTile - 1), g = kGmTile == 256 ? 0 : tid >> 7;
+            const int p = pt, g = kGmTile == 256 ? 0 : tid >> 7;
             float c1 = 1.0f, s1 = 0.0f;
             if (p < cnt) {
-                double rv = x[base + p];
+                double rv = CRIMP_GM_PREF ? xpre : x[base + p];
                 rv -= rint(rv);
                 sincos_rev_poly((float)rv, s1, c1);
             }
+            if (CRIMP_GM_PREF) xpre = base + kGmTile + p < end ? x[base + kGmTile + p] : 0.0;
             float cj = c1, sj = s1;
 #pragma unroll
             for (int j = 0; j < 2 * NM; ++j) {
@@ -1144,17 +1157,22 @@ __global__ __launch_bounds__(256) void k_toa_grid_mf(const double* __restrict__ 
             }
         }
         __syncthreads();
-        for (int q0 = 0; q0 < cnt; q0 += 32) {
-            f32x16 hv = {};
+        // one 32-photon chunk's template part (32 photons x the wave's 32 phShift columns) on the matrix cores
+        auto chunk_mfma = [&](int q0) -> f32x16 {
+            f32x16 h = {};
             if constexpr (CIN) {
 #pragma unroll
-                for (int r = 0; r < 16; ++r) hv[r] = nrs[0];
+                for (int r = 0; r < 16; ++r) h[r] = nrs[0];
             }
 #pragma unroll
             for (int m = 0; m < NM; ++m) {
                 const f16x8 av = __builtin_bit_cast(f16x8, afr[q0 + (lane & 31)][2 * m + hk]);
-                hv = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bf[m], hv, 0, 0, 0);
+                h = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bf[m], h, 0, 0, 0);
             }
+            return h;
+        };
+        // the likelihood part of one chunk on the VALU (hv: the chunk's MFMA results)
+        auto chunk_valu = [&](const f32x16& hv, int q0) {
             if constexpr (PROD == 8) {
                 // photon pairs: per norm, the 16 factors norm + h of the lane's chunk as 8 f32x2, multiplied down a tree
                 // to two products of eight (even and odd photons), one v_log_f32 each
@@ -1206,7 +1224,7 @@ __global__ __launch_bounds__(256) void k_toa_grid_mf(const double* __restrict__ 
                 }
 #pragma unroll
                 for (int a = 0; a < NN; ++a) acc[a] += (double)pl[a].x + (double)pl[a].y;
-                continue;
+                return;
             }
             f32x2 pa[NP];
 #pragma unroll
@@ -1249,6 +1267,18 @@ __global__ __launch_bounds__(256) void k_toa_grid_mf(const double* __restrict__ 
             }
 #pragma unroll
             for (int a = 0; a < NN; ++a) acc[a] += (double)pa[a / 2][a % 2];
+        };
+        if constexpr (CRIMP_GM_PIPE) {  // ping-pong: chunk q + 1's MFMAs issue before chunk q's VALU work
+            f32x16 ha = chunk_mfma(0), hb = {};
+            for (int q0 = 0; q0 < cnt; q0 += 64) {
+                if (q0 + 32 < cnt) hb = chunk_mfma(q0 + 32);
+                chunk_valu(ha, q0);
+                if (q0 + 32 >= cnt) break;
+                if (q0 + 64 < cnt) ha = chunk_mfma(q0 + 64);
+                chunk_valu(hb, q0 + 32);
+            }
+        } else {
+            for (int q0 = 0; q0 < cnt; q0 += 32) chunk_valu(chunk_mfma(q0), q0);
         }
     }
     // the column's two lane halves: half 0 + half 1

@@ -1,9 +1,6 @@
-# Round-4 session 9: occupancy A/B (then the SQ passes of tools/r04_session10.sh) of the certified brute grid -- cur (256-photon tile, padded rows: 28 KB LDS, 5
-# blocks per CU), p0 (no pad: 24.5 KB, 6 blocks), t128 / t128p0 (128-photon tiles) -- with digests.
+# Round-4 session 10: SQ counters of the final brute grid and fit (config 5 over tools/run_toa.py): instruction mix,
+# waits, matrix-pipe busy, LDS, clock -- each pass its own rocprofv3 run.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-mkdir -p gpurun_out
-timeout -k 10 500 python -u tools/ab_toa.py cur p0 t128 t128p0 cur p0 t128 t128p0 > gpurun_out/ab_toa_occ.log 2>&1 || exit $?
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 RUN=tools/run_toa.py TAG=toa_final PAT="k_toa_grid_mf k_toa_fit k_toa_grid_best" PMC_SETS="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY
