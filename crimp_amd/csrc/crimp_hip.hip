@@ -1061,13 +1061,14 @@ __global__ __launch_bounds__(kGridBlock) __attribute__((amdgpu_waves_per_eu(4)))
 #endif
 // CRIMP_GM_PREF: each thread loads its photon of the next tile right after building the current one, so the global
 // load's latency passes under the current tile's chunks instead of stalling every wave of the block at the build.
-// CRIMP_GM_PIPE: a wave issues the next chunk's MFMAs before the VALU work on the current chunk's results, so its
-// matrix instructions run under its own likelihood arithmetic.
+// (1.85 -> 1.82 ms per 1250 config-5 grids, profiles/r04/ab_toa_pipe.log.) CRIMP_GM_PIPE=1 (A/B build): a wave
+// issues the next chunk's MFMAs before the VALU work on the current chunk's results; it measured slower (1.88 ms):
+// the five resident waves per SIMD already overlap one wave's MFMAs with another's VALU work.
 #ifndef CRIMP_GM_PREF
 #define CRIMP_GM_PREF 1
 #endif
 #ifndef CRIMP_GM_PIPE
-#define CRIMP_GM_PIPE 1
+#define CRIMP_GM_PIPE 0
 #endif
 constexpr int kGmTile = CRIMP_GM_TILE, kGmPad = CRIMP_GM_PAD;
 static_assert(kGmTile == 128 || kGmTile == 256, "k_toa_grid_mf: one or two of the block's 256 threads per photon");
