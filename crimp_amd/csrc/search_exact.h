@@ -49,10 +49,18 @@ constexpr int kExDtSlots = 4;   // photon-time ring: chunks c-1 (being retired) 
 // int32 headroom per photon and level (balanced digits, |top digit| <= 64): level 3 <= 2 x 49152, level 4
 // <= 2 x 32768, level 5 <= 2 x 16384, level 6 <= 2 x 4096. Every kExCarry chunks (16384 photons: level 3
 // reaches 1.61e9 < 2^31) the level sums are carried upward exactly (acc_L = 256 q + r, r in [0, 255]:
-// acc_L <- r, acc_{L+1} += q), which leaves level 6 growing by <= 2^27 per period; every kExFold chunks
-// (131072 photons, 8 periods: level 6 < 2^30 + carries) they are folded into the int64 running sums.
+// acc_L <- r, acc_{L+1} += q), which leaves level 6 (never reduced) growing per period by at most 2^27 of its own
+// products plus the carry from level 5 (<= (2 x 16384 x 16384 + 2^22 + 255) / 256 < 2.14e6), 1.363e8 in all; every
+// kExFold chunks (CRIMP_EX_FOLD_PERIODS = 15 periods, 245760 photons: |level 6| <= 2.045e9 < 2^31 - 1) they are folded
+// into the int64 running sums. (8 periods until round 4: a split of the photons then held at most 131072 photons
+// without an int64 fold through global scratch, so config 3 needed 77 splits and 2.46 GB of 64-bit atomics per
+// search; 15 periods halve both.)
+#ifndef CRIMP_EX_FOLD_PERIODS
+#define CRIMP_EX_FOLD_PERIODS 15
+#endif
+static_assert(CRIMP_EX_FOLD_PERIODS >= 1 && CRIMP_EX_FOLD_PERIODS <= 15, "level 6 must stay inside int32 between folds");
 constexpr int kExCarry = 16384 / kExChunk;
-constexpr int kExFold = 131072 / kExChunk;
+constexpr int kExFold = CRIMP_EX_FOLD_PERIODS * kExCarry;
 constexpr int kExFoldVals = 64;             // int64 running sums per lane (2 fragments x 16 result rows x Re, Im)
 constexpr double kExUnit = 1.4551915228366852e-11;  // 2^-36: value of one unit of the int64 totals
 

@@ -14,6 +14,7 @@ crimp_toa_shape_points); with both, ampShift is freed after the readvaryparam fi
 import argparse
 import math
 import sys
+import time
 
 import numpy as np
 
@@ -254,7 +255,8 @@ _UPLOAD_STREAMS = {}
 
 def _measure_pipelined(TIMEMJD, tm, tmpl, model, starts, ends, exposures, phShiftRes, nbrBins, varyAmps, brutemin):
     """measure_intervals for host photon times of at least CRIMP_E2E_MIN_PHOTONS (default 2^24): the intervals are cut
-    into CRIMP_E2E_BLOCKS (default 4) consecutive blocks of shrinking size (_shrinking_blocks); a second host thread
+    into consecutive blocks of shrinking size (_E2E_WEIGHTS; CRIMP_E2E_BLOCKS = n: n blocks of shares n : ... : 1;
+    CRIMP_E2E_WEIGHTS = "a,b,...": those shares); a second host thread
     uploads block k + 1
     on its own stream (a pageable copy blocks only that thread; torch releases the GIL) while this thread folds, fits
     and H-tests block k on the device, so the PCIe upload hides the device work. Interval selection is the host's
@@ -280,7 +282,10 @@ def _measure_pipelined(TIMEMJD, tm, tmpl, model, starts, ends, exposures, phShif
     n = hi - lo
     if np.any(n <= 0):
         return None
-    blocks = _shrinking_blocks(n, int(os.environ.get("CRIMP_E2E_BLOCKS", 4)))
+    wenv = os.environ.get("CRIMP_E2E_WEIGHTS")
+    nbk = os.environ.get("CRIMP_E2E_BLOCKS")
+    weights = [float(v) for v in wenv.split(",")] if wenv else (None if nbk else _E2E_WEIGHTS)
+    blocks = _shrinking_blocks(n, len(weights) if weights is not None else int(nbk), weights)
     if len(blocks) < 2:
         return None
     E = np.asarray(exposures, dtype=np.float64)
@@ -291,14 +296,19 @@ def _measure_pipelined(TIMEMJD, tm, tmpl, model, starts, ends, exposures, phShif
     pinned = src.is_pinned()
     q = queue.Queue(maxsize=2)
 
+    trace = [] if os.environ.get("CRIMP_E2E_TRACE") else None  # (event, block, seconds): tools/e2e_breakdown.py
+    t_start = time.perf_counter()
+
     def uploader():
         try:
-            for b0, b1 in blocks:
+            for k, (b0, b1) in enumerate(blocks):
                 a, b = int(lo[b0]), int(np.max(hi[b0:b1]))
                 with torch.cuda.stream(up):
                     d = src[a:b].to(dev, non_blocking=pinned)
                     ev = torch.cuda.Event()
                     ev.record(up)
+                if trace is not None:
+                    trace.append(("uploaded", k, time.perf_counter() - t_start))
                 q.put((d, ev, a))
         except BaseException as e:  # handed to the main thread
             q.put(e)
@@ -339,8 +349,12 @@ def _measure_pipelined(TIMEMJD, tm, tmpl, model, starts, ends, exposures, phShif
             first = t[lo[b0:b1]]
             last = t[lo[b0:b1] + nb - 1]
             mids = ((last - first) / 2) + first                 # measureToAs.py:182
+            if trace is not None:
+                trace.append(("start", len(parts), time.perf_counter() - t_start))
             parts.append(_fit_block(allt, offs, mids, tm, tmpl, model, E[b0:b1], phShiftRes, nbrBins, varyAmps,
                                     brutemin))
+            if trace is not None:
+                trace.append(("done", len(parts) - 1, time.perf_counter() - t_start))
     finally:  # on an error here, keep taking the uploader's blocks until it has finished
         while th.is_alive():
             try:
@@ -351,13 +365,26 @@ def _measure_pipelined(TIMEMJD, tm, tmpl, model, starts, ends, exposures, phShif
         sys.setswitchinterval(switch)
     if not bool(ok):
         return None
-    return {k: np.concatenate([np.atleast_1d(np.asarray(p[k])) for p in parts]) for k in parts[0]}
+    out = {k: np.concatenate([np.atleast_1d(np.asarray(p[k])) for p in parts]) for k in parts[0]}
+    if trace is not None:
+        trace.append(("end", -1, time.perf_counter() - t_start))
+        print("e2e trace: " + ", ".join("%s %d %.2f ms" % (e, k, t * 1e3) for e, k, t in sorted(trace, key=lambda r: r[2])),
+              flush=True)
+    return out
 
 
-def _shrinking_blocks(counts, nblocks):
-    """Consecutive runs of intervals for the pipelined upload: photon shares nblocks, nblocks - 1, ..., 1 (out of
-    their sum), so that the last block -- whose device work follows the whole upload -- is the smallest."""
-    w = np.arange(nblocks, 0, -1, dtype=np.float64)
+# Photon shares of the pipelined upload's blocks (CRIMP_E2E_WEIGHTS overrides): a block's device work (~1.2 ms of
+# per-block latency + ~5 us per 1e5-photon interval on config 5) should end before the next block's upload (~14 us per
+# interval at 56 GB/s), and the last block -- whose work follows the whole upload -- be small: 50/23/15/12 % puts
+# every block's work under the next upload (profiles/r04/e2e_trace.log: 4:3:2:1 left block 3 waiting 0.6 ms).
+_E2E_WEIGHTS = (50.0, 23.0, 15.0, 12.0)
+
+
+def _shrinking_blocks(counts, nblocks, weights=None):
+    """Consecutive runs of intervals for the pipelined upload: photon shares by ``weights`` (default: nblocks,
+    nblocks - 1, ..., 1), non-increasing, so that the last block -- whose device work follows the whole upload -- is
+    among the smallest."""
+    w = np.asarray(weights, dtype=np.float64) if weights is not None else np.arange(nblocks, 0, -1, dtype=np.float64)
     cuts = np.cumsum(w)[:-1] / w.sum() * float(np.sum(counts))
     at = np.searchsorted(np.cumsum(counts), cuts, side="left") + 1
     edges = np.unique(np.concatenate([[0], np.clip(at, 1, len(counts) - 1), [len(counts)]]))

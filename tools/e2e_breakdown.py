@@ -82,13 +82,15 @@ for k, v in acc.items():
     print("%-13s %8.3f ms (min %.3f)" % (k, np.mean(v), np.min(v)), flush=True)
 print("%-13s %8.3f ms" % ("sum", tot), flush=True)
 pin = torch.from_numpy(mjd).pin_memory()
-runs = [("numpy", mjd, b) for b in os.environ.get("BLOCKS", "1,2,3,4,6,8").split(",")] + [("pinned", pin, "4")]
-for name, src, nbk in runs:
+runs = [("numpy", mjd, b) for b in os.environ.get("BLOCKS", "1,4,d").split(",")] + [("pinned", pin, "d")]
+for name, src, nbk in runs:  # nbk: "1" one shot, "n" n blocks of shares n : ... : 1, "d" the default shares
+    os.environ.pop("CRIMP_E2E_BLOCKS", None)
     if nbk == "1":
-        os.environ["CRIMP_E2E_MIN_PHOTONS"] = str(1 << 62)  # one shot
+        os.environ["CRIMP_E2E_MIN_PHOTONS"] = str(1 << 62)
     else:
         os.environ.pop("CRIMP_E2E_MIN_PHOTONS", None)
-        os.environ["CRIMP_E2E_BLOCKS"] = nbk
+        if nbk != "d":
+            os.environ["CRIMP_E2E_BLOCKS"] = nbk
     name = "%s/%s blocks" % (name, nbk)
     measure_intervals(src, par, tm, starts, ends, E, brutemin=True)
     ts = []
@@ -100,3 +102,8 @@ for name, src, nbk in runs:
         ts.append(time.perf_counter() - t0)
     print("measure_intervals from %-16s %8.3f ms (min %.3f), %.4g fits/s" % (name, np.mean(ts) * 1e3, np.min(ts) * 1e3,
                                                                           nint / np.mean(ts)), flush=True)
+os.environ.pop("CRIMP_E2E_MIN_PHOTONS", None)
+os.environ.pop("CRIMP_E2E_BLOCKS", None)
+os.environ["CRIMP_E2E_TRACE"] = "1"
+for _ in range(2):  # the pipeline's timeline: upload done / block start / block done per block
+    measure_intervals(mjd, par, tm, starts, ends, E, brutemin=True)
