@@ -83,9 +83,13 @@ for k, v in acc.items():
 print("%-13s %8.3f ms" % ("sum", tot), flush=True)
 pin = torch.from_numpy(mjd).pin_memory()
 runs = [("numpy", mjd, b) for b in os.environ.get("BLOCKS", "1,4,d").split(",")] + [("pinned", pin, "d")]
-for name, src, nbk in runs:  # nbk: "1" one shot, "n" n blocks of shares n : ... : 1, "d" the default shares
+for name, src, nbk in runs:  # nbk: "1" one shot, "n" n blocks of shares n : ... : 1, "un" n equal blocks, "d" default
     os.environ.pop("CRIMP_E2E_BLOCKS", None)
-    if nbk == "1":
+    os.environ.pop("CRIMP_E2E_WEIGHTS", None)
+    if nbk.startswith("u"):
+        os.environ.pop("CRIMP_E2E_MIN_PHOTONS", None)
+        os.environ["CRIMP_E2E_WEIGHTS"] = ",".join(["1"] * int(nbk[1:]))
+    elif nbk == "1":
         os.environ["CRIMP_E2E_MIN_PHOTONS"] = str(1 << 62)
     else:
         os.environ.pop("CRIMP_E2E_MIN_PHOTONS", None)
@@ -104,6 +108,9 @@ for name, src, nbk in runs:  # nbk: "1" one shot, "n" n blocks of shares n : ...
                                                                           nint / np.mean(ts)), flush=True)
 os.environ.pop("CRIMP_E2E_MIN_PHOTONS", None)
 os.environ.pop("CRIMP_E2E_BLOCKS", None)
+os.environ.pop("CRIMP_E2E_WEIGHTS", None)
+if os.environ.get("TRACE_WEIGHTS"):
+    os.environ["CRIMP_E2E_WEIGHTS"] = os.environ["TRACE_WEIGHTS"]
 os.environ["CRIMP_E2E_TRACE"] = "1"
 for _ in range(2):  # the pipeline's timeline: upload done / block start / block done per block
     measure_intervals(mjd, par, tm, starts, ends, E, brutemin=True)
