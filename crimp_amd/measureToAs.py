@@ -373,11 +373,13 @@ def _measure_pipelined(TIMEMJD, tm, tmpl, model, starts, ends, exposures, phShif
     return out
 
 
-# Photon shares of the pipelined upload's blocks (CRIMP_E2E_WEIGHTS overrides): a block's device work (~1.2 ms of
-# per-block latency + ~5 us per 1e5-photon interval on config 5) should end before the next block's upload (~14 us per
-# interval at 56 GB/s), and the last block -- whose work follows the whole upload -- be small: 50/23/15/12 % puts
-# every block's work under the next upload (profiles/r04/e2e_trace.log: 4:3:2:1 left block 3 waiting 0.6 ms).
-_E2E_WEIGHTS = (50.0, 23.0, 15.0, 12.0)
+# Photon shares of the pipelined upload's blocks (CRIMP_E2E_WEIGHTS overrides). A block's device work costs ~1.2 ms of
+# per-block latency (one round of fits, the H-test launch, the calls) + ~5.5 us per 1e5-photon interval on config 5,
+# its upload ~14.6 us per interval at 56 GB/s: the pipeline is balanced near 140 intervals per block, where every
+# block's work ends as the next block's upload does. Equal blocks, 8 of them (config 5 per GPU: 156 intervals each):
+# 21.2 ms against 26.1 one-shot and 21.1-22.5 for 50/23/15/12 %; 12 equal blocks fall behind (24.9 ms)
+# (profiles/r04/e2e_sched.log, e2e_trace_*.log).
+_E2E_WEIGHTS = (1.0,) * 8
 
 
 def _shrinking_blocks(counts, nblocks, weights=None):
