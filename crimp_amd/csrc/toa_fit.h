@@ -17,6 +17,15 @@
 // iterative profile's to ~1e-10, and the scan compares it with a 0.5 threshold).
 
 constexpr int kFitBlock = kPtsBlock;
+// the photon phases through a global address-space pointer: the fit's helpers take generic pointers (they are called
+// out of line), whose loads hipcc would issue as flat loads -- counted against the LDS counter too, so every wait for
+// a sin/cos table read would also wait for the next photon's load
+// (CRIMP_FIT_GLD=0: the generic loads, A/B)
+#ifndef CRIMP_FIT_GLD
+#define CRIMP_FIT_GLD 1
+#endif
+typedef const double __attribute__((address_space(1))) GDouble;
+__device__ __forceinline__ double gld(const double* p, int64_t i) { return CRIMP_FIT_GLD ? ((GDouble*)p)[i] : p[i]; }
 // fit_moments2 fills the second phShift's coefficients from threads 64 .. 64 + K - 1 (the first wave fills the first's)
 static_assert(kFitBlock >= 64 + CRIMP_MAX_COMP, "fit_moments2: the block must cover threads 64 .. 64 + CRIMP_MAX_COMP");
 constexpr double kHalfChi2OneSigma = 0.500021713558733;  // 0.5 * chi2.ppf(0.6827, 1)   (measureToAs.py:324)
@@ -141,11 +150,11 @@ __device__ FitEval fit_eval(const double* __restrict__ x, int64_t a, int64_t b, 
         // the first pass of a norm profile: the profile reads only LL, dLL/dnorm and d2LL/dnorm2, so the phShift
         // derivatives h', h'' are not formed (the Fourier template: 5 instead of 9 operations per harmonic); h and
         // the sums are formed exactly as in the full pass
-        double xn = a + tid < b ? x[a + tid] : 0.0;
+        double xn = a + tid < b ? gld(x, a + tid) : 0.0;
         for (int64_t i = a + tid; i < b; i += kFitBlock) {
             double s1, c1, h;
-            const double xv = kFitPrefetch ? xn : x[i];
-            if (kFitPrefetch && i + kFitBlock < b) xn = x[i + kFitBlock];
+            const double xv = kFitPrefetch ? xn : gld(x, i);
+            if (kFitPrefetch && i + kFitBlock < b) xn = gld(x, i + kFitBlock);
             fit_sincos(model, sh, xv, s1, c1);
             if constexpr (MODEL == CRIMP_MODEL_FOURIER && KF > 0) {
                 tpl_value_fourier<KF>(al, be, s1, c1, h);
@@ -162,11 +171,11 @@ __device__ FitEval fit_eval(const double* __restrict__ x, int64_t a, int64_t b, 
             mn = fmin(mn, mv);
         }
       } else {
-       double xn = a + tid < b ? x[a + tid] : 0.0;
+       double xn = a + tid < b ? gld(x, a + tid) : 0.0;
        for (int64_t i = a + tid; i < b; i += kFitBlock) {
         double s1, c1, h, h1, h2;
-        const double xv = kFitPrefetch ? xn : x[i];
-        if (kFitPrefetch && i + kFitBlock < b) xn = x[i + kFitBlock];
+        const double xv = kFitPrefetch ? xn : gld(x, i);
+        if (kFitPrefetch && i + kFitBlock < b) xn = gld(x, i + kFitBlock);
         fit_sincos(model, sh, xv, s1, c1);
         if constexpr (MODEL == CRIMP_MODEL_FOURIER && KF > 0)
             tpl_terms_fourier<KF>(al, be, s1, c1, h, h1, h2);
@@ -349,11 +358,11 @@ __device__ FitMom fit_moments(const double* __restrict__ x, int64_t a, int64_t b
             be[j] = sh.coef[1][j];
         }
     }
-    double xn = a + tid < b ? x[a + tid] : 0.0;
+    double xn = a + tid < b ? gld(x, a + tid) : 0.0;
     for (int64_t i = a + tid; i < b; i += kFitBlock) {
         double s1, c1, h;
         const double xv = xn;
-        if (i + kFitBlock < b) xn = x[i + kFitBlock];
+        if (i + kFitBlock < b) xn = gld(x, i + kFitBlock);
         fit_sincos(model, sh, xv, s1, c1);
         if constexpr (MODEL == CRIMP_MODEL_FOURIER && KF > 0) {
             tpl_value_fourier<KF>(al, be, s1, c1, h);
@@ -464,11 +473,11 @@ __device__ __noinline__ void fit_moments2(const double* __restrict__ x, int64_t 
     double acc0[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0}, acc1[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
     double mn0 = INFINITY, mn1 = INFINITY, pr0 = 1.0, pr1 = 1.0;
     int np = 0;
-    double xn = a + tid < b ? x[a + tid] : 0.0;
+    double xn = a + tid < b ? gld(x, a + tid) : 0.0;
     for (int64_t i = a + tid; i < b; i += kFitBlock) {
         double s1, c1;
         const double xv = xn;
-        if (i + kFitBlock < b) xn = x[i + kFitBlock];
+        if (i + kFitBlock < b) xn = gld(x, i + kFitBlock);
         fit_sincos(CRIMP_MODEL_FOURIER, sh, xv, s1, c1);
         // tpl_value_fourier for both coefficient rows on one recurrence (the same h, operation by operation)
         double h0 = 0.0, h1 = 0.0;
@@ -577,7 +586,7 @@ __device__ FitEval3 fit_eval3(const double* __restrict__ x, int64_t a, int64_t b
     double mn = INFINITY;
     for (int64_t i = a + tid; i < b; i += kFitBlock) {
         double s1, c1, h, h1, h2;
-        fit_sincos(model, sh, x[i], s1, c1);
+        fit_sincos(model, sh, gld(x, i), s1, c1);
         tpl_terms(T, model, K, sh.coef[0], sh.coef[1], s1, c1, h, h1, h2);
         const double mv = n + A * h;
         const double q = lk_rcp(mv);
