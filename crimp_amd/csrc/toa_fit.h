@@ -19,8 +19,9 @@
 constexpr int kFitBlock = kPtsBlock;
 // the photon phases through a global address-space pointer: the fit's helpers take generic pointers (they are called
 // out of line), whose loads hipcc would issue as flat loads -- counted against the LDS counter too, so every wait for
-// a sin/cos table read would also wait for the next photon's load
-// (CRIMP_FIT_GLD=0: the generic loads, A/B)
+// a sin/cos table read would also wait for the next photon's load (measured neutral: 2.90 vs 2.90 ms per 1250
+// config-5 fits, profiles/r04/ab_toa_gld.log -- the prefetch one photon ahead already hides it; CRIMP_FIT_GLD=0: the
+// generic loads)
 #ifndef CRIMP_FIT_GLD
 #define CRIMP_FIT_GLD 1
 #endif
