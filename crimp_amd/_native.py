@@ -25,6 +25,7 @@ FLAG_TIME_KERNELS = 128
 FLAG_F64 = 256
 FLAG_FAST = 512
 FLAG_NO_FIXUP = 1024
+FLAG_ASYNC = 2048
 
 STAT_Z2 = 0
 STAT_H = 1

@@ -2093,6 +2093,10 @@ extern "C" int crimp_search_sets(const double* t, const int64_t* offsets, int64_
         k_search_sets<<<(unsigned)nset, kSetBlock, 0, s>>>(dt, doff, df, nharm, stat, dout);
         HIPCHK(hipGetLastError());
         HIPCHK(copy_back(s, out, dout, (size_t)nset, dev));
+        // CRIMP_FLAG_ASYNC: with device pointers the call stages nothing and takes no scratch block (a block handed
+        // back while the kernel still ran could be given to another call on another stream), so it may return with
+        // the kernel queued
+        if (dev && (flags & CRIMP_FLAG_ASYNC) && sc.held.empty()) return CRIMP_OK;
     }
     return finish(s, flags);
 }

@@ -234,19 +234,37 @@ def measure_intervals(TIMEMJD, timMod, tempModPP, starts, ends, exposures, phShi
     return res
 
 
+_HTEST_STREAMS = {}
+
+
 def _fit_block(allt, offs, mids, tm, tmpl, model, E, phShiftRes, nbrBins, varyAmps, brutemin):
-    """Fold, fit and H-test one block of intervals whose photons (device tensor ``allt``, seconds MJD) are concatenated
-    at ``offs`` (measureToAs.py:186-226 for every interval of the block)."""
+    """Fold, fit and H-test one block of intervals whose photons (device tensor ``allt``, days MJD) are concatenated
+    at ``offs`` (measureToAs.py:186-226 for every interval of the block). The per-interval H-test does not depend on
+    the fit: it is queued first on a second stream (crimp_search_sets with CRIMP_FLAG_ASYNC) and runs beside the
+    folding and the fits."""
     import torch
+    from ._native import FLAG_ASYNC
+    dev = allt.device
+    freqs = np.atleast_1d(ephemTmjd(mids, tm)["freqAtTmjd"])          # :210
+    ts = allt * 86400
+    offs_d = torch.as_tensor(offs, device=dev)
+    freqs_d = torch.as_tensor(freqs, dtype=torch.float64, device=dev)
+    side = _HTEST_STREAMS.get(dev.index)
+    if side is None:
+        side = _HTEST_STREAMS[dev.index] = torch.cuda.Stream(device=dev)
+    cur = torch.cuda.current_stream(dev)
+    side.wait_stream(cur)
+    with torch.cuda.stream(side):
+        hp_d = ops.search_sets(ts, offs_d, freqs_d, 5, STAT_H, flags=FLAG_ASYNC)   # :211-212, one trial per interval
+    for t_ in (ts, offs_d, freqs_d, hp_d):
+        t_.record_stream(side)
     _, folded = calcphase(allt, tm)
     if model in ("cauchy", "vonmises"):
         folded = folded * (2 * np.pi)                  # :195, :200
     res = ToAFitter(folded, offs, E, tmpl, phShiftRes, nbrBins).fit(brutemin=brutemin, vary_amps=bool(varyAmps))
-    freqs = np.atleast_1d(ephemTmjd(mids, tm)["freqAtTmjd"])          # :210
-    hp = ops.search_sets(allt * 86400, torch.as_tensor(offs, device=allt.device),
-                         torch.as_tensor(freqs, dtype=torch.float64, device=allt.device), 5, STAT_H).cpu().numpy()
+    cur.wait_stream(side)
     res["ToA_mid"] = mids
-    res["htestPow"] = np.asarray(hp)
+    res["htestPow"] = hp_d.cpu().numpy()
     return res
 
 

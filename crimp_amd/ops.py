@@ -123,9 +123,10 @@ def search(t, t0, freq, nharm, stat, log10_negfdot=None, first=0, count=None, ou
     return out
 
 
-def search_sets(t, offsets, freq, nharm, stat):
+def search_sets(t, offsets, freq, nharm, stat, flags=0):
     """One-trial Z^2 / H of many photon sets (crimp_search_sets): set i = t[offsets[i]:offsets[i+1]] (seconds) at
-    freq[i], each with its own t0 = (first + last)/2. fp64."""
+    freq[i], each with its own t0 = (first + last)/2. fp64. ``flags`` N.FLAG_ASYNC (device tensors): returns with the
+    kernel queued on the current stream; synchronise with it before reading the result."""
     L = N.load()
     b = N.Buffers()
     tp = b.arg(t, np.float64)
@@ -135,7 +136,7 @@ def search_sets(t, offsets, freq, nharm, stat):
     out = _empty_like_input(t, nset, b)
     outp = b.arg(out, np.float64, writable=True)
     with b.device_guard():
-        N.check(L.crimp_search_sets(tp, op, nset, fp, int(nharm), int(stat), outp, b.flags(), b.stream()))
+        N.check(L.crimp_search_sets(tp, op, nset, fp, int(nharm), int(stat), outp, b.flags(flags), b.stream()))
     return out
 
 

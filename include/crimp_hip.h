@@ -49,6 +49,8 @@ extern "C" {
                                        mean power, not per trial; faster */
 #define CRIMP_FLAG_NO_FIXUP 1024u   /* search (diagnostic): the exact kernel's raw powers, without the fp64 fix-up
                                        of the trials its error bound cannot certify (crimp_last_fixups counts them) */
+#define CRIMP_FLAG_ASYNC 2048u     /* crimp_search_sets with device pointers: return once the kernel is queued, without
+                                     * draining the stream (the caller synchronises it before reading out) */
 
 #define CRIMP_STAT_Z2 0 /* Z^2_m  (periodsearch.py:57-71, :73-106) */
 #define CRIMP_STAT_H 1  /* H-test (periodsearch.py:109-125)         */
