@@ -2629,8 +2629,8 @@ static int toa_fit_impl(const double* x, const int64_t* offsets, int64_t nint, c
             }
             // Lazy-norm certificate (crimp_toa_fit_redchi2, whose histogram is at hand; CRIMP_TOA_NO_CERT: off): a lazy
             // point (norm n0, phi_k) is invalid when some photon has h <= -n0; it does where a bin b holds photons and
-            // the template's bound over that bin at phi_k (tpl_bin_max) is <= -n0 - 1e-3 (the margin covers the
-            // kernel's fp32 h). With the start rule decided by hb too (as kGridNoMin), the grid then needs no min h:
+            // the template's bound over that bin at phi_k (tpl_bin_max) is <= -n0 - margin (1e-3 + 1e-5 of the
+            // amplitude sum and n0: it covers the kernel's fp32 h). With the start rule decided by hb too (as kGridNoMin), the grid then needs no min h:
             // k_toa_grid_best marks those points -inf from the counts, and one it cannot show invalid reruns the grid
             // with the min (the flag below). Used only when every (lazy norm, phi_k) has such a bin.
             if (rq && nlazy > 0 && mode == kGridProd8 && rq->nbins <= 64 && getenv("CRIMP_TOA_NO_CERT") == nullptr) {
@@ -2659,12 +2659,17 @@ static int toa_fit_impl(const double* x, const int64_t* offsets, int64_t nint, c
                             hrow[(size_t)(i * nlazy + z)] = (int)r;
                         }
                     std::vector<uint64_t> hmask(vals.size() * (size_t)nphi, 0);
+                    // margin over the kernel's h: its f16 hi/lo terms and fp32 sums err by <~ 1e-6 of the amplitude
+                    // sum and of the norm inside the accumulators (k_toa_grid_mf), so 1e-5 of them plus 1e-3
+                    double asum = 0.0;
+                    for (int j = 0; j < T.K; ++j) asum += std::fabs(T.amp[j]);
                     bool all_k = true;
                     for (size_t r = 0; r < vals.size(); ++r)
                         for (int64_t k = 0; k < nphi; ++k) {
+                            const double margin = 1e-3 + 1e-5 * (asum + std::fabs(vals[r]));
                             uint64_t m = 0;
                             for (int b = 0; b < nb; ++b)
-                                if (bm[(size_t)k * nb + b] + 1e-3 <= -vals[r]) m |= 1ull << b;
+                                if (bm[(size_t)k * nb + b] + margin <= -vals[r]) m |= 1ull << b;
                             hmask[r * (size_t)nphi + (size_t)k] = m;
                             all_k = all_k && m != 0;
                         }

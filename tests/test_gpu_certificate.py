@@ -238,7 +238,8 @@ def test_fast_brute_grid_equals_full_kernel(gpu, monkeypatch):
 def test_lazy_norm_certificate_equals_min_path(gpu, monkeypatch):
     """The brute grid's lazy-norm certificate (kGridCert: the lazy points shown invalid by photon-holding histogram
     bins whose template bound is below -norm, no per-phShift min h) against the same kernel with the min
-    (CRIMP_TOA_NO_CERT): identical records and redChi2 for config-5-style intervals, host and device inputs; and no
+    (CRIMP_TOA_NO_CERT): identical records and redChi2 for config-5-style intervals, host and device inputs, and the
+    same shape 2 times brighter and 100 times fainter; and no
     certificate where no norm is lazy (a weak template: every candidate norm valid everywhere)."""
     from crimp_amd import _native as N
     from crimp_amd.synth import template_intervals_torch
@@ -246,12 +247,18 @@ def test_lazy_norm_certificate_equals_min_path(gpu, monkeypatch):
     from bench import T2259, _tmpl
     x, off, E, _ = template_intervals_torch(300, 50_000, T2259["norm"]["value"], T2259["amp"], T2259["ph"], seed=8,
                                             device=gpu)
-    for xs, os_ in ((x, off), (x.cpu().numpy(), off.cpu().numpy())):
+    for scale, (xs, os_) in ((1.0, (x, off)), (1.0, (x.cpu().numpy(), off.cpu().numpy())), (2.0, (x, off)),
+                             (0.01, (x, off))):
+        tm = _tmpl()  # the same shape 2 times brighter / 100 times fainter (lmfit's lattice keeps a lazy lowest norm)
+        for k in tm:
+            if k == "norm" or k.startswith("amp_"):
+                tm[k] = {"value": tm[k]["value"] * scale}
+        Es = E / scale
         monkeypatch.delenv("CRIMP_TOA_NO_CERT", raising=False)
-        a = ToAFitter(xs, os_, E, _tmpl()).fit(brutemin=True)
+        a = ToAFitter(xs, os_, Es, tm).fit(brutemin=True)
         assert N.load().crimp_last_toa_grid_fast() == 6
         monkeypatch.setenv("CRIMP_TOA_NO_CERT", "1")
-        b = ToAFitter(xs, os_, E, _tmpl()).fit(brutemin=True)
+        b = ToAFitter(xs, os_, Es, tm).fit(brutemin=True)
         assert N.load().crimp_last_toa_grid_fast() == 2
         for k in a:
             np.testing.assert_array_equal(np.asarray(a[k]), np.asarray(b[k]), err_msg=k)
