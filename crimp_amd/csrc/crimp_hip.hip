@@ -1029,8 +1029,10 @@ __global__ __launch_bounds__(kGridBlock) __attribute__((amdgpu_waves_per_eu(4)))
 // fp32 factor is carried as hi + lo f16 (search_fast.h split_xy; |x - hi - lo| <= 2^-22 |x|) and the four exact
 // products hi.hi, hi.lo, lo.hi, lo.lo of each term fill K = 8 per harmonic of v_mfma_f32_32x32x16_f16 (two harmonics
 // per instruction, fp32 accumulation). The VALU is left with the likelihood part: per point and evaluated norm an
-// add, 3/4 of a multiply and 1/4 of a v_log_f32 (log2 of products of 4 photons, as k_toa_grid), and the min.
-// Block: 4 waves, wave w owns the 32 phShift columns 128 bx + 32 w + (lane & 31); a 128-photon tile's A fragments
+// add, 3/4 of a multiply and 1/4 of a v_log_f32 (log2 of products of 4 photons, as k_toa_grid), and the min -- or,
+// on crimp_toa_fit's certified modes, 7/8 of a multiply and 1/8 of a log (PROD 8), no add (CIN: the accumulators
+// start at the norm) and no min (HMIN false).
+// Block: 4 waves, wave w owns the 32 phShift columns 128 bx + 32 w + (lane & 31); a kGmTile-photon tile's A fragments
 // (per photon and harmonic 16 bytes: hi, hi, lo, lo of cos then of sin) are built once per tile in LDS by the whole
 // block. MFMA result i of lane l is photon (i & 3) + 8 (i >> 2) + 4 (l >> 5) of the 32-photon chunk, phShift column
 // l & 31, so each lane multiplies 4 consecutive photons per group; the two lane halves' sums of a column are added
