@@ -19,6 +19,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <chrono>
 #include <functional>
 #include <vector>
 
@@ -2432,6 +2433,28 @@ __global__ __launch_bounds__(64) void k_toa_chi2(const unsigned long long* __res
                                                  const double* __restrict__ centers, int nb, int nfree,
                                                  double* __restrict__ out);
 
+// CRIMP_TOA_HOST_TRACE=1 (diagnostic): host-side phase times of each crimp_toa_fit(_redchi2) call on stderr
+struct HostTrace {
+    bool on;
+    std::chrono::steady_clock::time_point t0, last;
+    std::string line;
+    HostTrace() : on(getenv("CRIMP_TOA_HOST_TRACE") != nullptr) {
+        if (on) t0 = last = std::chrono::steady_clock::now();
+    }
+    void mark(const char* what) {
+        if (!on) return;
+        const auto t = std::chrono::steady_clock::now();
+        char b[96];
+        snprintf(b, sizeof(b), " %s %.1f", what, std::chrono::duration<double, std::micro>(t - last).count());
+        line += b;
+        last = t;
+    }
+    ~HostTrace() {
+        if (on) fprintf(stderr, "toa host trace (us):%s total %.1f\n", line.c_str(),
+                        std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+    }
+};
+
 static int toa_fit_impl(const double* x, const int64_t* offsets, int64_t nint, const crimp_template* tpl,
                         const double* exposure, double norm0, int32_t ph_shift_res, int32_t options, double* out,
                         uint32_t flags, void* stream, const RedChi2Req* rq) {
@@ -2452,6 +2475,7 @@ static int toa_fit_impl(const double* x, const int64_t* offsets, int64_t nint, c
     }
     const bool dev = flags & CRIMP_FLAG_DEVICE_PTRS;
     hipStream_t s = as_stream(stream);
+    HostTrace ht;
     g_last_grid_norms = 0;
     g_last_grid_fast = 0;
     std::vector<int64_t> hoff((size_t)nint + 1);
@@ -2464,6 +2488,7 @@ static int toa_fit_impl(const double* x, const int64_t* offsets, int64_t nint, c
     for (int64_t i = 0; i < nint; ++i)
         ARGCHK(hoff[i + 1] > hoff[i] && hoff[i] >= 0,
                "every ToA interval needs photons (measureToAs.py:182 fails on an empty one)");
+    ht.mark("offsets");
     // measureToAs.py:715-725 / :757-771 (readvaryparam=False) and :320-376
     FitCfg C;
     C.lo = norm0 / 100.0;
@@ -2518,6 +2543,7 @@ static int toa_fit_impl(const double* x, const int64_t* offsets, int64_t nint, c
                 HIPCHK(hipGetLastError());
             }
         }
+        ht.mark("stage+hist");
         TplDev* dT = nullptr;
         double* dstart = nullptr;
         HIPCHK(sc.alloc(&dT, 1));
@@ -2808,8 +2834,10 @@ static int toa_fit_impl(const double* x, const int64_t* offsets, int64_t nint, c
             (void)hipEventDestroy(e1);
             return r2;
         };
+        ht.mark("setup");
         rc = all(grid_mode);
         if (rc) return rc;
+        ht.mark("launch");
         if (run_brute && (grid_mode & kGridProd8) && !(grid_mode & kGridNoMin)) {
             // the runtime half of the certificates (eight factors, lazy norms): a flagged lattice point reruns the
             // grid and the fits with the full four-factor kernel
@@ -2821,6 +2849,7 @@ static int toa_fit_impl(const double* x, const int64_t* offsets, int64_t nint, c
                 if (rc) return rc;
             }
         }
+        ht.mark("unsafe");
         if (rq) {  // redChi2 from the final records
             if (ebin.e) HIPCHK(hipStreamWaitEvent(s, ebin.e, 0));
             k_toa_chi2<<<(unsigned)nint, 64, 0, s>>>(dcnt, T, de, dout, dcen, rq->nbins, rq->nfree, dred);
@@ -2829,6 +2858,7 @@ static int toa_fit_impl(const double* x, const int64_t* offsets, int64_t nint, c
         }
         HIPCHK(copy_back(s, out, dout, (size_t)nint * 8, dev));
         HIPCHK(hipStreamSynchronize(s));
+        ht.mark("chi2+sync");
     }
     return finish(s, flags);
 }
