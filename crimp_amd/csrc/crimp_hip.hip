@@ -206,6 +206,38 @@ static hipError_t copy_back(hipStream_t s, T* host, const T* devp, size_t count,
 
 // blocking host <-> device copies of small host-side tables
 static hipError_t h2d(void* d, const void* h, size_t bytes) { return hipMemcpy(d, h, bytes, hipMemcpyHostToDevice); }
+
+// Page-locked staging of a call's small host->device uploads (crimp_toa_fit: template, lattice, candidate norms,
+// certificate masks): copied into one hipHostMalloc'd buffer and queued with hipMemcpyAsync on the call's stream, so
+// the host does not wait for each pageable copy (~290 us of setup before the first kernel, profiles/r04). Calls are
+// serialised by g_mutex and drain their stream before returning, so the buffer is free again at the next call.
+struct PinnedStage {
+    char* p = nullptr;
+    size_t cap = 0, used = 0;
+};
+static PinnedStage g_pin;
+static void pin_begin(size_t bytes) {
+    g_pin.used = 0;
+    if (g_pin.cap >= bytes) return;
+    if (g_pin.p) (void)hipHostFree(g_pin.p);
+    g_pin.p = nullptr;
+    g_pin.cap = 0;
+    const size_t cap = std::max<size_t>(bytes, size_t(1) << 20);
+    if (hipHostMalloc(reinterpret_cast<void**>(&g_pin.p), cap, hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        g_pin.p = nullptr;  // no staging: h2d_async falls back to the blocking copy
+        return;
+    }
+    g_pin.cap = cap;
+}
+static hipError_t h2d_async(hipStream_t s, void* d, const void* h, size_t bytes) {
+    const size_t need = (bytes + 255) & ~size_t(255);
+    if (!g_pin.p || g_pin.used + need > g_pin.cap) return h2d(d, h, bytes);
+    char* q = g_pin.p + g_pin.used;
+    g_pin.used += need;
+    std::memcpy(q, h, bytes);
+    return hipMemcpyAsync(d, q, bytes, hipMemcpyHostToDevice, s);
+}
 static hipError_t d2h(hipStream_t s, void* h, const void* d, size_t bytes) {
     hipError_t e = hipStreamSynchronize(s);
     if (e != hipSuccess) return e;
@@ -2478,16 +2510,23 @@ static int toa_fit_impl(const double* x, const int64_t* offsets, int64_t nint, c
     HostTrace ht;
     g_last_grid_norms = 0;
     g_last_grid_fast = 0;
+    // the host's copies of the offsets, exposures and (crimp_toa_fit_redchi2) histogram edges: one stream drain for all
     std::vector<int64_t> hoff((size_t)nint + 1);
+    std::vector<double> hexp0((size_t)nint), hedg0(rq ? (size_t)rq->nbins + 1 : 0);
     if (dev) {
-        HIPCHK(d2h(s, hoff.data(), offsets, (nint + 1) * sizeof(int64_t)));
         HIPCHK(hipStreamSynchronize(s));
+        HIPCHK(hipMemcpy(hoff.data(), offsets, (nint + 1) * sizeof(int64_t), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(hexp0.data(), exposure, nint * sizeof(double), hipMemcpyDeviceToHost));
+        if (rq) HIPCHK(hipMemcpy(hedg0.data(), rq->edges, hedg0.size() * sizeof(double), hipMemcpyDeviceToHost));
     } else {
         std::memcpy(hoff.data(), offsets, (nint + 1) * sizeof(int64_t));
+        std::memcpy(hexp0.data(), exposure, nint * sizeof(double));
+        if (rq) std::memcpy(hedg0.data(), rq->edges, hedg0.size() * sizeof(double));
     }
     for (int64_t i = 0; i < nint; ++i)
         ARGCHK(hoff[i + 1] > hoff[i] && hoff[i] >= 0,
                "every ToA interval needs photons (measureToAs.py:182 fails on an empty one)");
+    pin_begin((size_t)65536 + (size_t)nint * 320);
     ht.mark("offsets");
     // measureToAs.py:715-725 / :757-771 (readvaryparam=False) and :320-376
     FitCfg C;
@@ -2547,7 +2586,7 @@ static int toa_fit_impl(const double* x, const int64_t* offsets, int64_t nint, c
         TplDev* dT = nullptr;
         double* dstart = nullptr;
         HIPCHK(sc.alloc(&dT, 1));
-        HIPCHK(h2d(dT, &T, sizeof(T)));
+        HIPCHK(h2d_async(s, dT, &T, sizeof(T)));
         HIPCHK(sc.alloc(&dstart, (size_t)(2 * nint)));
         std::vector<double> hphi, hnrm, hstart, grid_n;
         // the brute grid's state, used by the launches below the setup (run_brute)
@@ -2576,13 +2615,7 @@ static int toa_fit_impl(const double* x, const int64_t* offsets, int64_t nint, c
             // Config 5 and the worked example: 2 of the 20 norms.
             double hlo = 0.0, hhi = 0.0;
             tpl_bounds(T, &hlo, &hhi);
-            std::vector<double> hexp((size_t)nint);
-            if (dev) {
-                HIPCHK(d2h(s, hexp.data(), exposure, nint * sizeof(double)));
-                HIPCHK(hipStreamSynchronize(s));
-            } else {
-                std::memcpy(hexp.data(), exposure, nint * sizeof(double));
-            }
+            const std::vector<double>& hexp = hexp0;
             std::vector<int64_t> alo((size_t)nint), acnt((size_t)nint);
             int64_t ncand = 1;
             for (int64_t i = 0; i < nint; ++i) {
@@ -2614,8 +2647,8 @@ static int toa_fit_impl(const double* x, const int64_t* offsets, int64_t nint, c
                     hnrm[(size_t)(i * nc + c)] = grid_n[(size_t)(alo[(size_t)i] + std::min(c, acnt[(size_t)i] - 1))];
             HIPCHK(sc.alloc(&dphi, (size_t)nphi));
             HIPCHK(sc.alloc(&dnrm, (size_t)(nint * nc)));
-            HIPCHK(h2d(dphi, hphi.data(), nphi * sizeof(double)));
-            HIPCHK(h2d(dnrm, hnrm.data(), nint * nc * sizeof(double)));
+            HIPCHK(h2d_async(s, dphi, hphi.data(), nphi * sizeof(double)));
+            HIPCHK(h2d_async(s, dnrm, hnrm.data(), nint * nc * sizeof(double)));
             // test hook: start the ascent at the brute lattice point itself (not at the rate norm + parabola vertex)
             lattice_start = getenv("CRIMP_TOA_LATTICE_START") != nullptr;
             // Fast brute grid (k_toa_grid_mf, Fourier): without the per-phShift min h when a lower bound hb of h keeps
@@ -2669,12 +2702,7 @@ static int toa_fit_impl(const double* x, const int64_t* offsets, int64_t nint, c
                 }
                 if (srule) {
                     const int nb = rq->nbins;
-                    std::vector<double> hedg((size_t)nb + 1);
-                    if (dev) {
-                        HIPCHK(d2h(s, hedg.data(), rq->edges, (size_t)(nb + 1) * sizeof(double)));
-                    } else {
-                        std::memcpy(hedg.data(), rq->edges, (size_t)(nb + 1) * sizeof(double));
-                    }
+                    const std::vector<double>& hedg = hedg0;
                     const std::vector<double>& bm = tpl_bin_max(T, hphi, hedg.data(), nb);
                     std::vector<double> vals;  // the distinct lazy norms (lattice values)
                     std::vector<int> hrow((size_t)(nint * nlazy));
@@ -2704,8 +2732,8 @@ static int toa_fit_impl(const double* x, const int64_t* offsets, int64_t nint, c
                     if (all_k) {
                         HIPCHK(sc.alloc(&dlzmask, hmask.size()));
                         HIPCHK(sc.alloc(&dlzrow, hrow.size()));
-                        HIPCHK(h2d(dlzmask, hmask.data(), hmask.size() * sizeof(uint64_t)));
-                        HIPCHK(h2d(dlzrow, hrow.data(), hrow.size() * sizeof(int)));
+                        HIPCHK(h2d_async(s, dlzmask, hmask.data(), hmask.size() * sizeof(uint64_t)));
+                        HIPCHK(h2d_async(s, dlzrow, hrow.data(), hrow.size() * sizeof(int)));
                         mode |= kGridCert;
                     }
                 }
@@ -2750,7 +2778,7 @@ static int toa_fit_impl(const double* x, const int64_t* offsets, int64_t nint, c
                 hstart[(size_t)(2 * i)] = norm0;
                 hstart[(size_t)(2 * i + 1)] = 0.0;
             }
-            HIPCHK(h2d(dstart, hstart.data(), 2 * nint * sizeof(double)));
+            HIPCHK(h2d_async(s, dstart, hstart.data(), 2 * nint * sizeof(double)));
         }
         // the fit kernel over intervals [f0, f0 + fn) on stream st
         double* hcache = nullptr;  // per-photon template part for the iterative norm profiles of the 1-sigma scan (only
