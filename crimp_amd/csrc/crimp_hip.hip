@@ -218,7 +218,7 @@ struct PinnedStage {
 static PinnedStage g_pin;
 static void pin_begin(size_t bytes) {
     g_pin.used = 0;
-    if (g_pin.cap >= bytes) return;
+    if (g_pin.cap >= bytes || bytes > (size_t(64) << 20)) return;  // (huge batches: the blocking copies past the cap)
     if (g_pin.p) (void)hipHostFree(g_pin.p);
     g_pin.p = nullptr;
     g_pin.cap = 0;
@@ -2513,11 +2513,27 @@ static int toa_fit_impl(const double* x, const int64_t* offsets, int64_t nint, c
     // the host's copies of the offsets, exposures and (crimp_toa_fit_redchi2) histogram edges: one stream drain for all
     std::vector<int64_t> hoff((size_t)nint + 1);
     std::vector<double> hexp0((size_t)nint), hedg0(rq ? (size_t)rq->nbins + 1 : 0);
+    pin_begin((size_t)65536 + (size_t)nint * 340 + hedg0.size() * 8);
     if (dev) {
-        HIPCHK(hipStreamSynchronize(s));
-        HIPCHK(hipMemcpy(hoff.data(), offsets, (nint + 1) * sizeof(int64_t), hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(hexp0.data(), exposure, nint * sizeof(double), hipMemcpyDeviceToHost));
-        if (rq) HIPCHK(hipMemcpy(hedg0.data(), rq->edges, hedg0.size() * sizeof(double), hipMemcpyDeviceToHost));
+        const size_t bo = (nint + 1) * sizeof(int64_t), be = nint * sizeof(double), bg = hedg0.size() * sizeof(double);
+        const size_t need = ((bo + 255) & ~size_t(255)) + ((be + 255) & ~size_t(255)) + ((bg + 255) & ~size_t(255));
+        if (g_pin.p && need <= g_pin.cap) {  // three async reads into the staging buffer, one drain
+            char* q = g_pin.p;
+            HIPCHK(hipMemcpyAsync(q, offsets, bo, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipMemcpyAsync(q + ((bo + 255) & ~size_t(255)), exposure, be, hipMemcpyDeviceToHost, s));
+            if (rq)
+                HIPCHK(hipMemcpyAsync(q + ((bo + 255) & ~size_t(255)) + ((be + 255) & ~size_t(255)), rq->edges, bg,
+                                      hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+            std::memcpy(hoff.data(), q, bo);
+            std::memcpy(hexp0.data(), q + ((bo + 255) & ~size_t(255)), be);
+            if (rq) std::memcpy(hedg0.data(), q + ((bo + 255) & ~size_t(255)) + ((be + 255) & ~size_t(255)), bg);
+        } else {
+            HIPCHK(hipStreamSynchronize(s));
+            HIPCHK(hipMemcpy(hoff.data(), offsets, bo, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(hexp0.data(), exposure, be, hipMemcpyDeviceToHost));
+            if (rq) HIPCHK(hipMemcpy(hedg0.data(), rq->edges, bg, hipMemcpyDeviceToHost));
+        }
     } else {
         std::memcpy(hoff.data(), offsets, (nint + 1) * sizeof(int64_t));
         std::memcpy(hexp0.data(), exposure, nint * sizeof(double));
@@ -2526,7 +2542,7 @@ static int toa_fit_impl(const double* x, const int64_t* offsets, int64_t nint, c
     for (int64_t i = 0; i < nint; ++i)
         ARGCHK(hoff[i + 1] > hoff[i] && hoff[i] >= 0,
                "every ToA interval needs photons (measureToAs.py:182 fails on an empty one)");
-    pin_begin((size_t)65536 + (size_t)nint * 320);
+    g_pin.used = 0;  // the reads are in the host's vectors: the staging buffer starts over for the uploads
     ht.mark("offsets");
     // measureToAs.py:715-725 / :757-771 (readvaryparam=False) and :320-376
     FitCfg C;
