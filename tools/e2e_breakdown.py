@@ -83,10 +83,13 @@ for k, v in acc.items():
 print("%-13s %8.3f ms" % ("sum", tot), flush=True)
 pin = torch.from_numpy(mjd).pin_memory()
 runs = [("numpy", mjd, b) for b in os.environ.get("BLOCKS", "1,4,d").split(",")] + [("pinned", pin, "d")]
-for name, src, nbk in runs:  # nbk: "1" one shot, "n" n blocks of shares n : ... : 1, "un" n equal blocks, "d" default
+for name, src, nbk in runs:  # nbk: "1" one shot, "n" n blocks of shares n : ... : 1, "un" n equal blocks, "wa/b/..." shares a : b : ..., "d" default
     os.environ.pop("CRIMP_E2E_BLOCKS", None)
     os.environ.pop("CRIMP_E2E_WEIGHTS", None)
-    if nbk.startswith("u"):
+    if nbk.startswith("w"):  # "w1/1/0.5": those shares
+        os.environ.pop("CRIMP_E2E_MIN_PHOTONS", None)
+        os.environ["CRIMP_E2E_WEIGHTS"] = nbk[1:].replace("/", ",")
+    elif nbk.startswith("u"):
         os.environ.pop("CRIMP_E2E_MIN_PHOTONS", None)
         os.environ["CRIMP_E2E_WEIGHTS"] = ",".join(["1"] * int(nbk[1:]))
     elif nbk == "1":
