@@ -2453,9 +2453,11 @@ struct RedChi2Req {
     double* out;
 };
 
-struct EventGuard {  // an event destroyed on every return path (destruction waits for nothing)
+struct EventGuard {  // an event destroyed on every return path (destruction waits for nothing unless wait is set)
     hipEvent_t e = nullptr;
+    bool wait = false;  // synchronise before destroying: the event marks work that uses scratch blocks of this call
     ~EventGuard() {
+        if (e && wait) (void)hipEventSynchronize(e);
         if (e) (void)hipEventDestroy(e);
     }
 };
@@ -2573,7 +2575,10 @@ static int toa_fit_impl(const double* x, const int64_t* offsets, int64_t nint, c
         const double *dedg = nullptr, *dcen = nullptr;
         double* dred = nullptr;
         unsigned long long* dcnt = nullptr;
+        // destroyed before sc releases its blocks: on an error return between the histogram's launch on the
+        // auxiliary stream and the caller stream's wait for it, dcnt stays held until the histogram has finished
         EventGuard ebin;
+        ebin.wait = true;
         if (rq) {
             HIPCHK(stage_in(sc, rq->edges, (size_t)rq->nbins + 1, dev, &dedg));
             HIPCHK(stage_in(sc, rq->centers, (size_t)rq->nbins, dev, &dcen));
@@ -2678,7 +2683,10 @@ static int toa_fit_impl(const double* x, const int64_t* offsets, int64_t nint, c
             int mode = 0;
             bool mf_ok = false;
             gsc = std::ldexp(1.0, grid_mf_scale(T, &mf_ok));
-            if (getenv("CRIMP_TOA_GRID_SLOW") == nullptr && std::isfinite(hb)) {
+            // the fast modes exist on k_toa_grid_mf only (toa_grid_partials' own test): decided once here, so that
+            // a Cauchy / von Mises / K > kGridKMax fit sets up no mode state, certificate or unsafe readback
+            const bool mf_grid = T.model == CRIMP_MODEL_FOURIER && CRIMP_GRID_MFMA && T.K <= kGridKMax && mf_ok;
+            if (mf_grid && getenv("CRIMP_TOA_GRID_SLOW") == nullptr && std::isfinite(hb)) {
                 bool nomin = true, prod8 = true;
                 for (const double nv : hnrm) {
                     nomin = nomin && nv + hb > 0.0;
@@ -2695,13 +2703,20 @@ static int toa_fit_impl(const double* x, const int64_t* offsets, int64_t nint, c
             // Their lattice points are valid only where the per-phShift min h exceeds -norm; k_toa_grid_best marks the
             // rest -inf, as the full grid does, and a valid one sends the grid back to the full evaluation. (Config 5:
             // lmfit's lowest grid norm, norm0/100, is a candidate of every interval and invalid everywhere.)
+            // lazy_uniform: every interval has exactly nlazy leading lazy norms. The certificate below needs it: an
+            // interval with more would have evaluated norms with norm + hb <= 0 that k_toa_grid_best, without the min,
+            // could not judge.
+            bool lazy_uniform = false;
             if ((mode & kGridProd8) && !(mode & kGridNoMin)) {
                 nlazy = nc;
-                for (int64_t i = 0; i < nint && nlazy > 0; ++i) {
+                int64_t zmax = 0;
+                for (int64_t i = 0; i < nint; ++i) {
                     int64_t z = 0;
                     while (z < nc && hnrm[(size_t)(i * nc + z)] + hb <= 0.0) ++z;
                     nlazy = std::min(nlazy, z);
+                    zmax = std::max(zmax, z);
                 }
+                lazy_uniform = zmax == nlazy;
                 if (nlazy >= nc) nlazy = 0;  // every candidate lazy: evaluate them all
             }
             // Lazy-norm certificate (crimp_toa_fit_redchi2, whose histogram is at hand; CRIMP_TOA_NO_CERT: off): a lazy
@@ -2710,7 +2725,8 @@ static int toa_fit_impl(const double* x, const int64_t* offsets, int64_t nint, c
             // amplitude sum and n0: it covers the kernel's fp32 h). With the start rule decided by hb too (as kGridNoMin), the grid then needs no min h:
             // k_toa_grid_best marks those points -inf from the counts, and one it cannot show invalid reruns the grid
             // with the min (the flag below). Used only when every (lazy norm, phi_k) has such a bin.
-            if (rq && nlazy > 0 && mode == kGridProd8 && rq->nbins <= 64 && getenv("CRIMP_TOA_NO_CERT") == nullptr) {
+            if (rq && nlazy > 0 && lazy_uniform && mode == kGridProd8 && rq->nbins <= 64 &&
+                getenv("CRIMP_TOA_NO_CERT") == nullptr) {
                 bool srule = true;
                 for (int64_t i = 0; i < nint && srule; ++i) {
                     const double r = (double)(hoff[i + 1] - hoff[i]) / hexp[(size_t)i];

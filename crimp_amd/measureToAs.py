@@ -306,6 +306,10 @@ def _measure_pipelined(TIMEMJD, tm, tmpl, model, starts, ends, exposures, phShif
     blocks = _shrinking_blocks(n, len(weights) if weights is not None else int(nbk), weights)
     if len(blocks) < 2:
         return None
+    # uploaded photon range of every block: [min lo, max hi) of its intervals (intervals need not be in start order)
+    spans = [(int(np.min(lo[b0:b1])), int(np.max(hi[b0:b1]))) for b0, b1 in blocks]
+    if not _gaps_sorted(t, spans):
+        return None
     E = np.asarray(exposures, dtype=np.float64)
     dev = torch.device("cuda", torch.cuda.current_device())
     up = _UPLOAD_STREAMS.get(dev.index)
@@ -319,8 +323,7 @@ def _measure_pipelined(TIMEMJD, tm, tmpl, model, starts, ends, exposures, phShif
 
     def uploader():
         try:
-            for k, (b0, b1) in enumerate(blocks):
-                a, b = int(lo[b0]), int(np.max(hi[b0:b1]))
+            for k, (a, b) in enumerate(spans):
                 with torch.cuda.stream(up):
                     d = src[a:b].to(dev, non_blocking=pinned)
                     ev = torch.cuda.Event()
@@ -398,6 +401,26 @@ def _measure_pipelined(TIMEMJD, tm, tmpl, model, starts, ends, exposures, phShif
 # 21.2 ms against 26.1 one-shot and 21.1-22.5 for 50/23/15/12 %; 12 equal blocks fall behind (24.9 ms)
 # (profiles/r04/e2e_sched.log, e2e_trace_*.log).
 _E2E_WEIGHTS = (1.0,) * 8
+
+
+def _gaps_sorted(t, spans):
+    """Host half of the pipelined path's sortedness check: the photons that no block uploads (before the first
+    block, between blocks, after the last) are non-decreasing and join the uploaded ranges in order; the device
+    checks every uploaded range and the joins between consecutive blocks. Together they cover every photon, as the
+    reference's mask over the whole array (measureToAs.py:173) does. Blocks whose ranges overlap or run backwards
+    are not pipelined (False)."""
+    N = t.size
+    edges = [0]
+    for a, b in spans:
+        if a < edges[-1]:
+            return False
+        edges += [a, b]
+    edges.append(N)
+    for g0, g1 in zip(edges[0::2], edges[1::2]):  # gaps [g0, g1), each with one neighbour on either side
+        s = t[max(g0 - 1, 0):min(g1 + 1, N)]
+        if s.size > 1 and not np.all(s[1:] >= s[:-1]):
+            return False
+    return True
 
 
 def _shrinking_blocks(counts, nblocks, weights=None):

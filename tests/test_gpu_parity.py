@@ -567,11 +567,21 @@ def test_measure_intervals_blocks_equal_one_shot(gpu, monkeypatch):
 
     unsorted = mjd.copy()
     unsorted[offh[4] + 5], unsorted[offh[4] + 6] = mjd[offh[4] + 6], mjd[offh[4] + 5]
-    for src, en in ((mjd, ends), (mjd, ends_gap), (torch.from_numpy(mjd).pin_memory(), ends), (unsorted, ends)):
+    # an out-of-order photon that no block uploads (after the last interval) whose time lies inside interval 1: the
+    # reference's mask counts it; the host gap check sends the call to the one-shot path, which does too
+    ends_tail = ends.copy()
+    ends_tail[-1] = mjd[offh[-1] - 30] + 1e-9
+    stray = mjd.copy()
+    stray[offh[-1] - 5] = mjd[offh[1] + 100] + 1e-10
+    perm = np.array([2, 0, 5, 1, 4, 3])  # intervals out of start order (the block's upload starts at its min lo)
+    cases = ((mjd, starts, ends, E), (mjd, starts, ends_gap, E), (torch.from_numpy(mjd).pin_memory(), starts, ends, E),
+             (unsorted, starts, ends, E), (mjd, starts[perm], ends[perm], np.asarray(E)[perm]),
+             (stray, starts, ends_tail, E))
+    for src, st, en, ex in cases:
         monkeypatch.setenv("CRIMP_E2E_MIN_PHOTONS", str(1 << 40))
-        one = measure_intervals(src, par, tm, starts, en, E, brutemin=True)
+        one = measure_intervals(src, par, tm, st, en, ex, brutemin=True)
         monkeypatch.setenv("CRIMP_E2E_MIN_PHOTONS", "1000")  # blocks of 3, 2 and 1 intervals
-        same(one, measure_intervals(src, par, tm, starts, en, E, brutemin=True))
+        same(one, measure_intervals(src, par, tm, st, en, ex, brutemin=True))
 
 
 def test_measuretoas_rows_before_empty_interval(gpu, tmp_path, monkeypatch):
