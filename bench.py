@@ -16,7 +16,9 @@ Also reported:
   time from hipEvents around the harmonic-sum kernels on their stream; ``traffic`` from the same tree's rocprofv3
   PMC pass (profiles/r04/pmc_traffic.json, tools/pmc_round.sh) when it was taken on this workload;
 * ``cpu_baseline``: the oracle (oracle/liborc.so, fp64, OpenMP over trials) on a bounded sample;
-* ``fast_path``: the opt-in fp32 sin/cos path (precision="fast") on the same workload, for comparison;
+* ``nufft``: precision="nufft" (csrc/search_nufft.h) on the same workload: equivalent photon x trial evals/s (the
+  same per-trial results, not pairwise evaluations), its kernels' times (spread / merge / FFT / combine+finalize) and
+  the roofline of each against HBM or the fp64 peak;
 * ToA (config 5 per GPU): the device fit of 1250 intervals x 1e5 photons, and the end-to-end ``measure_intervals``
   (interval selection, calcphase, fits, per-interval H-test) from host MJD arrays, with the oracle's fits on all
   allowed host cores as its CPU baseline (a sample, extrapolated) and the fits' VALU roofline;
@@ -57,7 +59,7 @@ def parse():
     p.add_argument("--nharm", type=int, default=2)
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline legs")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
-    p.add_argument("--no-fast", action="store_true", help="skip the fast-path comparison")
+    p.add_argument("--no-nufft", action="store_true", help="skip the NUFFT search leg")
     p.add_argument("--toa-intervals", type=int, default=1250, help="ToA intervals per GPU (config 5: 1e4 over 8)")
     p.add_argument("--toa-photons", type=int, default=100_000)
     p.add_argument("--no-toa", action="store_true", help="skip the ToA legs")
@@ -492,6 +494,66 @@ def cpu_baseline(t, f0, df, nharm, budget_s):
                 n, m, nharm, el)}
 
 
+PEAK_F64_TFLOPS = 78.6  # MI355X spec fp64 (vector and matrix); mb_f64 measures 58 TF VALU FMA, 33.5 TF f64 MFMA
+
+
+def nufft_leg(a, t, t_h, f, rank, M, steps):
+    """The rank's trial slice by precision="nufft": one untimed search, then ``steps`` timed ones (wall time with the
+    stream drained, and the library's hipEvent spans: whole pipeline, spread, merge, FFT, combine + finalize). The
+    per-kernel rooflines use the plan the library chose (n = FFT length, P moments):
+      spread  fp64: the cell gather's ~30 + 3 P operations per photon and harmonic (k_nu_gather), or the MFMA form's
+              512 issued flops per photon-harmonic (k_nu_spread), against the fp64 peak;
+      merge   HBM: slots read + the FFT input written, 16 B per complex value;
+      fft     HBM: two passes, each reading and writing P * rows * n complex values per harmonic;
+      combine HBM: P complex values read per trial and harmonic."""
+    import torch
+    from crimp_amd import ops
+    from crimp_amd import _native as N
+    t0 = (t_h[0] + t_h[-1]) / 2
+    out = torch.empty(M, dtype=torch.float64, device=t.device)
+    ops.search(t, t0, f, a.nharm, 0, first=rank * M, count=M, out=out, precision="nufft")
+    torch.cuda.synchronize()
+    walls, spans = [], []
+    for _ in range(steps):
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        ops.search(t, t0, f, a.nharm, 0, first=rank * M, count=M, out=out, precision="nufft",
+                   flags=N.FLAG_TIME_KERNELS)
+        torch.cuda.synchronize()
+        walls.append(time.perf_counter() - t2)
+        spans.append(N.last_kernel_times())
+    path = N.load().crimp_last_search_path()
+    nfix = N.load().crimp_last_fixups()
+    wall = float(np.mean(walls))
+    sp = np.mean(np.array([s_[:5] for s_ in spans]), axis=0)  # total, spread, merge, fft, combine+finalize
+    n, P, form = N.last_nufft_plan()  # search_nufft.h nu_plan: least n P with x^P/P! <= 1e-14, x = pi (M/2) / n
+    m = a.nharm
+    # spread: the cell gather's fp64 work per photon and harmonic (premultiplier 2 two-products + cis ~ 30, then
+    # 3 per moment), or the MFMA form's issued 512 flops per photon-harmonic
+    spread_flops = (30.0 + 3.0 * P if form == "gather" else 512.0) * float(a.photons) * m
+    fft_bytes = 2 * 2 * 16.0 * P * n * m
+    merge_bytes = 16.0 * P * n * m * 2
+    comb_bytes = 16.0 * P * n * m
+    legs = {
+        "spread": {"bound": "fp64", "achieved": spread_flops / (sp[1] * 1e-3) / 1e12, "peak": PEAK_F64_TFLOPS,
+                   "unit": "TFLOP/s", "ms": sp[1]},
+        "merge": {"bound": "hbm", "achieved": merge_bytes / (sp[2] * 1e-3) / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                  "ms": sp[2]},
+        "fft": {"bound": "hbm", "achieved": fft_bytes / (sp[3] * 1e-3) / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "ms": sp[3]},
+        "combine": {"bound": "hbm", "achieved": comb_bytes / (sp[4] * 1e-3) / 1e9, "peak": PEAK_HBM_GBS,
+                    "unit": "GB/s", "ms": sp[4]},
+    }
+    for v in legs.values():
+        v["frac"] = v["achieved"] / v["peak"]
+    dom = max(legs, key=lambda k: legs[k]["ms"])
+    return {"evals_per_s": float(a.photons) * M / wall, "unit": "equivalent photon*trial evals/s (Z^2_%d)" % m,
+            "ms_per_search": wall * 1e3, "pipeline_ms": sp[0], "search_path": path, "fp64_fixup_trials": nfix,
+            "plan": {"fft_length": n, "moments": P, "spread": form}, "kernels": legs, "dominant": dom,
+            "roofline": dict({"kernel": dom}, **legs[dom]),
+            "precision": "fp64 moments (v_mfma_f64_16x16x4_f64), fp64 FFT, per-trial 1e-6 certificate + fp64 fix-up"}
+
+
 def pmc_traffic(photons, trials, nharm):
     """HBM bytes per search of this workload from the tree's own rocprofv3 PMC pass (tools/pmc_exact.sh ->
     profiles/r04/pmc_traffic.json), or None if that pass was not taken on this workload."""
@@ -637,16 +699,8 @@ def main():
         }
         if not a.no_cpu and world == 1:  # rank 0 at N=1 only
             rec["cpu_baseline"] = cpu_baseline(t_h, f0, df, a.nharm, a.cpu_seconds)
-        if not a.no_fast:  # the opt-in fp32 sin/cos path on the same inputs (not the metric)
-            t0 = (t_h[0] + t_h[-1]) / 2
-            out = torch.empty(M, dtype=torch.float64, device=dev)
-            ops.search(t, t0, f, a.nharm, 0, first=rank * M, count=M, out=out, precision="fast")
-            torch.cuda.synchronize()
-            t2 = time.perf_counter()
-            ops.search(t, t0, f, a.nharm, 0, first=rank * M, count=M, out=out, precision="fast")
-            torch.cuda.synchronize()
-            rec["fast_path"] = {"evals_per_s": float(a.photons) * M / (time.perf_counter() - t2),
-                                "precision": "fp32 sin/cos + f16-split MFMA: 1e-6 of the mean power, not per trial"}
+        if not a.no_nufft:  # precision="nufft" on the same inputs, beside the exact path
+            rec["nufft"] = nufft_leg(a, t, t_h, f, rank, M, a.steps)
     del t, f
     torch.cuda.empty_cache()
     if not a.no_calcphase and rank == 0:

@@ -18,14 +18,12 @@ LIB_PATH = os.environ.get("CRIMP_LIB") or os.path.join(_HERE, "lib", "libcrimp_h
 
 FLAG_DEVICE_PTRS = 1
 FLAG_SYNC = 2
-FLAG_FORCE_DIRECT = 4
 FLAG_FORCE_MFMA = 8
-FLAG_HW_SINCOS = 16
 FLAG_TIME_KERNELS = 128
 FLAG_F64 = 256
-FLAG_FAST = 512
 FLAG_NO_FIXUP = 1024
 FLAG_ASYNC = 2048
+FLAG_NUFFT = 4096
 
 STAT_Z2 = 0
 STAT_H = 1
@@ -57,7 +55,7 @@ class Template(ctypes.Structure):
 
 
 EXPORTS = ("crimp_version", "crimp_last_error", "crimp_last_kernel_ms", "crimp_last_kernel_times", "crimp_last_fixups",
-           "crimp_last_toa_grid_norms", "crimp_last_toa_grid_fast", "crimp_release_scratch",
+           "crimp_last_search_path", "crimp_last_nufft_plan", "crimp_last_toa_grid_norms", "crimp_last_toa_grid_fast", "crimp_release_scratch",
            "crimp_device_count", "crimp_calcphase", "crimp_search", "crimp_search_sets", "crimp_toa_points",
            "crimp_toa_grid", "crimp_toa_fit", "crimp_toa_redchi2", "crimp_toa_fit_redchi2", "crimp_toa_shape_points", "crimp_binphases")
 
@@ -86,6 +84,7 @@ def load(require_device=True):
             L.crimp_last_toa_grid_norms.restype = ctypes.c_int64
             L.crimp_last_toa_grid_fast.restype = ctypes.c_int64
             L.crimp_last_kernel_times.argtypes = [ctypes.POINTER(ctypes.c_double), i32]
+            L.crimp_last_nufft_plan.argtypes = [ctypes.POINTER(i64), ctypes.POINTER(i32), ctypes.POINTER(i32)]
             L.crimp_device_count.argtypes = [ctypes.POINTER(i32)]
             L.crimp_calcphase.argtypes = [P, i64, ctypes.POINTER(TimingModel), i32, P, P, u32, P]
             L.crimp_search.argtypes = [P, i64, ctypes.c_double, P, i64, P, i64, i32, i32, i64, i64, P, u32, P]
@@ -111,6 +110,14 @@ def load(require_device=True):
                                        "(there is no CPU fallback)")
             _dev_ok = True
     return _lib
+
+
+def last_nufft_plan():
+    """(FFT length, moments, spread form: 'gather' | 'mfma') of the last NUFFT search (crimp_last_nufft_plan)."""
+    L = load(require_device=False)
+    n, p, g = ctypes.c_int64(0), ctypes.c_int32(0), ctypes.c_int32(0)
+    L.crimp_last_nufft_plan(ctypes.byref(n), ctypes.byref(p), ctypes.byref(g))
+    return int(n.value), int(p.value), "gather" if g.value else "mfma"
 
 
 def last_kernel_times():

@@ -5,8 +5,8 @@
 //   1. runtime helpers (errors, stream-ordered scratch, staging of host buffers)
 //   2. fp32 sin/cos in revolutions (polynomial and hardware v_sin/v_cos)
 //   3. calcphase            -- HBM-bound fp64 phase folding
-//   4. periodicity search   -- exact i8-MFMA kernel (search_exact.h, default), fp64 kernel, fast f16-MFMA /
-//                              fp32 kernels (search_fast.h, opt-in), finalize
+//   4. periodicity search   -- exact i8-MFMA kernel (search_exact.h, default), NUFFT (search_nufft.h,
+//                              opt-in), fp64 kernel, finalize
 //   5. ToA likelihood scan  -- fp64 point evaluator, fp32 brute grid, binning
 //   6. C-ABI
 #include <hip/hip_runtime.h>
@@ -275,20 +275,6 @@ __device__ __forceinline__ void sincos_rev_poly(float r, float& s, float& c) {
     c = ((iq + 1) & 2) ? -c_a : c_a;
 }
 
-// Hardware transcendental: v_sin_f32 / v_cos_f32 take revolutions (D = sin(2*pi*S0)).
-__device__ __forceinline__ void sincos_rev_hw(float r, float& s, float& c) {
-    s = __builtin_amdgcn_sinf(r);
-    c = __builtin_amdgcn_cosf(r);
-}
-
-template <bool HW>
-__device__ __forceinline__ void sincos_rev(float r, float& s, float& c) {
-    if (HW)
-        sincos_rev_hw(r, s, c);
-    else
-        sincos_rev_poly(r, s, c);
-}
-
 // ============================================================== 3. calcphase
 struct CPModel {
     double pepoch;
@@ -375,11 +361,12 @@ __global__ __launch_bounds__(256) void k_calcphase_scalar(const double* __restri
 }
 
 // ============================================================== 4. periodicity search
-// Three kernels compute the per-trial harmonic sums C_k, S_k (periodsearch.py:67-69, :93-99, :120-121):
+// Three paths compute the per-trial harmonic sums C_k, S_k (periodsearch.py:67-69, :93-99, :120-121):
 //   k_search_exact (search_exact.h, the default for arithmetic-progression grids): i8 MFMA, exact integer sums;
+//   the NUFFT (search_nufft.h, opt-in CRIMP_FLAG_NUFFT, progressions of time-sorted photons): fp64 moments on
+//                   the f64 matrix cores, fp64 FFT, fp64 Horner sums;
 //   k_search_f64   (any grid; the default when the grid is not a progression or has < 256 trials, and the
-//                   fix-up of trials the exact kernel cannot certify): fp64 throughout;
-//   k_search_fast / k_search_direct (opt-in CRIMP_FLAG_FAST): fp32 sin/cos, f16 MFMA / VALU.
+//                   fix-up of trials the exact and NUFFT paths cannot certify): fp64 throughout.
 // dt[i] = t[i] - t0 (periodsearch.py: self.time - self.t0); dt2 = dt*dt for the 2-D grid.
 __global__ __launch_bounds__(256) void k_search_prep(const double* __restrict__ t, int64_t n, double t0,
                                                      double* __restrict__ dt, double* __restrict__ dt2) {
@@ -398,75 +385,6 @@ constexpr int kSearchFold = 32;
 
 __device__ __forceinline__ int64_t trial_index(const int64_t* __restrict__ tidx, int64_t first, int64_t t) {
     return first + (tidx ? tidx[t] : t);
-}
-
-// fp32 direct kernel (fast path, any grid): harmonics k0 .. k0+G-1 of one pass, centred fractional cycle,
-// fp32 sin/cos in revolutions (polynomial, or v_sin/v_cos with CRIMP_FLAG_HW_SINCOS), angle addition for k>k0,
-// fp32 sums over 32-photon blocks folded into fp64.
-template <int G, bool TWOD, bool FIRST, bool HW>
-__global__ __launch_bounds__(kSearchBlock) void k_search_direct(
-    const double* __restrict__ dt, const double* __restrict__ dt2, int64_t n, int64_t chunk,
-    const double* __restrict__ freq, int64_t nf, const double* __restrict__ c2row, int64_t first,
-    const int64_t* __restrict__ tidx, int64_t count, int k0, int ncomp, double* __restrict__ part) {
-    const int64_t t = (int64_t)blockIdx.x * kSearchBlock + threadIdx.x;
-    const int64_t split = blockIdx.y;
-    const int64_t g = trial_index(tidx, first, t < count ? t : count - 1);
-    const int64_t row = TWOD ? g / nf : 0;
-    const double f = freq[g - row * nf];
-    const double c2 = TWOD ? c2row[row] : 0.0;
-    const double kf = (double)k0;
-    const int64_t i0 = split * chunk;
-    const int64_t i1 = i0 + chunk < n ? i0 + chunk : n;
-
-    double C[G], S[G];
-#pragma unroll
-    for (int k = 0; k < G; ++k) C[k] = S[k] = 0.0;
-
-    for (int64_t ib = i0; ib < i1; ib += kSearchFold) {
-        float pc[G], ps[G];
-#pragma unroll
-        for (int k = 0; k < G; ++k) pc[k] = ps[k] = 0.0f;
-        const int64_t ie = ib + kSearchFold < i1 ? ib + kSearchFold : i1;
-#pragma unroll 4
-        for (int64_t i = ib; i < ie; ++i) {
-            const double d = dt[i];
-            const double ph = TWOD ? fma(f, d, c2 * dt2[i]) : f * d;
-            float s1, c1;
-            sincos_rev<HW>((float)(ph - rint(ph)), s1, c1);
-            float s, c;
-            if (FIRST) {
-                s = s1;
-                c = c1;
-            } else {
-                const double pk = ph * kf;
-                sincos_rev<HW>((float)(pk - rint(pk)), s, c);
-            }
-            pc[0] += c;
-            ps[0] += s;
-#pragma unroll
-            for (int k = 1; k < G; ++k) {
-                const float cn = __builtin_fmaf(c, c1, -s * s1);
-                const float sn = __builtin_fmaf(s, c1, c * s1);
-                c = cn;
-                s = sn;
-                pc[k] += c;
-                ps[k] += s;
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < G; ++k) {
-            C[k] += (double)pc[k];
-            S[k] += (double)ps[k];
-        }
-    }
-    if (t < count) {
-#pragma unroll
-        for (int k = 0; k < G; ++k) {
-            const int comp = 2 * (k0 - 1 + k);
-            part[(split * ncomp + comp) * count + t] = C[k];
-            part[(split * ncomp + comp + 1) * count + t] = S[k];
-        }
-    }
 }
 
 // fp64 kernel: the reference's arithmetic precision end to end. fp64 phase reduced to a centred fractional
@@ -555,7 +473,7 @@ __global__ __launch_bounds__(256) void k_search_finalize(const double* __restric
 }
 
 #include "mfma_drain.h"
-#include "search_fast.h"
+#include "f16_split.h"
 #include "search_exact.h"
 
 // ============================================================== 5. ToA likelihood scan
@@ -1059,7 +977,7 @@ __global__ __launch_bounds__(kGridBlock) __attribute__((amdgpu_waves_per_eu(4)))
 // CRIMP_GRID_MFMA=0 builds the VALU kernel above for them too). The template part of every (photon, phShift)
 // point is a product of the photon's basis (cos jx, sin jx) and the phShift's coefficients (a_j, b_j):
 // h = sum_j a_j cos jx + b_j sin jx, i.e. one (32 photons x 2K) . (2K x 32 phShifts) matrix product per tile. Each
-// fp32 factor is carried as hi + lo f16 (search_fast.h split_xy; |x - hi - lo| <= 2^-22 |x|) and the four exact
+// fp32 factor is carried as hi + lo f16 (f16_split.h split_xy; |x - hi - lo| <= 2^-22 |x|) and the four exact
 // products hi.hi, hi.lo, lo.hi, lo.lo of each term fill K = 8 per harmonic of v_mfma_f32_32x32x16_f16 (two harmonics
 // per instruction, fp32 accumulation). The VALU is left with the likelihood part: per point and evaluated norm an
 // add, 3/4 of a multiply and 1/4 of a v_log_f32 (log2 of products of 4 photons, as k_toa_grid), and the min -- or,
@@ -1669,21 +1587,6 @@ extern "C" int crimp_calcphase(const double* t_mjd, int64_t n, const crimp_timin
     return finish(s, flags);
 }
 
-template <bool TWOD, bool HW>
-static void launch_direct(int G, bool firstk, dim3 grid, hipStream_t s, const double* dt, const double* dt2,
-                          int64_t n, int64_t chunk, const double* fr, int64_t nf, const double* c2, int64_t first,
-                          const int64_t* tidx, int64_t count, int k0, int ncomp, double* part) {
-#define CRIMP_LD(GG, FF)                                                                                          \
-    k_search_direct<GG, TWOD, FF, HW><<<grid, kSearchBlock, 0, s>>>(dt, dt2, n, chunk, fr, nf, c2, first, tidx, \
-                                                                     count, k0, ncomp, part)
-    if (firstk) {
-        if (G == 4) CRIMP_LD(4, true); else if (G == 3) CRIMP_LD(3, true); else if (G == 2) CRIMP_LD(2, true); else CRIMP_LD(1, true);
-    } else {
-        if (G == 4) CRIMP_LD(4, false); else if (G == 3) CRIMP_LD(3, false); else if (G == 2) CRIMP_LD(2, false); else CRIMP_LD(1, false);
-    }
-#undef CRIMP_LD
-}
-
 template <bool TWOD>
 static void launch_f64(int G, dim3 grid, hipStream_t s, const double* dt, const double* dt2, int64_t n, int64_t chunk,
                        const double* fr, int64_t nf, const double* c2, int64_t first, const int64_t* tidx,
@@ -1695,18 +1598,8 @@ static void launch_f64(int G, dim3 grid, hipStream_t s, const double* dt, const 
 #undef CRIMP_LF
 }
 
-// Harmonic groups of the fp32 direct kernel. Inside a group harmonics come from the group's first harmonic
-// (exact fp64 phase) by angle addition with the fundamental. The fp32 sin/cos error is periodic in the quarter
-// turn, so a harmonic k = 0 (mod 4) reached by angle addition from the fundamental inherits a coherent bias
-// (its e^{-ik theta} error component sums over photons); groups therefore start at k = 1 and at every multiple
-// of 4: {1,2,3}, {4..7}, {8..11}, ...
-static int direct_group(int k0, int m) {
-    const int rem = m - k0 + 1;
-    return k0 == 1 ? (rem < 3 ? rem : 3) : (rem < 4 ? rem : 4);
-}
-
-// Per-trial device buffers of a search (fp64 per-split partial sums of the direct / fast kernels, int64 totals of
-// the exact kernel) are bounded by this many bytes (CRIMP_SEARCH_BUDGET_MB, default 2048): a larger trial range
+// Per-trial device buffers of a search (fp64 per-split partial sums of the fp64 kernel, int64 totals of the exact
+// kernel) are bounded by this many bytes (CRIMP_SEARCH_BUDGET_MB, default 2048): a larger trial range
 // is computed in blocks of trials.
 static int64_t part_budget() {
     static int64_t b = -1;
@@ -1730,13 +1623,12 @@ static double fixup_rel() {
     return r;
 }
 
-// Direct (one lane per trial) search over trials first + (tidx ? tidx[t] : t), t < count, of any grid, into
-// out[t] (or out[tidx[t]] with scatter): fp64 kernel (f64) or the fp32 one (fast path). The photon split count
-// is a function of the photon count only.
+// Direct (one lane per trial) fp64 search over trials first + (tidx ? tidx[t] : t), t < count, of any grid, into
+// out[t] (or out[tidx[t]] with scatter). The photon split count is a function of the photon count only.
 static int direct_search(Scratch& sc, hipStream_t s, const double* dt, const double* dt2, int64_t n,
                          const double* freq, int64_t nf, const double* c2, bool twod, int nharm, int stat,
-                         int64_t first, const int64_t* tidx, int64_t count, double* out, bool scatter, bool f64,
-                         bool hw, KernelTimer* kt) {
+                         int64_t first, const int64_t* tidx, int64_t count, double* out, bool scatter,
+                         KernelTimer* kt) {
     const int64_t splits0 = std::max<int64_t>(1, std::min<int64_t>(64, n / 16384));
     const int64_t chunk = cdiv(cdiv(n, splits0), kSearchFold) * kSearchFold;
     const int64_t splits = cdiv(n, chunk);
@@ -1751,24 +1643,11 @@ static int direct_search(Scratch& sc, hipStream_t s, const double* dt, const dou
         const int64_t* bt = tidx ? tidx + b0 : nullptr;
         const int64_t bfirst = tidx ? first : first + b0;
         dim3 grid((unsigned)cdiv(bc, kSearchBlock), (unsigned)splits);
-        int k0 = 1;
-        while (k0 <= nharm && f64) {  // groups of 8, 4, 2, 1 harmonics, each started from its exact phase
+        for (int k0 = 1; k0 <= nharm;) {  // groups of 8, 4, 2, 1 harmonics, each started from its exact phase
             const int rem = nharm - k0 + 1;
             const int G = rem >= 8 ? 8 : rem >= 4 ? 4 : rem >= 2 ? 2 : 1;
             if (twod) launch_f64<true>(G, grid, s, dt, dt2, n, chunk, freq, nf, c2, bfirst, bt, bc, k0, ncomp, part);
             else launch_f64<false>(G, grid, s, dt, dt2, n, chunk, freq, nf, c2, bfirst, bt, bc, k0, ncomp, part);
-            HIPCHK(hipGetLastError());
-            k0 += G;
-        }
-        while (k0 <= nharm) {
-            const int G = direct_group(k0, nharm);
-            if (twod) {
-                if (hw) launch_direct<true, true>(G, k0 == 1, grid, s, dt, dt2, n, chunk, freq, nf, c2, bfirst, bt, bc, k0, ncomp, part);
-                else launch_direct<true, false>(G, k0 == 1, grid, s, dt, dt2, n, chunk, freq, nf, c2, bfirst, bt, bc, k0, ncomp, part);
-            } else {
-                if (hw) launch_direct<false, true>(G, k0 == 1, grid, s, dt, dt2, n, chunk, freq, nf, c2, bfirst, bt, bc, k0, ncomp, part);
-                else launch_direct<false, false>(G, k0 == 1, grid, s, dt, dt2, n, chunk, freq, nf, c2, bfirst, bt, bc, k0, ncomp, part);
-            }
             HIPCHK(hipGetLastError());
             k0 += G;
         }
@@ -1831,41 +1710,6 @@ static int grid_is_progression(Scratch& sc, hipStream_t s, const double* freq, i
     double h[3];
     HIPCHK(d2h(s, h, info, sizeof(h)));
     *ok = std::isfinite(h[0]) && h[0] != 0.0 && h[1] <= 16.0 * 2.220446049250313e-16 * h[2];
-    return CRIMP_OK;
-}
-
-// Fast path (CRIMP_FLAG_FAST): the f16-split kernel over an arithmetic-progression grid.
-static int fast_search(Scratch& sc, hipStream_t s, const double* dt, const double* dt2, int64_t n, const double* freq,
-                       int64_t nf, const double* c2, const double* ap, bool twod, int nharm, int stat, int64_t first,
-                       int64_t count, double* out, KernelTimer* kt) {
-    const int64_t tpr = cdiv(nf, kTile);
-    // up to 64 photon splits of >= 64k photons (a function of the photon count only)
-    const int64_t best_s = std::min<int64_t>(64, std::max<int64_t>(1, n / 65536));
-    const int64_t chunk = cdiv(cdiv(n, best_s), kMfmaChunk) * kMfmaChunk;
-    const int64_t splits = cdiv(n, chunk);
-    const int ncomp = 2 * nharm;
-    const int64_t cbmax = std::max<int64_t>(kTile, part_budget() / (8 * splits * ncomp));
-    const int64_t cb = std::min<int64_t>(count, cdiv(cdiv(count, cdiv(count, cbmax)), kTile) * kTile);
-    double* part = nullptr;
-    HIPCHK(sc.alloc(&part, (size_t)(splits * ncomp * cb)));
-    if (kt) kt->start();
-    for (int64_t b0 = 0; b0 < count; b0 += cb) {
-        const int64_t bfirst = first + b0, bcount = std::min<int64_t>(cb, count - b0);
-        const int64_t last = bfirst + bcount - 1;
-        const int64_t tf = (bfirst / nf) * tpr + (bfirst % nf) / kTile;
-        const int64_t tl = (last / nf) * tpr + (last % nf) / kTile;
-        const int64_t nt = tl - tf + 1;
-        dim3 grid((unsigned)cdiv(nt, 4), (unsigned)splits);
-        for (const HarmGroup& hg : harmonic_groups(nharm)) {
-            if (twod) launch_fast<true>(hg, grid, s, dt, dt2, n, chunk, freq, nf, c2, ap, tf, nt, tpr, bfirst, bcount, ncomp, part);
-            else launch_fast<false>(hg, grid, s, dt, dt2, n, chunk, freq, nf, c2, ap, tf, nt, tpr, bfirst, bcount, ncomp, part);
-            HIPCHK(hipGetLastError());
-        }
-        if (kt && b0 + cb >= count) kt->stop();
-        k_search_finalize<<<(unsigned)cdiv(bcount, 256), 256, 0, s>>>(part, bcount, (int)splits, nharm, stat,
-                                                                     (double)n, nullptr, out + b0);
-        HIPCHK(hipGetLastError());
-    }
     return CRIMP_OK;
 }
 
@@ -2008,6 +1852,17 @@ static int exact_search(Scratch& sc, hipStream_t s, const double* dt, const doub
     return fixup_search(sc, s, dt, dt2, n, freq, nf, c2, twod, nharm, stat, first, flagged, nf_h, out);
 }
 
+#include "search_nufft.h"
+
+extern "C" int crimp_last_search_path(void) { return g_last_search_path; }
+
+extern "C" int crimp_last_nufft_plan(int64_t* fft_length, int32_t* moments, int32_t* gather) {
+    if (fft_length) *fft_length = g_last_nufft_n;
+    if (moments) *moments = g_last_nufft_p;
+    if (gather) *gather = g_last_nufft_gather;
+    return CRIMP_OK;
+}
+
 extern "C" int crimp_search(const double* t, int64_t n, double t0, const double* freq, int64_t nf,
                             const double* log10_negfdot, int64_t nfd, int32_t nharm, int32_t stat, int64_t first,
                             int64_t count, double* out, uint32_t flags, void* stream) {
@@ -2020,8 +1875,10 @@ extern "C" int crimp_search(const double* t, int64_t n, double t0, const double*
     const int64_t total = (twod ? nfd : 1) * nf;
     ARGCHK(first >= 0 && count >= 0 && first + count <= total, "trial range outside the grid");
     const bool f64 = flags & CRIMP_FLAG_F64;
-    const bool fast = flags & (CRIMP_FLAG_FAST | CRIMP_FLAG_FORCE_DIRECT | CRIMP_FLAG_FORCE_MFMA | CRIMP_FLAG_HW_SINCOS);
-    ARGCHK(!(f64 && fast), "CRIMP_FLAG_F64 excludes the fast-path flags");
+    const bool nufft = flags & CRIMP_FLAG_NUFFT;
+    ARGCHK(!(flags & CRIMP_FLAG_RETIRED_FAST), "the fp32 fast search path (flag bits 4, 16, 512) was retired: slower and "
+                                                "less precise than the default path");
+    ARGCHK(!(nufft && f64), "CRIMP_FLAG_NUFFT excludes CRIMP_FLAG_F64");
     if (count == 0) return CRIMP_OK;
     std::lock_guard<std::mutex> lk(g_mutex);
     if (flags & CRIMP_FLAG_TIME_KERNELS) {
@@ -2061,11 +1918,12 @@ extern "C" int crimp_search(const double* t, int64_t n, double t0, const double*
         // sharded search takes the kernel an unsharded search takes:
         //   default: exact i8 kernel for progressions of >= 256 trials per row and < 2^27 photons, fp64 kernel
         //            otherwise (a 2-D grid of short rows would fill its 2048-trial tiles with dead columns);
-        //   fast:    f16-split MFMA kernel for progressions of >= 256 trials per row, fp32 direct kernel otherwise;
+        //   nufft:   the NUFFT for progressions of >= 64 trials per row (per shard segment) and time-sorted photons,
+        //            the default path otherwise;
         //   f64:     fp64 kernel.
         KernelTimer kt(s, flags & CRIMP_FLAG_TIME_KERNELS);
-        bool factorised = !f64 && !(flags & CRIMP_FLAG_FORCE_DIRECT) &&
-                          (nf >= 256 || (flags & CRIMP_FLAG_FORCE_MFMA)) && (fast || n < kExactMaxPhotons);
+        bool factorised = !f64 && (nf >= 256 || (flags & CRIMP_FLAG_FORCE_MFMA) || (nufft && nf >= 64)) &&
+                          (nufft || n < kExactMaxPhotons);
         double* ap = nullptr;
         if (factorised) {
             bool ok = false;
@@ -2075,17 +1933,27 @@ extern "C" int crimp_search(const double* t, int64_t n, double t0, const double*
         }
         if ((flags & CRIMP_FLAG_FORCE_MFMA) && !factorised)
             return set_err(CRIMP_ERR_ARG, "factorised search not applicable (grid is not an arithmetic progression)");
-        int rc;
-        if (factorised && fast) {
-            rc = fast_search(sc, s, ddt, ddt2, n, dfr, nf, dc2, ap, twod, nharm, stat, first, count, dout, &kt);
+        int rc = CRIMP_OK;
+        bool done = false;
+        if (factorised && nufft) {  // NUFFT; unsorted photons or an out-of-range plan fall through to the exact path
+            int64_t nfix = 0;
+            rc = nufft_search(sc, s, ddt, ddt2, n, dfr, nf, twod ? nfd : 1, dc2, ap, twod, nharm, stat, first, count, dout,
+                              flags & CRIMP_FLAG_TIME_KERNELS, &nfix, (flags & CRIMP_FLAG_NO_FIXUP) != 0, &done);
+            if (rc) return rc;
+            if (done) g_last_fixups = nfix;
+            if (!done && n >= kExactMaxPhotons) factorised = false;
+        }
+        if (done) {
         } else if (factorised) {
+            g_last_search_path = 1;
             int64_t nfix = 0;
             rc = exact_search(sc, s, ddt, ddt2, n, dfr, nf, dc2, ap, twod, nharm, stat, first, count, dout, &kt, &nfix,
                               (flags & CRIMP_FLAG_NO_FIXUP) != 0);
             g_last_fixups = nfix;
         } else {
+            g_last_search_path = 0;
             rc = direct_search(sc, s, ddt, ddt2, n, dfr, nf, dc2, twod, nharm, stat, first, nullptr, count, dout,
-                               false, !fast, flags & CRIMP_FLAG_HW_SINCOS, &kt);
+                               false, &kt);
         }
         if (rc) return rc;
         HIPCHK(copy_back(s, out, dout, (size_t)count, dev));

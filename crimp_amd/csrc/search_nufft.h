@@ -1,0 +1,1042 @@
+// search_nufft.h -- Z^2_m / H periodicity search by a non-uniform FFT over an arithmetic-progression trial grid
+// (CRIMP_FLAG_NUFFT, PeriodSearch(..., precision="nufft")). Included by crimp_hip.hip after the exact path's host
+// code (it uses Scratch, grid_is_progression's delta and fixup_search).
+//
+// The reference (periodsearch.py:67, :93-99, :120-121) evaluates, for every trial f_j and harmonic k,
+//   A_k(f_j) = sum_i exp(2 pi i k (f_j dt_i + c2 dt_i^2))        (C_k = Re A_k, S_k = Im A_k)
+// photon by photon: O(N M) per harmonic. On an arithmetic progression f_j = fc + jc delta (jc = j - h, h = nf/2,
+// fc = f_0 + h delta) the sum over trials is a type-1 non-uniform DFT:
+//   A_k(j) = sum_i c_i exp(2 pi i jc u_i / n),   c_i = exp(2 pi i k (fc dt_i + c2 dt_i^2)),   u_i = n k delta dt_i,
+// with n a power of two >= nf. Writing u_i = g_i + e_i (g_i = rint(u_i), |e_i| <= 1/2) and expanding the
+// sub-cell factor exp(2 pi i jc e_i / n) to P terms (Taylor in e_i: "moments"):
+//   A_k(j) = sum_{p<P} (2 pi i jc / n)^p / p! * B_p(jc mod n),   B_p(J) = sum_g b_p[g] exp(2 pi i J g / n),
+//   b_p[g] = sum_{i : g_i = g (mod n)} c_i e_i^p.
+// Per photon the truncation is <= x^P / P! with x = pi |jc| / n (Lagrange remainder of e^{i theta}), so
+// |A_k error| <= N x^P / P! exactly; P <= 16 and n are chosen so that the bound is <= kNuEps at the grid's edge.
+// The cost is O(N m P) for the moments plus O(m P n log n) for the FFTs, against O(N M m) for the direct sum.
+//
+// Kernels (one pass = harmonics k0 .. k0+G-1 of up to 8 trial-grid rows):
+//   k_nu_spread   photons -> per-(chunk, cell) moment sums. Each wave owns a chunk of kNuCW time-ordered photons;
+//                 4 photons x 16 moments form the A operand and 4 photons x 8 rows x (re, im) of c_i the B operand
+//                 of v_mfma_f64_16x16x4_f64, whose accumulator sums the photons of the current cell in fp64 (no
+//                 reduction, no atomics). A cell change (photons are sorted, so cells only grow) flushes the 16 x 16
+//                 tile to the cell's slot: slot(chunk c, cell G) = G - G_min + c is unique per (c, G).
+//   k_nu_merge    slots -> W[batch][g]: every wrapped cell g sums its unwrapped cells G = g (mod n) and, per G, the
+//                 chunks that hold it, in chunk order (deterministic), transposed to batch-major rows.
+//   k_nu_fft_cols, k_nu_fft_rows   four-step FFT (n = n1 n2, Stockham autosort stages of radix 16/8/4/2 in LDS,
+//                 positive exponent); a single row pass for n <= 4096.
+//   k_nu_combine  Horner over the moments at every trial -> (C_k, S_k).
+//   k_nu_finalize Z^2 / H in the reference's formula order and the certificate (fix-up list, as the exact path).
+#pragma once
+
+typedef double nu_f64x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kNuCW = 1024;        // photons per wave chunk (256 K-groups of 4 photons)
+constexpr int kNuWaves = 4;        // chunks per 256-thread block
+constexpr int kNuRows = 8;         // trial-grid rows per pass (8 rows x re/im = the 16 MFMA columns)
+constexpr int kNuMaxP = 16;        // moments of the MFMA spread (its 16 A rows)
+constexpr int kNuGatherMaxP = 24;  // moments of the cell-gather spread (registers)
+constexpr int kNuMergeG = 16;      // wrapped cells per merge block
+constexpr int kNuMaxWrap = 32;     // unwrapped cells per wrapped cell (span of the photons over n)
+constexpr int kNuTile = 4096;      // complex elements per FFT block (64 KB of LDS), 16 per thread
+constexpr double kNuEps = 1e-14;   // truncation bound per photon at the grid's edge
+// Rounding bound per photon for the certificate, in units of |A_k|'s scale N: c_i (cis table + fp64 polynomial,
+// angle-addition over <= 8 harmonics: ~20 ulp), the MFMA's fp64 accumulation over <= 256 K-groups per cell run
+// (<= 256 ulp of the run's sum of |terms|, each <= 1), the merge, the FFT (~3 log2 n ulp) and Horner (e^x ulp):
+// < 4e-14 N; kept at 1e-13 N.
+constexpr double kNuRho = 1e-13;
+
+struct NuPass {          // one spread pass: the slot array of each harmonic k0 + kk
+    int64_t gmin[8];     // unwrapped cell of dt[0]
+    int64_t ubase[8];    // offset (doubles) of the harmonic's slots in U
+};
+
+struct NuTw {            // w_n^t = hi[t >> lbits] * lo[t & (2^lbits - 1)], t in [0, n)
+    const double2* lo;
+    const double2* hi;
+    int lbits;
+    int64_t mask;        // n - 1
+};
+
+__device__ __forceinline__ double2 nu_cmul(double2 a, double2 b) {
+    return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ double2 nu_add(double2 a, double2 b) { return make_double2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ double2 nu_sub(double2 a, double2 b) { return make_double2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ double2 nu_muli(double2 a) { return make_double2(-a.y, a.x); }  // i * a
+
+__device__ __forceinline__ double2 nu_tw(const NuTw& T, int64_t t) {
+    t &= T.mask;
+    return nu_cmul(T.hi[t >> T.lbits], T.lo[t & ((int64_t(1) << T.lbits) - 1)]);
+}
+
+// e^{2 pi i x}, |x| <= 0.5 (+ a few ulp): 1024-entry table of the coarse angle and the fp64 series of the residual
+// angle |theta| <= pi/1024 (omitted terms < 1e-24).
+__device__ __forceinline__ double2 nu_cis(const double2* __restrict__ tab, double x) {
+    const double t = rint(x * 1024.0);
+    const double r = fma(t, -1.0 / 1024.0, x);  // exact
+    const double th = r * 6.283185307179586476925286766559;
+    const double t2 = th * th;
+    const double c = fma(t2, fma(t2, fma(t2, fma(t2, 1.0 / 40320.0, -1.0 / 720.0), 1.0 / 24.0), -0.5), 1.0);
+    const double s = th * fma(t2, fma(t2, fma(t2, fma(t2, 1.0 / 362880.0, -1.0 / 5040.0), 1.0 / 120.0), -1.0 / 6.0), 1.0);
+    const double2 T = tab[((int)t) & 1023];
+    return make_double2(T.x * c - T.y * s, T.x * s + T.y * c);
+}
+
+// frac(a * d) for a = ahi + alo (double-double), as hi part reduced exactly plus the product's rounding error.
+// Contraction off: fused into fma(ahi, d, -rint(p)), the reduction would already hold the rounding error that pe
+// adds again (a phase error of ulp(a d), ~1e-11 cycles at config-3 arguments).
+__device__ __forceinline__ double nu_frac_prod(double ahi, double alo, double d) {
+#pragma clang fp contract(off)
+    const double p = ahi * d;
+    const double pe = fma(ahi, d, -p) + alo * d;
+    return (p - rint(p)) + pe;
+}
+
+// frac(c2 d^2) with d^2 = d2 + d2e (double-double), contraction off as nu_frac_prod
+__device__ __forceinline__ double nu_frac_c2(double c2, double d2, double d2e) {
+#pragma clang fp contract(off)
+    const double qv = c2 * d2;
+    const double qe = fma(c2, d2, -qv) + c2 * d2e;
+    return (qv - rint(qv)) + qe;
+}
+
+// frac(k phi) for |phi| <= 1/2, the product's rounding error carried (contraction off)
+__device__ __forceinline__ double nu_frac_k(double kd, double phi) {
+#pragma clang fp contract(off)
+    const double hk = kd * phi;
+    const double hl = fma(kd, phi, -hk);
+    return (hk - rint(hk)) + hl;
+}
+
+__device__ __forceinline__ int64_t nu_readlane64(int64_t v, int lane) {
+    const int lo = __builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)v, lane);
+    const int hi = __builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), lane);
+    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint64_t)(uint32_t)lo);
+}
+
+// sortedness of dt (the spread's cells only grow along a chunk)
+__global__ __launch_bounds__(256) void k_nu_sorted(const double* __restrict__ dt, int64_t n, int* __restrict__ bad) {
+    int b = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i + 1 < n; i += (int64_t)gridDim.x * blockDim.x)
+        b |= !(dt[i] <= dt[i + 1]);
+    if (__any(b) && (threadIdx.x & 63) == 0) atomicOr(bad, 1);
+}
+
+// host-side scalars of the plan in one read-back: delta, f_0, dt[0], dt[n-1]
+__global__ void k_nu_scalars(const double* __restrict__ ap, const double* __restrict__ freq,
+                             const double* __restrict__ dt, int64_t n, double* __restrict__ out) {
+    if (threadIdx.x == 0) {
+        out[0] = ap[0];
+        out[1] = freq[0];
+        out[2] = dt[0];
+        out[3] = dt[n - 1];
+    }
+}
+
+// Moments of harmonics k0 .. k0+G-1 for rows [0, nrow) of the pass (c2row points at the pass's first row).
+// Lane l: photon q = l >> 4 of the K-group, A row (moment) p = l & 15, B column col = l & 15 = 2 row + (re/im).
+template <int G, bool TWOD>
+__global__ __launch_bounds__(256) void k_nu_spread(const double* __restrict__ dt, int64_t n, int64_t nchunk, double s1,
+                                                   double fch, double fcl, const double* __restrict__ c2row, int nrow,
+                                                   int k0, int P, const NuPass* __restrict__ ps,
+                                                   const double2* __restrict__ tab, double* __restrict__ U,
+                                                   int64_t* __restrict__ ctab) {
+    const int lane = threadIdx.x & 63;
+    const int64_t c = (int64_t)blockIdx.x * kNuWaves + (threadIdx.x >> 6);
+    if (c >= nchunk) return;  // wave-uniform
+    const int q = lane >> 4, col = lane & 15, prow = col >> 1, reim = col & 1, pp = lane & 15;
+    const bool rowok = prow < nrow, pok = pp < P;
+    const double c2 = (TWOD && rowok) ? c2row[prow] : 0.0;
+    const int64_t i0 = c * kNuCW, i1 = i0 + kNuCW < n ? i0 + kNuCW : n;
+    const int64_t SL = 2 * (int64_t)P * nrow;  // doubles per slot: [p][row][re, im]
+    nu_f64x4 acc[G];
+    int64_t gcur[G];
+    {
+        const double u1 = dt[i0] * s1;
+#pragma unroll
+        for (int kk = 0; kk < G; ++kk) {
+            acc[kk] = nu_f64x4{0.0, 0.0, 0.0, 0.0};
+            gcur[kk] = (int64_t)rint((double)(k0 + kk) * u1);
+            if (lane == 0) ctab[(kk * nchunk + c) * 2] = gcur[kk];  // the chunk's first cell
+        }
+    }
+    auto flush = [&](int kk) {
+        const int64_t slot = gcur[kk] - ps->gmin[kk] + c;
+        double* const base = U + ps->ubase[kk] + slot * SL;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int p = q + 4 * r;  // D row of register r
+            if (p < P && rowok) base[(p * nrow + prow) * 2 + reim] = acc[kk][r];
+        }
+        acc[kk] = nu_f64x4{0.0, 0.0, 0.0, 0.0};
+    };
+    // cells the chunk's photons skip (observation gaps): their slots lie inside the chunk's cell range, which the
+    // merge reads, so they are written as zeros
+    auto zero_gap = [&](int kk, int64_t from, int64_t to) {
+        for (int64_t cell = from + 1; cell < to; ++cell) {
+            double* const base = U + ps->ubase[kk] + (cell - ps->gmin[kk] + c) * SL;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int p = q + 4 * r;
+                if (p < P && rowok) base[(p * nrow + prow) * 2 + reim] = 0.0;
+            }
+        }
+    };
+    for (int64_t ib = i0; ib < i1; ib += 64) {
+        const int64_t il = ib + lane;
+        const double dv = dt[il < n ? il : n - 1];  // past the end: the last photon's time (same cell, zero weight)
+#pragma unroll 1
+        for (int g = 0; g < 16; ++g) {
+            if (ib + 4 * g >= i1) break;  // wave-uniform
+            const double d = __shfl(dv, 4 * g + q, 64);
+            const bool valid = ib + 4 * g + q < i1;
+            // premultiplier phase (cycles): frac(fc d) + frac(c2 d^2), in double-double, then harmonic k0
+            double phi = nu_frac_prod(fch, fcl, d);
+            if (TWOD) {
+                const double d2 = d * d, d2e = fma(d, d, -d2);
+                phi += nu_frac_c2(c2, d2, d2e);
+            }
+            phi -= rint(phi);
+            const double2 c1 = nu_cis(tab, phi);
+            double2 ck = c1;
+            if (k0 > 1) ck = nu_cis(tab, nu_frac_k((double)k0, phi));
+            const double u1 = d * s1;
+#pragma unroll
+            for (int kk = 0; kk < G; ++kk) {
+                if (kk > 0) ck = nu_cmul(ck, c1);
+                const double uk = (double)(k0 + kk) * u1;
+                const double gk = rint(uk);
+                const double e = uk - gk;
+                const double e2 = e * e, e4 = e2 * e2, e8 = e4 * e4;
+                double a = (pp & 1) ? e : 1.0;
+                a = (pp & 2) ? a * e2 : a;
+                a = (pp & 4) ? a * e4 : a;
+                a = (pp & 8) ? a * e8 : a;
+                a = (valid && pok) ? a : 0.0;
+                const double b = (valid && rowok) ? (reim ? ck.y : ck.x) : 0.0;
+                const int64_t G64 = (int64_t)gk;
+                const int64_t g0 = nu_readlane64(G64, 0), g3 = nu_readlane64(G64, 48);
+                if (g0 == gcur[kk] && g3 == gcur[kk]) {
+                    acc[kk] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[kk], 0, 0, 0);
+                } else {
+                    // the K-group crosses cells: photons of the current cell first, then each later cell in turn
+                    const int64_t g1 = nu_readlane64(G64, 16), g2 = nu_readlane64(G64, 32);
+                    for (;;) {
+                        if (g0 <= gcur[kk]) {
+                            const double am = (G64 == gcur[kk]) ? a : 0.0;
+                            acc[kk] = __builtin_amdgcn_mfma_f64_16x16x4f64(am, b, acc[kk], 0, 0, 0);
+                        }
+                        if (g3 == gcur[kk]) break;
+                        flush(kk);
+                        const int64_t nx = g0 > gcur[kk] ? g0 : g1 > gcur[kk] ? g1 : g2 > gcur[kk] ? g2 : g3;
+                        if (nx > gcur[kk] + 1) zero_gap(kk, gcur[kk], nx);
+                        gcur[kk] = nx;
+                    }
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int kk = 0; kk < G; ++kk) {
+        flush(kk);
+        if (lane == 0) ctab[(kk * nchunk + c) * 2 + 1] = gcur[kk];  // the chunk's last cell
+    }
+}
+
+// ---- cell-gather spread (a pass of <= kNuGatherRows rows, one harmonic): one lane per wrapped cell ----
+// start[G - gmin] = the first photon whose cell (rint(k (dt s1)), the spread's arithmetic) is >= G, for the
+// unwrapped cells G in [gmin, gmax + 1]; photons are time-sorted, so cell G holds photons [start[G], start[G+1]).
+__global__ __launch_bounds__(256) void k_nu_cellstart(const double* __restrict__ dt, int64_t n, double s1, int k,
+                                                      int64_t gmin, int64_t span, int64_t* __restrict__ start) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t g = (int64_t)rint((double)k * (dt[i] * s1));
+        const int64_t gp = i == 0 ? gmin - 1 : (int64_t)rint((double)k * (dt[i - 1] * s1));
+        for (int64_t G = gp + 1; G <= g; ++G) start[G - gmin] = i;
+        if (i == n - 1) start[span] = n;
+    }
+}
+
+// The lane of wrapped cell g sums, over its unwrapped cells G = g (mod n) and their photons in time order, the
+// moments c_r e^p of rows r < nrow: b_p,r[g] = sum c_{i,r} e_i^p with c = e^{2 pi i k (fc dt + c2_r dt^2)},
+// e = k dt s1 - G, in registers (no reduction, deterministic), and writes W[p * nrow + r][g]. fp64 VALU throughout:
+// per photon, row and harmonic one premultiplier phase and cis, then 3 operations per moment.
+constexpr int kNuGatherRows = 2;
+template <int R, bool TWOD>
+__global__ __launch_bounds__(256) void k_nu_gather(const double* __restrict__ dt, const int64_t* __restrict__ start,
+                                                   int64_t gmin, int64_t gmax, int64_t nfft, double s1, double fch,
+                                                   double fcl, const double* __restrict__ c2row, int nrow, int k,
+                                                   int P, const double2* __restrict__ tab, double2* __restrict__ W) {
+    const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (g >= nfft) return;
+    double ar[R][kNuGatherMaxP], ai[R][kNuGatherMaxP];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int p = 0; p < kNuGatherMaxP; ++p) ar[r][p] = ai[r][p] = 0.0;
+    double c2[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) c2[r] = (TWOD && r < nrow) ? c2row[r] : 0.0;
+    const double kd = (double)k;
+    for (int64_t G = gmin + (((g - gmin) % nfft) + nfft) % nfft; G <= gmax; G += nfft) {
+        const int64_t i0 = start[G - gmin], i1 = start[G - gmin + 1];
+        const double Gd = (double)G;
+        for (int64_t i = i0; i < i1; ++i) {
+            const double d = dt[i];
+            const double e = kd * (d * s1) - Gd;
+            const double p1 = nu_frac_prod(fch, fcl, d);
+            double d2 = 0.0, d2e = 0.0;
+            if (TWOD) {
+                d2 = d * d;
+                d2e = fma(d, d, -d2);
+            }
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                if (r < nrow) {
+                    double phi = p1;
+                    if (TWOD) phi += nu_frac_c2(c2[r], d2, d2e);
+                    phi -= rint(phi);
+                    const double2 c = nu_cis(tab, nu_frac_k(kd, phi));
+                    double ep = 1.0;
+#pragma unroll
+                    for (int p = 0; p < kNuGatherMaxP; ++p) {
+                        if (p < P) {
+                            ar[r][p] = fma(c.x, ep, ar[r][p]);
+                            ai[r][p] = fma(c.y, ep, ai[r][p]);
+                            ep *= e;
+                        }
+                    }
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int p = 0; p < kNuGatherMaxP; ++p)
+            if (r < nrow && p < P) W[((int64_t)p * nrow + r) * nfft + g] = make_double2(ar[r][p], ai[r][p]);
+}
+
+// slots -> W[beta][g] (beta = p * nrow + row, complex), for the wrapped cells g of one block
+__global__ __launch_bounds__(256) void k_nu_merge(const double* __restrict__ U, int64_t SL,
+                                                  const int64_t* __restrict__ ctab, int64_t nchunk, int64_t gmin,
+                                                  int64_t gmax, int64_t nfft, double2* __restrict__ W) {
+    __shared__ int64_t rs[kNuMergeG][kNuMaxWrap];
+    __shared__ int rc[kNuMergeG][kNuMaxWrap];
+    __shared__ int nr[kNuMergeG];
+    extern __shared__ double nu_acc[];  // [kNuMergeG][SL]
+    const int64_t g0 = (int64_t)blockIdx.x * kNuMergeG;
+    const int tid = threadIdx.x;
+    if (tid < kNuMergeG) {
+        const int64_t g = g0 + tid;
+        int cnt = 0;
+        if (g < nfft) {
+            int64_t Gu = gmin + (((g - gmin) % nfft) + nfft) % nfft;  // smallest unwrapped cell >= gmin, = g mod n
+            for (; Gu <= gmax && cnt < kNuMaxWrap; Gu += nfft) {
+                int64_t lo = 0, hi = nchunk;  // first chunk whose last cell is >= Gu
+                while (lo < hi) {
+                    const int64_t mid = (lo + hi) >> 1;
+                    if (ctab[2 * mid + 1] < Gu)
+                        lo = mid + 1;
+                    else
+                        hi = mid;
+                }
+                int len = 0;
+                while (lo + len < nchunk && ctab[2 * (lo + len)] <= Gu) ++len;
+                if (len > 0) {
+                    rs[tid][cnt] = Gu - gmin + lo;
+                    rc[tid][cnt] = len;
+                    ++cnt;
+                }
+            }
+        }
+        nr[tid] = cnt;
+    }
+    __syncthreads();
+    for (int64_t idx = tid; idx < kNuMergeG * SL; idx += 256) {
+        const int t = (int)(idx / SL);
+        const int64_t e = idx - t * SL;
+        double v = 0.0;
+        for (int r = 0; r < nr[t]; ++r)
+            for (int k = 0; k < rc[t][r]; ++k) v += U[(rs[t][r] + k) * SL + e];
+        nu_acc[idx] = v;
+    }
+    __syncthreads();
+    const int64_t B = SL / 2;
+    for (int64_t idx = tid; idx < kNuMergeG * B; idx += 256) {
+        const int t = (int)(idx % kNuMergeG);
+        const int64_t beta = idx / kNuMergeG;
+        const int64_t g = g0 + t;
+        if (g < nfft) W[beta * nfft + g] = make_double2(nu_acc[t * SL + 2 * beta], nu_acc[t * SL + 2 * beta + 1]);
+    }
+}
+
+// ---- FFT: DFTs of radix 2..16 in registers (X_k = sum_j x_j w_R^{+jk}, natural order) ----
+__device__ __forceinline__ void nu_dft2(double2* v) {
+    const double2 a = v[0], b = v[1];
+    v[0] = nu_add(a, b);
+    v[1] = nu_sub(a, b);
+}
+__device__ __forceinline__ void nu_dft4(double2& a0, double2& a1, double2& a2, double2& a3) {
+    const double2 t0 = nu_add(a0, a2), t1 = nu_sub(a0, a2), t2 = nu_add(a1, a3), t3 = nu_muli(nu_sub(a1, a3));
+    a0 = nu_add(t0, t2);
+    a2 = nu_sub(t0, t2);
+    a1 = nu_add(t1, t3);
+    a3 = nu_sub(t1, t3);
+}
+__device__ __forceinline__ void nu_dft4v(double2* v) { nu_dft4(v[0], v[1], v[2], v[3]); }
+__device__ __forceinline__ void nu_dft8(double2* v) {
+    double2 e[4] = {v[0], v[2], v[4], v[6]}, o[4] = {v[1], v[3], v[5], v[7]};
+    nu_dft4v(e);
+    nu_dft4v(o);
+    const double s = 0.70710678118654752440084436210485;
+    const double2 w[4] = {make_double2(1.0, 0.0), make_double2(s, s), make_double2(0.0, 1.0), make_double2(-s, s)};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const double2 t = k == 0 ? o[0] : k == 2 ? nu_muli(o[2]) : nu_cmul(o[k], w[k]);
+        v[k] = nu_add(e[k], t);
+        v[k + 4] = nu_sub(e[k], t);
+    }
+}
+__device__ __forceinline__ void nu_dft16(double2* v) {
+    double2 e[8], o[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        e[k] = v[2 * k];
+        o[k] = v[2 * k + 1];
+    }
+    nu_dft8(e);
+    nu_dft8(o);
+    const double c1 = 0.92387953251128675612818318939679, s1 = 0.38268343236508977172845998403040,
+                 r2 = 0.70710678118654752440084436210485;
+    const double2 w[8] = {make_double2(1.0, 0.0), make_double2(c1, s1), make_double2(r2, r2), make_double2(s1, c1),
+                          make_double2(0.0, 1.0), make_double2(-s1, c1), make_double2(-r2, r2), make_double2(-c1, s1)};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const double2 t = k == 0 ? o[0] : k == 4 ? nu_muli(o[4]) : nu_cmul(o[k], w[k]);
+        v[k] = nu_add(e[k], t);
+        v[k + 8] = nu_sub(e[k], t);
+    }
+}
+template <int R>
+__device__ __forceinline__ void nu_dft(double2* v) {
+    if (R == 2) nu_dft2(v);
+    else if (R == 4) nu_dft4v(v);
+    else if (R == 8) nu_dft8(v);
+    else nu_dft16(v);
+}
+
+// One Stockham autosort stage of radix R over 2^lc transforms of length 2^ll held in LDS at s[a*sa + cc*sc]:
+// butterfly (j, cc) reads x[j + r L/R], twiddles by w_{Ns R}^{(j mod Ns) r}, and writes
+// y[(j / Ns) Ns R + (j mod Ns) + r Ns]. 16 / R butterflies per thread (a tile holds <= 16 elements per thread).
+template <int R>
+__device__ __forceinline__ void nu_stage(double2* s, int ll, int lc, int sa, int sc, int lns, const NuTw& T,
+                                         int lnfft) {
+    constexpr int NB = 16 / R;
+    constexpr int LR = R == 2 ? 1 : R == 4 ? 2 : R == 8 ? 3 : 4;
+    const int L = 1 << ll, Ns = 1 << lns;
+    const int nbt = (L >> LR) << lc;
+    double2 v[NB][R];
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+        const int b = threadIdx.x + 256 * k;
+        if (b < nbt) {
+            const int cc = b & ((1 << lc) - 1), j = b >> lc;
+#pragma unroll
+            for (int r = 0; r < R; ++r) v[k][r] = s[(j + (r << (ll - LR))) * sa + cc * sc];
+            if (lns > 0) {
+                // w_{Ns R}^{(j mod Ns)} = w_n^{(j mod Ns) n / (Ns R)}
+                const double2 w = nu_tw(T, (int64_t)(j & (Ns - 1)) << (lnfft - lns - LR));
+                double2 wr = w;
+#pragma unroll
+                for (int r = 1; r < R; ++r) {
+                    v[k][r] = nu_cmul(v[k][r], wr);
+                    if (r + 1 < R) wr = nu_cmul(wr, w);
+                }
+            }
+            nu_dft<R>(v[k]);
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+        const int b = threadIdx.x + 256 * k;
+        if (b < nbt) {
+            const int cc = b & ((1 << lc) - 1), j = b >> lc;
+            const int base = ((j >> lns) << (lns + LR)) + (j & (Ns - 1));
+#pragma unroll
+            for (int r = 0; r < R; ++r) s[(base + r * Ns) * sa + cc * sc] = v[k][r];
+        }
+    }
+    __syncthreads();
+}
+
+// 2^lc transforms of length 2^ll in LDS (Stockham: natural order in, natural order out)
+__device__ void nu_fft_lds(double2* s, int ll, int lc, int sa, int sc, const NuTw& T, int lnfft) {
+    int lns = 0;
+    while (lns < ll) {
+        const int rem = ll - lns;
+        if (rem >= 4) {
+            nu_stage<16>(s, ll, lc, sa, sc, lns, T, lnfft);
+            lns += 4;
+        } else if (rem == 3) {
+            nu_stage<8>(s, ll, lc, sa, sc, lns, T, lnfft);
+            lns += 3;
+        } else if (rem == 2) {
+            nu_stage<4>(s, ll, lc, sa, sc, lns, T, lnfft);
+            lns += 2;
+        } else {
+            nu_stage<2>(s, ll, lc, sa, sc, lns, T, lnfft);
+            lns += 1;
+        }
+    }
+}
+
+// pass 1 of the four-step FFT: view each batch as [n1][n2]; DFT along a of 2^lc consecutive columns b, times
+// w_n^{b k1}, stored at y[k1 n2 + b]
+__global__ __launch_bounds__(256) void k_nu_fft_cols(const double2* __restrict__ X, double2* __restrict__ Y,
+                                                     int lnfft, int ln1, int lc, NuTw T) {
+    extern __shared__ double2 nu_s[];
+    const int64_t nfft = int64_t(1) << lnfft;
+    const int ln2 = lnfft - ln1, c = 1 << lc, n1 = 1 << ln1;
+    const int64_t b0 = (int64_t)blockIdx.x << lc;
+    const double2* x = X + (int64_t)blockIdx.y * nfft;
+    double2* y = Y + (int64_t)blockIdx.y * nfft;
+    for (int e = threadIdx.x; e < (n1 << lc); e += 256) {
+        const int a = e >> lc, cc = e & (c - 1);
+        nu_s[e] = x[((int64_t)a << ln2) + b0 + cc];
+    }
+    __syncthreads();
+    nu_fft_lds(nu_s, ln1, lc, c, 1, T, lnfft);
+    for (int e = threadIdx.x; e < (n1 << lc); e += 256) {
+        const int k1 = e >> lc, cc = e & (c - 1);
+        const int64_t b = b0 + cc;
+        y[((int64_t)k1 << ln2) + b] = nu_cmul(nu_s[e], nu_tw(T, b * k1));
+    }
+}
+
+// pass 2 (or the only pass): DFT of 2^lr contiguous rows of length 2^ll each, in place
+__global__ __launch_bounds__(256) void k_nu_fft_rows(double2* __restrict__ X, int ll, int lr, int lnfft, NuTw T) {
+    extern __shared__ double2 nu_s[];
+    const int L = 1 << ll;
+    double2* x = X + ((int64_t)blockIdx.x << (ll + lr));
+    for (int e = threadIdx.x; e < (L << lr); e += 256) nu_s[e] = x[e];
+    __syncthreads();
+    nu_fft_lds(nu_s, ll, lr, 1, L, T, lnfft);
+    for (int e = threadIdx.x; e < (L << lr); e += 256) x[e] = nu_s[e];
+}
+
+// (C_k, S_k) of the trials of one harmonic: position pos = k1 n2 + k2 of the FFT output holds J = k1 + n1 k2
+// (ln1 = 0: natural order); J = jc mod n. Horner over the moments with z = 2 pi i jc / n.
+__global__ __launch_bounds__(256) void k_nu_combine(const double2* __restrict__ Z, int lnfft, int ln1, int P, int nrow,
+                                                    int64_t nf, int64_t nseg, int64_t h, int64_t jbase, int64_t row0,
+                                                    int64_t tb0, int64_t nbt, double2* __restrict__ CS) {
+    const int64_t nfft = int64_t(1) << lnfft;
+    const int64_t pos = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int row = blockIdx.y;
+    if (pos >= nfft) return;
+    const int ln2 = lnfft - ln1;
+    const int64_t J = (pos >> ln2) + ((pos & ((int64_t(1) << ln2) - 1)) << ln1);
+    int64_t jc;
+    if (J <= nseg - 1 - h)
+        jc = J;
+    else if (J >= nfft - h)
+        jc = J - nfft;
+    else
+        return;
+    const int64_t t = (row0 + row) * nf + jbase + jc - tb0;
+    if (t < 0 || t >= nbt) return;
+    const double th = ((double)jc / (double)nfft) * 6.283185307179586476925286766559;
+    double2 A = Z[((int64_t)(P - 1) * nrow + row) * nfft + pos];
+    for (int p = P - 2; p >= 0; --p) {
+        const double f = th / (double)(p + 1);
+        const double2 b = Z[((int64_t)p * nrow + row) * nfft + pos];
+        A = make_double2(fma(-f, A.y, b.x), fma(f, A.x, b.y));
+    }
+    CS[t] = A;
+}
+
+// Z^2 / H of trials tb0 .. tb0+nbt-1 (flat, relative to the call's first) from CS[k][t], in the reference's formula
+// order, with the certificate: |A_k error| <= E = N (x^P / P! + kNuRho), x = pi |jc| / n, so Z2_k = (2/N)|A_k|^2
+// errs by <= (2/N)(2 |A_k| E + E^2); Z^2 sums them, H = max_k g_k takes the largest bound among the g_k that the
+// errors could lift to the maximum (as k_search_finalize_exact). A trial whose bound exceeds rel |power| goes to the
+// fp64 fix-up list.
+__global__ __launch_bounds__(256) void k_nu_finalize(const double2* __restrict__ CS, int64_t nbt, int m, int stat,
+                                                     double nph, int64_t nf, int64_t jbase, int64_t nfft, int P,
+                                                     double invfact, double rel, int64_t tb0, int64_t first,
+                                                     double* __restrict__ out, int* __restrict__ nflag,
+                                                     int64_t* __restrict__ flagged) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nbt) return;
+    const int64_t flat = tb0 + t + first;
+    const int64_t jc = flat % nf - jbase;
+    const double x = 3.14159265358979323846 * fabs((double)jc) / (double)nfft;
+    double xp = 1.0;
+    for (int p = 0; p < P; ++p) xp *= x;
+    const double E = nph * (xp * invfact + kNuRho);
+    const double w = 2.0 / nph;
+    auto zk = [&](int k, double* amag) {
+        const double2 a = CS[(int64_t)k * nbt + t];
+        const double z = a.x * a.x + a.y * a.y;
+        *amag = sqrt(z);
+        return z;
+    };
+    double p, err;
+    if (stat == CRIMP_STAT_Z2) {
+        double zsum = 0.0, eb = 0.0, am;
+        for (int k = 0; k < m; ++k) {
+            zsum += zk(k, &am);
+            eb += 2.0 * am * E + E * E;
+        }
+        p = zsum * w;
+        err = eb * w;
+    } else {
+        double cum = 0.0, best = -INFINITY, ebest = 0.0, eacc = 0.0, am;
+        for (int k = 0; k < m; ++k) {
+            const double z = zk(k, &am);
+            cum += z * w;
+            eacc += (2.0 * am * E + E * E) * w;
+            const double v = cum - 4.0 * (double)k;
+            if (v > best) {
+                best = v;
+                ebest = eacc;
+            }
+        }
+        p = best;
+        err = ebest;
+        cum = 0.0;
+        eacc = 0.0;
+        for (int k = 0; k < m; ++k) {
+            const double z = zk(k, &am);
+            cum += z * w;
+            eacc += (2.0 * am * E + E * E) * w;
+            if (cum - 4.0 * (double)k + eacc >= best - ebest) err = fmax(err, eacc);
+        }
+    }
+    out[tb0 + t] = p;
+    if (!(err <= rel * fabs(p))) flagged[atomicAdd(nflag, 1)] = tb0 + t;
+}
+
+// ---- host ----
+static int g_last_search_path = 0;  // crimp_last_search_path(): 0 fp64 direct, 1 exact, 2 nufft
+static int64_t g_last_nufft_n = 0;   // crimp_last_nufft_plan(): the last NUFFT's largest FFT length, its moments,
+static int g_last_nufft_p = 0;       // and its spread form (1 cell gather, 0 MFMA slots)
+static int g_last_nufft_gather = 0;
+
+static double nu_trunc(double x, int P, double* invfact) {  // x^P / P!
+    double f = 1.0, xp = 1.0;
+    for (int p = 1; p <= P; ++p) {
+        f *= (double)p;
+        xp *= x;
+    }
+    *invfact = 1.0 / f;
+    return xp / f;
+}
+
+static int ilog2(int64_t v) {
+    int l = 0;
+    while ((int64_t(1) << l) < v) ++l;
+    return l;
+}
+
+// per-call twiddle (w_n^t) and cis tables, fp64 from long double
+static int nu_tables(Scratch& sc, hipStream_t s, int lnfft, NuTw* T, const double2** cis) {
+    const int lbits = std::min(lnfft, 11);
+    const int64_t nlo = int64_t(1) << lbits, nhi = int64_t(1) << (lnfft - lbits);
+    std::vector<double2> h((size_t)(nlo + nhi + 1024));
+    const long double tp = 6.283185307179586476925286766559L;
+    const long double nf = (long double)(int64_t(1) << lnfft);
+    for (int64_t i = 0; i < nlo; ++i) {
+        const long double a = tp * (long double)i / nf;
+        h[(size_t)i] = make_double2((double)cosl(a), (double)sinl(a));
+    }
+    for (int64_t i = 0; i < nhi; ++i) {
+        const long double a = tp * (long double)(i << lbits) / nf;
+        h[(size_t)(nlo + i)] = make_double2((double)cosl(a), (double)sinl(a));
+    }
+    for (int i = 0; i < 1024; ++i) {
+        const long double a = tp * (long double)i / 1024.0L;
+        h[(size_t)(nlo + nhi + i)] = make_double2((double)cosl(a), (double)sinl(a));
+    }
+    double2* d = nullptr;
+    HIPCHK(sc.alloc(&d, h.size()));
+    HIPCHK(hipMemcpyAsync(d, h.data(), h.size() * sizeof(double2), hipMemcpyHostToDevice, s));
+    HIPCHK(hipStreamSynchronize(s));  // h is pageable and local
+    T->lo = d;
+    T->hi = d + nlo;
+    T->lbits = lbits;
+    T->mask = (int64_t(1) << lnfft) - 1;
+    *cis = d + nlo + nhi;
+    return CRIMP_OK;
+}
+
+template <bool TWOD>
+static void nu_launch_spread(int G, dim3 grid, hipStream_t s, const double* dt, int64_t n, int64_t nchunk, double s1,
+                             double fch, double fcl, const double* c2, int nrow, int k0, int P, const NuPass* ps,
+                             const double2* tab, double* U, int64_t* ctab) {
+#define CRIMP_NS(GG) k_nu_spread<GG, TWOD><<<grid, 256, 0, s>>>(dt, n, nchunk, s1, fch, fcl, c2, nrow, k0, P, ps, tab, U, ctab)
+    if (G == 8) CRIMP_NS(8); else if (G == 4) CRIMP_NS(4); else CRIMP_NS(2);
+#undef CRIMP_NS
+}
+
+// Budget of the NUFFT path's device buffers (CRIMP_NUFFT_BUDGET_MB, default 6144): slots, FFT ping-pong, sums.
+static int64_t nufft_budget() {
+    static int64_t b = -1;
+    if (b < 0) {
+        const char* e = getenv("CRIMP_NUFFT_BUDGET_MB");
+        const long long mb = e ? atoll(e) : 6144;
+        b = (int64_t)(mb > 0 ? mb : 6144) << 20;
+    }
+    return b;
+}
+
+// One group of rows that share their trial segment: rows [r0, r1), trials j0 .. j0+nseg-1 of each, planned on that
+// segment alone (a rank's slice of a row is its own progression, so a sharded search costs its share).
+struct NuPlan {
+    int64_t r0 = 0, r1 = 0, j0 = 0, nseg = 0, h = 0;  // jc = j - (j0 + h) in [-h, nseg - 1 - h]
+    int lnfft = 0, P = 0;
+    double invfact = 1.0, s1 = 0.0, fch = 0.0, fcl = 0.0;
+    std::vector<int64_t> gmin, gmax;                     // unwrapped cells of dt[0], dt[n-1] per harmonic
+};
+
+// n and P: among the powers of two n >= nseg (up to 2^24) whose edge truncation x^P / P! <= kNuEps within P <= pmax
+// moments, the one with the least FFT work n P; false when none exists or the photons wrap the grid more than
+// kNuMaxWrap times
+static bool nu_plan(NuPlan* pl, double delta, double f0, double dt0, double dtn, int nharm, int64_t nchunk, int pmax) {
+    const int64_t h = pl->nseg / 2;
+    pl->h = h;
+    int lnfft = 0, P = 0;
+    double invfact = 1.0;
+    for (int l = std::max(ilog2(pl->nseg), 6); l <= 24; ++l) {
+        const double x = M_PI * (double)std::max<int64_t>(h, pl->nseg - 1 - h) / (double)(int64_t(1) << l);
+        int p = 1;
+        while (p <= pmax && nu_trunc(x, p, &invfact) > kNuEps) ++p;
+        if (p > pmax) continue;
+        if (lnfft == 0 || ((int64_t)p << l) < ((int64_t)P << lnfft)) {
+            lnfft = l;
+            P = p;
+        }
+        if (p <= 4) break;  // larger n only adds work
+    }
+    if (lnfft == 0) return false;
+    nu_trunc(0.0, P, &invfact);
+    pl->lnfft = lnfft;
+    pl->P = P;
+    pl->invfact = invfact;
+    const int64_t nfft = int64_t(1) << lnfft;
+    pl->s1 = (double)nfft * delta;
+    // fc = f_0 + (j0 + h) delta in double-double (the whole grid's progression model, whatever the segment)
+    const double c = (double)(pl->j0 + h);
+    const double hp = c * delta, hpe = std::fma(c, delta, -hp);
+    const double fch = f0 + hp, bb = fch - f0;  // TwoSum(f0, hp)
+    pl->fch = fch;
+    pl->fcl = ((f0 - (fch - bb)) + (hp - bb)) + hpe;
+    // the kernel's arithmetic: rint(k * (dt * s1))
+    const double u0 = dt0 * pl->s1, un = dtn * pl->s1;
+    pl->gmin.assign((size_t)nharm, 0);
+    pl->gmax.assign((size_t)nharm, 0);
+    (void)nchunk;
+    for (int k = 1; k <= nharm; ++k) {
+        pl->gmin[(size_t)(k - 1)] = (int64_t)std::rint((double)k * u0);
+        pl->gmax[(size_t)(k - 1)] = (int64_t)std::rint((double)k * un);
+        if ((pl->gmax[(size_t)(k - 1)] - pl->gmin[(size_t)(k - 1)]) / nfft + 1 > kNuMaxWrap) return false;
+    }
+    return true;
+}
+
+// Z^2 / H by NUFFT over trials [first, first + count) of the fd-outer grid (nf trials per row, arithmetic
+// progression with step ap[0]). *applicable = false (nothing computed) for unsorted photons or an out-of-range plan:
+// the caller takes the exact path.
+static int nufft_search(Scratch& sc, hipStream_t s, const double* dt, const double* dt2, int64_t n, const double* freq,
+                        int64_t nf, int64_t nrows_grid, const double* c2, const double* ap, bool twod, int nharm,
+                        int stat, int64_t first,
+                        int64_t count, double* out, bool timed, int64_t* nfixed, bool no_fixup, bool* applicable) {
+    *applicable = false;
+    *nfixed = 0;
+    int* dflag = nullptr;
+    double* dsc = nullptr;
+    HIPCHK(sc.alloc(&dflag, 4));
+    HIPCHK(sc.alloc(&dsc, 4));
+    HIPCHK(hipMemsetAsync(dflag, 0, 4 * sizeof(int), s));
+    k_nu_sorted<<<(unsigned)std::min<int64_t>(cdiv(n, 256), 2048), 256, 0, s>>>(dt, n, dflag);
+    k_nu_scalars<<<1, 64, 0, s>>>(ap, freq, dt, n, dsc);
+    HIPCHK(hipGetLastError());
+    int bad = 0;
+    double hs[4];
+    HIPCHK(d2h(s, &bad, dflag, sizeof(int)));
+    HIPCHK(hipMemcpy(hs, dsc, sizeof(hs), hipMemcpyDeviceToHost));
+    if (bad) return CRIMP_OK;
+    const double delta = hs[0], f0 = hs[1], dt0 = hs[2], dtn = hs[3];
+    const int64_t nchunk = cdiv(n, kNuCW);
+    // spread form: the cell gather (VALU, one lane per wrapped cell) for grids of <= kNuGatherRows rows, the MFMA
+    // slots otherwise -- decided from the whole grid, so that row shards compute exactly what the whole grid does
+    // (CRIMP_NUFFT_SPREAD=gather|mfma forces one, a test hook)
+    const char* spread_env = getenv("CRIMP_NUFFT_SPREAD");
+    const bool gather_grid = spread_env && !strcmp(spread_env, "gather")  ? true
+                             : spread_env && !strcmp(spread_env, "mfma") ? false
+                                                                         : nrows_grid <= kNuGatherRows;
+    // row groups: the first row's segment, the full rows between, the last row's segment
+    const int64_t r_lo = first / nf, r_hi = (first + count - 1) / nf;
+    std::vector<NuPlan> plans;
+    for (int64_t r = r_lo; r <= r_hi;) {
+        const int64_t a = std::max<int64_t>(first, r * nf) - r * nf, b = std::min<int64_t>(first + count, (r + 1) * nf) - r * nf;
+        int64_t r1 = r + 1;
+        if (a == 0 && b == nf)
+            while (r1 <= r_hi && std::min<int64_t>(first + count, (r1 + 1) * nf) - r1 * nf == nf) ++r1;
+        NuPlan pl;
+        pl.r0 = r;
+        pl.r1 = r1;
+        pl.j0 = a;
+        pl.nseg = b - a;
+        if (pl.nseg < 64 || !nu_plan(&pl, delta, f0, dt0, dtn, nharm + 1, nchunk, gather_grid ? kNuGatherMaxP : kNuMaxP))
+            return CRIMP_OK;
+        plans.push_back(std::move(pl));
+        r = r1;
+    }
+    *applicable = true;
+    g_last_search_path = 2;
+    g_last_nufft_n = 0;
+    for (const NuPlan& pl : plans)
+        if ((int64_t(1) << pl.lnfft) > g_last_nufft_n) {
+            g_last_nufft_n = int64_t(1) << pl.lnfft;
+            g_last_nufft_p = pl.P;
+        }
+    g_last_nufft_gather = gather_grid ? 1 : 0;
+    // buffers sized for the largest group; harmonics per spread pass: the largest G in {8, 4, 2, 1} whose slots fit
+    // the budget beside W, Y and the sums
+    int64_t Bmax = 0, nfmax = 0, csmax = 0, nrow_all = 0;
+    for (const NuPlan& pl : plans) {
+        const int64_t nrow_max = std::min<int64_t>(kNuRows, pl.r1 - pl.r0);
+        const int lrow = 12 - std::min(pl.lnfft, 12);
+        Bmax = std::max<int64_t>(Bmax, (cdiv((int64_t)pl.P * nrow_max, int64_t(1) << lrow) << lrow) << pl.lnfft);
+        csmax = std::max<int64_t>(csmax, (int64_t)nharm * nrow_max * pl.nseg);
+        nfmax = std::max<int64_t>(nfmax, int64_t(1) << pl.lnfft);
+        nrow_all = std::max<int64_t>(nrow_all, nrow_max);
+    }
+    const int64_t fixed_bytes = 2 * Bmax * 16 + csmax * 16;
+    std::vector<std::pair<int, int>> passes;  // (k0, harmonics) of each spread pass, harmonics a power of two
+    int64_t ubytes = 0;
+    for (int G = 8;; G /= 2) {  // G >= 2
+        passes.clear();
+        ubytes = 0;
+        for (int k0 = 1; k0 <= nharm;) {
+            const int g = std::min(G, nharm - k0 + 1);
+            const int gl = g >= 8 ? 8 : g >= 4 ? 4 : 2;  // (a single last harmonic rides with the one past nharm)
+            for (const NuPlan& pl : plans) {
+                const int64_t SLmax = 2 * (int64_t)pl.P * std::min<int64_t>(kNuRows, pl.r1 - pl.r0);
+                int64_t sl = 0;
+                for (int k = k0; k < k0 + gl; ++k)
+                    sl += (pl.gmax[(size_t)(k - 1)] - pl.gmin[(size_t)(k - 1)] + 1 + nchunk) * SLmax;
+                ubytes = std::max<int64_t>(ubytes, sl * 8);
+            }
+            passes.emplace_back(k0, gl);
+            k0 += gl;
+        }
+        if (G == 2 || ubytes + fixed_bytes <= nufft_budget()) break;
+    }
+    auto use_gather = [&](const NuPlan&) { return gather_grid; };
+    bool any_mfma = false;
+    int64_t starts_max = 0;
+    for (const NuPlan& pl : plans) {
+        if (!use_gather(pl)) {
+            any_mfma = true;
+            continue;
+        }
+        int64_t tot = 0;
+        for (int k = 1; k <= nharm; ++k) tot += pl.gmax[(size_t)(k - 1)] - pl.gmin[(size_t)(k - 1)] + 2;
+        starts_max = std::max<int64_t>(starts_max, tot);
+    }
+    double* U = nullptr;
+    double2 *W = nullptr, *Y = nullptr, *CS = nullptr;
+    int64_t* ctab = nullptr;
+    int64_t* cstart = nullptr;
+    int64_t* flagged = nullptr;
+    int* nflag = dflag + 1;
+    if (any_mfma) {
+        HIPCHK(sc.alloc(&U, (size_t)(ubytes / 8)));
+        HIPCHK(sc.alloc(&ctab, (size_t)(2 * 8 * nchunk)));
+    }
+    if (starts_max > 0) HIPCHK(sc.alloc(&cstart, (size_t)starts_max));
+    HIPCHK(sc.alloc(&W, (size_t)Bmax));
+    HIPCHK(sc.alloc(&Y, (size_t)Bmax));
+    HIPCHK(sc.alloc(&CS, (size_t)csmax));
+    HIPCHK(sc.alloc(&flagged, (size_t)count));
+    // every MFMA (group, row batch, pass)'s slot table, uploaded once before the launches
+    std::vector<NuPass> hps;
+    for (const NuPlan& pl : plans) {
+        if (use_gather(pl)) continue;
+        for (int64_t rb = pl.r0; rb < pl.r1; rb += kNuRows) {
+            const int64_t SL = 2 * (int64_t)pl.P * std::min<int64_t>(kNuRows, pl.r1 - rb);
+            for (const auto& pass : passes) {
+                NuPass ps{};
+                int64_t off = 0;
+                for (int kk = 0; kk < pass.second; ++kk) {
+                    const int k = pass.first + kk;
+                    ps.gmin[kk] = pl.gmin[(size_t)(k - 1)];
+                    ps.ubase[kk] = off;
+                    off += (pl.gmax[(size_t)(k - 1)] - pl.gmin[(size_t)(k - 1)] + 1 + nchunk) * SL;
+                }
+                hps.push_back(ps);
+            }
+        }
+    }
+    NuPass* dps = nullptr;
+    if (!hps.empty()) {
+        HIPCHK(sc.alloc(&dps, hps.size()));
+        HIPCHK(hipMemcpyAsync(dps, hps.data(), hps.size() * sizeof(NuPass), hipMemcpyHostToDevice, s));
+    }
+    size_t ipass = 0;
+    const size_t lds_fft = (size_t)kNuTile * sizeof(double2);
+    // timed spans (CRIMP_FLAG_TIME_KERNELS): the whole pipeline, then spread / merge / fft / combine+finalize sums
+    std::vector<hipEvent_t> ev;
+    std::vector<int> evcls;  // class of the span ending at each mark: 0 spread, 1 merge, 2 fft, 3 combine/finalize
+    auto mark = [&]() -> hipError_t {
+        if (!timed) return hipSuccess;
+        hipEvent_t e = nullptr;
+        hipError_t r = hipEventCreate(&e);
+        if (r != hipSuccess) return r;
+        ev.push_back(e);
+        return hipEventRecord(e, s);
+    };
+    auto span = [&](int cls) -> hipError_t {
+        if (!timed) return hipSuccess;
+        evcls.push_back(cls);
+        return mark();
+    };
+    HIPCHK(hipMemsetAsync(nflag, 0, sizeof(int), s));
+    int cur_lnfft = -1;
+    NuTw T{};
+    const double2* cis = nullptr;
+    for (const NuPlan& pl : plans) {
+        if (pl.lnfft != cur_lnfft) {  // tables for this group's n (a group's first launch follows their upload)
+            const int rc = nu_tables(sc, s, pl.lnfft, &T, &cis);
+            if (rc) return rc;
+            cur_lnfft = pl.lnfft;
+        }
+        if (ev.empty()) HIPCHK(mark());
+        const int lnfft = pl.lnfft, P = pl.P;
+        const int64_t nfft = int64_t(1) << lnfft;
+        // FFT shape: one row pass for n <= kNuTile (2^lrow transforms per block), else columns (n1 = n / 4096 <= 4096)
+        // then rows of 4096
+        const int ln2 = std::min(lnfft, 12), ln1 = lnfft - ln2;
+        const int lcol = 12 - ln1;  // columns per block in pass 1 (n1 * c = 4096)
+        const int lrow = 12 - ln2;  // rows per block in pass 2
+        const int64_t jbase = pl.j0 + pl.h;
+        // W (moments of harmonic k, rows [rb, rb + nrow)) -> FFT -> (C_k, S_k) of the batch's trials
+        auto fft_combine = [&](int k, int64_t rb, int nrow, int64_t tb0, int64_t nbt) -> int {
+            const int64_t Bp = (int64_t)P * nrow;
+            double2* Zo = W;
+            if (ln1 > 0) {
+                k_nu_fft_cols<<<dim3((unsigned)(int64_t(1) << (ln2 - lcol)), (unsigned)Bp), 256, lds_fft, s>>>(
+                    W, Y, lnfft, ln1, lcol, T);
+                HIPCHK(hipGetLastError());
+                Zo = Y;
+            }
+            k_nu_fft_rows<<<(unsigned)cdiv(Bp << ln1, int64_t(1) << lrow), 256, lds_fft, s>>>(Zo, ln2, lrow, lnfft, T);
+            HIPCHK(hipGetLastError());
+            HIPCHK(span(2));
+            k_nu_combine<<<dim3((unsigned)cdiv(nfft, 256), (unsigned)nrow), 256, 0, s>>>(
+                Zo, lnfft, ln1, P, nrow, nf, pl.nseg, pl.h, jbase, rb, tb0 + first, nbt, CS + (int64_t)(k - 1) * nbt);
+            HIPCHK(hipGetLastError());
+            HIPCHK(span(3));
+            return CRIMP_OK;
+        };
+        auto finalize = [&](int64_t tb0, int64_t nbt) -> int {
+            k_nu_finalize<<<(unsigned)cdiv(nbt, 256), 256, 0, s>>>(CS, nbt, nharm, stat, (double)n, nf, jbase, nfft, P,
+                                                                   pl.invfact, fixup_rel(), tb0, first, out, nflag,
+                                                                   flagged);
+            HIPCHK(hipGetLastError());
+            HIPCHK(span(3));
+            return CRIMP_OK;
+        };
+        if (use_gather(pl)) {
+            std::vector<int64_t> soff((size_t)nharm);
+            int64_t off = 0;
+            for (int k = 1; k <= nharm; ++k) {
+                const int64_t spank = pl.gmax[(size_t)(k - 1)] - pl.gmin[(size_t)(k - 1)] + 1;
+                soff[(size_t)(k - 1)] = off;
+                k_nu_cellstart<<<(unsigned)std::min<int64_t>(cdiv(n, 256), 8192), 256, 0, s>>>(
+                    dt, n, pl.s1, k, pl.gmin[(size_t)(k - 1)], spank, cstart + off);
+                HIPCHK(hipGetLastError());
+                off += spank + 1;
+            }
+            HIPCHK(span(0));
+            for (int64_t rb = pl.r0; rb < pl.r1; rb += kNuGatherRows) {
+                const int nrow = (int)std::min<int64_t>(kNuGatherRows, pl.r1 - rb);
+                const int64_t tb0 = std::max<int64_t>(first, rb * nf) - first;
+                const int64_t nbt = std::min<int64_t>(first + count, (rb + nrow) * nf) - first - tb0;
+                for (int k = 1; k <= nharm; ++k) {
+                    const dim3 grid((unsigned)cdiv(nfft, 256));
+                    if (twod)
+                        k_nu_gather<kNuGatherRows, true><<<grid, 256, 0, s>>>(
+                            dt, cstart + soff[(size_t)(k - 1)], pl.gmin[(size_t)(k - 1)], pl.gmax[(size_t)(k - 1)], nfft,
+                            pl.s1, pl.fch, pl.fcl, c2 + rb, nrow, k, P, cis, W);
+                    else
+                        k_nu_gather<1, false><<<grid, 256, 0, s>>>(
+                            dt, cstart + soff[(size_t)(k - 1)], pl.gmin[(size_t)(k - 1)], pl.gmax[(size_t)(k - 1)], nfft,
+                            pl.s1, pl.fch, pl.fcl, nullptr, nrow, k, P, cis, W);
+                    HIPCHK(hipGetLastError());
+                    HIPCHK(span(0));
+                    int rc = fft_combine(k, rb, nrow, tb0, nbt);
+                    if (rc) return rc;
+                }
+                int rc = finalize(tb0, nbt);
+                if (rc) return rc;
+            }
+            continue;
+        }
+        for (int64_t rb = pl.r0; rb < pl.r1; rb += kNuRows) {
+            const int nrow = (int)std::min<int64_t>(kNuRows, pl.r1 - rb);
+            const int64_t tb0 = std::max<int64_t>(first, rb * nf) - first;
+            const int64_t tb1 = std::min<int64_t>(first + count, (rb + nrow) * nf) - first;
+            const int64_t nbt = tb1 - tb0;
+            const int64_t SL = 2 * (int64_t)P * nrow;
+            for (const auto& pass : passes) {
+                const int k0 = pass.first, gl = pass.second;
+                const NuPass& ps = hps[ipass];
+                const NuPass* dp = dps + ipass++;
+                dim3 grid((unsigned)cdiv(nchunk, kNuWaves));
+                if (twod)
+                    nu_launch_spread<true>(gl, grid, s, dt, n, nchunk, pl.s1, pl.fch, pl.fcl, c2 + rb, nrow, k0, P, dp, cis,
+                                           U, ctab);
+                else
+                    nu_launch_spread<false>(gl, grid, s, dt, n, nchunk, pl.s1, pl.fch, pl.fcl, c2 + rb, nrow, k0, P, dp,
+                                            cis, U, ctab);
+                HIPCHK(hipGetLastError());
+                HIPCHK(span(0));
+                for (int kk = 0; kk < gl && k0 + kk <= nharm; ++kk) {
+                    const int k = k0 + kk;
+                    k_nu_merge<<<(unsigned)cdiv(nfft, kNuMergeG), 256, (size_t)kNuMergeG * SL * sizeof(double), s>>>(
+                        U + ps.ubase[kk], SL, ctab + 2 * kk * nchunk, nchunk, ps.gmin[kk], pl.gmax[(size_t)(k - 1)],
+                        nfft, W);
+                    HIPCHK(hipGetLastError());
+                    HIPCHK(span(1));
+                    int rc = fft_combine(k, rb, nrow, tb0, nbt);
+                    if (rc) return rc;
+                }
+            }
+            int rc = finalize(tb0, nbt);
+            if (rc) return rc;
+        }
+    }
+    if (timed) {
+        HIPCHK(hipEventSynchronize(ev.back()));
+        float tot = 0.0f;
+        double cls[4] = {0, 0, 0, 0};
+        HIPCHK(hipEventElapsedTime(&tot, ev.front(), ev.back()));
+        for (size_t i = 1; i < ev.size(); ++i) {
+            float ms = 0.0f;
+            HIPCHK(hipEventElapsedTime(&ms, ev[i - 1], ev[i]));
+            cls[evcls[i - 1]] += ms;
+        }
+        for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+        if (g_kernel_times.empty()) g_last_kernel_ms = tot;
+        g_kernel_times.push_back(tot);
+        for (double v : cls) g_kernel_times.push_back(v);
+    }
+    int nf_h = 0;
+    HIPCHK(d2h(s, &nf_h, nflag, sizeof(int)));
+    *nfixed = nf_h;
+    if (nf_h == 0 || no_fixup) return CRIMP_OK;
+    return fixup_search(sc, s, dt, dt2, n, freq, nf, c2, twod, nharm, stat, first, flagged, nf_h, out);
+}

@@ -70,38 +70,35 @@ def _empty_like_input(a, n, b, dtype=np.float64):
 
 
 def search_flags():
-    """Extra search flags from the environment: CRIMP_PRECISION=f64|fast, and for the fast path
-    CRIMP_SEARCH=direct|mfma and CRIMP_SINCOS=hw."""
+    """Extra search flags from the environment for unmodified callers: CRIMP_PRECISION=f64|nufft, and
+    CRIMP_SEARCH=mfma (fail unless a factorised kernel applies)."""
     f = 0
     prec = os.environ.get("CRIMP_PRECISION", "").lower()
     if prec == "f64":
         f |= N.FLAG_F64
-    elif prec == "fast":
-        f |= N.FLAG_FAST
-    mode = os.environ.get("CRIMP_SEARCH", "").lower()
-    if mode == "direct":
-        f |= N.FLAG_FORCE_DIRECT
-    elif mode == "mfma":
+    elif prec == "nufft":
+        f |= N.FLAG_NUFFT
+    elif prec not in ("", "exact"):
+        raise ValueError("CRIMP_PRECISION must be exact, nufft or f64 (the fp32 'fast' path was retired)")
+    if os.environ.get("CRIMP_SEARCH", "").lower() == "mfma":
         f |= N.FLAG_FORCE_MFMA
-    if os.environ.get("CRIMP_SINCOS", "").lower() == "hw":
-        f |= N.FLAG_HW_SINCOS
     return f
 
 
-PRECISIONS = (None, "exact", "fast", "f64")
+PRECISIONS = (None, "exact", "f64", "nufft")
 
 
 def search(t, t0, freq, nharm, stat, log10_negfdot=None, first=0, count=None, out=None, flags=0, precision=None):
     """Z^2 / H over the fd-outer grid; computes flat trials [first, first+count).
     ``precision``: None/"exact" (default: exact-integer i8 MFMA kernel on progressions, fp64 otherwise, every
-    trial within 1e-6 relative of the reference), "fast" (fp32 sin/cos kernels, ~1e-6 of the grid's mean
-    power) or "f64" (fp64 kernel everywhere)."""
+    trial within 1e-6 relative of the reference), "nufft" (non-uniform FFT on progressions of time-sorted photons,
+    the default path otherwise; the same per-trial contract) or "f64" (fp64 kernel everywhere)."""
     if precision not in PRECISIONS:
-        raise ValueError("precision must be one of %s" % (PRECISIONS,))
+        raise ValueError("precision must be one of %s (the fp32 'fast' path was retired)" % (PRECISIONS,))
     if precision == "f64":
         flags |= N.FLAG_F64
-    elif precision == "fast":
-        flags |= N.FLAG_FAST
+    elif precision == "nufft":
+        flags |= N.FLAG_NUFFT
     L = N.load()
     b = N.Buffers()
     tp = b.arg(t, np.float64)

@@ -10,7 +10,7 @@ negative fdot (:95). ``twod_htest`` is this package's extension (H-test on the
 same 2-D grid).
 
 All statistics come from ``crimp_search`` (csrc/crimp_hip.hip section 4, the default
-exact kernel in csrc/search_exact.h, the opt-in fast kernel in csrc/search_fast.h);
+exact kernel in csrc/search_exact.h, the opt-in NUFFT in csrc/search_nufft.h);
 there is no NumPy fallback.
 """
 import numpy as np
@@ -27,8 +27,10 @@ class PeriodSearch:
       fp64 recomputation of every trial that its 10-sigma error bound cannot place within 1e-6 relative; other
       grids take the fp64 kernel. Per-trial contract: 1e-6 relative of the reference's fp64 value, except where
       the reference's own argument rounding is larger (noise-level H at config-4 arguments; DESIGN.md section 8);
-    * "f64": every term in fp64 like the reference (~1e-9 relative on every trial, near-zero bins included);
-    * "fast": fp32 sin/cos on f16-split MFMA, within 1e-6 of the grid's mean power (not per trial)."""
+    * "nufft": non-uniform FFT over the progression (time-sorted photons; otherwise the default path): fp64
+      moments of the photons' sub-cell offsets, an fp64 FFT per moment and harmonic, the same per-trial 1e-6
+      certificate and fp64 fix-up as the default path; O(N m + M log M) instead of O(N M m);
+    * "f64": every term in fp64 like the reference (~1e-9 relative on every trial, near-zero bins included)."""
 
     def __init__(self, time, freq, nbrHarm: int = 2, *, precision=None):
         self.time = time

@@ -40,17 +40,21 @@ extern "C" {
  * 1e-6 relative are recomputed in fp64 -- crimp_last_fixups()), the fp64 kernel otherwise. Tested within 1e-6 of the
  * reference on every checked trial; the reference's own fp64 argument rounding (~1e-6 of a noise-level H_20) is
  * the floor of any fp64 implementation. */
-#define CRIMP_FLAG_FORCE_DIRECT 4u /* fast search: the fp32 direct kernel even on a progression (implies FAST) */
-#define CRIMP_FLAG_FORCE_MFMA 8u   /* search: fail unless a factorised kernel applies (with FAST: the f16 one) */
-#define CRIMP_FLAG_HW_SINCOS 16u   /* fast direct search: hardware v_sin/v_cos (implies FAST) */
+#define CRIMP_FLAG_FORCE_MFMA 8u   /* search: fail unless a factorised kernel (exact i8 MFMA or NUFFT) applies */
 #define CRIMP_FLAG_TIME_KERNELS 128u /* search / calcphase: time the kernels with hipEvents (crimp_last_kernel_ms) */
 #define CRIMP_FLAG_F64 256u         /* search: fp64 kernel on every grid */
-#define CRIMP_FLAG_FAST 512u        /* search: fp32 sin/cos kernels (f16-split MFMA / direct): ~1e-6 of the grid's
-                                       mean power, not per trial; faster */
-#define CRIMP_FLAG_NO_FIXUP 1024u   /* search (diagnostic): the exact kernel's raw powers, without the fp64 fix-up
-                                       of the trials its error bound cannot certify (crimp_last_fixups counts them) */
+#define CRIMP_FLAG_NO_FIXUP 1024u   /* search (diagnostic): the exact kernel's / the NUFFT's raw powers, without the
+                                       fp64 fix-up of the trials their error bound cannot certify (crimp_last_fixups
+                                       counts them) */
+/* Bits 4, 16 and 512 selected the fp32 "fast" search (round 1-4), retired in round 5: slower than the default exact
+ * path and only within 1e-6 of the grid's mean power. A search call that sets any of them fails with CRIMP_ERR_ARG. */
+#define CRIMP_FLAG_RETIRED_FAST (4u | 16u | 512u)
 #define CRIMP_FLAG_ASYNC 2048u     /* crimp_search_sets with device pointers: return once the kernel is queued, without
                                      * draining the stream (the caller synchronises it before reading out) */
+
+#define CRIMP_FLAG_NUFFT 4096u     /* search: non-uniform FFT over an arithmetic-progression grid of >= 64 trials per
+                                    * row and time-sorted photons (search_nufft.h; otherwise the default path), every
+                                    * trial certified within 1e-6 relative like the default path, fp64 fix-up included */
 
 #define CRIMP_STAT_Z2 0 /* Z^2_m  (periodsearch.py:57-71, :73-106) */
 #define CRIMP_STAT_H 1  /* H-test (periodsearch.py:109-125)         */
@@ -99,6 +103,13 @@ double crimp_last_kernel_ms(void);
 int crimp_last_kernel_times(double* ms, int32_t cap);
 /* Trials of the last crimp_search (default precision) whose power was recomputed by the fp64 fix-up. */
 int64_t crimp_last_fixups(void);
+/* Kernel family of the last crimp_search: 0 fp64 direct, 1 exact i8 MFMA, 2 NUFFT. With
+ * CRIMP_FLAG_TIME_KERNELS a NUFFT search's crimp_last_kernel_times are: the whole pipeline, then its spread, merge,
+ * FFT and combine + finalize kernels (sums). Measurement hook for tests and bench.py, not in the reference. */
+int crimp_last_search_path(void);
+/* The plan of the last NUFFT search: its (largest) FFT length n, moments P, and spread form (1 = cell gather, one lane
+ * per wrapped cell on the VALU; 0 = MFMA slots). Measurement hook for bench.py, not in the reference. */
+int crimp_last_nufft_plan(int64_t* fft_length, int32_t* moments, int32_t* gather);
 /* Brute-grid norms evaluated per phShift by the last crimp_toa_fit with CRIMP_TOA_BRUTE (the pruned candidates of
  * lmfit's 20-norm lattice, padded to 2, 4 or 20, less the lazy norms the eight-factor grid leaves out; 0 without a
  * brute grid). Measurement hook for bench.py's
@@ -125,9 +136,11 @@ int crimp_calcphase(const double* t_mjd, int64_t n, const crimp_timing_model* mo
  * shards of one search share it); freq [nf] (Hz); log10_negfdot [nfd] or NULL (1-D); the trial
  * grid is fd-outer/f-inner (periodsearch.py:264-278) and this call computes flat trials
  * [first, first+count) of it into out[count]. stat = CRIMP_STAT_Z2 or CRIMP_STAT_H (the latter
- * over the 2-D grid is this library's extension). Precision: the CRIMP_FLAG_F64 / _FAST notes
+ * over the 2-D grid is this library's extension). Precision: the CRIMP_FLAG_F64 / _NUFFT notes
  * above; the kernel is chosen from the whole grid (nf, nfd, progression), not from [first, count), so a sharded
- * search computes every trial exactly as an unsharded one. */
+ * search computes every trial exactly as an unsharded one -- except that CRIMP_FLAG_NUFFT plans each row segment of
+ * [first, count) on its own (a shard of a row is its own progression, so it costs its share): whole rows are
+ * bit-identical, a cut row agrees within the plans' ~1e-13 error. */
 int crimp_search(const double* t, int64_t n, double t0, const double* freq, int64_t nf,
                  const double* log10_negfdot, int64_t nfd, int32_t nharm, int32_t stat, int64_t first,
                  int64_t count, double* out, uint32_t flags, void* stream);

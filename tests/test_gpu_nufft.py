@@ -1,0 +1,157 @@
+"""precision="nufft" (csrc/search_nufft.h) through the C-ABI: the non-uniform-FFT Z^2 / H search against the
+reference's goldens and the oracle at the default path's per-trial contract (plain 1e-6 relative, best trial
+exact), its raw powers (fix-up off) against the fp64 kernel, determinism, row sharding, and the routes it leaves
+to the default path (unsorted photons, short or non-uniform grids). Full-size configs: tests/test_gpu_fullsize.py."""
+import numpy as np
+import pytest
+
+from conftest import gold
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def close_rel(got, ref, rtol=1e-6):
+    got, ref = np.asarray(got), np.asarray(ref)
+    err = np.abs(got - ref) / np.abs(ref)
+    assert err.max() <= rtol, "max relative error %.3g at %d" % (err.max(), int(err.argmax()))
+    return err.max()
+
+
+def _path():
+    from crimp_amd import _native as N
+    return N.load().crimp_last_search_path()
+
+
+SPREADS = ["auto", "gather", "mfma"]
+
+
+def _spread(monkeypatch, spread):
+    """auto: the library's choice (cell gather for <= 2 rows, MFMA slots otherwise); gather / mfma force one form."""
+    if spread != "auto":
+        monkeypatch.setenv("CRIMP_NUFFT_SPREAD", spread)
+
+
+@pytest.mark.parametrize("spread", SPREADS)
+def test_nufft_config1_goldens(gpu, spread, monkeypatch):
+    """Config 1 (the reference's own outputs on the bundled 1e2259 events, 400-trial progression)."""
+    from crimp_amd.periodsearch import PeriodSearch
+    _spread(monkeypatch, spread)
+    g = gold("periodsearch_1e2259.npz")
+    z = PeriodSearch(g["time"], g["freq"], 2, precision="nufft").ztest()
+    assert _path() == 2
+    assert int(np.argmax(z)) == 200
+    close_rel(z, g["z2_m2"])
+    h = PeriodSearch(g["time"], g["freq"], 20, precision="nufft").htest()
+    assert _path() == 2
+    assert int(np.argmax(h)) == 200
+    close_rel(h, g["h_m20"])
+    arr, df = PeriodSearch(g["time"], g["fsub"], 2, precision="nufft").twod_ztest(g["fd"])
+    np.testing.assert_array_equal(arr[:, :2], g["z2d_m2"][:, :2])
+    close_rel(arr[:, 2], g["z2d_m2"][:, 2])
+    assert list(df.columns) == ["Freq", "Freq_dot", "Z2pow"]
+
+
+def test_nufft_synthetic_goldens_and_routes(gpu):
+    """Synthetic goldens m = 1..20; grids the NUFFT does not take (non-uniform, < 64 trials, unsorted photons) go to
+    the default path with the same results."""
+    from crimp_amd.periodsearch import PeriodSearch
+    g = gold("periodsearch_synth.npz")
+    t, f = g["time"], g["freq"]
+    for m in (1, 2, 3, 5):
+        z = PeriodSearch(t, f, m, precision="nufft").ztest()
+        assert _path() == 2
+        close_rel(z, g["z_m%d" % m])
+        assert np.argmax(z) == np.argmax(g["z_m%d" % m])
+    for m in (1, 5, 20):
+        close_rel(PeriodSearch(t, f, m, precision="nufft").htest(), g["h_m%d" % m])
+        assert _path() == 2
+    close_rel(PeriodSearch(t, f[64:128], 2, precision="nufft").twod_ztest(g["fd"])[0][:, 2], g["z2d_m2"][:, 2])
+    assert _path() == 2
+    close_rel(PeriodSearch(t, f[64:128], 3, precision="nufft").twod_ztest(g["fd"])[0][:, 2], g["z2d_m3"][:, 2])
+    close_rel(PeriodSearch(g["time_perm"], g["freq_nu"], 2, precision="nufft").ztest(), g["z_nonuniform_m2"])
+    assert _path() != 2
+    close_rel(PeriodSearch(t[:2], f[:8], 3, precision="nufft").htest(), g["h_n2"])
+    close_rel(PeriodSearch(t, f[100:101], 2, precision="nufft").ztest(), g["z_m1trial"])
+
+
+@pytest.mark.parametrize("spread", SPREADS)
+def test_nufft_vs_oracle_larger(gpu, spread, monkeypatch):
+    """2e5 photons x 2048 trials (Z^2_2), a 3 x 1024 2-D grid (H_3) and H_20 on 4096 trials against the oracle."""
+    from crimp_amd.periodsearch import PeriodSearch
+    _spread(monkeypatch, spread)
+    from crimp_amd.synth import pulsed_events
+    from crimp_amd import _native as N
+    t = pulsed_events(200000, 2.0e5, 7.123456789, pulsed_frac=0.05, seed=4)
+    f = 7.123456789 + (np.arange(-1024, 1024) / (10 * 2.0e5))
+    z = PeriodSearch(t, f, 2, precision="nufft").ztest()
+    assert _path() == 2
+    zr = O.search(t, f, 2)
+    assert int(np.argmax(z)) == int(np.argmax(zr))
+    close_rel(z, zr)
+    assert N.load().crimp_last_fixups() <= 4
+    fd = np.array([-13.0, -12.0, -11.5])
+    a = PeriodSearch(t, f[512:1536], 3, precision="nufft").twod_htest(fd)[0][:, 2]
+    ar = O.search(t, f[512:1536], 3, freq_dot=fd, stat="h")
+    assert int(np.argmax(a)) == int(np.argmax(ar))
+    close_rel(a, ar)
+    f2 = 7.123456789 + (np.arange(-2048, 2048) / (10 * 2.0e5))
+    h = PeriodSearch(t, f2, 20, precision="nufft").htest()
+    hr = O.search(t, f2, 20, stat="h")
+    assert int(np.argmax(h)) == int(np.argmax(hr))
+    close_rel(h, hr)
+
+
+@pytest.mark.parametrize("spread", SPREADS)
+def test_nufft_raw_powers_vs_f64(gpu, spread, monkeypatch):
+    """The NUFFT itself (fix-up off) against the fp64 kernel on every trial: 1-D Z^2_2 and 2-D H_20 over 16 rows
+    (two row passes), odd trial counts per row (h = nf // 2 with nf odd)."""
+    from crimp_amd import ops, _native as N
+    _spread(monkeypatch, spread)
+    from crimp_amd.synth import pulsed_events
+    t = pulsed_events(300000, 3.0e5, 3.3, pulsed_frac=0.05, fdot=-2e-11, seed=7)
+    t0 = (t[0] + t[-1]) / 2
+    f = 3.3 + (np.arange(-700, 701) / (10 * 3.0e5))
+    ref = ops.search(t, t0, f, 2, 0, precision="f64")
+    z = ops.search(t, t0, f, 2, 0, flags=N.FLAG_NO_FIXUP, precision="nufft")
+    assert _path() == 2
+    close_rel(z, ref, 1e-6)
+    fd = np.linspace(-12.5, -10.0, 16)
+    ref = ops.search(t, t0, f[:301], 20, 1, log10_negfdot=fd, precision="f64")
+    h = ops.search(t, t0, f[:301], 20, 1, log10_negfdot=fd, flags=N.FLAG_NO_FIXUP, precision="nufft")
+    assert _path() == 2
+    close_rel(h, ref, 1e-6)
+
+
+def test_nufft_deterministic_and_row_shards(gpu):
+    """Repeat runs are bit-identical; a 2-D grid computed as row ranges (what each rank of a row-sharded search
+    computes) equals the whole grid bit for bit. A range that cuts rows is planned on its own segment of the row
+    (another n, centre and moment count), so it agrees with the whole grid within the plans' error, not bitwise."""
+    from crimp_amd import ops
+    from crimp_amd.synth import pulsed_events
+    t = pulsed_events(100000, 1.0e5, 3.0, pulsed_frac=0.1, seed=9)
+    f = 3.0 + np.arange(-300, 300) / 1.0e6
+    fd = np.array([-12.0, -11.0, -10.5])
+    t0 = (t[0] + t[-1]) / 2
+    full = ops.search(t, t0, f, 2, 0, log10_negfdot=fd, precision="nufft")
+    np.testing.assert_array_equal(ops.search(t, t0, f, 2, 0, log10_negfdot=fd, precision="nufft"), full)
+    rows = [ops.search(t, t0, f, 2, 0, log10_negfdot=fd, first=r * 600, count=600, precision="nufft") for r in range(3)]
+    np.testing.assert_array_equal(np.concatenate(rows), full)
+    parts = [ops.search(t, t0, f, 2, 0, log10_negfdot=fd, first=a, count=b - a, precision="nufft")
+             for a, b in ((0, 333), (333, 901), (901, 1800))]
+    cut = np.concatenate(parts)
+    close_rel(cut, full, 1e-6)
+    assert np.median(np.abs(cut - full) / np.abs(full)) <= 1e-12
+
+
+def test_nufft_unsorted_photons_take_default_path(gpu):
+    from crimp_amd.periodsearch import PeriodSearch
+    from crimp_amd.synth import pulsed_events
+    t = pulsed_events(50000, 5.0e4, 2.5, pulsed_frac=0.2, seed=3)
+    f = 2.5 + np.arange(-256, 256) / (10 * 5.0e4)
+    rng = np.random.default_rng(0)
+    tp = t[rng.permutation(t.size)]
+    tp[0], tp[-1] = t[0], t[-1]  # same t0
+    z = PeriodSearch(tp, f, 2, precision="nufft").ztest()
+    assert _path() == 1
+    close_rel(z, O.search(tp, f, 2))

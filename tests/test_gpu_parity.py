@@ -3,8 +3,7 @@
 Tolerances (BASELINE.json north_star): Z^2/H powers within 1e-6 relative PER TRIAL (plain relative error,
 no scale floor: ``close_rel``) for the default search path (exact-integer i8 MFMA kernel, fp64 kernel on
 other grids) and the fp64 path; best-trial index bit-exact; ToA phase shifts within 1e-4 cycles;
-calcphase within 1e-9 cycles; LL within 1e-9 relative (fp64 kernel). The opt-in fast path
-(precision="fast", fp32 sin/cos) is held to 1e-6 of max(|ref|, mean(ref)) per trial (``close_z``).
+calcphase within 1e-9 cycles; LL within 1e-9 relative (fp64 kernel). precision="nufft": tests/test_gpu_nufft.py.
 """
 import json
 import math
@@ -25,15 +24,6 @@ def close_rel(got, ref, rtol=RTOL):
     got, ref = np.asarray(got), np.asarray(ref)
     err = np.abs(got - ref) / np.abs(ref)
     assert err.max() <= rtol, "max relative error %.3g at %d" % (err.max(), int(err.argmax()))
-    return err.max()
-
-
-def close_z(got, ref, rtol=RTOL):
-    """Fast path: error per trial relative to max(|ref|, mean|ref|)."""
-    got, ref = np.asarray(got), np.asarray(ref)
-    scale = np.maximum(np.abs(ref), np.mean(np.abs(ref)))
-    err = np.abs(got - ref) / scale
-    assert err.max() <= rtol, "max scaled error %.3g at %d" % (err.max(), int(err.argmax()))
     return err.max()
 
 
@@ -76,18 +66,15 @@ def test_search_synthetic_golden_and_edges(gpu):
         PeriodSearch(t[:0], f, 2)
 
 
-@pytest.mark.parametrize("mode", ["exact", "f64", "fast", "fast-direct"])
-def test_search_vs_oracle_larger(gpu, mode, monkeypatch):
-    """Every search kernel on 2e5 photons x 2048 trials (Z^2_2) and a 3 x 1024 2-D grid (H_3): the exact kernel
-    (default) and the fp64 one per trial within 1e-6 relative, the fast f16-MFMA and fp32 direct kernels within
-    1e-6 of the power scale; best trial exact."""
+@pytest.mark.parametrize("mode", ["exact", "f64", "nufft"])
+def test_search_vs_oracle_larger(gpu, mode):
+    """Every search path on 2e5 photons x 2048 trials (Z^2_2) and a 3 x 1024 2-D grid (H_3): per trial within 1e-6
+    relative; best trial exact."""
     from crimp_amd.periodsearch import PeriodSearch
     from crimp_amd.synth import pulsed_events
     from crimp_amd import _native as N
-    prec = {"exact": None, "f64": "f64", "fast": "fast", "fast-direct": "fast"}[mode]
-    if mode == "fast-direct":
-        monkeypatch.setenv("CRIMP_SEARCH", "direct")
-    check = close_z if prec == "fast" else close_rel
+    prec = {"exact": None, "f64": "f64", "nufft": "nufft"}[mode]
+    check = close_rel
     t = pulsed_events(200000, 2.0e5, 7.123456789, pulsed_frac=0.05, seed=4)
     f = 7.123456789 + (np.arange(-1024, 1024) / (10 * 2.0e5))
     z = PeriodSearch(t, f, 2, precision=prec).ztest()
@@ -140,6 +127,8 @@ def test_search_f64_larger_vs_oracle(gpu):
     close_rel(PeriodSearch(t, f[:256], 20, precision="f64").htest(), hr, 1e-7)
     with pytest.raises(ValueError):
         PeriodSearch(t, f, 2, precision="f16").ztest()
+    with pytest.raises(ValueError):  # the fp32 fast path was retired (round 5)
+        PeriodSearch(t, f, 2, precision="fast").ztest()
 
 
 def test_search_sharded_ranges_equal_full(gpu):
@@ -162,26 +151,6 @@ def test_search_sharded_ranges_equal_full(gpu):
         ref = ops.search(t, t0, f, 2, 0, log10_negfdot=twod, precision="f64")
         z = ops.search(t, t0, f, 2, 0, log10_negfdot=twod, flags=N.FLAG_NO_FIXUP)
         close_rel(z, ref, 1e-6)
-
-
-def test_sincos_variants_accuracy_report(gpu, monkeypatch, capsys):
-    """Fast path: hardware v_sin/v_cos vs the polynomial in the fp32 direct kernel (reported; polynomial must pass
-    the fast path's scaled bound)."""
-    from crimp_amd.periodsearch import PeriodSearch
-    from crimp_amd.synth import pulsed_events
-    t = pulsed_events(300000, 3.0e5, 5.0, pulsed_frac=0.02, seed=12)
-    f = 5.0 + np.arange(-512, 512) / 3.0e6
-    zr = O.search(t, f, 2)
-    monkeypatch.setenv("CRIMP_SEARCH", "direct")
-    errs = {}
-    for hw in ("", "hw"):
-        monkeypatch.setenv("CRIMP_SINCOS", hw)
-        z = PeriodSearch(t, f, 2, precision="fast").ztest()
-        scale = np.maximum(np.abs(zr), zr.mean())
-        errs[hw or "poly"] = float((np.abs(z - zr) / scale).max())
-    with capsys.disabled():
-        print("\n[sincos] max scaled Z2 error: %s" % errs)
-    assert errs["poly"] <= RTOL
 
 
 def test_calcphase_golden(gpu):

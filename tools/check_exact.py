@@ -1,5 +1,5 @@
 """GPU check of the exact-integer search kernel: plain per-trial relative error against the reference's
-goldens and the oracle, bit-identity of trial partitions, and config-3 timing next to the fast path."""
+goldens and the oracle, bit-identity of trial partitions, and config-3 timing next to the NUFFT path."""
 import os
 import sys
 import time
@@ -27,7 +27,7 @@ def main():
     from oracle import oracle as O
     L = N.load()
     g = gold("periodsearch_1e2259.npz")
-    for prec in (None, "fast"):
+    for prec in (None, "nufft"):
         z = PeriodSearch(g["time"], g["freq"], 2, precision=prec).ztest()
         print("config1 Z2_2 %s: argmax %d  rel(max, at, p50, p99) %s  fixups %d" % (
             prec, int(np.argmax(z)), rel(z, g["z2_m2"]), L.crimp_last_fixups()), flush=True)
@@ -44,7 +44,7 @@ def main():
     t = pulsed_events(200000, 2.0e5, 7.123456789, pulsed_frac=0.05, seed=4)
     f = 7.123456789 + (np.arange(-1024, 1024) / (10 * 2.0e5))
     zr = O.search(t, f, 2)
-    for prec in (None, "fast"):
+    for prec in (None, "nufft"):
         z = PeriodSearch(t, f, 2, precision=prec).ztest()
         print("2e5x2048 Z2 %s: rel %s fixups %d  min power %.3g" % (prec, rel(z, zr), L.crimp_last_fixups(), zr.min()),
               flush=True)
@@ -60,7 +60,7 @@ def main():
     ff = torch.as_tensor(f_h, device="cuda")
     t0 = (t_h[0] + t_h[-1]) / 2
     res = {}
-    for prec in (None, "fast"):
+    for prec in (None, "nufft"):
         z = ops.search(tt, t0, ff, 2, 0, precision=prec)
         torch.cuda.synchronize()
         ts = []
@@ -76,11 +76,11 @@ def main():
     rng = np.random.default_rng(1)
     idx = np.unique(np.concatenate([[M // 2, M // 2 - 1, M // 2 + 1, 0, M - 1], rng.integers(0, M, 11)]))
     zr = O.search(t_h, f_h[idx], 2)
-    print("config3 sampled rel exact %s   fast %s" % (rel(res[None][idx], zr), rel(res["fast"][idx], zr)), flush=True)
+    print("config3 sampled rel exact %s   nufft %s" % (rel(res[None][idx], zr), rel(res["nufft"][idx], zr)), flush=True)
     a = ops.search(tt, t0, ff, 2, 0, first=0, count=M // 2 + 123).cpu().numpy()
     b = ops.search(tt, t0, ff, 2, 0, first=M // 2 + 123, count=M - (M // 2 + 123)).cpu().numpy()
     print("config3 partition bit-identical:", bool(np.array_equal(np.concatenate([a, b]), res[None])), flush=True)
-    print("exact vs fast scaled diff: %.3g" % float((np.abs(res[None] - res["fast"]) / np.mean(res[None])).max()))
+    print("exact vs nufft scaled diff: %.3g" % float((np.abs(res[None] - res["nufft"]) / np.mean(res[None])).max()))
 
 
 if __name__ == "__main__":
