@@ -499,13 +499,15 @@ PEAK_F64_TFLOPS = 78.6  # MI355X spec fp64 (vector and matrix); mb_f64 measures 
 
 def nufft_leg(a, t, t_h, f, rank, M, steps):
     """The rank's trial slice by precision="nufft": one untimed search, then ``steps`` timed ones (wall time with the
-    stream drained, and the library's hipEvent spans: whole pipeline, spread, merge, FFT, combine + finalize). The
-    per-kernel rooflines use the plan the library chose (n = FFT length, P moments):
-      spread  fp64: the cell gather's ~30 + 3 P operations per photon and harmonic (k_nu_gather), or the MFMA form's
-              512 issued flops per photon-harmonic (k_nu_spread), against the fp64 peak;
-      merge   HBM: slots read + the FFT input written, 16 B per complex value;
-      fft     HBM: two passes, each reading and writing P * rows * n complex values per harmonic;
-      combine HBM: P complex values read per trial and harmonic."""
+    stream drained, and the library's hipEvent spans: whole pipeline, spread, merge, FFT, combine + finalize). Each
+    kernel class is priced by the algorithmic work the library counted for the plan it chose (crimp_last_nufft_work;
+    DESIGN.md section 5):
+      spread  fp64 flops: the cell gather's ~40 + 5 P per photon, row and harmonic (k_nu_gather), or the MFMA form's
+              issued 512 per photon-harmonic (k_nu_spread), against the fp64 peak;
+      merge   HBM: MFMA slots read + the FFT input written (absent for the cell gather, which writes W directly);
+      fft     HBM: pass 1 reading the occupied rows and writing all, pass 2 reading all (fused with the Horner
+              combine, which writes one complex sum per trial and harmonic);
+      combine HBM: the finalize reading the harmonic sums and writing the powers."""
     import torch
     from crimp_amd import ops
     from crimp_amd import _native as N
@@ -527,23 +529,19 @@ def nufft_leg(a, t, t_h, f, rank, M, steps):
     wall = float(np.mean(walls))
     sp = np.mean(np.array([s_[:5] for s_ in spans]), axis=0)  # total, spread, merge, fft, combine+finalize
     n, P, form = N.last_nufft_plan()  # search_nufft.h nu_plan: least n P with x^P/P! <= 1e-14, x = pi (M/2) / n
+    w = N.last_nufft_work()
     m = a.nharm
-    # spread: the cell gather's fp64 work per photon and harmonic (premultiplier 2 two-products + cis ~ 30, then
-    # 3 per moment), or the MFMA form's issued 512 flops per photon-harmonic
-    spread_flops = (30.0 + 3.0 * P if form == "gather" else 512.0) * float(a.photons) * m
-    fft_bytes = 2 * 2 * 16.0 * P * n * m
-    merge_bytes = 16.0 * P * n * m * 2
-    comb_bytes = 16.0 * P * n * m
-    legs = {
-        "spread": {"bound": "fp64", "achieved": spread_flops / (sp[1] * 1e-3) / 1e12, "peak": PEAK_F64_TFLOPS,
-                   "unit": "TFLOP/s", "ms": sp[1]},
-        "merge": {"bound": "hbm", "achieved": merge_bytes / (sp[2] * 1e-3) / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                  "ms": sp[2]},
-        "fft": {"bound": "hbm", "achieved": fft_bytes / (sp[3] * 1e-3) / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                "ms": sp[3]},
-        "combine": {"bound": "hbm", "achieved": comb_bytes / (sp[4] * 1e-3) / 1e9, "peak": PEAK_HBM_GBS,
-                    "unit": "GB/s", "ms": sp[4]},
-    }
+    legs = {}
+    for name, ms, work, bound in (("spread", sp[1], w["spread_flops"], "fp64"), ("merge", sp[2], w["merge_bytes"], "hbm"),
+                                  ("fft", sp[3], w["fft_bytes"], "hbm"), ("combine", sp[4], w["combine_bytes"], "hbm")):
+        if ms <= 0.0 or work <= 0.0:
+            continue  # no such kernel in this plan (the cell gather has no merge)
+        if bound == "fp64":
+            legs[name] = {"bound": bound, "achieved": work / (ms * 1e-3) / 1e12, "peak": PEAK_F64_TFLOPS,
+                          "unit": "TFLOP/s", "ms": ms, "work": work}
+        else:
+            legs[name] = {"bound": bound, "achieved": work / (ms * 1e-3) / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                          "ms": ms, "work": work}
     for v in legs.values():
         v["frac"] = v["achieved"] / v["peak"]
     dom = max(legs, key=lambda k: legs[k]["ms"])
@@ -551,7 +549,8 @@ def nufft_leg(a, t, t_h, f, rank, M, steps):
             "ms_per_search": wall * 1e3, "pipeline_ms": sp[0], "search_path": path, "fp64_fixup_trials": nfix,
             "plan": {"fft_length": n, "moments": P, "spread": form}, "kernels": legs, "dominant": dom,
             "roofline": dict({"kernel": dom}, **legs[dom]),
-            "precision": "fp64 moments (v_mfma_f64_16x16x4_f64), fp64 FFT, per-trial 1e-6 certificate + fp64 fix-up"}
+            "precision": "fp64 moments (%s), fp64 FFT, per-trial 1e-6 certificate + fp64 fix-up"
+                         % ("VALU cell gather" if form == "gather" else "v_mfma_f64_16x16x4_f64 slots")}
 
 
 def pmc_traffic(photons, trials, nharm):

@@ -55,7 +55,7 @@ class Template(ctypes.Structure):
 
 
 EXPORTS = ("crimp_version", "crimp_last_error", "crimp_last_kernel_ms", "crimp_last_kernel_times", "crimp_last_fixups",
-           "crimp_last_search_path", "crimp_last_nufft_plan", "crimp_last_toa_grid_norms", "crimp_last_toa_grid_fast", "crimp_release_scratch",
+           "crimp_last_search_path", "crimp_last_nufft_plan", "crimp_last_nufft_work", "crimp_last_toa_grid_norms", "crimp_last_toa_grid_fast", "crimp_release_scratch",
            "crimp_device_count", "crimp_calcphase", "crimp_search", "crimp_search_sets", "crimp_toa_points",
            "crimp_toa_grid", "crimp_toa_fit", "crimp_toa_redchi2", "crimp_toa_fit_redchi2", "crimp_toa_shape_points", "crimp_binphases")
 
@@ -85,6 +85,7 @@ def load(require_device=True):
             L.crimp_last_toa_grid_fast.restype = ctypes.c_int64
             L.crimp_last_kernel_times.argtypes = [ctypes.POINTER(ctypes.c_double), i32]
             L.crimp_last_nufft_plan.argtypes = [ctypes.POINTER(i64), ctypes.POINTER(i32), ctypes.POINTER(i32)]
+            L.crimp_last_nufft_work.argtypes = [ctypes.POINTER(ctypes.c_double), i32]
             L.crimp_device_count.argtypes = [ctypes.POINTER(i32)]
             L.crimp_calcphase.argtypes = [P, i64, ctypes.POINTER(TimingModel), i32, P, P, u32, P]
             L.crimp_search.argtypes = [P, i64, ctypes.c_double, P, i64, P, i64, i32, i32, i64, i64, P, u32, P]
@@ -118,6 +119,15 @@ def last_nufft_plan():
     n, p, g = ctypes.c_int64(0), ctypes.c_int32(0), ctypes.c_int32(0)
     L.crimp_last_nufft_plan(ctypes.byref(n), ctypes.byref(p), ctypes.byref(g))
     return int(n.value), int(p.value), "gather" if g.value else "mfma"
+
+
+def last_nufft_work():
+    """The last NUFFT search's algorithmic work (crimp_last_nufft_work): spread flops, spread / merge / FFT /
+    combine + finalize HBM bytes."""
+    L = load(require_device=False)
+    w = (ctypes.c_double * 5)()
+    L.crimp_last_nufft_work(w, 5)
+    return {"spread_flops": w[0], "spread_bytes": w[1], "merge_bytes": w[2], "fft_bytes": w[3], "combine_bytes": w[4]}
 
 
 def last_kernel_times():

@@ -1705,7 +1705,7 @@ static int grid_is_progression(Scratch& sc, hipStream_t s, const double* freq, i
     *ap = reinterpret_cast<double*>(info);
     if (nf < 2) return CRIMP_OK;
     HIPCHK(hipMemsetAsync(info, 0, 3 * sizeof(unsigned long long), s));
-    k_ap_check<<<(unsigned)std::min<int64_t>(cdiv(nf, 256), 1024), 256, 0, s>>>(freq, nf, info);
+    k_ap_check<<<(unsigned)std::min<int64_t>(cdiv(nf, 256), 128), 256, 0, s>>>(freq, nf, info);
     HIPCHK(hipGetLastError());
     double h[3];
     HIPCHK(d2h(s, h, info, sizeof(h)));
@@ -1715,7 +1715,8 @@ static int grid_is_progression(Scratch& sc, hipStream_t s, const double* freq, i
 
 // Default path: the exact integer-MFMA kernel (search_exact.h) over an arithmetic-progression grid, then the
 // fp64 fix-up of the trials whose power is too small for the kernel's error bound (k_search_finalize_exact).
-// int64 totals in units of 2^-36 hold |C_k| <= n exactly for n < 2^27 photons.
+// int64 totals in units of 2^-36 hold |C_k| <= n exactly for n < 2^27 photons; a larger search runs its photons in
+// chunks of < 2^27, each into its own totals, summed exactly by the finalize (periodsearch.py:57-71 has no limit).
 static const int64_t kExactMaxPhotons = int64_t(1) << 27;
 static const int64_t kExFoldMaxBlocks = 8192;  // fold scratch of one launch <= 1 GiB
 static const int64_t kExFoldPhotons = (int64_t)kExFold * kExChunk;  // photons between int64 folds (search_exact.h)
@@ -1782,10 +1783,13 @@ static int exact_search(Scratch& sc, hipStream_t s, const double* dt, const doub
                         int64_t count, double* out, KernelTimer* kt, int64_t* nfixed, bool no_fixup) {
     const int64_t tpr = cdiv(nf, kExTileTrials);
     const int ncomp = 2 * nharm;
+    // photon chunks of < 2^27 (one for every search below that), each with its own int64 totals
+    const int64_t nchunk = cdiv(n, kExactMaxPhotons - 1);
+    const int64_t pc = cdiv(n, nchunk);
     // Trial blocks are bounded by the int64 totals buffer (part_budget) and by the tiles one launch may hold
     // (<= kExFoldMaxBlocks block columns, so that a fold scratch stays <= 1 GiB: a 2-D grid's rows each start a
     // new tile, so a block of short rows holds more tiles than its trial count suggests); whole tiles.
-    int64_t want = std::max<int64_t>(kExTileTrials, part_budget() / (8 * ncomp)), cb = 0;
+    int64_t want = std::max<int64_t>(kExTileTrials, part_budget() / (8 * ncomp * nchunk)), cb = 0;
     struct Blk { int64_t bfirst, bcount, tf, nt, bpg, chunk, splits; };
     std::vector<Blk> blks;
     int64_t fold_blocks = 0;  // the largest bpg * splits of the blocks whose splits fold into the int64 scratch
@@ -1804,7 +1808,7 @@ static int exact_search(Scratch& sc, hipStream_t s, const double* dt, const doub
             k.nt = tl - k.tf + 1;
             k.bpg = cdiv(k.nt, kExWaves);
             fits = k.bpg <= kExFoldMaxBlocks;
-            exact_splits(n, k.bpg, &k.chunk, &k.splits);
+            exact_splits(pc, k.bpg, &k.chunk, &k.splits);
             if (k.chunk > kExFoldPhotons) fold_blocks = std::max<int64_t>(fold_blocks, k.bpg * k.splits);
             blks.push_back(k);
         }
@@ -1817,7 +1821,7 @@ static int exact_search(Scratch& sc, hipStream_t s, const double* dt, const doub
     long long* fold = nullptr;
     int64_t* flagged = nullptr;
     int* nflag = nullptr;
-    HIPCHK(sc.alloc(&tot, (size_t)(ncomp * cb)));
+    HIPCHK(sc.alloc(&tot, (size_t)(ncomp * cb * nchunk)));
     HIPCHK(sc.alloc(&flagged, (size_t)count));
     HIPCHK(sc.alloc(&nflag, 1));
     // fold scratch only when some block's splits are longer than one fold period; shorter splits never touch it
@@ -1828,21 +1832,28 @@ static int exact_search(Scratch& sc, hipStream_t s, const double* dt, const doub
     for (size_t bi = 0; bi < blks.size(); ++bi) {
         const Blk& k = blks[bi];
         const int64_t b0 = k.bfirst - first;
-        HIPCHK(hipMemsetAsync(tot, 0, (size_t)(ncomp * k.bcount) * sizeof(unsigned long long), s));
+        const int64_t cstride = (int64_t)ncomp * k.bcount;  // one chunk's totals
+        HIPCHK(hipMemsetAsync(tot, 0, (size_t)(cstride * nchunk) * sizeof(unsigned long long), s));
         dim3 grid((unsigned)k.bpg, (unsigned)k.splits);
-        for (int h = 1; h <= nharm; ++h) {
-            if (twod)
-                k_search_exact<true><<<grid, kExBlock, 0, s>>>(dt, dt2, n, k.chunk, freq, nf, c2, ap, k.tf, k.nt, tpr,
-                                                               k.bfirst, k.bcount, h, tot, fold);
-            else
-                k_search_exact<false><<<grid, kExBlock, 0, s>>>(dt, dt2, n, k.chunk, freq, nf, c2, ap, k.tf, k.nt, tpr,
-                                                                k.bfirst, k.bcount, h, tot, fold);
-            HIPCHK(hipGetLastError());
+        for (int64_t pch = 0; pch < nchunk; ++pch) {
+            const int64_t p0 = pch * pc, np_ = std::min<int64_t>(pc, n - p0);
+            unsigned long long* tc = tot + pch * cstride;
+            for (int h = 1; h <= nharm; ++h) {
+                if (twod)
+                    k_search_exact<true><<<grid, kExBlock, 0, s>>>(dt + p0, dt2 ? dt2 + p0 : nullptr, np_, k.chunk, freq,
+                                                                   nf, c2, ap, k.tf, k.nt, tpr, k.bfirst, k.bcount, h, tc,
+                                                                   fold);
+                else
+                    k_search_exact<false><<<grid, kExBlock, 0, s>>>(dt + p0, dt2 ? dt2 + p0 : nullptr, np_, k.chunk,
+                                                                    freq, nf, c2, ap, k.tf, k.nt, tpr, k.bfirst, k.bcount,
+                                                                    h, tc, fold);
+                HIPCHK(hipGetLastError());
+            }
         }
         if (kt && bi + 1 == blks.size()) kt->stop();
         k_search_finalize_exact<<<(unsigned)cdiv(k.bcount, 256), 256, 0, s>>>(
             reinterpret_cast<const long long*>(tot), k.bcount, nharm, stat, (double)n, sigc, fixup_rel(), b0, out + b0,
-            nflag, flagged);
+            nflag, flagged, (int)nchunk, cstride);
         HIPCHK(hipGetLastError());
     }
     int nf_h = 0;
@@ -1861,6 +1872,11 @@ extern "C" int crimp_last_nufft_plan(int64_t* fft_length, int32_t* moments, int3
     if (moments) *moments = g_last_nufft_p;
     if (gather) *gather = g_last_nufft_gather;
     return CRIMP_OK;
+}
+
+extern "C" int crimp_last_nufft_work(double* work, int32_t cap) {
+    for (int i = 0; i < 5 && i < cap; ++i) work[i] = g_nu_work[i];
+    return 5;
 }
 
 extern "C" int crimp_search(const double* t, int64_t n, double t0, const double* freq, int64_t nf,
@@ -1922,8 +1938,7 @@ extern "C" int crimp_search(const double* t, int64_t n, double t0, const double*
         //            the default path otherwise;
         //   f64:     fp64 kernel.
         KernelTimer kt(s, flags & CRIMP_FLAG_TIME_KERNELS);
-        bool factorised = !f64 && (nf >= 256 || (flags & CRIMP_FLAG_FORCE_MFMA) || (nufft && nf >= 64)) &&
-                          (nufft || n < kExactMaxPhotons);
+        bool factorised = !f64 && (nf >= 256 || (flags & CRIMP_FLAG_FORCE_MFMA) || (nufft && nf >= 64));
         double* ap = nullptr;
         if (factorised) {
             bool ok = false;
@@ -1941,7 +1956,6 @@ extern "C" int crimp_search(const double* t, int64_t n, double t0, const double*
                               flags & CRIMP_FLAG_TIME_KERNELS, &nfix, (flags & CRIMP_FLAG_NO_FIXUP) != 0, &done);
             if (rc) return rc;
             if (done) g_last_fixups = nfix;
-            if (!done && n >= kExactMaxPhotons) factorised = false;
         }
         if (done) {
         } else if (factorised) {

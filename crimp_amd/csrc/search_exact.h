@@ -830,17 +830,33 @@ __global__ __launch_bounds__(kExBlock, 1) void k_search_exact(
 // harmonics i <= k (Z2, and H's cumulative g_k = sum_{i<=k} Z2_i - 4(k-1)) has standard deviation
 // (4/N) sc sqrt(sum_{i<=k} (C_i^2 + S_i^2)); the bound is kappa = 10 of them plus the bias. H = max_k g_k moves
 // by at most the bound of any g_k that can reach the maximum (g_k + err_k >= H - err_k*), so only those count.
+// nchunk > 1 (searches of >= 2^27 photons): the photons ran in chunks of < 2^27, each into its own int64 totals
+// (tot + c * chunk_stride, exact per chunk); their sum is formed exactly as 32-bit halves summed in int64 (each
+// half-sum < nchunk 2^32) and converted once.
+__device__ __forceinline__ double ex_total(const long long* __restrict__ tot, int64_t idx, int nchunk,
+                                           int64_t chunk_stride) {
+    if (nchunk == 1) return (double)tot[idx] * kExUnit;
+    long long hi = 0, lo = 0;
+    for (int c = 0; c < nchunk; ++c) {
+        const long long v = tot[(int64_t)c * chunk_stride + idx];
+        hi += v >> 32;                 // arithmetic shift: v = hi 2^32 + lo, 0 <= lo < 2^32
+        lo += v & 0xffffffffLL;
+    }
+    return ((double)hi * 4294967296.0 + (double)lo) * kExUnit;
+}
+
 __global__ __launch_bounds__(256) void k_search_finalize_exact(const long long* __restrict__ tot, int64_t count, int m,
                                                                int stat, double n, double sc, double rel, int64_t tbase,
                                                                double* __restrict__ out, int* __restrict__ nflag,
-                                                               int64_t* __restrict__ flagged) {
+                                                               int64_t* __restrict__ flagged, int nchunk,
+                                                               int64_t chunk_stride) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= count) return;
     const double w = 2.0 / n, kappa = 10.0;
     const double lin = kappa * 2.0 * w * sc, quad = w * 2.0 * (kappa * sc) * (kappa * sc);
     auto zk = [&](int k) {
-        const double c = (double)tot[(int64_t)(2 * k) * count + t] * kExUnit;
-        const double s = (double)tot[(int64_t)(2 * k + 1) * count + t] * kExUnit;
+        const double c = ex_total(tot, (int64_t)(2 * k) * count + t, nchunk, chunk_stride);
+        const double s = ex_total(tot, (int64_t)(2 * k + 1) * count + t, nchunk, chunk_stride);
         return c * c + s * s;
     };
     double p, err;
@@ -891,7 +907,16 @@ __global__ __launch_bounds__(256) void k_ap_check(const double* __restrict__ f, 
         dev = fmax(dev, __shfl_xor(dev, o));
         fm = fmax(fm, __shfl_xor(fm, o));
     }
+    // one atomic pair per block (same-address atomics from every wave serialise at L2)
+    __shared__ double red[2][4];
     if ((threadIdx.x & 63) == 0) {
+        red[0][threadIdx.x >> 6] = dev;
+        red[1][threadIdx.x >> 6] = fm;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        dev = fmax(fmax(red[0][0], red[0][1]), fmax(red[0][2], red[0][3]));
+        fm = fmax(fmax(red[1][0], red[1][1]), fmax(red[1][2], red[1][3]));
         atomicMax(&info[1], (unsigned long long)__double_as_longlong(dev));
         atomicMax(&info[2], (unsigned long long)__double_as_longlong(fm));
     }

@@ -257,18 +257,24 @@ __global__ __launch_bounds__(256) void k_nu_cellstart(const double* __restrict__
     }
 }
 
-// The lane of wrapped cell g sums, over its unwrapped cells G = g (mod n) and their photons in time order, the
-// moments c_r e^p of rows r < nrow: b_p,r[g] = sum c_{i,r} e_i^p with c = e^{2 pi i k (fc dt + c2_r dt^2)},
-// e = k dt s1 - G, in registers (no reduction, deterministic), and writes W[p * nrow + r][g]. fp64 VALU throughout:
-// per photon, row and harmonic one premultiplier phase and cis, then 3 operations per moment.
+// L lanes per wrapped cell g sum, over its unwrapped cells G = g (mod n) and their photons in time order (lane s
+// takes the cell's photons s, s + L, ...), the moments c_r e^p of rows r < nrow: b_p,r[g] = sum c_{i,r} e_i^p with
+// c = e^{2 pi i k (fc dt + c2_r dt^2)}, e = k dt s1 - G, in registers; an xor butterfly over the L lanes (a fixed
+// order: deterministic) completes the sums and lane s writes the moments p = s (mod L) to W[p * nrow + r][g].
+// fp64 VALU throughout: per photon, row and harmonic one premultiplier phase and cis, then 3 operations per moment.
+// L > 1 spreads a cell's photons over several lanes when cells are dense (many photons per cell, few cells).
 constexpr int kNuGatherRows = 2;
-template <int R, bool TWOD>
+template <int R, bool TWOD, int L>
 __global__ __launch_bounds__(256) void k_nu_gather(const double* __restrict__ dt, const int64_t* __restrict__ start,
-                                                   int64_t gmin, int64_t gmax, int64_t nfft, double s1, double fch,
-                                                   double fcl, const double* __restrict__ c2row, int nrow, int k,
-                                                   int P, const double2* __restrict__ tab, double2* __restrict__ W) {
-    const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (g >= nfft) return;
+                                                   int64_t gmin, int64_t gmax, int64_t nfft, int64_t gbase,
+                                                   int64_t gcount, double s1, double fch, double fcl,
+                                                   const double* __restrict__ c2row, int nrow, int k, int P,
+                                                   const double2* __restrict__ tab, double2* __restrict__ W) {
+    const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t idx = tid / L;
+    const int sub = (int)(tid % L);
+    if (idx >= gcount) return;  // whole L-groups leave together (L divides 64)
+    const int64_t g = (gbase + idx) & (nfft - 1);  // the FFT's occupied rows only (nu_occupied)
     double ar[R][kNuGatherMaxP], ai[R][kNuGatherMaxP];
 #pragma unroll
     for (int r = 0; r < R; ++r)
@@ -281,7 +287,7 @@ __global__ __launch_bounds__(256) void k_nu_gather(const double* __restrict__ dt
     for (int64_t G = gmin + (((g - gmin) % nfft) + nfft) % nfft; G <= gmax; G += nfft) {
         const int64_t i0 = start[G - gmin], i1 = start[G - gmin + 1];
         const double Gd = (double)G;
-        for (int64_t i = i0; i < i1; ++i) {
+        for (int64_t i = i0 + sub; i < i1; i += L) {
             const double d = dt[i];
             const double e = kd * (d * s1) - Gd;
             const double p1 = nu_frac_prod(fch, fcl, d);
@@ -311,26 +317,38 @@ __global__ __launch_bounds__(256) void k_nu_gather(const double* __restrict__ dt
         }
     }
 #pragma unroll
+    for (int o = L / 2; o > 0; o >>= 1)
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int p = 0; p < kNuGatherMaxP; ++p)
+                if (p < P) {
+                    ar[r][p] += __shfl_xor(ar[r][p], o);
+                    ai[r][p] += __shfl_xor(ai[r][p], o);
+                }
+#pragma unroll
     for (int r = 0; r < R; ++r)
 #pragma unroll
         for (int p = 0; p < kNuGatherMaxP; ++p)
-            if (r < nrow && p < P) W[((int64_t)p * nrow + r) * nfft + g] = make_double2(ar[r][p], ai[r][p]);
+            if (r < nrow && p < P && (p % L) == sub)
+                W[((int64_t)p * nrow + r) * nfft + g] = make_double2(ar[r][p], ai[r][p]);
 }
 
 // slots -> W[beta][g] (beta = p * nrow + row, complex), for the wrapped cells g of one block
 __global__ __launch_bounds__(256) void k_nu_merge(const double* __restrict__ U, int64_t SL,
                                                   const int64_t* __restrict__ ctab, int64_t nchunk, int64_t gmin,
-                                                  int64_t gmax, int64_t nfft, double2* __restrict__ W) {
+                                                  int64_t gmax, int64_t nfft, int64_t gbase, int64_t gcount,
+                                                  double2* __restrict__ W) {
     __shared__ int64_t rs[kNuMergeG][kNuMaxWrap];
     __shared__ int rc[kNuMergeG][kNuMaxWrap];
     __shared__ int nr[kNuMergeG];
     extern __shared__ double nu_acc[];  // [kNuMergeG][SL]
-    const int64_t g0 = (int64_t)blockIdx.x * kNuMergeG;
+    const int64_t i0 = (int64_t)blockIdx.x * kNuMergeG;  // cells gbase + i (mod n), i < gcount: the occupied rows
     const int tid = threadIdx.x;
     if (tid < kNuMergeG) {
-        const int64_t g = g0 + tid;
+        const int64_t g = (gbase + i0 + tid) & (nfft - 1);
         int cnt = 0;
-        if (g < nfft) {
+        if (i0 + tid < gcount) {
             int64_t Gu = gmin + (((g - gmin) % nfft) + nfft) % nfft;  // smallest unwrapped cell >= gmin, = g mod n
             for (; Gu <= gmax && cnt < kNuMaxWrap; Gu += nfft) {
                 int64_t lo = 0, hi = nchunk;  // first chunk whose last cell is >= Gu
@@ -366,8 +384,10 @@ __global__ __launch_bounds__(256) void k_nu_merge(const double* __restrict__ U, 
     for (int64_t idx = tid; idx < kNuMergeG * B; idx += 256) {
         const int t = (int)(idx % kNuMergeG);
         const int64_t beta = idx / kNuMergeG;
-        const int64_t g = g0 + t;
-        if (g < nfft) W[beta * nfft + g] = make_double2(nu_acc[t * SL + 2 * beta], nu_acc[t * SL + 2 * beta + 1]);
+        if (i0 + t < gcount) {
+            const int64_t g = (gbase + i0 + t) & (nfft - 1);
+            W[beta * nfft + g] = make_double2(nu_acc[t * SL + 2 * beta], nu_acc[t * SL + 2 * beta + 1]);
+        }
     }
 }
 
@@ -495,16 +515,16 @@ __device__ void nu_fft_lds(double2* s, int ll, int lc, int sa, int sc, const NuT
 // pass 1 of the four-step FFT: view each batch as [n1][n2]; DFT along a of 2^lc consecutive columns b, times
 // w_n^{b k1}, stored at y[k1 n2 + b]
 __global__ __launch_bounds__(256) void k_nu_fft_cols(const double2* __restrict__ X, double2* __restrict__ Y,
-                                                     int lnfft, int ln1, int lc, NuTw T) {
+                                                     int lnfft, int ln1, int lc, NuTw T, int alo, int acnt) {
     extern __shared__ double2 nu_s[];
     const int64_t nfft = int64_t(1) << lnfft;
     const int ln2 = lnfft - ln1, c = 1 << lc, n1 = 1 << ln1;
     const int64_t b0 = (int64_t)blockIdx.x << lc;
     const double2* x = X + (int64_t)blockIdx.y * nfft;
     double2* y = Y + (int64_t)blockIdx.y * nfft;
-    for (int e = threadIdx.x; e < (n1 << lc); e += 256) {
+    for (int e = threadIdx.x; e < (n1 << lc); e += 256) {  // rows a outside [alo, alo + acnt) (mod n1) hold no cell
         const int a = e >> lc, cc = e & (c - 1);
-        nu_s[e] = x[((int64_t)a << ln2) + b0 + cc];
+        nu_s[e] = ((a - alo) & (n1 - 1)) < acnt ? x[((int64_t)a << ln2) + b0 + cc] : make_double2(0.0, 0.0);
     }
     __syncthreads();
     nu_fft_lds(nu_s, ln1, lc, c, 1, T, lnfft);
@@ -524,6 +544,58 @@ __global__ __launch_bounds__(256) void k_nu_fft_rows(double2* __restrict__ X, in
     __syncthreads();
     nu_fft_lds(nu_s, ll, lr, 1, L, T, lnfft);
     for (int e = threadIdx.x; e < (L << lr); e += 256) x[e] = nu_s[e];
+}
+
+// Pass 2 of the FFT fused with the combine: block (k1, r) transforms row k1 (length 2^ll = n2) of every moment p of
+// trial-grid row r, from p = P-1 down to 0, and keeps the Horner sum A = B_p + (z / (p+1)) A of its 2^ll positions in
+// registers (z = 2 pi i jc / n), so the moments' transforms are read once and never written back; the trials' (C_k,
+// S_k) go to CS as k_nu_combine writes them. X[beta][pos], beta = p * nrow + r, pos = k1 n2 + k2 holds J = k1 + n1 k2.
+constexpr int kNuFusedPer = kNuTile / 256;  // positions per thread
+__global__ __launch_bounds__(256) void k_nu_fft_rows_combine(const double2* __restrict__ X, int ll, int lnfft, NuTw T,
+                                                             int P, int nrow, int64_t nf, int64_t jhi, int64_t h,
+                                                             int64_t tbase, int64_t nbt, double2* __restrict__ CS) {
+    extern __shared__ double2 nu_s[];
+    const int64_t nfft = int64_t(1) << lnfft;
+    const int L = 1 << ll, ln1 = lnfft - ll;
+    const int64_t k1 = blockIdx.x;
+    const int r = blockIdx.y;
+    double2 acc[kNuFusedPer];
+#pragma unroll
+    for (int q = 0; q < kNuFusedPer; ++q) acc[q] = make_double2(0.0, 0.0);
+    for (int p = P - 1; p >= 0; --p) {
+        const double2* x = X + ((int64_t)p * nrow + r) * nfft + (k1 << ll);
+        for (int e = threadIdx.x; e < L; e += 256) nu_s[e] = x[e];
+        __syncthreads();
+        nu_fft_lds(nu_s, ll, 0, 1, L, T, lnfft);
+#pragma unroll
+        for (int q = 0; q < kNuFusedPer; ++q) {
+            const int b = threadIdx.x + 256 * q;
+            if (b < L) {
+                const double2 v = nu_s[b];
+                const int64_t J = k1 + ((int64_t)b << ln1);
+                const int64_t jc = J <= jhi ? J : J - nfft;  // positions between the two ends hold no trial
+                // k_nu_combine's arithmetic exactly: th = (jc / n) 2 pi, f = th / (p + 1)
+                const double f = (((double)jc / (double)nfft) * 6.283185307179586476925286766559) / (double)(p + 1);
+                acc[q] = make_double2(fma(-f, acc[q].y, v.x), fma(f, acc[q].x, v.y));
+            }
+        }
+        __syncthreads();  // the next moment's load overwrites the tile
+    }
+#pragma unroll
+    for (int q = 0; q < kNuFusedPer; ++q) {
+        const int b = threadIdx.x + 256 * q;
+        if (b >= L) continue;
+        const int64_t J = k1 + ((int64_t)b << ln1);
+        int64_t jc;
+        if (J <= jhi)
+            jc = J;
+        else if (J >= nfft - h)
+            jc = J - nfft;
+        else
+            continue;
+        const int64_t t = tbase + r * nf + jc;  // (row0 + r) nf + jbase + jc - tb0
+        if (t >= 0 && t < nbt) CS[t] = acc[q];
+    }
 }
 
 // (C_k, S_k) of the trials of one harmonic: position pos = k1 n2 + k2 of the FFT output holds J = k1 + n1 k2
@@ -622,6 +694,9 @@ static int g_last_search_path = 0;  // crimp_last_search_path(): 0 fp64 direct, 
 static int64_t g_last_nufft_n = 0;   // crimp_last_nufft_plan(): the last NUFFT's largest FFT length, its moments,
 static int g_last_nufft_p = 0;       // and its spread form (1 cell gather, 0 MFMA slots)
 static int g_last_nufft_gather = 0;
+// crimp_last_nufft_work(): the last NUFFT's algorithmic work per kernel class -- spread fp64 flops, spread HBM bytes,
+// merge bytes, FFT bytes (pass 2 fused with the Horner combine included), combine + finalize bytes
+static double g_nu_work[5] = {0, 0, 0, 0, 0};
 
 static double nu_trunc(double x, int P, double* invfact) {  // x^P / P!
     double f = 1.0, xp = 1.0;
@@ -670,6 +745,22 @@ static int nu_tables(Scratch& sc, hipStream_t s, int lnfft, NuTw* T, const doubl
     return CRIMP_OK;
 }
 
+// The FFT input's occupied rows a in [alo, alo + acnt) (mod n1) of the four-step view [n1][n2]: the wrapped cells
+// of harmonic k's unwrapped range [gmin, gmax], widened to whole rows; a single-pass FFT (n1 = 1) or a range that
+// wraps the grid takes all rows. Only those rows are spread into and read by pass 1; the others are zero.
+static void nu_occupied(int64_t gmin, int64_t gmax, int lnfft, int ln1, int* alo, int* acnt) {
+    const int64_t nfft = int64_t(1) << lnfft, n1 = int64_t(1) << ln1;
+    const int ln2 = lnfft - ln1;
+    *alo = 0;
+    *acnt = (int)n1;
+    if (ln1 == 0 || gmax - gmin + 1 >= nfft) return;
+    const int64_t glo = gmin & (nfft - 1), ghi = glo + (gmax - gmin);  // unwrapped end
+    const int64_t a0 = glo >> ln2, a1 = ghi >> ln2;
+    if (a1 - a0 + 1 >= n1) return;
+    *alo = (int)a0;
+    *acnt = (int)(a1 - a0 + 1);
+}
+
 template <bool TWOD>
 static void nu_launch_spread(int G, dim3 grid, hipStream_t s, const double* dt, int64_t n, int64_t nchunk, double s1,
                              double fch, double fcl, const double* c2, int nrow, int k0, int P, const NuPass* ps,
@@ -680,6 +771,32 @@ static void nu_launch_spread(int G, dim3 grid, hipStream_t s, const double* dt, 
 }
 
 // Budget of the NUFFT path's device buffers (CRIMP_NUFFT_BUDGET_MB, default 6144): slots, FFT ping-pong, sums.
+template <int R, bool TWOD>
+static void launch_gather_r(int L, int64_t gcount, const double* dt, const int64_t* start, int64_t gmin, int64_t gmax,
+                            int64_t nfft, int64_t gbase, double s1, double fch, double fcl, const double* c2, int nrow,
+                            int k, int P, const double2* tab, double2* W, hipStream_t s) {
+    const dim3 grid((unsigned)cdiv(gcount * L, 256));
+#define NU_GATHER(LL) k_nu_gather<R, TWOD, LL><<<grid, 256, 0, s>>>(dt, start, gmin, gmax, nfft, gbase, gcount, s1, \
+                                                                     fch, fcl, c2, nrow, k, P, tab, W)
+    switch (L) {
+        case 8: NU_GATHER(8); break;
+        case 4: NU_GATHER(4); break;
+        case 2: NU_GATHER(2); break;
+        default: NU_GATHER(1); break;
+    }
+#undef NU_GATHER
+}
+static void launch_gather(int L, bool twod, int64_t gcount, const double* dt, const int64_t* start, int64_t gmin,
+                          int64_t gmax, int64_t nfft, int64_t gbase, double s1, double fch, double fcl,
+                          const double* c2, int nrow, int k, int P, const double2* tab, double2* W, hipStream_t s) {
+    if (twod)
+        launch_gather_r<kNuGatherRows, true>(L, gcount, dt, start, gmin, gmax, nfft, gbase, s1, fch, fcl, c2, nrow, k,
+                                             P, tab, W, s);
+    else
+        launch_gather_r<1, false>(L, gcount, dt, start, gmin, gmax, nfft, gbase, s1, fch, fcl, c2, nrow, k, P, tab, W,
+                                  s);
+}
+
 static int64_t nufft_budget() {
     static int64_t b = -1;
     if (b < 0) {
@@ -802,6 +919,7 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* dt, const doub
             g_last_nufft_p = pl.P;
         }
     g_last_nufft_gather = gather_grid ? 1 : 0;
+    for (double& w : g_nu_work) w = 0.0;
     // buffers sized for the largest group; harmonics per spread pass: the largest G in {8, 4, 2, 1} whose slots fit
     // the budget beside W, Y and the sums
     int64_t Bmax = 0, nfmax = 0, csmax = 0, nrow_all = 0;
@@ -835,6 +953,13 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* dt, const doub
         if (G == 2 || ubytes + fixed_bytes <= nufft_budget()) break;
     }
     auto use_gather = [&](const NuPlan&) { return gather_grid; };
+    // pass 2 fused with the combine (default); CRIMP_NUFFT_FUSED=0 runs them as two kernels (A/B hook)
+    const char* fused_env = getenv("CRIMP_NUFFT_FUSED");
+    const bool fused_combine = !(fused_env && !strcmp(fused_env, "0"));
+    const char* lanes_s = getenv("CRIMP_NUFFT_LANES");
+    const int lanes_env = lanes_s ? atoi(lanes_s) : 0;
+    ARGCHK(lanes_env == 0 || lanes_env == 1 || lanes_env == 2 || lanes_env == 4 || lanes_env == 8,
+           "CRIMP_NUFFT_LANES must be 1, 2, 4 or 8");
     bool any_mfma = false;
     int64_t starts_max = 0;
     for (const NuPlan& pl : plans) {
@@ -923,15 +1048,33 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* dt, const doub
         const int lrow = 12 - ln2;  // rows per block in pass 2
         const int64_t jbase = pl.j0 + pl.h;
         // W (moments of harmonic k, rows [rb, rb + nrow)) -> FFT -> (C_k, S_k) of the batch's trials
+        auto occupied = [&](int k, int* alo, int* acnt) {
+            nu_occupied(pl.gmin[(size_t)(k - 1)], pl.gmax[(size_t)(k - 1)], lnfft, ln1, alo, acnt);
+        };
         auto fft_combine = [&](int k, int64_t rb, int nrow, int64_t tb0, int64_t nbt) -> int {
             const int64_t Bp = (int64_t)P * nrow;
+            const double plane = 16.0 * (double)Bp * (double)nfft;  // one complex FFT buffer of the batch
             double2* Zo = W;
             if (ln1 > 0) {
+                int alo = 0, acnt = 0;
+                occupied(k, &alo, &acnt);
+                g_nu_work[3] += plane * ((double)acnt / (double)(int64_t(1) << ln1)) + plane;  // occupied rows in, all out
                 k_nu_fft_cols<<<dim3((unsigned)(int64_t(1) << (ln2 - lcol)), (unsigned)Bp), 256, lds_fft, s>>>(
-                    W, Y, lnfft, ln1, lcol, T);
+                    W, Y, lnfft, ln1, lcol, T, alo, acnt);
                 HIPCHK(hipGetLastError());
                 Zo = Y;
             }
+            if (fused_combine) {  // pass 2 and the moments' Horner sum in one kernel (FFT span)
+                g_nu_work[3] += plane + 16.0 * (double)nbt;
+                k_nu_fft_rows_combine<<<dim3((unsigned)(int64_t(1) << ln1), (unsigned)nrow), 256, lds_fft, s>>>(
+                    Zo, ln2, lnfft, T, P, nrow, nf, pl.nseg - 1 - pl.h, pl.h, rb * nf + jbase - (tb0 + first), nbt,
+                    CS + (int64_t)(k - 1) * nbt);
+                HIPCHK(hipGetLastError());
+                HIPCHK(span(2));
+                return CRIMP_OK;
+            }
+            g_nu_work[3] += 2.0 * plane;
+            g_nu_work[4] += plane + 16.0 * (double)nbt;
             k_nu_fft_rows<<<(unsigned)cdiv(Bp << ln1, int64_t(1) << lrow), 256, lds_fft, s>>>(Zo, ln2, lrow, lnfft, T);
             HIPCHK(hipGetLastError());
             HIPCHK(span(2));
@@ -942,6 +1085,7 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* dt, const doub
             return CRIMP_OK;
         };
         auto finalize = [&](int64_t tb0, int64_t nbt) -> int {
+            g_nu_work[4] += 16.0 * (double)nharm * (double)nbt + 8.0 * (double)nbt;
             k_nu_finalize<<<(unsigned)cdiv(nbt, 256), 256, 0, s>>>(CS, nbt, nharm, stat, (double)n, nf, jbase, nfft, P,
                                                                    pl.invfact, fixup_rel(), tb0, first, out, nflag,
                                                                    flagged);
@@ -966,15 +1110,21 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* dt, const doub
                 const int64_t tb0 = std::max<int64_t>(first, rb * nf) - first;
                 const int64_t nbt = std::min<int64_t>(first + count, (rb + nrow) * nf) - first - tb0;
                 for (int k = 1; k <= nharm; ++k) {
-                    const dim3 grid((unsigned)cdiv(nfft, 256));
-                    if (twod)
-                        k_nu_gather<kNuGatherRows, true><<<grid, 256, 0, s>>>(
-                            dt, cstart + soff[(size_t)(k - 1)], pl.gmin[(size_t)(k - 1)], pl.gmax[(size_t)(k - 1)], nfft,
-                            pl.s1, pl.fch, pl.fcl, c2 + rb, nrow, k, P, cis, W);
-                    else
-                        k_nu_gather<1, false><<<grid, 256, 0, s>>>(
-                            dt, cstart + soff[(size_t)(k - 1)], pl.gmin[(size_t)(k - 1)], pl.gmax[(size_t)(k - 1)], nfft,
-                            pl.s1, pl.fch, pl.fcl, nullptr, nrow, k, P, cis, W);
+                    int alo = 0, acnt = 0;
+                    occupied(k, &alo, &acnt);
+                    const int64_t gbase = (int64_t)alo << ln2, gcount = (int64_t)acnt << ln2;
+                    // lanes per cell: about >= 32 photons per lane, at most 8
+                    const int64_t kspan = pl.gmax[(size_t)(k - 1)] - pl.gmin[(size_t)(k - 1)] + 1;
+                    const int64_t ppc = n / std::max<int64_t>(1, std::min<int64_t>(kspan, nfft));
+                    int L = 1;
+                    while (L < 8 && ppc >= 32 * 2 * L) L *= 2;
+                    if (lanes_env > 0) L = lanes_env;  // test hook: CRIMP_NUFFT_LANES=1|2|4|8
+                    // per photon and row: premultiplier phase + cis ~ 40 flops, then 2 FMA + 1 multiply per moment
+                    g_nu_work[0] += (40.0 + 5.0 * P) * (double)n * nrow;
+                    g_nu_work[1] += 8.0 * (double)n + 16.0 * (double)P * nrow * (double)gcount;
+                    launch_gather(L, twod, gcount, dt, cstart + soff[(size_t)(k - 1)], pl.gmin[(size_t)(k - 1)],
+                                  pl.gmax[(size_t)(k - 1)], nfft, gbase, pl.s1, pl.fch, pl.fcl,
+                                  twod ? c2 + rb : nullptr, nrow, k, P, cis, W, s);
                     HIPCHK(hipGetLastError());
                     HIPCHK(span(0));
                     int rc = fft_combine(k, rb, nrow, tb0, nbt);
@@ -996,6 +1146,12 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* dt, const doub
                 const NuPass& ps = hps[ipass];
                 const NuPass* dp = dps + ipass++;
                 dim3 grid((unsigned)cdiv(nchunk, kNuWaves));
+                // issued: one 16x16x4 f64 MFMA (2048 flops) per 4 photons and harmonic; slots written
+                g_nu_work[0] += 512.0 * (double)n * gl;
+                g_nu_work[1] += 8.0 * (double)n;
+                for (int kk = 0; kk < gl; ++kk)
+                    g_nu_work[1] += 8.0 * (double)SL *
+                                    (double)(pl.gmax[(size_t)(k0 + kk - 1)] - ps.gmin[kk] + 1 + nchunk);
                 if (twod)
                     nu_launch_spread<true>(gl, grid, s, dt, n, nchunk, pl.s1, pl.fch, pl.fcl, c2 + rb, nrow, k0, P, dp, cis,
                                            U, ctab);
@@ -1006,9 +1162,14 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* dt, const doub
                 HIPCHK(span(0));
                 for (int kk = 0; kk < gl && k0 + kk <= nharm; ++kk) {
                     const int k = k0 + kk;
-                    k_nu_merge<<<(unsigned)cdiv(nfft, kNuMergeG), 256, (size_t)kNuMergeG * SL * sizeof(double), s>>>(
+                    int alo = 0, acnt = 0;
+                    occupied(k, &alo, &acnt);
+                    const int64_t gbase = (int64_t)alo << ln2, gcount = (int64_t)acnt << ln2;
+                    g_nu_work[2] += 8.0 * (double)SL * (double)(pl.gmax[(size_t)(k - 1)] - ps.gmin[kk] + 1 + nchunk) +
+                                    16.0 * (double)P * nrow * (double)gcount;
+                    k_nu_merge<<<(unsigned)cdiv(gcount, kNuMergeG), 256, (size_t)kNuMergeG * SL * sizeof(double), s>>>(
                         U + ps.ubase[kk], SL, ctab + 2 * kk * nchunk, nchunk, ps.gmin[kk], pl.gmax[(size_t)(k - 1)],
-                        nfft, W);
+                        nfft, gbase, gcount, W);
                     HIPCHK(hipGetLastError());
                     HIPCHK(span(1));
                     int rc = fft_combine(k, rb, nrow, tb0, nbt);

@@ -8,7 +8,9 @@ ranks, one collective per search.
                        ``all_gather`` of each rank's best (power, index) (``gather='best'``);
                        ties resolve to the lowest flat index, as ``np.argmax`` does;
 * ``sharded_toa_fit``  each rank fits a contiguous block of intervals, loading only their photons
-                       (``interval_shard``); one ``all_gather`` of the per-interval result records.
+                       (``interval_shard``: blocks cut at quantiles of the intervals' photon counts, a fit's cost
+                       being photon-proportional, plus a fixed per-interval share); one ``all_gather`` of the
+                       per-interval result records.
 The search's photon arrays are replicated (every rank holds all photons; 8 B/photon). The collectives go
 through ``torch.distributed`` (backend ``nccl`` = RCCL over xGMI on the GPU box; ``gloo`` in the
 CPU tests). ``compute`` hooks let the CPU tests drive the same collective logic without a GPU.
@@ -111,11 +113,37 @@ def sharded_search(time, freq, nharm=2, stat=0, freq_dot=None, gather="all", com
     return out.cpu().numpy()
 
 
-def interval_shard(offsets, world, rank):
-    """(first interval, interval count, first photon, photon end) of ``rank``'s contiguous block of intervals:
-    the photon range [a, b) is all that rank has to load."""
+# A fit's cost per interval in photon units beyond its photons: the workgroup's fixed passes and reductions (config 5:
+# ~1e5 photons per interval, so balance is by photons; a block of tiny intervals still costs per interval)
+INTERVAL_OVERHEAD_PHOTONS = 4096
+
+
+def interval_blocks(offsets, world, overhead=INTERVAL_OVERHEAD_PHOTONS):
+    """Block boundaries b_0 = 0 <= b_1 <= ... <= b_world = nint: rank r fits intervals [b_r, b_{r+1}). Each boundary
+    is the interval edge nearest to r/world of the total cost (photons + ``overhead`` per interval), so ranks hold
+    equal photon loads however ragged the intervals are (within one interval of the even share); N x k equal intervals
+    give every rank k."""
     off = np.asarray(offsets, dtype=np.int64)
-    first, count = shard_range(off.size - 1, world, rank)
+    nint = off.size - 1
+    cum = np.concatenate([[0.0], np.cumsum(np.diff(off).astype(np.float64) + float(overhead))])
+    b = [0]
+    for r in range(1, world):
+        target = cum[-1] * r / world
+        i = int(np.searchsorted(cum, target, side="left"))
+        i = min(max(i, 1), nint)
+        if abs(cum[i - 1] - target) <= abs(cum[i] - target):
+            i -= 1
+        b.append(max(b[-1], i))
+    b.append(nint)
+    return b
+
+
+def interval_shard(offsets, world, rank):
+    """(first interval, interval count, first photon, photon end) of ``rank``'s contiguous block of intervals
+    (``interval_blocks``): the photon range [a, b) is all that rank has to load."""
+    off = np.asarray(offsets, dtype=np.int64)
+    b = interval_blocks(off, world)
+    first, count = b[rank], b[rank + 1] - b[rank]
     return first, count, int(off[first]), int(off[first + count])
 
 
@@ -133,7 +161,9 @@ def sharded_toa_fit(x, offsets, exposure, tmpl, brutemin=False, ph_shift_res=100
     nint = off.size - 1
     first, count, pa, pb = interval_shard(off, world, rank)
     keys = ("phShi", "phShi_LL", "phShi_UL", "reducedChi2", "norm", "LLmax")
-    rec = np.full((shard_range(nint, world, 0)[1], len(keys)), np.nan)
+    blocks = interval_blocks(off, world)
+    width = max(1, max(blocks[r + 1] - blocks[r] for r in range(world)))
+    rec = np.full((width, len(keys)), np.nan)
     if count:
         sl = off[first:first + count + 1]
         if callable(x):
@@ -154,5 +184,5 @@ def sharded_toa_fit(x, offsets, exposure, tmpl, brutemin=False, ph_shift_res=100
         allr = torch.empty(world * rec.size, dtype=torch.float64, device=dev)
         dist.all_gather_into_tensor(allr, t)
         allr = allr.cpu().numpy().reshape((world,) + rec.shape)
-        out = np.concatenate([allr[r, :shard_range(nint, world, r)[1]] for r in range(world)])
+        out = np.concatenate([allr[r, :blocks[r + 1] - blocks[r]] for r in range(world)])
     return {k: out[:, i] for i, k in enumerate(keys)}

@@ -110,6 +110,10 @@ int crimp_last_search_path(void);
 /* The plan of the last NUFFT search: its (largest) FFT length n, moments P, and spread form (1 = cell gather, one lane
  * per wrapped cell on the VALU; 0 = MFMA slots). Measurement hook for bench.py, not in the reference. */
 int crimp_last_nufft_plan(int64_t* fft_length, int32_t* moments, int32_t* gather);
+/* The last NUFFT search's algorithmic work per kernel class, up to cap of: spread fp64 flops, spread HBM bytes, merge
+ * bytes, FFT bytes (pass 2 with the fused Horner combine), combine + finalize bytes; returns 5. For bench.py's
+ * rooflines, not in the reference. */
+int crimp_last_nufft_work(double* work, int32_t cap);
 /* Brute-grid norms evaluated per phShift by the last crimp_toa_fit with CRIMP_TOA_BRUTE (the pruned candidates of
  * lmfit's 20-norm lattice, padded to 2, 4 or 20, less the lazy norms the eight-factor grid leaves out; 0 without a
  * brute grid). Measurement hook for bench.py's

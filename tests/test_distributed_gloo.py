@@ -69,10 +69,45 @@ def _worker(rank, world, port, out_path):
     _, _, pa, pb = interval_shard(off, world, rank)
     assert asked == [(pa, pb)] and pb - pa < x.size
     assert np.array_equal(toa2["phShi"], toa["phShi"])
+    # ragged intervals (rows 35-41 of the worked example are 5,136-10,000 photons): blocks balanced by photons
+    xr, offr, Er = _ragged_intervals()
+    toar = sharded_toa_fit(xr, offr, Er, tmpl, brutemin=True, fitter=_OracleFitter)
     if rank == 0:
-        np.savez(out_path, full=full, best=np.array(best), phShi=toa["phShi"], LL=toa["phShi_LL"])
+        np.savez(out_path, full=full, best=np.array(best), phShi=toa["phShi"], LL=toa["phShi_LL"],
+                 rphShi=toar["phShi"], rLL=toar["phShi_LL"], rUL=toar["phShi_UL"])
     dist.barrier()
     dist.destroy_process_group()
+
+
+def _ragged_intervals():
+    """Seven intervals of 300..4000 photons (ragged as the worked example's rows 35-41) drawn from one template."""
+    from crimp_amd.synth import template_intervals
+    sizes = [4000, 300, 2500, 900, 3500, 600, 1800]
+    xs, Es = [], []
+    for i, n in enumerate(sizes):
+        x, _, E, _ = template_intervals(1, n, 10.0, [2.0, 1.0], [0.3, -1.0], seed=20 + i)
+        xs.append(np.asarray(x))
+        Es.append(float(np.asarray(E)[0]))
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    return np.concatenate(xs), off, np.array(Es)
+
+
+def test_interval_blocks_balance_photons():
+    from crimp_amd.sharding import interval_blocks, interval_shard, shard_range
+    rng = np.random.default_rng(0)
+    for world in (1, 2, 3, 8):
+        for sizes in (np.full(16, 1000), rng.integers(1000, 100000, 37), np.r_[np.full(20, 100), [10 ** 6]]):
+            off = np.concatenate([[0], np.cumsum(sizes)])
+            b = interval_blocks(off, world)
+            assert b[0] == 0 and b[-1] == sizes.size and all(b[r] <= b[r + 1] for r in range(world))
+            cost = np.array([np.sum(sizes[b[r]:b[r + 1]] + 4096.0) for r in range(world)])
+            biggest = np.max(sizes + 4096.0)
+            assert cost.max() - cost.sum() / world <= biggest  # within one interval of the even share
+            for r in range(world):
+                first, count, pa, pb = interval_shard(off, world, r)
+                assert (first, count) == (b[r], b[r + 1] - b[r]) and (pa, pb) == (off[b[r]], off[b[r + 1]])
+    off = np.arange(0, 8 * 1250 + 1) * 100  # config 5 on 8 ranks: 1250 equal intervals each, as before
+    assert [interval_shard(off, 8, r)[:2] for r in range(8)] == [shard_range(8 * 1250, 8, r) for r in range(8)]
 
 
 def test_two_rank_sharded_search_and_toas(tmp_path):
@@ -94,6 +129,10 @@ def test_two_rank_sharded_search_and_toas(tmp_path):
     for i in range(5):
         o = O.fit_toa(x[off[i]:off[i + 1]], E[i], tmpl, brutemin=True)
         assert r["phShi"][i] == o["phShi"] and r["LL"][i] == o["phShi_LL"]
+    xr, offr, Er = _ragged_intervals()
+    for i in range(offr.size - 1):
+        o = O.fit_toa(xr[offr[i]:offr[i + 1]], Er[i], tmpl, brutemin=True)
+        assert r["rphShi"][i] == o["phShi"] and r["rLL"][i] == o["phShi_LL"] and r["rUL"][i] == o["phShi_UL"]
 
 
 def test_shard_range_partitions():

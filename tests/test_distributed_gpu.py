@@ -23,6 +23,23 @@ def _free_port():
     return p
 
 
+def _ragged(tm, dev):
+    """Intervals of 3,000..25,000 photons from the worked example's template (rows 35-41 range 5,136-10,000)."""
+    import torch
+    from crimp_amd.synth import template_intervals_torch
+    K = sum(1 for k in tm if k.startswith("amp_"))
+    amps = [tm["amp_%d" % j]["value"] for j in range(1, K + 1)]
+    phs = [tm["ph_%d" % j]["value"] for j in range(1, K + 1)]
+    sizes = [25_000, 3_000, 12_000, 6_000, 18_000, 4_000, 9_000]
+    xs, Es = [], []
+    for i, n in enumerate(sizes):
+        x, _, E, _ = template_intervals_torch(1, n, tm["norm"]["value"], amps, phs, seed=30 + i, device=dev)
+        xs.append(x)
+        Es.append(float(np.asarray(E)[0]))
+    off = torch.as_tensor(np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64), device=dev)
+    return torch.cat(xs), off, np.array(Es)
+
+
 def _worker(rank, world, port, out_path):
     import sys
     sys.path.insert(0, ROOT)
@@ -55,11 +72,15 @@ def _worker(rank, world, port, out_path):
                                             seed=3, device=dev)
     toa = sharded_toa_fit(x, off, E, tm, brutemin=True)
     rtoa = ToAFitter(x, off, E, tm).fit(brutemin=True)
+    xr, offr, Er = _ragged(tm, dev)   # ragged intervals: photon-balanced blocks
+    tr = sharded_toa_fit(xr, offr, Er, tm, brutemin=True)
+    rtr = ToAFitter(xr, offr, Er, tm).fit(brutemin=True)
     if rank == 0:
         keys = sorted(toa)
         np.savez(out_path, full=full.cpu().numpy(), full_is_dev=np.array(full.is_cuda), ref=ref.cpu().numpy(),
                  best=np.array(best, dtype=np.float64), refh=refh, keys=np.array(keys),
-                 toa=np.stack([toa[k] for k in keys]), rtoa=np.stack([rtoa[k] for k in keys]))
+                 toa=np.stack([toa[k] for k in keys]), rtoa=np.stack([rtoa[k] for k in keys]),
+                 tr=np.stack([tr[k] for k in keys]), rtr=np.stack([rtr[k] for k in keys]))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -72,6 +93,7 @@ def test_two_gloo_ranks_on_gpu_bit_identical_to_unsharded(tmp_path):
     np.testing.assert_array_equal(r["full"], r["ref"])
     assert r["best"][0] == r["refh"].max() and int(r["best"][1]) == int(np.argmax(r["refh"]))
     np.testing.assert_array_equal(r["toa"], r["rtoa"])
+    np.testing.assert_array_equal(r["tr"], r["rtr"])
 
 
 def _nccl_worker(rank, world, port, out_path):

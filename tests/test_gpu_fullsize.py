@@ -267,6 +267,50 @@ def test_config5_toas_vs_oracle(gpu):
     for i in sample:
         _fit_vs_oracle(r, i, xh[oh[i]:oh[i + 1]], E[i], tm)
     assert margins[ties[0]] < 1e-5       # the sample did include a near-tie of the lattice
+    _every_interval_vs_oracle_profile(r, xh, oh, E, tm)
+
+
+def _every_interval_vs_oracle_profile(r, xh, oh, E, tm, ph_shift_res=1000):
+    """Every interval of a device fit against the oracle's fp64 extended likelihood (templatemodels.py:98-121), a
+    few likelihood passes each instead of a whole oracle fit (measureToAs.py:320-376):
+    * optimum: at the device's (norm, phShift) the profile's Newton step -g_phi / (H_pp - H_pn^2 / H_nn) is below
+      1e-6 cycles and the norm's -g_n / H_nn below 1e-9 of the norm (the device optimum is the oracle's);
+    * 1-sigma scan: with k* = kk - 1 the scan step the reported bound kk * step + step / 2 implies on each side, the
+      norm-profiled LL at phShift -+ (k* - 1) step lies within 0.5 chi2_1(0.6827) = 0.500021713558733 of LLmax and
+      at -+ k* step beyond it -- the crossing is exactly where the device reported it (lmfit's clip to the phShift
+      bounds at +-pi as the oracle's fit_toa; the phShiftRes / 2 cap excepted)."""
+    import math
+    thr = 0.500021713558733
+    tarr = O.template_arrays(tm)
+    n0 = float(tm["norm"]["value"])
+    lo, hi = n0 / 100.0, 500.0
+    step = 2 * math.pi / ph_shift_res
+    worst_phi = worst_n = 0.0
+    for i in range(len(E)):
+        x = xh[oh[i]:oh[i + 1]]
+        phi, n = float(r["phShi"][i]), float(r["norm"][i])
+        o = O.toa_eval(x, E[i], tarr, n, phi)
+        heff = o[5] - o[4] * o[4] / o[3]
+        worst_phi = max(worst_phi, abs(o[2] / heff) / (2 * math.pi))
+        if lo < n < hi:
+            worst_n = max(worst_n, abs(o[1] / o[3]) / n)
+        llmax = O._profile_norm(x, E[i], tarr, phi, lo, hi, n)[1][0]
+        for side, bound in ((-1, r["phShi_LL"][i]), (1, r["phShi_UL"][i])):
+            kk = int(round((bound - step / 2) / step))
+            kstar = kk - 1
+            if kstar + 1 > ph_shift_res / 2:
+                continue                                       # capped scan
+            if abs(phi) + (kstar + 1) * step >= math.pi:
+                continue      # the scan reached +-pi: lmfit's clip-to-bound steps (tests/test_gpu_scan_edges.py)
+            for k, inside in ((kstar - 1, True), (kstar, False)):
+                if k < 1:
+                    continue
+                p = min(max(phi + side * k * step, -math.pi), math.pi)
+                _, ok = O._profile_norm(x, E[i], tarr, p, lo, hi, n)
+                diff = llmax - ok[0]
+                assert (diff <= thr) if inside else (diff > thr), (i, side, k, kstar, diff)
+    assert worst_phi <= 1e-6, worst_phi
+    assert worst_n <= 1e-9, worst_n
 
 
 def _sample_template(tm, n, shift, rng):
@@ -353,25 +397,30 @@ def test_exact_many_harmonics_and_ragged_partitions(gpu):
     np.testing.assert_array_equal(np.concatenate(parts), whole)
 
 
-def test_exact_path_photon_limit_routes_to_fp64(gpu):
-    """The exact kernel's int64 totals hold N < 2^27 photons; at N = 2^27 the search routes to the fp64 kernel
-    (bit-identical to precision='f64'), just below it takes the exact path (within 1e-6 of the fp64 path)."""
+def test_exact_path_above_2_27_photons(gpu):
+    """The exact kernel's int64 totals hold < 2^27 photons; 1.5e8 photons (a config-4-style search, which
+    periodsearch.py:57-71 puts no limit on) run in two photon chunks, each into its own totals, summed exactly by the
+    finalize: the exact path (not the fp64 kernel) runs, with few fix-ups, within 1e-6 of the fp64 path on every
+    trial; the NUFFT agrees too. Just below 2^27 a single chunk runs and matches the same way."""
     import torch
-    from crimp_amd import ops
+    from crimp_amd import ops, _native as N
     g = torch.Generator(device=gpu)
     g.manual_seed(5)
-    n = 1 << 27
-    t = 5.0e9 + torch.rand(n, generator=g, dtype=torch.float64, device=gpu) * 1.0e6
+    n = 150_000_000
+    t = torch.sort(5.0e9 + torch.rand(n, generator=g, dtype=torch.float64, device=gpu) * 1.0e6).values
     f = torch.as_tensor(1.7 + (np.arange(256) - 128) / 1.0e7, device=gpu)
-    t0 = 5.0e9 + 5.0e5
-    z_at = ops.search(t, t0, f, 2, 0).cpu().numpy()
-    z_at64 = ops.search(t, t0, f, 2, 0, precision="f64").cpu().numpy()
-    np.testing.assert_array_equal(z_at, z_at64)
-    tb = t[: n - 1]
-    z_below = ops.search(tb, t0, f, 2, 0).cpu().numpy()
-    z_below64 = ops.search(tb, t0, f, 2, 0, precision="f64").cpu().numpy()
-    assert _rel_err(z_below, z_below64).max() <= 1e-6
-    assert not np.array_equal(z_below, z_below64)       # a different (exact) kernel ran
+    t0 = float((t[0] + t[-1]).item()) / 2
+    for nn in (n, (1 << 27) - 1):
+        tt = t[:nn]
+        z = ops.search(tt, t0, f, 2, 0).cpu().numpy()
+        assert N.load().crimp_last_search_path() == 1
+        assert N.load().crimp_last_fixups() <= 8
+        z64 = ops.search(tt, t0, f, 2, 0, precision="f64").cpu().numpy()
+        assert _rel_err(z, z64).max() <= 1e-6
+        assert not np.array_equal(z, z64)       # a different (exact) kernel ran
+        zn = ops.search(tt, t0, f, 2, 0, precision="nufft").cpu().numpy()
+        assert N.load().crimp_last_search_path() == 2
+        assert _rel_err(zn, z64).max() <= 1e-6
 
 
 def test_exact_long_splits_fold_path_bit_identical(gpu):

@@ -155,3 +155,47 @@ def test_nufft_unsorted_photons_take_default_path(gpu):
     z = PeriodSearch(tp, f, 2, precision="nufft").ztest()
     assert _path() == 1
     close_rel(z, O.search(tp, f, 2))
+
+
+def test_nufft_fused_pass2_equals_separate_combine(gpu, monkeypatch):
+    """FFT pass 2 fused with the moments' Horner sum (default) against pass 2 and k_nu_combine as two kernels
+    (CRIMP_NUFFT_FUSED=0): the same arithmetic, so bit-identical powers -- single-pass (n <= 4096) and four-step
+    FFTs, 1-D and 2-D grids, both spread forms."""
+    from crimp_amd import ops, _native as N
+    from crimp_amd.synth import pulsed_events
+    t = pulsed_events(200000, 2.0e5, 3.3, pulsed_frac=0.05, fdot=-2e-11, seed=8)
+    t0 = (t[0] + t[-1]) / 2
+    fd = np.array([-12.0, -11.0, -10.5])
+    for f, m, fdv in ((3.3 + np.arange(-700, 701) / 2.0e6, 2, None), (3.3 + np.arange(-40000, 40000) / 2.0e6, 3, None),
+                      (3.3 + np.arange(-1500, 1500) / 2.0e6, 5, fd)):
+        a = ops.search(t, t0, f, m, 1, log10_negfdot=fdv, precision="nufft", flags=N.FLAG_NO_FIXUP)
+        monkeypatch.setenv("CRIMP_NUFFT_FUSED", "0")
+        b = ops.search(t, t0, f, m, 1, log10_negfdot=fdv, precision="nufft", flags=N.FLAG_NO_FIXUP)
+        monkeypatch.delenv("CRIMP_NUFFT_FUSED")
+        np.testing.assert_array_equal(a, b)
+
+
+def test_nufft_gather_lane_splits(gpu, monkeypatch):
+    """The cell gather with 1, 2, 4 and 8 lanes per cell (CRIMP_NUFFT_LANES; the default picks from photons per
+    cell): each against the fp64 kernel at the per-trial contract with fix-up off, and against each other to
+    summation-order rounding -- a dense 1-D grid (many photons per cell) and a 2-row 2-D grid."""
+    from crimp_amd import ops, _native as N
+    from crimp_amd.synth import pulsed_events
+    monkeypatch.setenv("CRIMP_NUFFT_SPREAD", "gather")
+    t = pulsed_events(400000, 2.0e5, 3.3, pulsed_frac=0.05, fdot=-2e-11, seed=11)
+    t0 = (t[0] + t[-1]) / 2
+    f = 3.3 + np.arange(-600, 600) / 2.0e6
+    fd = np.array([-12.0, -10.5])
+    for m, fdv in ((3, None), (2, fd)):
+        ref = ops.search(t, t0, f, m, 1, log10_negfdot=fdv, precision="f64")
+        got = []
+        for lanes in ("1", "2", "4", "8"):
+            monkeypatch.setenv("CRIMP_NUFFT_LANES", lanes)
+            got.append(ops.search(t, t0, f, m, 1, log10_negfdot=fdv, precision="nufft", flags=N.FLAG_NO_FIXUP))
+            assert _path() == 2
+            close_rel(got[-1], ref, 1e-6)
+        for g in got[1:]:
+            assert np.median(np.abs(g - got[0]) / np.abs(got[0])) <= 1e-12
+    monkeypatch.setenv("CRIMP_NUFFT_LANES", "3")
+    with pytest.raises(Exception):
+        ops.search(t, t0, f, 2, 1, precision="nufft")

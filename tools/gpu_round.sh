@@ -38,6 +38,15 @@ if [[ $STEPS == *prof* ]]; then
   stop_on_fault $? rocprof
   find "$OUT/prof" -name "*stats*" | head
 fi
+if [[ $STEPS == *nufft* ]]; then  # config-3 NUFFT search: timing, then a rocprofv3 kernel-trace profile
+  CRIMP_PRECISION=nufft REPS=${NUFFT_REPS:-5} timeout -k 10 300 python -u tools/run_search.py > "$OUT/nufft_run.log" 2>&1
+  stop_on_fault $? nufft_run
+  cat "$OUT/nufft_run.log"
+  CRIMP_PRECISION=nufft REPS=${NUFFT_REPS:-5} timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_nufft" \
+      -o run --output-format csv -- python -u tools/run_search.py > "$OUT/prof_nufft.log" 2>&1
+  stop_on_fault $? prof_nufft
+  find "$OUT/prof_nufft" -name "*stats*" | head
+fi
 if [[ $STEPS == *h20* ]]; then  # H-test (m = 20) timing
   NHARM=20 NPH=2000000 NTR=1000000 timeout -k 10 200 python3 tools/run_search.py >> "$OUT/h20.log" 2>&1
   stop_on_fault $? h20
