@@ -270,10 +270,13 @@ __global__ __launch_bounds__(256) void k_nu_gather(const double* __restrict__ dt
                                                    int64_t gcount, double s1, double fch, double fcl,
                                                    const double* __restrict__ c2row, int nrow, int k, int P,
                                                    const double2* __restrict__ tab, double2* __restrict__ W) {
+    __shared__ double2 stab[1024];  // the cis table (nu_cis), read per photon: LDS, not L2 latency
+    for (int e = threadIdx.x; e < 1024; e += 256) stab[e] = tab[e];
+    __syncthreads();
     const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x;
     const int64_t idx = tid / L;
     const int sub = (int)(tid % L);
-    if (idx >= gcount) return;  // whole L-groups leave together (L divides 64)
+    if (idx >= gcount) return;  // whole L-groups leave together (L divides 64); no barrier below
     const int64_t g = (gbase + idx) & (nfft - 1);  // the FFT's occupied rows only (nu_occupied)
     double ar[R][kNuGatherMaxP], ai[R][kNuGatherMaxP];
 #pragma unroll
@@ -287,8 +290,10 @@ __global__ __launch_bounds__(256) void k_nu_gather(const double* __restrict__ dt
     for (int64_t G = gmin + (((g - gmin) % nfft) + nfft) % nfft; G <= gmax; G += nfft) {
         const int64_t i0 = start[G - gmin], i1 = start[G - gmin + 1];
         const double Gd = (double)G;
+        double dn = i0 + sub < i1 ? dt[i0 + sub] : 0.0;  // one photon ahead
         for (int64_t i = i0 + sub; i < i1; i += L) {
-            const double d = dt[i];
+            const double d = dn;
+            if (i + L < i1) dn = dt[i + L];
             const double e = kd * (d * s1) - Gd;
             const double p1 = nu_frac_prod(fch, fcl, d);
             double d2 = 0.0, d2e = 0.0;
@@ -302,7 +307,7 @@ __global__ __launch_bounds__(256) void k_nu_gather(const double* __restrict__ dt
                     double phi = p1;
                     if (TWOD) phi += nu_frac_c2(c2[r], d2, d2e);
                     phi -= rint(phi);
-                    const double2 c = nu_cis(tab, nu_frac_k(kd, phi));
+                    const double2 c = nu_cis(stab, nu_frac_k(kd, phi));
                     double ep = 1.0;
 #pragma unroll
                     for (int p = 0; p < kNuGatherMaxP; ++p) {
@@ -446,12 +451,54 @@ __device__ __forceinline__ void nu_dft(double2* v) {
     else nu_dft16(v);
 }
 
+// Twiddles of the in-LDS transforms (length <= 2^lt, lt = min(log2 n, 12)): w^m = e^{2 pi i m / 2^lt} as
+// hi[m >> 6] * lo[m & 63], two 64-entry tables in LDS filled by fp64 sincospi at the kernel's start.
+struct NuTile {
+    double2 hi[64], lo[64];
+};
+__device__ __forceinline__ void nu_tile_init(NuTile* tw, int lt) {
+    const int t = threadIdx.x;
+    if (t < 128) {
+        const int m = t < 64 ? t : (t - 64) << 6;
+        double sv, cv;
+        sincospi(ldexp((double)m, 1 - lt), &sv, &cv);  // 2 m / 2^lt
+        if (t < 64)
+            tw->lo[t] = make_double2(cv, sv);
+        else
+            tw->hi[t - 64] = make_double2(cv, sv);
+    }
+}
+__device__ __forceinline__ double2 nu_tw_tile(const NuTile* tw, int m) { return nu_cmul(tw->hi[m >> 6], tw->lo[m & 63]); }
+
+// v[r] *= w^r for r = 1 .. R-1: w^r as the product of w, w^2, w^4, w^8 over the bits of r (few live registers,
+// product depth <= 3 after the squarings, instead of a chain of R - 2 products)
+template <int R>
+__device__ __forceinline__ void nu_twiddle(double2 w, double2* v) {
+    double2 b[4];
+    b[0] = w;
+#pragma unroll
+    for (int i = 1; i < 4; ++i)
+        if ((1 << i) < R) b[i] = nu_cmul(b[i - 1], b[i - 1]);
+#pragma unroll
+    for (int r = 1; r < R; ++r) {
+        double2 wr = make_double2(1.0, 0.0);
+        bool first = true;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (r & (1 << i)) {
+                wr = first ? b[i] : nu_cmul(wr, b[i]);
+                first = false;
+            }
+        v[r] = nu_cmul(v[r], wr);
+    }
+}
+
 // One Stockham autosort stage of radix R over 2^lc transforms of length 2^ll held in LDS at s[a*sa + cc*sc]:
 // butterfly (j, cc) reads x[j + r L/R], twiddles by w_{Ns R}^{(j mod Ns) r}, and writes
 // y[(j / Ns) Ns R + (j mod Ns) + r Ns]. 16 / R butterflies per thread (a tile holds <= 16 elements per thread).
 template <int R>
-__device__ __forceinline__ void nu_stage(double2* s, int ll, int lc, int sa, int sc, int lns, const NuTw& T,
-                                         int lnfft) {
+__device__ __forceinline__ void nu_stage(double2* s, int ll, int lc, int sa, int sc, int lns, const NuTile* tw,
+                                         int lt) {
     constexpr int NB = 16 / R;
     constexpr int LR = R == 2 ? 1 : R == 4 ? 2 : R == 8 ? 3 : 4;
     const int L = 1 << ll, Ns = 1 << lns;
@@ -465,14 +512,8 @@ __device__ __forceinline__ void nu_stage(double2* s, int ll, int lc, int sa, int
 #pragma unroll
             for (int r = 0; r < R; ++r) v[k][r] = s[(j + (r << (ll - LR))) * sa + cc * sc];
             if (lns > 0) {
-                // w_{Ns R}^{(j mod Ns)} = w_n^{(j mod Ns) n / (Ns R)}
-                const double2 w = nu_tw(T, (int64_t)(j & (Ns - 1)) << (lnfft - lns - LR));
-                double2 wr = w;
-#pragma unroll
-                for (int r = 1; r < R; ++r) {
-                    v[k][r] = nu_cmul(v[k][r], wr);
-                    if (r + 1 < R) wr = nu_cmul(wr, w);
-                }
+                // w_{Ns R}^{(j mod Ns)} = w_{2^lt}^{(j mod Ns) 2^lt / (Ns R)}
+                nu_twiddle<R>(nu_tw_tile(tw, (j & (Ns - 1)) << (lt - lns - LR)), v[k]);
             }
             nu_dft<R>(v[k]);
         }
@@ -492,21 +533,21 @@ __device__ __forceinline__ void nu_stage(double2* s, int ll, int lc, int sa, int
 }
 
 // 2^lc transforms of length 2^ll in LDS (Stockham: natural order in, natural order out)
-__device__ void nu_fft_lds(double2* s, int ll, int lc, int sa, int sc, const NuTw& T, int lnfft) {
+__device__ __forceinline__ void nu_fft_lds(double2* s, int ll, int lc, int sa, int sc, const NuTile* tw, int lt) {
     int lns = 0;
     while (lns < ll) {
         const int rem = ll - lns;
         if (rem >= 4) {
-            nu_stage<16>(s, ll, lc, sa, sc, lns, T, lnfft);
+            nu_stage<16>(s, ll, lc, sa, sc, lns, tw, lt);
             lns += 4;
         } else if (rem == 3) {
-            nu_stage<8>(s, ll, lc, sa, sc, lns, T, lnfft);
+            nu_stage<8>(s, ll, lc, sa, sc, lns, tw, lt);
             lns += 3;
         } else if (rem == 2) {
-            nu_stage<4>(s, ll, lc, sa, sc, lns, T, lnfft);
+            nu_stage<4>(s, ll, lc, sa, sc, lns, tw, lt);
             lns += 2;
         } else {
-            nu_stage<2>(s, ll, lc, sa, sc, lns, T, lnfft);
+            nu_stage<2>(s, ll, lc, sa, sc, lns, tw, lt);
             lns += 1;
         }
     }
@@ -514,11 +555,14 @@ __device__ void nu_fft_lds(double2* s, int ll, int lc, int sa, int sc, const NuT
 
 // pass 1 of the four-step FFT: view each batch as [n1][n2]; DFT along a of 2^lc consecutive columns b, times
 // w_n^{b k1}, stored at y[k1 n2 + b]
-__global__ __launch_bounds__(256) void k_nu_fft_cols(const double2* __restrict__ X, double2* __restrict__ Y,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_nu_fft_cols(const double2* __restrict__ X, double2* __restrict__ Y,
                                                      int lnfft, int ln1, int lc, NuTw T, int alo, int acnt) {
     extern __shared__ double2 nu_s[];
-    const int64_t nfft = int64_t(1) << lnfft;
+    __shared__ NuTile tw;
+    const int lt = lnfft < 12 ? lnfft : 12;
+    nu_tile_init(&tw, lt);
     const int ln2 = lnfft - ln1, c = 1 << lc, n1 = 1 << ln1;
+    const int64_t nfft = int64_t(1) << lnfft;
     const int64_t b0 = (int64_t)blockIdx.x << lc;
     const double2* x = X + (int64_t)blockIdx.y * nfft;
     double2* y = Y + (int64_t)blockIdx.y * nfft;
@@ -527,22 +571,30 @@ __global__ __launch_bounds__(256) void k_nu_fft_cols(const double2* __restrict__
         nu_s[e] = ((a - alo) & (n1 - 1)) < acnt ? x[((int64_t)a << ln2) + b0 + cc] : make_double2(0.0, 0.0);
     }
     __syncthreads();
-    nu_fft_lds(nu_s, ln1, lc, c, 1, T, lnfft);
-    for (int e = threadIdx.x; e < (n1 << lc); e += 256) {
-        const int k1 = e >> lc, cc = e & (c - 1);
-        const int64_t b = b0 + cc;
-        y[((int64_t)k1 << ln2) + b] = nu_cmul(nu_s[e], nu_tw(T, b * k1));
+    nu_fft_lds(nu_s, ln1, lc, c, 1, &tw, lt);
+    // times the inter-pass twiddles w_n^{b k1} (n1 c = 4096: 16 outputs per thread)
+#pragma unroll
+    for (int q = 0; q < kNuTile / 256; ++q) {
+        const int e = threadIdx.x + 256 * q;
+        if (e < (n1 << lc)) {
+            const int k1 = e >> lc, cc = e & (c - 1);
+            const int64_t b = b0 + cc;
+            y[((int64_t)k1 << ln2) + b] = nu_cmul(nu_s[e], nu_tw(T, b * k1));
+        }
     }
 }
 
 // pass 2 (or the only pass): DFT of 2^lr contiguous rows of length 2^ll each, in place
-__global__ __launch_bounds__(256) void k_nu_fft_rows(double2* __restrict__ X, int ll, int lr, int lnfft, NuTw T) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_nu_fft_rows(double2* __restrict__ X, int ll, int lr, int lnfft) {
     extern __shared__ double2 nu_s[];
+    __shared__ NuTile tw;
+    const int lt = lnfft < 12 ? lnfft : 12;
+    nu_tile_init(&tw, lt);
     const int L = 1 << ll;
     double2* x = X + ((int64_t)blockIdx.x << (ll + lr));
     for (int e = threadIdx.x; e < (L << lr); e += 256) nu_s[e] = x[e];
     __syncthreads();
-    nu_fft_lds(nu_s, ll, lr, 1, L, T, lnfft);
+    nu_fft_lds(nu_s, ll, lr, 1, L, &tw, lt);
     for (int e = threadIdx.x; e < (L << lr); e += 256) x[e] = nu_s[e];
 }
 
@@ -551,22 +603,40 @@ __global__ __launch_bounds__(256) void k_nu_fft_rows(double2* __restrict__ X, in
 // registers (z = 2 pi i jc / n), so the moments' transforms are read once and never written back; the trials' (C_k,
 // S_k) go to CS as k_nu_combine writes them. X[beta][pos], beta = p * nrow + r, pos = k1 n2 + k2 holds J = k1 + n1 k2.
 constexpr int kNuFusedPer = kNuTile / 256;  // positions per thread
-__global__ __launch_bounds__(256) void k_nu_fft_rows_combine(const double2* __restrict__ X, int ll, int lnfft, NuTw T,
-                                                             int P, int nrow, int64_t nf, int64_t jhi, int64_t h,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k_nu_fft_rows_combine(const double2* __restrict__ X, int ll, int lnfft, int P,
+                                                             int nrow, int64_t nf, int64_t jhi, int64_t h,
                                                              int64_t tbase, int64_t nbt, double2* __restrict__ CS) {
     extern __shared__ double2 nu_s[];
+    __shared__ NuTile tw;
+    const int lt = lnfft < 12 ? lnfft : 12;
+    nu_tile_init(&tw, lt);
     const int64_t nfft = int64_t(1) << lnfft;
     const int L = 1 << ll, ln1 = lnfft - ll;
     const int64_t k1 = blockIdx.x;
     const int r = blockIdx.y;
-    double2 acc[kNuFusedPer];
+    double2 acc[kNuFusedPer], nx[kNuFusedPer];
+    const double2* xr = X + (int64_t)r * nfft + (k1 << ll);  // moment p's row at xr + p nrow nfft
+    const int64_t pstride = (int64_t)nrow * nfft;
 #pragma unroll
-    for (int q = 0; q < kNuFusedPer; ++q) acc[q] = make_double2(0.0, 0.0);
+    for (int q = 0; q < kNuFusedPer; ++q) {
+        acc[q] = make_double2(0.0, 0.0);
+        const int e = threadIdx.x + 256 * q;
+        nx[q] = e < L ? xr[(int64_t)(P - 1) * pstride + e] : make_double2(0.0, 0.0);
+    }
     for (int p = P - 1; p >= 0; --p) {
-        const double2* x = X + ((int64_t)p * nrow + r) * nfft + (k1 << ll);
-        for (int e = threadIdx.x; e < L; e += 256) nu_s[e] = x[e];
+        // this moment's row into the tile, the next one's loads issued before the transform
+        const int64_t pn = (int64_t)(p > 0 ? p - 1 : 0) * pstride;
+#pragma unroll
+        for (int q = 0; q < kNuFusedPer; ++q) {
+            const int e = threadIdx.x + 256 * q;
+            if (e < L) {
+                nu_s[e] = nx[q];
+                nx[q] = xr[pn + e];
+            }
+        }
         __syncthreads();
-        nu_fft_lds(nu_s, ll, 0, 1, L, T, lnfft);
+        nu_fft_lds(nu_s, ll, 0, 1, L, &tw, lt);
+        const double ip = 1.0 / (double)(p + 1);
 #pragma unroll
         for (int q = 0; q < kNuFusedPer; ++q) {
             const int b = threadIdx.x + 256 * q;
@@ -574,12 +644,12 @@ __global__ __launch_bounds__(256) void k_nu_fft_rows_combine(const double2* __re
                 const double2 v = nu_s[b];
                 const int64_t J = k1 + ((int64_t)b << ln1);
                 const int64_t jc = J <= jhi ? J : J - nfft;  // positions between the two ends hold no trial
-                // k_nu_combine's arithmetic exactly: th = (jc / n) 2 pi, f = th / (p + 1)
-                const double f = (((double)jc / (double)nfft) * 6.283185307179586476925286766559) / (double)(p + 1);
+                // k_nu_combine's arithmetic exactly: th = (jc 2^-lnfft) 2 pi (exact scaling), f = th fl(1 / (p + 1))
+                const double f = (ldexp((double)jc, -lnfft) * 6.283185307179586476925286766559) * ip;
                 acc[q] = make_double2(fma(-f, acc[q].y, v.x), fma(f, acc[q].x, v.y));
             }
         }
-        __syncthreads();  // the next moment's load overwrites the tile
+        __syncthreads();  // the next moment's store overwrites the tile
     }
 #pragma unroll
     for (int q = 0; q < kNuFusedPer; ++q) {
@@ -618,10 +688,10 @@ __global__ __launch_bounds__(256) void k_nu_combine(const double2* __restrict__ 
         return;
     const int64_t t = (row0 + row) * nf + jbase + jc - tb0;
     if (t < 0 || t >= nbt) return;
-    const double th = ((double)jc / (double)nfft) * 6.283185307179586476925286766559;
+    const double th = ldexp((double)jc, -lnfft) * 6.283185307179586476925286766559;
     double2 A = Z[((int64_t)(P - 1) * nrow + row) * nfft + pos];
     for (int p = P - 2; p >= 0; --p) {
-        const double f = th / (double)(p + 1);
+        const double f = th * (1.0 / (double)(p + 1));
         const double2 b = Z[((int64_t)p * nrow + row) * nfft + pos];
         A = make_double2(fma(-f, A.y, b.x), fma(f, A.x, b.y));
     }
@@ -1067,7 +1137,7 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* dt, const doub
             if (fused_combine) {  // pass 2 and the moments' Horner sum in one kernel (FFT span)
                 g_nu_work[3] += plane + 16.0 * (double)nbt;
                 k_nu_fft_rows_combine<<<dim3((unsigned)(int64_t(1) << ln1), (unsigned)nrow), 256, lds_fft, s>>>(
-                    Zo, ln2, lnfft, T, P, nrow, nf, pl.nseg - 1 - pl.h, pl.h, rb * nf + jbase - (tb0 + first), nbt,
+                    Zo, ln2, lnfft, P, nrow, nf, pl.nseg - 1 - pl.h, pl.h, rb * nf + jbase - (tb0 + first), nbt,
                     CS + (int64_t)(k - 1) * nbt);
                 HIPCHK(hipGetLastError());
                 HIPCHK(span(2));
@@ -1075,7 +1145,7 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* dt, const doub
             }
             g_nu_work[3] += 2.0 * plane;
             g_nu_work[4] += plane + 16.0 * (double)nbt;
-            k_nu_fft_rows<<<(unsigned)cdiv(Bp << ln1, int64_t(1) << lrow), 256, lds_fft, s>>>(Zo, ln2, lrow, lnfft, T);
+            k_nu_fft_rows<<<(unsigned)cdiv(Bp << ln1, int64_t(1) << lrow), 256, lds_fft, s>>>(Zo, ln2, lrow, lnfft);
             HIPCHK(hipGetLastError());
             HIPCHK(span(2));
             k_nu_combine<<<dim3((unsigned)cdiv(nfft, 256), (unsigned)nrow), 256, 0, s>>>(
@@ -1113,11 +1183,12 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* dt, const doub
                     int alo = 0, acnt = 0;
                     occupied(k, &alo, &acnt);
                     const int64_t gbase = (int64_t)alo << ln2, gcount = (int64_t)acnt << ln2;
-                    // lanes per cell: about >= 32 photons per lane, at most 8
+                    // lanes per cell: enough threads for ~2 rounds of 3 resident waves per SIMD, keeping >= 4
+                    // photons per lane, at most 8
                     const int64_t kspan = pl.gmax[(size_t)(k - 1)] - pl.gmin[(size_t)(k - 1)] + 1;
                     const int64_t ppc = n / std::max<int64_t>(1, std::min<int64_t>(kspan, nfft));
                     int L = 1;
-                    while (L < 8 && ppc >= 32 * 2 * L) L *= 2;
+                    while (L < 8 && gcount * L < (int64_t(1) << 19) && ppc >= 4 * 2 * L) L *= 2;
                     if (lanes_env > 0) L = lanes_env;  // test hook: CRIMP_NUFFT_LANES=1|2|4|8
                     // per photon and row: premultiplier phase + cis ~ 40 flops, then 2 FMA + 1 multiply per moment
                     g_nu_work[0] += (40.0 + 5.0 * P) * (double)n * nrow;

@@ -280,21 +280,23 @@ def _every_interval_vs_oracle_profile(r, xh, oh, E, tm, ph_shift_res=1000):
       at -+ k* step beyond it -- the crossing is exactly where the device reported it (lmfit's clip to the phShift
       bounds at +-pi as the oracle's fit_toa; the phShiftRes / 2 cap excepted)."""
     import math
+    import os
+    from concurrent.futures import ThreadPoolExecutor
     thr = 0.500021713558733
     tarr = O.template_arrays(tm)
     n0 = float(tm["norm"]["value"])
     lo, hi = n0 / 100.0, 500.0
     step = 2 * math.pi / ph_shift_res
-    worst_phi = worst_n = 0.0
-    for i in range(len(E)):
+
+    def one(i):  # the oracle's C calls release the GIL: intervals run on a thread pool
         x = xh[oh[i]:oh[i + 1]]
         phi, n = float(r["phShi"][i]), float(r["norm"][i])
         o = O.toa_eval(x, E[i], tarr, n, phi)
         heff = o[5] - o[4] * o[4] / o[3]
-        worst_phi = max(worst_phi, abs(o[2] / heff) / (2 * math.pi))
-        if lo < n < hi:
-            worst_n = max(worst_n, abs(o[1] / o[3]) / n)
+        wphi = abs(o[2] / heff) / (2 * math.pi)
+        wn = abs(o[1] / o[3]) / n if lo < n < hi else 0.0
         llmax = O._profile_norm(x, E[i], tarr, phi, lo, hi, n)[1][0]
+        bad = []
         for side, bound in ((-1, r["phShi_LL"][i]), (1, r["phShi_UL"][i])):
             kk = int(round((bound - step / 2) / step))
             kstar = kk - 1
@@ -308,7 +310,17 @@ def _every_interval_vs_oracle_profile(r, xh, oh, E, tm, ph_shift_res=1000):
                 p = min(max(phi + side * k * step, -math.pi), math.pi)
                 _, ok = O._profile_norm(x, E[i], tarr, p, lo, hi, n)
                 diff = llmax - ok[0]
-                assert (diff <= thr) if inside else (diff > thr), (i, side, k, kstar, diff)
+                if not ((diff <= thr) if inside else (diff > thr)):
+                    bad.append((i, side, k, kstar, diff))
+        return wphi, wn, bad
+
+    workers = max(1, min(16, len(os.sched_getaffinity(0))))
+    with ThreadPoolExecutor(workers) as ex:
+        res = list(ex.map(one, range(len(E))))
+    bad = [b for _, _, bb in res for b in bb]
+    assert not bad, bad[:5]
+    worst_phi = max(w for w, _, _ in res)
+    worst_n = max(w for _, w, _ in res)
     assert worst_phi <= 1e-6, worst_phi
     assert worst_n <= 1e-9, worst_n
 
