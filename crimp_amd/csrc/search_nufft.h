@@ -668,6 +668,84 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k
     }
 }
 
+// k_nu_fft_rows_combine for n2 = 4096 (the four-step FFT's rows; three radix-16 stages): the same arithmetic as
+// nu_fft_lds (the same stages, twiddles and butterflies, so bit-identical powers) with stage 1 on the row as loaded
+// into registers (thread t holds elements t + 256 r) and stage 3's outputs -- positions t + 256 r -- kept in registers
+// for the Horner sum: the tile is written and read twice per moment instead of four times. Two 64 KB tiles (stage 1
+// -> A, stage 2 -> B) leave two barriers per moment; element i of a tile is stored at i ^ ((i >> 4) & 15), which
+// spreads stage 1's stride-16 writes over all banks. The next moment's row loads are issued before the transform.
+__device__ __forceinline__ int nu_sw(int i) { return i ^ ((i >> 4) & 15); }
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k_nu_rows4096_combine(
+    const double2* __restrict__ X, int lnfft, int P, int nrow, int64_t nf, int64_t jhi, int64_t h, int64_t tbase,
+    int64_t nbt, double2* __restrict__ CS) {
+    extern __shared__ double2 nu_s[];  // [2][4096]
+    __shared__ NuTile tw;
+    nu_tile_init(&tw, 12);
+    double2* A = nu_s;
+    double2* B = nu_s + 4096;
+    const int64_t nfft = int64_t(1) << lnfft;
+    const int ln1 = lnfft - 12;
+    const int64_t k1 = blockIdx.x;
+    const int r = blockIdx.y;
+    const int t = threadIdx.x;
+    const double2* xr = X + (int64_t)r * nfft + (k1 << 12);
+    const int64_t pstride = (int64_t)nrow * nfft;
+    double2 acc[16], nx[16], v[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        acc[q] = make_double2(0.0, 0.0);
+        nx[q] = xr[(int64_t)(P - 1) * pstride + t + 256 * q];
+    }
+    // twiddle indices of this thread's butterflies (units of w_4096): stage 2 w_256^{t & 15}, stage 3 w_4096^t
+    const int m2 = (t & 15) << 4, m3 = t;
+    const int z0 = ((t >> 4) << 8) + (t & 15);  // stage 2's output base
+    __syncthreads();                            // tw
+    for (int p = P - 1; p >= 0; --p) {
+        const int64_t pn = (int64_t)(p > 0 ? p - 1 : 0) * pstride;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            v[q] = nx[q];
+            nx[q] = xr[pn + t + 256 * q];
+        }
+        nu_dft16(v);  // stage 1 (Ns = 1: no twiddles)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) A[nu_sw(16 * t + q)] = v[q];
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 16; ++q) v[q] = A[nu_sw(t + 256 * q)];
+        nu_twiddle<16>(nu_tw_tile(&tw, m2), v);
+        nu_dft16(v);  // stage 2 (Ns = 16)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) B[nu_sw(z0 + 16 * q)] = v[q];
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 16; ++q) v[q] = B[nu_sw(t + 256 * q)];
+        nu_twiddle<16>(nu_tw_tile(&tw, m3), v);
+        nu_dft16(v);  // stage 3 (Ns = 256): output position t + 256 q
+        const double ip = 1.0 / (double)(p + 1);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int64_t J = k1 + ((int64_t)(t + 256 * q) << ln1);
+            const int64_t jc = J <= jhi ? J : J - nfft;
+            const double f = (ldexp((double)jc, -lnfft) * 6.283185307179586476925286766559) * ip;
+            acc[q] = make_double2(fma(-f, acc[q].y, v[q].x), fma(f, acc[q].x, v[q].y));
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int64_t J = k1 + ((int64_t)(t + 256 * q) << ln1);
+        int64_t jc;
+        if (J <= jhi)
+            jc = J;
+        else if (J >= nfft - h)
+            jc = J - nfft;
+        else
+            continue;
+        const int64_t tt = tbase + r * nf + jc;
+        if (tt >= 0 && tt < nbt) CS[tt] = acc[q];
+    }
+}
+
 // (C_k, S_k) of the trials of one harmonic: position pos = k1 n2 + k2 of the FFT output holds J = k1 + n1 k2
 // (ln1 = 0: natural order); J = jc mod n. Horner over the moments with z = 2 pi i jc / n.
 __global__ __launch_bounds__(256) void k_nu_combine(const double2* __restrict__ Z, int lnfft, int ln1, int P, int nrow,
@@ -785,28 +863,44 @@ static int ilog2(int64_t v) {
 }
 
 // per-call twiddle (w_n^t) and cis tables, fp64 from long double
+// Twiddle (w_n, two-level) and cis tables for n = 2^lnfft, built once per device and n (long double on the host) and
+// kept for the process: a search reuses them without an upload.
 static int nu_tables(Scratch& sc, hipStream_t s, int lnfft, NuTw* T, const double2** cis) {
+    (void)sc;
+    static std::mutex mu;
+    static std::map<std::pair<int, int>, double2*> cache;
     const int lbits = std::min(lnfft, 11);
     const int64_t nlo = int64_t(1) << lbits, nhi = int64_t(1) << (lnfft - lbits);
-    std::vector<double2> h((size_t)(nlo + nhi + 1024));
-    const long double tp = 6.283185307179586476925286766559L;
-    const long double nf = (long double)(int64_t(1) << lnfft);
-    for (int64_t i = 0; i < nlo; ++i) {
-        const long double a = tp * (long double)i / nf;
-        h[(size_t)i] = make_double2((double)cosl(a), (double)sinl(a));
-    }
-    for (int64_t i = 0; i < nhi; ++i) {
-        const long double a = tp * (long double)(i << lbits) / nf;
-        h[(size_t)(nlo + i)] = make_double2((double)cosl(a), (double)sinl(a));
-    }
-    for (int i = 0; i < 1024; ++i) {
-        const long double a = tp * (long double)i / 1024.0L;
-        h[(size_t)(nlo + nhi + i)] = make_double2((double)cosl(a), (double)sinl(a));
-    }
+    int dev = 0;
+    HIPCHK(hipGetDevice(&dev));
     double2* d = nullptr;
-    HIPCHK(sc.alloc(&d, h.size()));
-    HIPCHK(hipMemcpyAsync(d, h.data(), h.size() * sizeof(double2), hipMemcpyHostToDevice, s));
-    HIPCHK(hipStreamSynchronize(s));  // h is pageable and local
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        auto it = cache.find({dev, lnfft});
+        if (it != cache.end()) {
+            d = it->second;
+        } else {
+            std::vector<double2> h((size_t)(nlo + nhi + 1024));
+            const long double tp = 6.283185307179586476925286766559L;
+            const long double nf = (long double)(int64_t(1) << lnfft);
+            for (int64_t i = 0; i < nlo; ++i) {
+                const long double a = tp * (long double)i / nf;
+                h[(size_t)i] = make_double2((double)cosl(a), (double)sinl(a));
+            }
+            for (int64_t i = 0; i < nhi; ++i) {
+                const long double a = tp * (long double)(i << lbits) / nf;
+                h[(size_t)(nlo + i)] = make_double2((double)cosl(a), (double)sinl(a));
+            }
+            for (int i = 0; i < 1024; ++i) {
+                const long double a = tp * (long double)i / 1024.0L;
+                h[(size_t)(nlo + nhi + i)] = make_double2((double)cosl(a), (double)sinl(a));
+            }
+            HIPCHK(hipMalloc(&d, h.size() * sizeof(double2)));
+            HIPCHK(hipMemcpyAsync(d, h.data(), h.size() * sizeof(double2), hipMemcpyHostToDevice, s));
+            HIPCHK(hipStreamSynchronize(s));  // h is pageable and local
+            cache[{dev, lnfft}] = d;
+        }
+    }
     T->lo = d;
     T->hi = d + nlo;
     T->lbits = lbits;
@@ -940,18 +1034,17 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* dt, const doub
                         int64_t count, double* out, bool timed, int64_t* nfixed, bool no_fixup, bool* applicable) {
     *applicable = false;
     *nfixed = 0;
-    int* dflag = nullptr;
-    double* dsc = nullptr;
-    HIPCHK(sc.alloc(&dflag, 4));
-    HIPCHK(sc.alloc(&dsc, 4));
-    HIPCHK(hipMemsetAsync(dflag, 0, 4 * sizeof(int), s));
+    double* dsc = nullptr;  // [delta, f0, dt[0], dt[n-1], unsorted flag (int)]: one readback
+    HIPCHK(sc.alloc(&dsc, 6));
+    int* dflag = reinterpret_cast<int*>(dsc + 4);
+    HIPCHK(hipMemsetAsync(dflag, 0, sizeof(double), s));
     k_nu_sorted<<<(unsigned)std::min<int64_t>(cdiv(n, 256), 2048), 256, 0, s>>>(dt, n, dflag);
     k_nu_scalars<<<1, 64, 0, s>>>(ap, freq, dt, n, dsc);
     HIPCHK(hipGetLastError());
+    double hs[5];
+    HIPCHK(d2h(s, hs, dsc, sizeof(hs)));
     int bad = 0;
-    double hs[4];
-    HIPCHK(d2h(s, &bad, dflag, sizeof(int)));
-    HIPCHK(hipMemcpy(hs, dsc, sizeof(hs), hipMemcpyDeviceToHost));
+    memcpy(&bad, hs + 4, sizeof(int));
     if (bad) return CRIMP_OK;
     const double delta = hs[0], f0 = hs[1], dt0 = hs[2], dtn = hs[3];
     const int64_t nchunk = cdiv(n, kNuCW);
@@ -1026,6 +1119,21 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* dt, const doub
     // pass 2 fused with the combine (default); CRIMP_NUFFT_FUSED=0 runs them as two kernels (A/B hook)
     const char* fused_env = getenv("CRIMP_NUFFT_FUSED");
     const bool fused_combine = !(fused_env && !strcmp(fused_env, "0"));
+    // CRIMP_NUFFT_ROWS4096=0 runs 4096-element rows through the generic fused kernel (A/B and identity test hook)
+    const char* r4_env = getenv("CRIMP_NUFFT_ROWS4096");
+    const bool rows4096 = !(r4_env && !strcmp(r4_env, "0"));
+    {  // 128 KB of dynamic LDS for k_nu_rows4096_combine, set once per device
+        static std::mutex mu;
+        static uint64_t done = 0;
+        int dev = 0;
+        HIPCHK(hipGetDevice(&dev));
+        std::lock_guard<std::mutex> lk(mu);
+        if (dev >= 64 || !(done >> dev & 1)) {
+            HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_nu_rows4096_combine),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kNuTile * (int)sizeof(double2)));
+            if (dev < 64) done |= uint64_t(1) << dev;
+        }
+    }
     const char* lanes_s = getenv("CRIMP_NUFFT_LANES");
     const int lanes_env = lanes_s ? atoi(lanes_s) : 0;
     ARGCHK(lanes_env == 0 || lanes_env == 1 || lanes_env == 2 || lanes_env == 4 || lanes_env == 8,
@@ -1133,6 +1241,15 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* dt, const doub
                     W, Y, lnfft, ln1, lcol, T, alo, acnt);
                 HIPCHK(hipGetLastError());
                 Zo = Y;
+            }
+            if (fused_combine && ln2 == 12 && rows4096) {  // the specialised form for 4096-element rows
+                g_nu_work[3] += plane + 16.0 * (double)nbt;
+                k_nu_rows4096_combine<<<dim3((unsigned)(int64_t(1) << ln1), (unsigned)nrow), 256, 2 * lds_fft, s>>>(
+                    Zo, lnfft, P, nrow, nf, pl.nseg - 1 - pl.h, pl.h, rb * nf + jbase - (tb0 + first), nbt,
+                    CS + (int64_t)(k - 1) * nbt);
+                HIPCHK(hipGetLastError());
+                HIPCHK(span(2));
+                return CRIMP_OK;
             }
             if (fused_combine) {  // pass 2 and the moments' Horner sum in one kernel (FFT span)
                 g_nu_work[3] += plane + 16.0 * (double)nbt;

@@ -293,7 +293,11 @@ def _every_interval_vs_oracle_profile(r, xh, oh, E, tm, ph_shift_res=1000):
         phi, n = float(r["phShi"][i]), float(r["norm"][i])
         o = O.toa_eval(x, E[i], tarr, n, phi)
         heff = o[5] - o[4] * o[4] / o[3]
-        wphi = abs(o[2] / heff) / (2 * math.pi)
+        step_phi = -(o[2] - o[4] * o[1] / o[3]) / heff  # profile Newton step (norm re-maximised)
+        if abs(phi) >= math.pi - 1e-9 and step_phi * phi > 0:
+            wphi = 0.0  # the maximum lies past the phShift bound: the bounded fit stops there (lmfit's bounds)
+        else:
+            wphi = abs(step_phi) / (2 * math.pi)
         wn = abs(o[1] / o[3]) / n if lo < n < hi else 0.0
         llmax = O._profile_norm(x, E[i], tarr, phi, lo, hi, n)[1][0]
         bad = []
@@ -319,10 +323,11 @@ def _every_interval_vs_oracle_profile(r, xh, oh, E, tm, ph_shift_res=1000):
         res = list(ex.map(one, range(len(E))))
     bad = [b for _, _, bb in res for b in bb]
     assert not bad, bad[:5]
-    worst_phi = max(w for w, _, _ in res)
-    worst_n = max(w for _, w, _ in res)
-    assert worst_phi <= 1e-6, worst_phi
-    assert worst_n <= 1e-9, worst_n
+    iphi = int(np.argmax([w for w, _, _ in res]))
+    inrm = int(np.argmax([w for _, w, _ in res]))
+    worst_phi, worst_n = res[iphi][0], res[inrm][1]
+    assert worst_phi <= 1e-6, (iphi, worst_phi, float(r["phShi"][iphi]), float(r["norm"][iphi]))
+    assert worst_n <= 1e-9, (inrm, worst_n, float(r["phShi"][inrm]), float(r["norm"][inrm]))
 
 
 def _sample_template(tm, n, shift, rng):

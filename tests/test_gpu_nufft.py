@@ -159,7 +159,8 @@ def test_nufft_unsorted_photons_take_default_path(gpu):
 
 def test_nufft_fused_pass2_equals_separate_combine(gpu, monkeypatch):
     """FFT pass 2 fused with the moments' Horner sum (default) against pass 2 and k_nu_combine as two kernels
-    (CRIMP_NUFFT_FUSED=0): the same arithmetic, so bit-identical powers -- single-pass (n <= 4096) and four-step
+    (CRIMP_NUFFT_FUSED=0), and the 4096-row kernel (k_nu_rows4096_combine) against the generic fused one
+    (CRIMP_NUFFT_ROWS4096=0): the same arithmetic, so bit-identical powers -- single-pass (n <= 4096) and four-step
     FFTs, 1-D and 2-D grids, both spread forms."""
     from crimp_amd import ops, _native as N
     from crimp_amd.synth import pulsed_events
@@ -173,6 +174,11 @@ def test_nufft_fused_pass2_equals_separate_combine(gpu, monkeypatch):
         b = ops.search(t, t0, f, m, 1, log10_negfdot=fdv, precision="nufft", flags=N.FLAG_NO_FIXUP)
         monkeypatch.delenv("CRIMP_NUFFT_FUSED")
         np.testing.assert_array_equal(a, b)
+        # 4096-element rows (n >= 2^13): the specialised kernel against the generic fused one
+        monkeypatch.setenv("CRIMP_NUFFT_ROWS4096", "0")
+        c = ops.search(t, t0, f, m, 1, log10_negfdot=fdv, precision="nufft", flags=N.FLAG_NO_FIXUP)
+        monkeypatch.delenv("CRIMP_NUFFT_ROWS4096")
+        np.testing.assert_array_equal(a, c)
 
 
 def test_nufft_gather_lane_splits(gpu, monkeypatch):
