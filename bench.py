@@ -1,24 +1,25 @@
-"""Benchmark: Z^2_2 photon x trial evaluations per second (BASELINE.json metric, config 3), plus the ToA-fit and
-calcphase legs.
+"""Benchmark: Z^2_2 photon x trial evaluations per second (BASELINE.json metric, config 3), plus the exact-path,
+ToA-fit, calcphase, config-4 and config-2 legs.
 
-One step = one complete Z^2_2 search of the config-3 workload per GPU on the default (exact) path: 1e7 synthetic
-pulsed photons (T = 1e6 s, p = 0.1, f0 = 7.123456789 Hz, seed 0) against 1e6 trial frequencies spaced 1/(10T),
+One step = one complete Z^2_2 search of the config-3 workload per GPU: 1e7 synthetic pulsed photons (T = 1e6 s,
+p = 0.1, f0 = 7.123456789 Hz, seed 0, time-sorted as event files are) against 1e6 trial frequencies spaced 1/(10T),
 inputs resident in HBM, followed by the search's one exchange step (every rank's best trial gathered so that all
 ranks agree on the global best, ties -> lowest index). With N ranks each rank searches its own 1e6-trial slice of
-an N*1e6 grid (weak scaling); ``value`` = all ranks' evaluations / max-over-ranks time.
+an N*1e6 grid (weak scaling); ``value`` = all ranks' evaluations / max-over-ranks time. The step runs
+``precision="nufft"`` (csrc/search_nufft.h: Taylor-moment NUFFT in fp64, every trial within 1e-6 of the reference
+by its certificate + fp64 fix-up, tests/test_gpu_nufft.py, test_gpu_fullsize.py); ``--precision exact`` times the
+default exact-integer MFMA path instead. "Evaluations" are the photon x trial pairs the reference evaluates
+directly; the NUFFT returns the same per-trial powers without evaluating every pair.
 
 Also reported:
-* ``roofline``: the exact kernel (k_search_exact) is bound by the i8 matrix cores. Per 4 photons x 2048 trials x
-  harmonic it issues 8 dense v_mfma_i32_32x32x32_i8 (65536 ops each) and 4 2:4-sparse v_smfmac_i32_32x32x64_i8
-  (131072 nominal ops each) = 128 ops per photon*trial*harmonic; both take 32 cycles of a SIMD's matrix pipe, so
-  the peak of this instruction mix is 2/3 x 5.0 + 1/3 x 10.0 = 6.67 POP/s (the i8 dense peak, 2x BF16's 2.5 PF,
-  and the 2:4-sparse peak, 2x dense) and ``frac`` is the matrix pipe's occupancy at the nominal 2.4 GHz; kernel
-  time from hipEvents around the harmonic-sum kernels on their stream; ``traffic`` from the same tree's rocprofv3
-  PMC pass (profiles/r04/pmc_traffic.json, tools/pmc_round.sh) when it was taken on this workload;
-* ``cpu_baseline``: the oracle (oracle/liborc.so, fp64, OpenMP over trials) on a bounded sample;
-* ``nufft``: precision="nufft" (csrc/search_nufft.h) on the same workload: equivalent photon x trial evals/s (the
-  same per-trial results, not pairwise evaluations), its kernels' times (spread / merge / FFT / combine+finalize) and
-  the roofline of each against HBM or the fp64 peak;
+* ``roofline``: the NUFFT's dominant kernel class, its algorithmic work per launch (crimp_last_nufft_work) over the
+  mean launch time (hipEvents on the library's stream); every class under ``nufft.kernels``;
+* ``exact_path``: the default exact-integer path (k_search_exact) on the same inputs, ``--exact-steps`` steps, with
+  its i8 matrix-core roofline: per 4 photons x 2048 trials x harmonic it issues 8 dense v_mfma_i32_32x32x32_i8
+  (65536 ops each) and 4 2:4-sparse v_smfmac_i32_32x32x64_i8 (131072 nominal ops each) = 128 ops per
+  photon*trial*harmonic, against the 6.67 POP/s peak of that 2:1 mix; ``traffic`` from the tree's rocprofv3 PMC pass
+  (profiles/r04/pmc_traffic.json) when it was taken on this workload;
+* ``cpu_baseline``: the oracle (oracle/liborc.so, fp64 direct sums, OpenMP over trials) on a bounded sample;
 * ToA (config 5 per GPU): the device fit of 1250 intervals x 1e5 photons, and the end-to-end ``measure_intervals``
   (interval selection, calcphase, fits, per-interval H-test) from host MJD arrays, with the oracle's fits on all
   allowed host cores as its CPU baseline (a sample, extrapolated) and the fits' VALU roofline;
@@ -59,7 +60,10 @@ def parse():
     p.add_argument("--nharm", type=int, default=2)
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline legs")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
-    p.add_argument("--no-nufft", action="store_true", help="skip the NUFFT search leg")
+    p.add_argument("--precision", default="nufft", choices=["nufft", "exact"],
+                   help="the search path of `value` (the other one is timed beside it)")
+    p.add_argument("--exact-steps", type=int, default=3, help="timed steps of the exact-path leg (~0.8 s each)")
+    p.add_argument("--no-exact", action="store_true", help="skip the exact-path leg (when value is nufft)")
     p.add_argument("--toa-intervals", type=int, default=1250, help="ToA intervals per GPU (config 5: 1e4 over 8)")
     p.add_argument("--toa-photons", type=int, default=100_000)
     p.add_argument("--no-toa", action="store_true", help="skip the ToA legs")
@@ -499,15 +503,17 @@ PEAK_F64_TFLOPS = 78.6  # MI355X spec fp64 (vector and matrix); mb_f64 measures 
 
 def nufft_leg(a, t, t_h, f, rank, M, steps):
     """The rank's trial slice by precision="nufft": one untimed search, then ``steps`` timed ones (wall time with the
-    stream drained, and the library's hipEvent spans: whole pipeline, spread, merge, FFT, combine + finalize). Each
-    kernel class is priced by the algorithmic work the library counted for the plan it chose (crimp_last_nufft_work;
-    DESIGN.md section 5):
-      spread  fp64 flops: the cell gather's ~40 + 5 P per photon, row and harmonic (k_nu_gather), or the MFMA form's
-              issued 512 per photon-harmonic (k_nu_spread), against the fp64 peak;
-      merge   HBM: MFMA slots read + the FFT input written (absent for the cell gather, which writes W directly);
-      fft     HBM: pass 1 reading the occupied rows and writing all, pass 2 reading all (fused with the Horner
-              combine, which writes one complex sum per trial and harmonic);
-      combine HBM: the finalize reading the harmonic sums and writing the powers."""
+    stream drained, and the library's hipEvent spans: the whole pipeline and each kernel class's time and launches).
+    Each class is priced by the algorithmic work the library counted for the plan it chose (crimp_last_nufft_work;
+    DESIGN.md section 5.3):
+      spread   fp64 flops: the cell gather's ~40 + 5 P per photon, row and harmonic (k_nu_gather), or the MFMA form's
+               issued 512 per photon-harmonic (k_nu_spread), against the fp64 peak;
+      merge    HBM: MFMA slots read + the FFT input written (absent for the cell gather, which writes W directly);
+      pass1    HBM: the FFT's column pass reading the occupied rows and writing all (k_nu_cols256 / k_nu_fft_cols);
+      pass2    HBM: the row pass fused with the Horner sum over moments, reading all and writing one complex sum per
+               trial and harmonic (k_nu_rows4096_combine / k_nu_fft_rows_combine);
+      finalize HBM: the harmonic sums read, the powers written (k_nu_finalize).
+    The cell starts (k_nu_cellstart) are timed but not priced."""
     import torch
     from crimp_amd import ops
     from crimp_amd import _native as N
@@ -523,30 +529,37 @@ def nufft_leg(a, t, t_h, f, rank, M, steps):
                    flags=N.FLAG_TIME_KERNELS)
         torch.cuda.synchronize()
         walls.append(time.perf_counter() - t2)
-        spans.append(N.last_kernel_times())
+        spans.append(N.last_kernel_times()[:15])
     path = N.load().crimp_last_search_path()
     nfix = N.load().crimp_last_fixups()
     wall = float(np.mean(walls))
-    sp = np.mean(np.array([s_[:5] for s_ in spans]), axis=0)  # total, spread, merge, fft, combine+finalize
+    sp = np.mean(np.array(spans), axis=0)  # total, then 7 class sums (ms), then 7 launch counts
     n, P, form = N.last_nufft_plan()  # search_nufft.h nu_plan: least n P with x^P/P! <= 1e-14, x = pi (M/2) / n
     w = N.last_nufft_work()
     m = a.nharm
+    work = {"spread": (w["spread_flops"], "fp64"), "merge": (w["merge_bytes"], "hbm"), "pass1": (w["pass1_bytes"], "hbm"),
+            "pass2": (w["pass2_bytes"], "hbm"), "combine": (w["combine_bytes"], "hbm"),
+            "finalize": (w["finalize_bytes"], "hbm")}
     legs = {}
-    for name, ms, work, bound in (("spread", sp[1], w["spread_flops"], "fp64"), ("merge", sp[2], w["merge_bytes"], "hbm"),
-                                  ("fft", sp[3], w["fft_bytes"], "hbm"), ("combine", sp[4], w["combine_bytes"], "hbm")):
-        if ms <= 0.0 or work <= 0.0:
+    for c, name in enumerate(N.NUFFT_CLASSES):
+        ms, launches = float(sp[1 + c]), int(round(sp[8 + c]))
+        if ms <= 0.0 or launches == 0:
             continue  # no such kernel in this plan (the cell gather has no merge)
-        if bound == "fp64":
-            legs[name] = {"bound": bound, "achieved": work / (ms * 1e-3) / 1e12, "peak": PEAK_F64_TFLOPS,
-                          "unit": "TFLOP/s", "ms": ms, "work": work}
-        else:
-            legs[name] = {"bound": bound, "achieved": work / (ms * 1e-3) / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                          "ms": ms, "work": work}
-    for v in legs.values():
-        v["frac"] = v["achieved"] / v["peak"]
-    dom = max(legs, key=lambda k: legs[k]["ms"])
+        leg = {"ms": ms, "launches": launches, "ms_per_launch": ms / launches}
+        if name in work and work[name][0] > 0:
+            wk, bound = work[name]
+            per_launch = wk / launches
+            if bound == "fp64":
+                leg.update({"bound": bound, "achieved": per_launch / (leg["ms_per_launch"] * 1e-3) / 1e12,
+                            "peak": PEAK_F64_TFLOPS, "unit": "TFLOP/s", "work_per_launch": per_launch})
+            else:
+                leg.update({"bound": bound, "achieved": per_launch / (leg["ms_per_launch"] * 1e-3) / 1e9,
+                            "peak": PEAK_HBM_GBS, "unit": "GB/s", "work_per_launch": per_launch})
+            leg["frac"] = leg["achieved"] / leg["peak"]
+        legs[name] = leg
+    dom = max((k for k in legs if "frac" in legs[k]), key=lambda k: legs[k]["ms"])
     return {"evals_per_s": float(a.photons) * M / wall, "unit": "equivalent photon*trial evals/s (Z^2_%d)" % m,
-            "ms_per_search": wall * 1e3, "pipeline_ms": sp[0], "search_path": path, "fp64_fixup_trials": nfix,
+            "ms_per_search": wall * 1e3, "pipeline_ms": float(sp[0]), "search_path": path, "fp64_fixup_trials": nfix,
             "plan": {"fft_length": n, "moments": P, "spread": form}, "kernels": legs, "dominant": dom,
             "roofline": dict({"kernel": dom}, **legs[dom]),
             "precision": "fp64 moments (%s), fp64 FFT, per-trial 1e-6 certificate + fp64 fix-up"
@@ -621,52 +634,71 @@ def main():
     from crimp_amd.sharding import sharded_search, shard_range
     assert shard_range(world * M, world, rank) == (rank * M, M)
 
-    kms, fixups, bests = [], [], []
+    def timed_steps(precision, steps, warmup, flags=0):
+        """warmup untimed steps, then `steps` timed between barriers: (max-over-ranks seconds, kernel ms, fix-ups,
+        last best, per-step hipEvent ms). A step is this rank's slice through crimp_search and one all_gather of
+        every rank's (best power, flat index), ties -> lowest index (the tested path, tests/test_distributed_*)."""
+        kms, fixups, bests = [], [], []
 
-    def step():
-        # the tested multi-GPU path (tests/test_distributed_*.py): this rank's slice through crimp_search, then one
-        # all_gather of every rank's (best power, flat index); ties -> lowest index
-        b = sharded_search(t, f, a.nharm, 0, gather="best", flags=N.FLAG_TIME_KERNELS)
-        kms.append(N.load().crimp_last_kernel_ms())
-        fixups.append(N.load().crimp_last_fixups())
-        bests.append(b)
-        return b
+        def step():
+            b = sharded_search(t, f, a.nharm, 0, gather="best", flags=flags, precision=precision)
+            kms.append(N.load().crimp_last_kernel_ms())
+            fixups.append(N.load().crimp_last_fixups())
+            bests.append(b)
 
-    for _ in range(a.warmup):
-        step()
-    kms.clear()
-    fixups.clear()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    stream = torch.cuda.current_stream()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
-    t1 = time.perf_counter()
-    for k in range(a.steps):
-        evs[k][0].record(stream)
-        step()
-        evs[k][1].record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t1
-    elt = torch.tensor([el], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(elt, op=dist.ReduceOp.MAX)
-    el = float(elt.item())
-    step_ms = float(np.mean([s.elapsed_time(e) for s, e in evs]))
-    kern_ms = float(np.mean(kms))  # hipEvents around the harmonic-sum kernels, on the stream they run on
-    best_pow, best_idx = bests[-1]
+        for _ in range(warmup):
+            step()
+        kms.clear()
+        fixups.clear()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        stream = torch.cuda.current_stream()
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        t1 = time.perf_counter()
+        for k in range(steps):
+            evs[k][0].record(stream)
+            step()
+            evs[k][1].record(stream)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t1
+        elt = torch.tensor([el], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(elt, op=dist.ReduceOp.MAX)
+        return (float(elt.item()), float(np.mean(kms)) if kms else 0.0, float(np.mean(fixups)), bests[-1],
+                float(np.mean([s_.elapsed_time(e) for s_, e in evs])), N.load().crimp_last_search_path())
 
-    evals = float(a.photons) * M * world * a.steps
-    value = evals / el
-    rec = None
-    if rank == 0:
+    def exact_record(el, kern_ms, nfix, steps):
         ops_per_launch = OPS_PER_EVAL_HARM * a.nharm * float(a.photons) * M
         achieved = ops_per_launch / (kern_ms * 1e-3) / 1e12
         traffic, tsrc = pmc_traffic(a.photons, M, a.nharm)
+        return {"value": float(a.photons) * M * world * steps / el, "unit": "photon*trial evals/s", "steps": steps,
+                "ms_per_step": el / steps * 1e3, "fp64_fixup_trials_per_step": nfix,
+                "dtype": "int8 digits on i8 MFMA, exact int32/int64 sums (fp64 phase, 2^30 fixed-point cos/sin)",
+                "roofline": {"kernel": "k_search_exact", "bound": "mfma", "achieved": achieved, "peak": PEAK_I8_TOPS,
+                             "unit": "TFLOP/s", "frac": achieved / PEAK_I8_TOPS, "traffic": traffic, "kernel_ms": kern_ms,
+                             "pmc": pmc_clock(),
+                             "note": "int8 matrix ops issued: 128 per photon*trial*harmonic (8 v_mfma_i32_32x32x32_i8 + "
+                                     "4 2:4-sparse v_smfmac_i32_32x32x64_i8 per 4 photons x 2048 trials) / mean "
+                                     "duration of the harmonic-sum kernels (hipEvents in libcrimp_hip on their stream); "
+                                     "peak = that 2:1 dense:sparse instruction mix at 32 cycles each (I8 dense 5.0 "
+                                     "POP/s, sparse 10.0): frac = matrix-pipe occupancy at 2.4 GHz; traffic: %s" % (
+                                         tsrc or "no PMC pass on this workload")}}
+
+    el, kern_ms, nfix, (best_pow, best_idx), step_ms, path = timed_steps(
+        a.precision, a.steps, a.warmup, flags=N.FLAG_TIME_KERNELS if a.precision == "exact" else 0)
+    value = float(a.photons) * M * world * a.steps / el
+    exact = None
+    if a.precision == "nufft" and not a.no_exact:
+        e_el, e_kms, e_nfix, e_best, _, _ = timed_steps("exact", a.exact_steps, 1, flags=N.FLAG_TIME_KERNELS)
+        exact = exact_record(e_el, e_kms, e_nfix, a.exact_steps)
+        exact["best_trial_index"], exact["best_power"] = e_best[1], float(e_best[0])
+    rec = None
+    if rank == 0:
         rec = {
             "metric": "Z^2_2 photon*trial evals/sec (node)",
             "value": value,
@@ -678,28 +710,33 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "int8 digits on i8 MFMA, exact int32/int64 sums (fp64 phase, 2^30 fixed-point cos/sin)",
+            "dtype": "f64" if a.precision == "nufft" else
+                     "int8 digits on i8 MFMA, exact int32/int64 sums (fp64 phase, 2^30 fixed-point cos/sin)",
             "data": "synthetic (seeded Poisson pulsed events, crimp_amd/synth.py)",
             "config": {"workload": "config3: synthetic %d photons x %d trials/GPU, Z^2_%d" % (a.photons, M, a.nharm),
                        "photons": a.photons, "trials_per_gpu": M, "nharm": a.nharm, "span_s": span, "f0": f0,
                        "trial_step_hz": df,
                        "parallelism": "trial-sharded dp%d: sharding.sharded_search + all_gather(best)" % world,
                        "best_trial_index": best_idx, "best_power": float(best_pow),
-                       "search_path": "exact (default precision)", "fp64_fixup_trials_per_step": float(np.mean(fixups))},
-            "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_I8_TOPS, "unit": "TFLOP/s",
-                         "frac": achieved / PEAK_I8_TOPS, "traffic": traffic,
-                         "kernel_ms": kern_ms, "step_ms": step_ms, "pmc": pmc_clock(),
-                         "note": "int8 matrix ops issued: 128 per photon*trial*harmonic (8 v_mfma_i32_32x32x32_i8 + 4 "
-                                 "2:4-sparse v_smfmac_i32_32x32x64_i8 per 4 photons x 2048 trials) / mean duration of "
-                                 "the harmonic-sum kernels (hipEvents in libcrimp_hip on their stream); peak = that "
-                                 "2:1 dense:sparse instruction mix at 32 cycles each (I8 dense 5.0 POP/s, sparse 10.0): "
-                                 "frac = matrix-pipe occupancy at 2.4 GHz; traffic: %s" % (
-                                     tsrc or "no PMC pass on this workload")},
+                       "search_path": {0: "fp64", 1: "exact", 2: "nufft"}.get(path, path),
+                       "precision": a.precision, "fp64_fixup_trials_per_step": nfix},
         }
+        if a.precision == "exact":
+            ex = exact_record(el, kern_ms, nfix, a.steps)
+            rec["roofline"] = dict(ex["roofline"], step_ms=step_ms)
+        else:
+            # the NUFFT's per-kernel rooflines from separately timed searches (hipEvent spans per kernel class)
+            nu = nufft_leg(a, t, t_h, f, rank, M, max(3, a.steps))
+            rec["roofline"] = dict(nu["roofline"], traffic=None, step_ms=step_ms,
+                                   note="dominant kernel class of the NUFFT search (DESIGN.md 5.3): algorithmic "
+                                        "work per launch (crimp_last_nufft_work) / mean launch duration (hipEvents "
+                                        "on the library's stream); all classes under `nufft.kernels`")
+            rec["nufft"] = nu
+            if exact is not None:
+                rec["exact_path"] = exact
+                rec["exact_path"]["same_best_trial"] = (exact["best_trial_index"] == best_idx)
         if not a.no_cpu and world == 1:  # rank 0 at N=1 only
             rec["cpu_baseline"] = cpu_baseline(t_h, f0, df, a.nharm, a.cpu_seconds)
-        if not a.no_nufft:  # precision="nufft" on the same inputs, beside the exact path
-            rec["nufft"] = nufft_leg(a, t, t_h, f, rank, M, a.steps)
     del t, f
     torch.cuda.empty_cache()
     if not a.no_calcphase and rank == 0:

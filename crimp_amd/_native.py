@@ -122,20 +122,24 @@ def last_nufft_plan():
 
 
 def last_nufft_work():
-    """The last NUFFT search's algorithmic work (crimp_last_nufft_work): spread flops, spread / merge / FFT /
-    combine + finalize HBM bytes."""
+    """The last NUFFT search's algorithmic work (crimp_last_nufft_work): the spread's fp64 flops and the HBM bytes of
+    each kernel class."""
     L = load(require_device=False)
-    w = (ctypes.c_double * 5)()
-    L.crimp_last_nufft_work(w, 5)
-    return {"spread_flops": w[0], "spread_bytes": w[1], "merge_bytes": w[2], "fft_bytes": w[3], "combine_bytes": w[4]}
+    w = (ctypes.c_double * 7)()
+    L.crimp_last_nufft_work(w, 7)
+    return {"spread_flops": w[0], "spread_bytes": w[1], "merge_bytes": w[2], "pass1_bytes": w[3], "pass2_bytes": w[4],
+            "combine_bytes": w[5], "finalize_bytes": w[6]}
+
+
+NUFFT_CLASSES = ("cellstart", "spread", "merge", "pass1", "pass2", "combine", "finalize")
 
 
 def last_kernel_times():
     """Every timed span (ms) of the last native call made with FLAG_TIME_KERNELS (crimp_last_kernel_times)."""
     L = load(require_device=False)
-    buf = (ctypes.c_double * 16)()
-    n = L.crimp_last_kernel_times(buf, 16)
-    return [buf[i] for i in range(min(n, 16))]
+    buf = (ctypes.c_double * 64)()
+    n = L.crimp_last_kernel_times(buf, 64)
+    return [buf[i] for i in range(min(n, 64))]
 
 
 def check(rc):

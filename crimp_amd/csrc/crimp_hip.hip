@@ -1876,8 +1876,8 @@ extern "C" int crimp_last_nufft_plan(int64_t* fft_length, int32_t* moments, int3
 }
 
 extern "C" int crimp_last_nufft_work(double* work, int32_t cap) {
-    for (int i = 0; i < 5 && i < cap; ++i) work[i] = g_nu_work[i];
-    return 5;
+    for (int i = 0; i < kNuCls && i < cap; ++i) work[i] = g_nu_work[i];
+    return kNuCls;
 }
 
 extern "C" int crimp_search(const double* t, int64_t n, double t0, const double* freq, int64_t nf,

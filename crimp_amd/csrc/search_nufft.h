@@ -264,7 +264,7 @@ __global__ __launch_bounds__(256) void k_nu_cellstart(const double* __restrict__
 // fp64 VALU throughout: per photon, row and harmonic one premultiplier phase and cis, then 3 operations per moment.
 // L > 1 spreads a cell's photons over several lanes when cells are dense (many photons per cell, few cells).
 constexpr int kNuGatherRows = 2;
-template <int R, bool TWOD, int L>
+template <int R, bool TWOD, int L, int PP>  // PP >= P moments accumulated unconditionally (no per-moment selects)
 __global__ __launch_bounds__(256) void k_nu_gather(const double* __restrict__ dt, const int64_t* __restrict__ start,
                                                    int64_t gmin, int64_t gmax, int64_t nfft, int64_t gbase,
                                                    int64_t gcount, double s1, double fch, double fcl,
@@ -278,11 +278,11 @@ __global__ __launch_bounds__(256) void k_nu_gather(const double* __restrict__ dt
     const int sub = (int)(tid % L);
     if (idx >= gcount) return;  // whole L-groups leave together (L divides 64); no barrier below
     const int64_t g = (gbase + idx) & (nfft - 1);  // the FFT's occupied rows only (nu_occupied)
-    double ar[R][kNuGatherMaxP], ai[R][kNuGatherMaxP];
+    double ar[R][PP], ai[R][PP];
 #pragma unroll
     for (int r = 0; r < R; ++r)
 #pragma unroll
-        for (int p = 0; p < kNuGatherMaxP; ++p) ar[r][p] = ai[r][p] = 0.0;
+        for (int p = 0; p < PP; ++p) ar[r][p] = ai[r][p] = 0.0;
     double c2[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) c2[r] = (TWOD && r < nrow) ? c2row[r] : 0.0;
@@ -290,10 +290,16 @@ __global__ __launch_bounds__(256) void k_nu_gather(const double* __restrict__ dt
     for (int64_t G = gmin + (((g - gmin) % nfft) + nfft) % nfft; G <= gmax; G += nfft) {
         const int64_t i0 = start[G - gmin], i1 = start[G - gmin + 1];
         const double Gd = (double)G;
-        double dn = i0 + sub < i1 ? dt[i0 + sub] : 0.0;  // one photon ahead
+        // photon times four iterations ahead (HBM latency is several iterations of one wave)
+        double dn[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) dn[q] = i0 + sub + q * L < i1 ? dt[i0 + sub + q * L] : 0.0;
         for (int64_t i = i0 + sub; i < i1; i += L) {
-            const double d = dn;
-            if (i + L < i1) dn = dt[i + L];
+            const double d = dn[0];
+            dn[0] = dn[1];
+            dn[1] = dn[2];
+            dn[2] = dn[3];
+            if (i + 4 * L < i1) dn[3] = dt[i + 4 * L];
             const double e = kd * (d * s1) - Gd;
             const double p1 = nu_frac_prod(fch, fcl, d);
             double d2 = 0.0, d2e = 0.0;
@@ -310,12 +316,10 @@ __global__ __launch_bounds__(256) void k_nu_gather(const double* __restrict__ dt
                     const double2 c = nu_cis(stab, nu_frac_k(kd, phi));
                     double ep = 1.0;
 #pragma unroll
-                    for (int p = 0; p < kNuGatherMaxP; ++p) {
-                        if (p < P) {
-                            ar[r][p] = fma(c.x, ep, ar[r][p]);
-                            ai[r][p] = fma(c.y, ep, ai[r][p]);
-                            ep *= e;
-                        }
+                    for (int p = 0; p < PP; ++p) {
+                        ar[r][p] = fma(c.x, ep, ar[r][p]);
+                        ai[r][p] = fma(c.y, ep, ai[r][p]);
+                        ep *= e;
                     }
                 }
             }
@@ -326,15 +330,15 @@ __global__ __launch_bounds__(256) void k_nu_gather(const double* __restrict__ dt
 #pragma unroll
         for (int r = 0; r < R; ++r)
 #pragma unroll
-            for (int p = 0; p < kNuGatherMaxP; ++p)
-                if (p < P) {
+            for (int p = 0; p < PP; ++p)
+                if (p < P) {  // uniform
                     ar[r][p] += __shfl_xor(ar[r][p], o);
                     ai[r][p] += __shfl_xor(ai[r][p], o);
                 }
 #pragma unroll
     for (int r = 0; r < R; ++r)
 #pragma unroll
-        for (int p = 0; p < kNuGatherMaxP; ++p)
+        for (int p = 0; p < PP; ++p)
             if (r < nrow && p < P && (p % L) == sub)
                 W[((int64_t)p * nrow + r) * nfft + g] = make_double2(ar[r][p], ai[r][p]);
 }
@@ -582,6 +586,46 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
             y[((int64_t)k1 << ln2) + b] = nu_cmul(nu_s[e], nu_tw(T, b * k1));
         }
     }
+}
+
+// k_nu_fft_cols for n1 = 256 (two radix-16 stages, 16 columns per block): the same arithmetic as the generic
+// kernel with stage 1 on the columns as loaded into registers (thread (j, cc): rows j + 16 r of column cc) and stage
+// 2's outputs (rows k1 = j + 16 r) twiddled and stored from registers: one LDS write and read instead of six.
+// The inter-pass twiddles are fetched before the barrier.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_nu_cols256(
+    const double2* __restrict__ X, double2* __restrict__ Y, int lnfft, NuTw T, int alo, int acnt) {
+    extern __shared__ double2 nu_s[];  // [256 rows][16 columns]
+    __shared__ NuTile tw;
+    nu_tile_init(&tw, 12);
+    const int ln2 = lnfft - 8;
+    const int64_t nfft = int64_t(1) << lnfft;
+    const int cc = threadIdx.x & 15, j = threadIdx.x >> 4;
+    const int64_t b = ((int64_t)blockIdx.x << 4) + cc;
+    const double2* x = X + (int64_t)blockIdx.y * nfft + b;
+    double2* y = Y + (int64_t)blockIdx.y * nfft + b;
+    double2 v[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {  // rows outside [alo, alo + acnt) (mod 256) hold no cell
+        const int a = j + 16 * r;
+        v[r] = ((a - alo) & 255) < acnt ? x[(int64_t)a << ln2] : make_double2(0.0, 0.0);
+    }
+    nu_dft16(v);  // stage 1 (Ns = 1)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) nu_s[((j << 4) + r) * 16 + cc] = v[r];
+    double2 wh[16], wl[16];  // w_n^{b k1}, k1 = j + 16 r, as the table pair nu_tw multiplies
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int64_t m = (b * (int64_t)(j + 16 * r)) & T.mask;
+        wh[r] = T.hi[m >> T.lbits];
+        wl[r] = T.lo[m & ((int64_t(1) << T.lbits) - 1)];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = nu_s[(j + 16 * r) * 16 + cc];
+    nu_twiddle<16>(nu_tw_tile(&tw, j << 4), v);  // w_256^{j r}
+    nu_dft16(v);                                 // stage 2 (Ns = 16): output rows k1 = j + 16 r
+#pragma unroll
+    for (int r = 0; r < 16; ++r) y[(int64_t)(j + 16 * r) << ln2] = nu_cmul(v[r], nu_cmul(wh[r], wl[r]));
 }
 
 // pass 2 (or the only pass): DFT of 2^lr contiguous rows of length 2^ll each, in place
@@ -842,9 +886,12 @@ static int g_last_search_path = 0;  // crimp_last_search_path(): 0 fp64 direct, 
 static int64_t g_last_nufft_n = 0;   // crimp_last_nufft_plan(): the last NUFFT's largest FFT length, its moments,
 static int g_last_nufft_p = 0;       // and its spread form (1 cell gather, 0 MFMA slots)
 static int g_last_nufft_gather = 0;
-// crimp_last_nufft_work(): the last NUFFT's algorithmic work per kernel class -- spread fp64 flops, spread HBM bytes,
-// merge bytes, FFT bytes (pass 2 fused with the Horner combine included), combine + finalize bytes
-static double g_nu_work[5] = {0, 0, 0, 0, 0};
+// Kernel classes of a NUFFT search (timed spans and work counts): cell starts, spread (cell gather or MFMA slots),
+// merge, FFT pass 1 (columns), FFT pass 2 (rows, with the Horner sum when fused), the separate Horner sum, finalize.
+enum { kNuClsCellStart, kNuClsSpread, kNuClsMerge, kNuClsPass1, kNuClsPass2, kNuClsCombine, kNuClsFinalize, kNuCls };
+// crimp_last_nufft_work(): the last NUFFT's algorithmic work -- [0] spread fp64 flops, then HBM bytes per class 1..6
+// ([1] the spread's bytes; class 0, the cell starts, is not counted)
+static double g_nu_work[kNuCls] = {0, 0, 0, 0, 0, 0, 0};
 
 static double nu_trunc(double x, int P, double* invfact) {  // x^P / P!
     double f = 1.0, xp = 1.0;
@@ -940,14 +987,21 @@ static void launch_gather_r(int L, int64_t gcount, const double* dt, const int64
                             int64_t nfft, int64_t gbase, double s1, double fch, double fcl, const double* c2, int nrow,
                             int k, int P, const double2* tab, double2* W, hipStream_t s) {
     const dim3 grid((unsigned)cdiv(gcount * L, 256));
-#define NU_GATHER(LL) k_nu_gather<R, TWOD, LL><<<grid, 256, 0, s>>>(dt, start, gmin, gmax, nfft, gbase, gcount, s1, \
-                                                                     fch, fcl, c2, nrow, k, P, tab, W)
-    switch (L) {
-        case 8: NU_GATHER(8); break;
-        case 4: NU_GATHER(4); break;
-        case 2: NU_GATHER(2); break;
-        default: NU_GATHER(1); break;
+#define NU_GATHER(LL, PPP) k_nu_gather<R, TWOD, LL, PPP><<<grid, 256, 0, s>>>(dt, start, gmin, gmax, nfft, gbase, \
+                                                                              gcount, s1, fch, fcl, c2, nrow, k, P, tab, W)
+#define NU_GATHER_L(PPP)              \
+    switch (L) {                      \
+        case 8: NU_GATHER(8, PPP); break; \
+        case 4: NU_GATHER(4, PPP); break; \
+        case 2: NU_GATHER(2, PPP); break; \
+        default: NU_GATHER(1, PPP); break; \
     }
+    if (P <= 16) {
+        NU_GATHER_L(16)
+    } else {
+        NU_GATHER_L(kNuGatherMaxP)
+    }
+#undef NU_GATHER_L
 #undef NU_GATHER
 }
 static void launch_gather(int L, bool twod, int64_t gcount, const double* dt, const int64_t* start, int64_t gmin,
@@ -1119,7 +1173,8 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* dt, const doub
     // pass 2 fused with the combine (default); CRIMP_NUFFT_FUSED=0 runs them as two kernels (A/B hook)
     const char* fused_env = getenv("CRIMP_NUFFT_FUSED");
     const bool fused_combine = !(fused_env && !strcmp(fused_env, "0"));
-    // CRIMP_NUFFT_ROWS4096=0 runs 4096-element rows through the generic fused kernel (A/B and identity test hook)
+    // CRIMP_NUFFT_ROWS4096=0 runs 4096-element rows and 256-element columns through the generic kernels (A/B and
+    // identity test hook)
     const char* r4_env = getenv("CRIMP_NUFFT_ROWS4096");
     const bool rows4096 = !(r4_env && !strcmp(r4_env, "0"));
     {  // 128 KB of dynamic LDS for k_nu_rows4096_combine, set once per device
@@ -1190,9 +1245,9 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* dt, const doub
     }
     size_t ipass = 0;
     const size_t lds_fft = (size_t)kNuTile * sizeof(double2);
-    // timed spans (CRIMP_FLAG_TIME_KERNELS): the whole pipeline, then spread / merge / fft / combine+finalize sums
+    // timed spans (CRIMP_FLAG_TIME_KERNELS): the whole pipeline, then each kernel class's sum and launch count
     std::vector<hipEvent_t> ev;
-    std::vector<int> evcls;  // class of the span ending at each mark: 0 spread, 1 merge, 2 fft, 3 combine/finalize
+    std::vector<int> evcls;  // class of the span ending at each mark (kNuCls*)
     auto mark = [&]() -> hipError_t {
         if (!timed) return hipSuccess;
         hipEvent_t e = nullptr;
@@ -1236,48 +1291,55 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* dt, const doub
             if (ln1 > 0) {
                 int alo = 0, acnt = 0;
                 occupied(k, &alo, &acnt);
-                g_nu_work[3] += plane * ((double)acnt / (double)(int64_t(1) << ln1)) + plane;  // occupied rows in, all out
-                k_nu_fft_cols<<<dim3((unsigned)(int64_t(1) << (ln2 - lcol)), (unsigned)Bp), 256, lds_fft, s>>>(
-                    W, Y, lnfft, ln1, lcol, T, alo, acnt);
-                HIPCHK(hipGetLastError());
+                g_nu_work[kNuClsPass1] += plane * ((double)acnt / (double)(int64_t(1) << ln1)) + plane;  // occupied rows in, all out
+                if (ln1 == 8 && rows4096) {
+                    k_nu_cols256<<<dim3((unsigned)(int64_t(1) << (ln2 - 4)), (unsigned)Bp), 256, lds_fft, s>>>(
+                        W, Y, lnfft, T, alo, acnt);
+                    HIPCHK(hipGetLastError());
+                } else {
+                    k_nu_fft_cols<<<dim3((unsigned)(int64_t(1) << (ln2 - lcol)), (unsigned)Bp), 256, lds_fft, s>>>(
+                        W, Y, lnfft, ln1, lcol, T, alo, acnt);
+                    HIPCHK(hipGetLastError());
+                }
                 Zo = Y;
+                HIPCHK(span(kNuClsPass1));
             }
             if (fused_combine && ln2 == 12 && rows4096) {  // the specialised form for 4096-element rows
-                g_nu_work[3] += plane + 16.0 * (double)nbt;
+                g_nu_work[kNuClsPass2] += plane + 16.0 * (double)nbt;
                 k_nu_rows4096_combine<<<dim3((unsigned)(int64_t(1) << ln1), (unsigned)nrow), 256, 2 * lds_fft, s>>>(
                     Zo, lnfft, P, nrow, nf, pl.nseg - 1 - pl.h, pl.h, rb * nf + jbase - (tb0 + first), nbt,
                     CS + (int64_t)(k - 1) * nbt);
                 HIPCHK(hipGetLastError());
-                HIPCHK(span(2));
+                HIPCHK(span(kNuClsPass2));
                 return CRIMP_OK;
             }
-            if (fused_combine) {  // pass 2 and the moments' Horner sum in one kernel (FFT span)
-                g_nu_work[3] += plane + 16.0 * (double)nbt;
+            if (fused_combine) {  // pass 2 and the moments' Horner sum in one kernel
+                g_nu_work[kNuClsPass2] += plane + 16.0 * (double)nbt;
                 k_nu_fft_rows_combine<<<dim3((unsigned)(int64_t(1) << ln1), (unsigned)nrow), 256, lds_fft, s>>>(
                     Zo, ln2, lnfft, P, nrow, nf, pl.nseg - 1 - pl.h, pl.h, rb * nf + jbase - (tb0 + first), nbt,
                     CS + (int64_t)(k - 1) * nbt);
                 HIPCHK(hipGetLastError());
-                HIPCHK(span(2));
+                HIPCHK(span(kNuClsPass2));
                 return CRIMP_OK;
             }
-            g_nu_work[3] += 2.0 * plane;
-            g_nu_work[4] += plane + 16.0 * (double)nbt;
+            g_nu_work[kNuClsPass2] += 2.0 * plane;
+            g_nu_work[kNuClsCombine] += plane + 16.0 * (double)nbt;
             k_nu_fft_rows<<<(unsigned)cdiv(Bp << ln1, int64_t(1) << lrow), 256, lds_fft, s>>>(Zo, ln2, lrow, lnfft);
             HIPCHK(hipGetLastError());
-            HIPCHK(span(2));
+            HIPCHK(span(kNuClsPass2));
             k_nu_combine<<<dim3((unsigned)cdiv(nfft, 256), (unsigned)nrow), 256, 0, s>>>(
                 Zo, lnfft, ln1, P, nrow, nf, pl.nseg, pl.h, jbase, rb, tb0 + first, nbt, CS + (int64_t)(k - 1) * nbt);
             HIPCHK(hipGetLastError());
-            HIPCHK(span(3));
+            HIPCHK(span(kNuClsCombine));
             return CRIMP_OK;
         };
         auto finalize = [&](int64_t tb0, int64_t nbt) -> int {
-            g_nu_work[4] += 16.0 * (double)nharm * (double)nbt + 8.0 * (double)nbt;
+            g_nu_work[kNuClsFinalize] += 16.0 * (double)nharm * (double)nbt + 8.0 * (double)nbt;
             k_nu_finalize<<<(unsigned)cdiv(nbt, 256), 256, 0, s>>>(CS, nbt, nharm, stat, (double)n, nf, jbase, nfft, P,
                                                                    pl.invfact, fixup_rel(), tb0, first, out, nflag,
                                                                    flagged);
             HIPCHK(hipGetLastError());
-            HIPCHK(span(3));
+            HIPCHK(span(kNuClsFinalize));
             return CRIMP_OK;
         };
         if (use_gather(pl)) {
@@ -1291,7 +1353,7 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* dt, const doub
                 HIPCHK(hipGetLastError());
                 off += spank + 1;
             }
-            HIPCHK(span(0));
+            HIPCHK(span(kNuClsCellStart));
             for (int64_t rb = pl.r0; rb < pl.r1; rb += kNuGatherRows) {
                 const int nrow = (int)std::min<int64_t>(kNuGatherRows, pl.r1 - rb);
                 const int64_t tb0 = std::max<int64_t>(first, rb * nf) - first;
@@ -1309,12 +1371,12 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* dt, const doub
                     if (lanes_env > 0) L = lanes_env;  // test hook: CRIMP_NUFFT_LANES=1|2|4|8
                     // per photon and row: premultiplier phase + cis ~ 40 flops, then 2 FMA + 1 multiply per moment
                     g_nu_work[0] += (40.0 + 5.0 * P) * (double)n * nrow;
-                    g_nu_work[1] += 8.0 * (double)n + 16.0 * (double)P * nrow * (double)gcount;
+                    g_nu_work[kNuClsSpread] += 8.0 * (double)n + 16.0 * (double)P * nrow * (double)gcount;
                     launch_gather(L, twod, gcount, dt, cstart + soff[(size_t)(k - 1)], pl.gmin[(size_t)(k - 1)],
                                   pl.gmax[(size_t)(k - 1)], nfft, gbase, pl.s1, pl.fch, pl.fcl,
                                   twod ? c2 + rb : nullptr, nrow, k, P, cis, W, s);
                     HIPCHK(hipGetLastError());
-                    HIPCHK(span(0));
+                    HIPCHK(span(kNuClsSpread));
                     int rc = fft_combine(k, rb, nrow, tb0, nbt);
                     if (rc) return rc;
                 }
@@ -1336,9 +1398,9 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* dt, const doub
                 dim3 grid((unsigned)cdiv(nchunk, kNuWaves));
                 // issued: one 16x16x4 f64 MFMA (2048 flops) per 4 photons and harmonic; slots written
                 g_nu_work[0] += 512.0 * (double)n * gl;
-                g_nu_work[1] += 8.0 * (double)n;
+                g_nu_work[kNuClsSpread] += 8.0 * (double)n;
                 for (int kk = 0; kk < gl; ++kk)
-                    g_nu_work[1] += 8.0 * (double)SL *
+                    g_nu_work[kNuClsSpread] += 8.0 * (double)SL *
                                     (double)(pl.gmax[(size_t)(k0 + kk - 1)] - ps.gmin[kk] + 1 + nchunk);
                 if (twod)
                     nu_launch_spread<true>(gl, grid, s, dt, n, nchunk, pl.s1, pl.fch, pl.fcl, c2 + rb, nrow, k0, P, dp, cis,
@@ -1347,19 +1409,19 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* dt, const doub
                     nu_launch_spread<false>(gl, grid, s, dt, n, nchunk, pl.s1, pl.fch, pl.fcl, c2 + rb, nrow, k0, P, dp,
                                             cis, U, ctab);
                 HIPCHK(hipGetLastError());
-                HIPCHK(span(0));
+                HIPCHK(span(kNuClsSpread));
                 for (int kk = 0; kk < gl && k0 + kk <= nharm; ++kk) {
                     const int k = k0 + kk;
                     int alo = 0, acnt = 0;
                     occupied(k, &alo, &acnt);
                     const int64_t gbase = (int64_t)alo << ln2, gcount = (int64_t)acnt << ln2;
-                    g_nu_work[2] += 8.0 * (double)SL * (double)(pl.gmax[(size_t)(k - 1)] - ps.gmin[kk] + 1 + nchunk) +
+                    g_nu_work[kNuClsMerge] += 8.0 * (double)SL * (double)(pl.gmax[(size_t)(k - 1)] - ps.gmin[kk] + 1 + nchunk) +
                                     16.0 * (double)P * nrow * (double)gcount;
                     k_nu_merge<<<(unsigned)cdiv(gcount, kNuMergeG), 256, (size_t)kNuMergeG * SL * sizeof(double), s>>>(
                         U + ps.ubase[kk], SL, ctab + 2 * kk * nchunk, nchunk, ps.gmin[kk], pl.gmax[(size_t)(k - 1)],
                         nfft, gbase, gcount, W);
                     HIPCHK(hipGetLastError());
-                    HIPCHK(span(1));
+                    HIPCHK(span(kNuClsMerge));
                     int rc = fft_combine(k, rb, nrow, tb0, nbt);
                     if (rc) return rc;
                 }
@@ -1371,17 +1433,20 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* dt, const doub
     if (timed) {
         HIPCHK(hipEventSynchronize(ev.back()));
         float tot = 0.0f;
-        double cls[4] = {0, 0, 0, 0};
+        double cls[kNuCls] = {0, 0, 0, 0, 0, 0, 0}, cnt[kNuCls] = {0, 0, 0, 0, 0, 0, 0};
         HIPCHK(hipEventElapsedTime(&tot, ev.front(), ev.back()));
         for (size_t i = 1; i < ev.size(); ++i) {
             float ms = 0.0f;
             HIPCHK(hipEventElapsedTime(&ms, ev[i - 1], ev[i]));
             cls[evcls[i - 1]] += ms;
+            cnt[evcls[i - 1]] += 1.0;  // launches: one per span except the cell starts (one span per nharm launches)
         }
+        cnt[kNuClsCellStart] *= nharm;
         for (hipEvent_t e : ev) (void)hipEventDestroy(e);
         if (g_kernel_times.empty()) g_last_kernel_ms = tot;
-        g_kernel_times.push_back(tot);
+        g_kernel_times.push_back(tot);  // then the classes' ms, then their launch counts
         for (double v : cls) g_kernel_times.push_back(v);
+        for (double v : cnt) g_kernel_times.push_back(v);
     }
     int nf_h = 0;
     HIPCHK(d2h(s, &nf_h, nflag, sizeof(int)));

@@ -39,12 +39,13 @@ def _device_for_backend(dist):
     return torch.device("cpu")
 
 
-def _gpu_slice(time, t0, freq, nharm, stat, freq_dot, first, count, flags=0):
+def _gpu_slice(time, t0, freq, nharm, stat, freq_dot, first, count, flags=0, precision=None):
     from . import ops
     import torch
     if isinstance(time, torch.Tensor) and freq_dot is not None and not isinstance(freq_dot, torch.Tensor):
         freq_dot = torch.as_tensor(np.asarray(freq_dot, dtype=np.float64), device=time.device)
-    return ops.search(time, t0, freq, nharm, stat, log10_negfdot=freq_dot, first=first, count=count, flags=flags)
+    return ops.search(time, t0, freq, nharm, stat, log10_negfdot=freq_dot, first=first, count=count, flags=flags,
+                      precision=precision)
 
 
 def _as_comm(local, dev):
@@ -56,18 +57,19 @@ def _as_comm(local, dev):
     return torch.as_tensor(np.asarray(local), dtype=torch.float64, device=dev)
 
 
-def sharded_search(time, freq, nharm=2, stat=0, freq_dot=None, gather="all", compute=None, flags=0):
+def sharded_search(time, freq, nharm=2, stat=0, freq_dot=None, gather="all", compute=None, flags=0, precision=None):
     """Z^2 (stat=0) / H (stat=1) over the fd-outer grid, sharded across the process group.
 
     Returns the full power array (gather='all'; a tensor on the rank's device when ``time`` is a device
     tensor, else a numpy array) or ``(best_power, best_flat_index)`` (gather='best'), identical on every rank.
     With the nccl backend the gather runs on the device buffers the search wrote (no host staging).
-    ``flags`` go to the rank's crimp_search call (e.g. FLAG_TIME_KERNELS for bench.py).
+    ``flags`` and ``precision`` (None | "exact" | "nufft" | "f64", as PeriodSearch) go to the rank's crimp_search
+    call (e.g. FLAG_TIME_KERNELS for bench.py).
     """
     import functools
     import torch
     dist, world, rank = _dist()
-    compute = compute or functools.partial(_gpu_slice, flags=flags)
+    compute = compute or functools.partial(_gpu_slice, flags=flags, precision=precision)
     as_tensor = isinstance(time, torch.Tensor)
     if as_tensor:
         t0 = float((time[0] + time[-1]).item()) / 2

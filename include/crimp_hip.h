@@ -104,15 +104,16 @@ int crimp_last_kernel_times(double* ms, int32_t cap);
 /* Trials of the last crimp_search (default precision) whose power was recomputed by the fp64 fix-up. */
 int64_t crimp_last_fixups(void);
 /* Kernel family of the last crimp_search: 0 fp64 direct, 1 exact i8 MFMA, 2 NUFFT. With
- * CRIMP_FLAG_TIME_KERNELS a NUFFT search's crimp_last_kernel_times are: the whole pipeline, then its spread, merge,
- * FFT and combine + finalize kernels (sums). Measurement hook for tests and bench.py, not in the reference. */
+ * CRIMP_FLAG_TIME_KERNELS a NUFFT search's crimp_last_kernel_times are: the whole pipeline, then the summed ms of its
+ * seven kernel classes (cell starts, spread, merge, FFT pass 1, FFT pass 2, Horner sum, finalize), then their launch
+ * counts. Measurement hook for tests and bench.py, not in the reference. */
 int crimp_last_search_path(void);
 /* The plan of the last NUFFT search: its (largest) FFT length n, moments P, and spread form (1 = cell gather, one lane
  * per wrapped cell on the VALU; 0 = MFMA slots). Measurement hook for bench.py, not in the reference. */
 int crimp_last_nufft_plan(int64_t* fft_length, int32_t* moments, int32_t* gather);
-/* The last NUFFT search's algorithmic work per kernel class, up to cap of: spread fp64 flops, spread HBM bytes, merge
- * bytes, FFT bytes (pass 2 with the fused Horner combine), combine + finalize bytes; returns 5. For bench.py's
- * rooflines, not in the reference. */
+/* The last NUFFT search's algorithmic work, up to cap of: [0] the spread's fp64 flops, then HBM bytes of [1] the
+ * spread, [2] merge, [3] FFT pass 1, [4] FFT pass 2 (with the fused Horner sum), [5] the separate Horner sum, [6]
+ * finalize; returns 7. For bench.py's rooflines, not in the reference. */
 int crimp_last_nufft_work(double* work, int32_t cap);
 /* Brute-grid norms evaluated per phShift by the last crimp_toa_fit with CRIMP_TOA_BRUTE (the pruned candidates of
  * lmfit's 20-norm lattice, padded to 2, 4 or 20, less the lazy norms the eight-factor grid leaves out; 0 without a

@@ -159,8 +159,8 @@ def test_nufft_unsorted_photons_take_default_path(gpu):
 
 def test_nufft_fused_pass2_equals_separate_combine(gpu, monkeypatch):
     """FFT pass 2 fused with the moments' Horner sum (default) against pass 2 and k_nu_combine as two kernels
-    (CRIMP_NUFFT_FUSED=0), and the 4096-row kernel (k_nu_rows4096_combine) against the generic fused one
-    (CRIMP_NUFFT_ROWS4096=0): the same arithmetic, so bit-identical powers -- single-pass (n <= 4096) and four-step
+    (CRIMP_NUFFT_FUSED=0), and the 4096-row and 256-row-column kernels (k_nu_rows4096_combine, k_nu_cols256)
+    against the generic ones (CRIMP_NUFFT_ROWS4096=0): the same arithmetic, so bit-identical powers -- single-pass (n <= 4096) and four-step
     FFTs, 1-D and 2-D grids, both spread forms."""
     from crimp_amd import ops, _native as N
     from crimp_amd.synth import pulsed_events
@@ -168,7 +168,8 @@ def test_nufft_fused_pass2_equals_separate_combine(gpu, monkeypatch):
     t0 = (t[0] + t[-1]) / 2
     fd = np.array([-12.0, -11.0, -10.5])
     for f, m, fdv in ((3.3 + np.arange(-700, 701) / 2.0e6, 2, None), (3.3 + np.arange(-40000, 40000) / 2.0e6, 3, None),
-                      (3.3 + np.arange(-1500, 1500) / 2.0e6, 5, fd)):
+                      (3.3 + np.arange(-1500, 1500) / 2.0e6, 5, fd),
+                      (3.3 + np.arange(-300000, 300000) / 2.0e7, 2, None)):  # n = 2^20: 256-row columns
         a = ops.search(t, t0, f, m, 1, log10_negfdot=fdv, precision="nufft", flags=N.FLAG_NO_FIXUP)
         monkeypatch.setenv("CRIMP_NUFFT_FUSED", "0")
         b = ops.search(t, t0, f, m, 1, log10_negfdot=fdv, precision="nufft", flags=N.FLAG_NO_FIXUP)
