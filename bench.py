@@ -631,6 +631,7 @@ def main():
     f_h = f0 + (np.arange(world * M) - (world * M) // 2) * df
     t = torch.as_tensor(t_h, device=dev)
     f = torch.as_tensor(f_h, device=dev)
+    t0_h = (t_h[0] + t_h[-1]) / 2  # periodsearch.py:54 on the host copy (the device tensor holds the same values)
     from crimp_amd.sharding import sharded_search, shard_range
     assert shard_range(world * M, world, rank) == (rank * M, M)
 
@@ -641,7 +642,7 @@ def main():
         kms, fixups, bests = [], [], []
 
         def step():
-            b = sharded_search(t, f, a.nharm, 0, gather="best", flags=flags, precision=precision)
+            b = sharded_search(t, f, a.nharm, 0, gather="best", flags=flags, precision=precision, t0=t0_h)
             kms.append(N.load().crimp_last_kernel_ms())
             fixups.append(N.load().crimp_last_fixups())
             bests.append(b)

@@ -239,7 +239,25 @@ static hipError_t h2d_async(hipStream_t s, void* d, const void* h, size_t bytes)
     std::memcpy(q, h, bytes);
     return hipMemcpyAsync(d, q, bytes, hipMemcpyHostToDevice, s);
 }
+// Device -> host after the stream's queued work. Small reads (flags, counts, grid scalars: the routing readbacks
+// of a search) go through a page-locked per-thread buffer with one async copy and one stream sync: a blocking
+// pageable hipMemcpy of a few bytes after the sync cost ~30 us per readback (rocprofv3 sys-trace, profiles/r05).
 static hipError_t d2h(hipStream_t s, void* h, const void* d, size_t bytes) {
+    constexpr size_t kSmall = 4096;
+    thread_local void* pin = nullptr;
+    if (bytes <= kSmall) {
+        if (!pin && hipHostMalloc(&pin, kSmall, hipHostMallocDefault) != hipSuccess) {
+            (void)hipGetLastError();
+            pin = nullptr;
+        }
+        if (pin) {
+            hipError_t e = hipMemcpyAsync(pin, d, bytes, hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            if (e != hipSuccess) return e;
+            std::memcpy(h, pin, bytes);
+            return hipSuccess;
+        }
+    }
     hipError_t e = hipStreamSynchronize(s);
     if (e != hipSuccess) return e;
     return hipMemcpy(h, d, bytes, hipMemcpyDeviceToHost);
@@ -1698,19 +1716,35 @@ static int fixup_search(Scratch& sc, hipStream_t s, const double* dt, const doub
 }
 
 // Arithmetic-progression check of the (device) frequency grid: 16 ulp of max|f| (k_ap_check). Writes delta
-// into ap[0] on the device (read by the factorised kernels) and returns whether the grid qualifies.
-static int grid_is_progression(Scratch& sc, hipStream_t s, const double* freq, int64_t nf, double** ap, bool* ok) {
+// into ap[0] on the device (read by the factorised kernels) and returns whether the grid qualifies. With nu_dt
+// (a NUFFT search) the NUFFT's own checks -- photon order and the grid scalars (k_nu_sorted, k_nu_scalars) -- are
+// queued behind it and read back in the same transfer: nu_hs = [delta, f0, dt[0], dt[n-1], unsorted flag].
+static int grid_is_progression(Scratch& sc, hipStream_t s, const double* freq, int64_t nf, double** ap, bool* ok,
+                               const double* nu_t = nullptr, double t0 = 0.0, int64_t n = 0, double* nu_hs = nullptr);
+#include "search_nufft.h"
+static int grid_is_progression(Scratch& sc, hipStream_t s, const double* freq, int64_t nf, double** ap, bool* ok,
+                               const double* nu_t, double t0, int64_t n, double* nu_hs) {
     *ok = false;
     unsigned long long* info = nullptr;
-    HIPCHK(sc.alloc(&info, 3));
+    HIPCHK(sc.alloc(&info, 3 + 6));
     *ap = reinterpret_cast<double*>(info);
     if (nf < 2) return CRIMP_OK;
-    HIPCHK(hipMemsetAsync(info, 0, 3 * sizeof(unsigned long long), s));
+    HIPCHK(hipMemsetAsync(info, 0, (3 + 6) * sizeof(unsigned long long), s));
     k_ap_check<<<(unsigned)std::min<int64_t>(cdiv(nf, 256), 128), 256, 0, s>>>(freq, nf, info);
     HIPCHK(hipGetLastError());
-    double h[3];
-    HIPCHK(d2h(s, h, info, sizeof(h)));
+    double h[3 + 5];
+    size_t bytes = 3 * sizeof(double);
+    if (nu_t) {
+        double* dsc = reinterpret_cast<double*>(info + 3);
+        k_nu_sorted<<<(unsigned)std::min<int64_t>(cdiv(n, 256), 2048), 256, 0, s>>>(nu_t, t0, n,
+                                                                                  reinterpret_cast<int*>(dsc + 4));
+        k_nu_scalars<<<1, 64, 0, s>>>(*ap, freq, nu_t, t0, n, dsc);
+        HIPCHK(hipGetLastError());
+        bytes = sizeof(h);
+    }
+    HIPCHK(d2h(s, h, info, bytes));
     *ok = std::isfinite(h[0]) && h[0] != 0.0 && h[1] <= 16.0 * 2.220446049250313e-16 * h[2];
+    if (nu_t) std::memcpy(nu_hs, h + 3, 5 * sizeof(double));
     return CRIMP_OK;
 }
 
@@ -1864,8 +1898,6 @@ static int exact_search(Scratch& sc, hipStream_t s, const double* dt, const doub
     return fixup_search(sc, s, dt, dt2, n, freq, nf, c2, twod, nharm, stat, first, flagged, nf_h, out);
 }
 
-#include "search_nufft.h"
-
 extern "C" int crimp_last_search_path(void) { return g_last_search_path; }
 
 extern "C" int crimp_last_nufft_plan(int64_t* fft_length, int32_t* moments, int32_t* gather) {
@@ -1925,11 +1957,16 @@ extern "C" int crimp_search(const double* t, int64_t n, double t0, const double*
             HIPCHK(sc.alloc(&dc2, (size_t)nfd));
             HIPCHK(h2d(dc2, c2h.data(), nfd * sizeof(double)));
         }
+        // dt = t - t0 (and dt^2) for the exact / fp64 kernels; the NUFFT forms dt in its kernels and skips this
         double *ddt = nullptr, *ddt2 = nullptr;
-        HIPCHK(sc.alloc(&ddt, (size_t)n));
-        if (twod) HIPCHK(sc.alloc(&ddt2, (size_t)n));
-        k_search_prep<<<(int)std::min<int64_t>(cdiv(n, 256), 4096), 256, 0, s>>>(dtm, n, t0, ddt, ddt2);
-        HIPCHK(hipGetLastError());
+        auto prep = [&]() -> hipError_t {
+            hipError_t e = sc.alloc(&ddt, (size_t)n);
+            if (e == hipSuccess && twod) e = sc.alloc(&ddt2, (size_t)n);
+            if (e != hipSuccess) return e;
+            k_search_prep<<<(int)std::min<int64_t>(cdiv(n, 256), 4096), 256, 0, s>>>(dtm, n, t0, ddt, ddt2);
+            return hipGetLastError();
+        };
+        if (!nufft) HIPCHK(prep());
 
         // Routing by properties of the whole grid (not of this call's trial range), so that every shard of a
         // sharded search takes the kernel an unsharded search takes:
@@ -1941,9 +1978,10 @@ extern "C" int crimp_search(const double* t, int64_t n, double t0, const double*
         KernelTimer kt(s, flags & CRIMP_FLAG_TIME_KERNELS);
         bool factorised = !f64 && (nf >= 256 || (flags & CRIMP_FLAG_FORCE_MFMA) || (nufft && nf >= 64));
         double* ap = nullptr;
+        double nu_hs[5] = {0, 0, 0, 0, 0};
         if (factorised) {
             bool ok = false;
-            int rc = grid_is_progression(sc, s, dfr, nf, &ap, &ok);
+            int rc = grid_is_progression(sc, s, dfr, nf, &ap, &ok, nufft ? dtm : nullptr, t0, n, nu_hs);
             if (rc) return rc;
             factorised = ok;
         }
@@ -1953,11 +1991,12 @@ extern "C" int crimp_search(const double* t, int64_t n, double t0, const double*
         bool done = false;
         if (factorised && nufft) {  // NUFFT; unsorted photons or an out-of-range plan fall through to the exact path
             int64_t nfix = 0;
-            rc = nufft_search(sc, s, ddt, ddt2, n, dfr, nf, twod ? nfd : 1, dc2, ap, twod, nharm, stat, first, count, dout,
-                              flags & CRIMP_FLAG_TIME_KERNELS, &nfix, (flags & CRIMP_FLAG_NO_FIXUP) != 0, &done);
+            rc = nufft_search(sc, s, dtm, t0, n, dfr, nf, twod ? nfd : 1, dc2, nu_hs, twod, nharm, stat, first, count,
+                              dout, flags & CRIMP_FLAG_TIME_KERNELS, &nfix, (flags & CRIMP_FLAG_NO_FIXUP) != 0, &done);
             if (rc) return rc;
             if (done) g_last_fixups = nfix;
         }
+        if (nufft && !done) HIPCHK(prep());  // the NUFFT did not apply: the default path's kernels read dt
         if (done) {
         } else if (factorised) {
             g_last_search_path = 1;

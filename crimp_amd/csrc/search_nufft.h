@@ -116,28 +116,28 @@ __device__ __forceinline__ int64_t nu_readlane64(int64_t v, int lane) {
 }
 
 // sortedness of dt (the spread's cells only grow along a chunk)
-__global__ __launch_bounds__(256) void k_nu_sorted(const double* __restrict__ dt, int64_t n, int* __restrict__ bad) {
+__global__ __launch_bounds__(256) void k_nu_sorted(const double* __restrict__ tt, double t0, int64_t n, int* __restrict__ bad) {
     int b = 0;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i + 1 < n; i += (int64_t)gridDim.x * blockDim.x)
-        b |= !(dt[i] <= dt[i + 1]);
+        b |= !((tt[i] - t0) <= (tt[i + 1] - t0));
     if (__any(b) && (threadIdx.x & 63) == 0) atomicOr(bad, 1);
 }
 
 // host-side scalars of the plan in one read-back: delta, f_0, dt[0], dt[n-1]
 __global__ void k_nu_scalars(const double* __restrict__ ap, const double* __restrict__ freq,
-                             const double* __restrict__ dt, int64_t n, double* __restrict__ out) {
+                             const double* __restrict__ tt, double t0, int64_t n, double* __restrict__ out) {
     if (threadIdx.x == 0) {
         out[0] = ap[0];
         out[1] = freq[0];
-        out[2] = dt[0];
-        out[3] = dt[n - 1];
+        out[2] = (tt[0] - t0);
+        out[3] = (tt[n - 1] - t0);
     }
 }
 
 // Moments of harmonics k0 .. k0+G-1 for rows [0, nrow) of the pass (c2row points at the pass's first row).
 // Lane l: photon q = l >> 4 of the K-group, A row (moment) p = l & 15, B column col = l & 15 = 2 row + (re/im).
 template <int G, bool TWOD>
-__global__ __launch_bounds__(256) void k_nu_spread(const double* __restrict__ dt, int64_t n, int64_t nchunk, double s1,
+__global__ __launch_bounds__(256) void k_nu_spread(const double* __restrict__ tt, double t0, int64_t n, int64_t nchunk, double s1,
                                                    double fch, double fcl, const double* __restrict__ c2row, int nrow,
                                                    int k0, int P, const NuPass* __restrict__ ps,
                                                    const double2* __restrict__ tab, double* __restrict__ U,
@@ -153,7 +153,7 @@ __global__ __launch_bounds__(256) void k_nu_spread(const double* __restrict__ dt
     nu_f64x4 acc[G];
     int64_t gcur[G];
     {
-        const double u1 = dt[i0] * s1;
+        const double u1 = (tt[i0] - t0) * s1;
 #pragma unroll
         for (int kk = 0; kk < G; ++kk) {
             acc[kk] = nu_f64x4{0.0, 0.0, 0.0, 0.0};
@@ -185,7 +185,7 @@ __global__ __launch_bounds__(256) void k_nu_spread(const double* __restrict__ dt
     };
     for (int64_t ib = i0; ib < i1; ib += 64) {
         const int64_t il = ib + lane;
-        const double dv = dt[il < n ? il : n - 1];  // past the end: the last photon's time (same cell, zero weight)
+        const double dv = (tt[il < n ? il : n - 1] - t0);  // past the end: the last photon's time (same cell, zero weight)
 #pragma unroll 1
         for (int g = 0; g < 16; ++g) {
             if (ib + 4 * g >= i1) break;  // wave-uniform
@@ -247,13 +247,27 @@ __global__ __launch_bounds__(256) void k_nu_spread(const double* __restrict__ dt
 // ---- cell-gather spread (a pass of <= kNuGatherRows rows, one harmonic): one lane per wrapped cell ----
 // start[G - gmin] = the first photon whose cell (rint(k (dt s1)), the spread's arithmetic) is >= G, for the
 // unwrapped cells G in [gmin, gmax + 1]; photons are time-sorted, so cell G holds photons [start[G], start[G+1]).
-__global__ __launch_bounds__(256) void k_nu_cellstart(const double* __restrict__ dt, int64_t n, double s1, int k,
-                                                      int64_t gmin, int64_t span, int64_t* __restrict__ start) {
+// Up to kNuCellK harmonics k0 .. k0+nk-1 per launch (one read of the photon times): harmonic k0 + j writes its
+// table at start + off[j] for cells gmin[j] .. gmin[j] + span[j] - 1.
+constexpr int kNuCellK = 4;
+struct NuCellArgs {
+    int64_t gmin[kNuCellK], span[kNuCellK], off[kNuCellK];
+};
+__global__ __launch_bounds__(256) void k_nu_cellstart(const double* __restrict__ tt, double t0, int64_t n, double s1,
+                                                      int k0, int nk, NuCellArgs a, int64_t* __restrict__ start) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t g = (int64_t)rint((double)k * (dt[i] * s1));
-        const int64_t gp = i == 0 ? gmin - 1 : (int64_t)rint((double)k * (dt[i - 1] * s1));
-        for (int64_t G = gp + 1; G <= g; ++G) start[G - gmin] = i;
-        if (i == n - 1) start[span] = n;
+        const double u = (tt[i] - t0) * s1;
+        const double up = i == 0 ? 0.0 : (tt[i - 1] - t0) * s1;
+#pragma unroll
+        for (int j = 0; j < kNuCellK; ++j) {
+            if (j >= nk) break;
+            const double kd = (double)(k0 + j);
+            const int64_t g = (int64_t)rint(kd * u);
+            const int64_t gp = i == 0 ? a.gmin[j] - 1 : (int64_t)rint(kd * up);
+            int64_t* st = start + a.off[j];
+            for (int64_t G = gp + 1; G <= g; ++G) st[G - a.gmin[j]] = i;
+            if (i == n - 1) st[a.span[j]] = n;
+        }
     }
 }
 
@@ -265,7 +279,7 @@ __global__ __launch_bounds__(256) void k_nu_cellstart(const double* __restrict__
 // L > 1 spreads a cell's photons over several lanes when cells are dense (many photons per cell, few cells).
 constexpr int kNuGatherRows = 2;
 template <int R, bool TWOD, int L, int PP>  // PP >= P moments accumulated unconditionally (no per-moment selects)
-__global__ __launch_bounds__(256) void k_nu_gather(const double* __restrict__ dt, const int64_t* __restrict__ start,
+__global__ __launch_bounds__(256) void k_nu_gather(const double* __restrict__ tt, double t0, const int64_t* __restrict__ start,
                                                    int64_t gmin, int64_t gmax, int64_t nfft, int64_t gbase,
                                                    int64_t gcount, double s1, double fch, double fcl,
                                                    const double* __restrict__ c2row, int nrow, int k, int P,
@@ -293,13 +307,13 @@ __global__ __launch_bounds__(256) void k_nu_gather(const double* __restrict__ dt
         // photon times four iterations ahead (HBM latency is several iterations of one wave)
         double dn[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) dn[q] = i0 + sub + q * L < i1 ? dt[i0 + sub + q * L] : 0.0;
+        for (int q = 0; q < 4; ++q) dn[q] = i0 + sub + q * L < i1 ? (tt[i0 + sub + q * L] - t0) : 0.0;
         for (int64_t i = i0 + sub; i < i1; i += L) {
             const double d = dn[0];
             dn[0] = dn[1];
             dn[1] = dn[2];
             dn[2] = dn[3];
-            if (i + 4 * L < i1) dn[3] = dt[i + 4 * L];
+            if (i + 4 * L < i1) dn[3] = (tt[i + 4 * L] - t0);
             const double e = kd * (d * s1) - Gd;
             const double p1 = nu_frac_prod(fch, fcl, d);
             double d2 = 0.0, d2e = 0.0;
@@ -973,21 +987,24 @@ static void nu_occupied(int64_t gmin, int64_t gmax, int lnfft, int ln1, int* alo
 }
 
 template <bool TWOD>
-static void nu_launch_spread(int G, dim3 grid, hipStream_t s, const double* dt, int64_t n, int64_t nchunk, double s1,
+static void nu_launch_spread(int G, dim3 grid, hipStream_t s, const double* tt, double t0, int64_t n, int64_t nchunk,
+                             double s1,
                              double fch, double fcl, const double* c2, int nrow, int k0, int P, const NuPass* ps,
                              const double2* tab, double* U, int64_t* ctab) {
-#define CRIMP_NS(GG) k_nu_spread<GG, TWOD><<<grid, 256, 0, s>>>(dt, n, nchunk, s1, fch, fcl, c2, nrow, k0, P, ps, tab, U, ctab)
+#define CRIMP_NS(GG) \
+    k_nu_spread<GG, TWOD><<<grid, 256, 0, s>>>(tt, t0, n, nchunk, s1, fch, fcl, c2, nrow, k0, P, ps, tab, U, ctab)
     if (G == 8) CRIMP_NS(8); else if (G == 4) CRIMP_NS(4); else CRIMP_NS(2);
 #undef CRIMP_NS
 }
 
 // Budget of the NUFFT path's device buffers (CRIMP_NUFFT_BUDGET_MB, default 6144): slots, FFT ping-pong, sums.
 template <int R, bool TWOD>
-static void launch_gather_r(int L, int64_t gcount, const double* dt, const int64_t* start, int64_t gmin, int64_t gmax,
+static void launch_gather_r(int L, int64_t gcount, const double* tt, double t0, const int64_t* start, int64_t gmin,
+                            int64_t gmax,
                             int64_t nfft, int64_t gbase, double s1, double fch, double fcl, const double* c2, int nrow,
                             int k, int P, const double2* tab, double2* W, hipStream_t s) {
     const dim3 grid((unsigned)cdiv(gcount * L, 256));
-#define NU_GATHER(LL, PPP) k_nu_gather<R, TWOD, LL, PPP><<<grid, 256, 0, s>>>(dt, start, gmin, gmax, nfft, gbase, \
+#define NU_GATHER(LL, PPP) k_nu_gather<R, TWOD, LL, PPP><<<grid, 256, 0, s>>>(tt, t0, start, gmin, gmax, nfft, gbase, \
                                                                               gcount, s1, fch, fcl, c2, nrow, k, P, tab, W)
 #define NU_GATHER_L(PPP)              \
     switch (L) {                      \
@@ -998,20 +1015,23 @@ static void launch_gather_r(int L, int64_t gcount, const double* dt, const int64
     }
     if (P <= 16) {
         NU_GATHER_L(16)
+    } else if (P <= 20) {
+        NU_GATHER_L(20)
     } else {
         NU_GATHER_L(kNuGatherMaxP)
     }
 #undef NU_GATHER_L
 #undef NU_GATHER
 }
-static void launch_gather(int L, bool twod, int64_t gcount, const double* dt, const int64_t* start, int64_t gmin,
+static void launch_gather(int L, bool twod, int64_t gcount, const double* tt, double t0, const int64_t* start,
+                          int64_t gmin,
                           int64_t gmax, int64_t nfft, int64_t gbase, double s1, double fch, double fcl,
                           const double* c2, int nrow, int k, int P, const double2* tab, double2* W, hipStream_t s) {
     if (twod)
-        launch_gather_r<kNuGatherRows, true>(L, gcount, dt, start, gmin, gmax, nfft, gbase, s1, fch, fcl, c2, nrow, k,
+        launch_gather_r<kNuGatherRows, true>(L, gcount, tt, t0, start, gmin, gmax, nfft, gbase, s1, fch, fcl, c2, nrow, k,
                                              P, tab, W, s);
     else
-        launch_gather_r<1, false>(L, gcount, dt, start, gmin, gmax, nfft, gbase, s1, fch, fcl, c2, nrow, k, P, tab, W,
+        launch_gather_r<1, false>(L, gcount, tt, t0, start, gmin, gmax, nfft, gbase, s1, fch, fcl, c2, nrow, k, P, tab, W,
                                   s);
 }
 
@@ -1082,21 +1102,15 @@ static bool nu_plan(NuPlan* pl, double delta, double f0, double dt0, double dtn,
 // Z^2 / H by NUFFT over trials [first, first + count) of the fd-outer grid (nf trials per row, arithmetic
 // progression with step ap[0]). *applicable = false (nothing computed) for unsorted photons or an out-of-range plan:
 // the caller takes the exact path.
-static int nufft_search(Scratch& sc, hipStream_t s, const double* dt, const double* dt2, int64_t n, const double* freq,
-                        int64_t nf, int64_t nrows_grid, const double* c2, const double* ap, bool twod, int nharm,
+// hs: [delta, f0, dt[0], dt[n-1], unsorted flag (int bits)] as grid_is_progression read them back.
+// t: photon times (seconds), t0 the search's reference time: the kernels form dt = t - t0 as k_search_prep does;
+// dt (and dt^2) arrays are made only for a fix-up.
+static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, int64_t n, const double* freq,
+                        int64_t nf, int64_t nrows_grid, const double* c2, const double* hs, bool twod, int nharm,
                         int stat, int64_t first,
                         int64_t count, double* out, bool timed, int64_t* nfixed, bool no_fixup, bool* applicable) {
     *applicable = false;
     *nfixed = 0;
-    double* dsc = nullptr;  // [delta, f0, dt[0], dt[n-1], unsorted flag (int)]: one readback
-    HIPCHK(sc.alloc(&dsc, 6));
-    int* dflag = reinterpret_cast<int*>(dsc + 4);
-    HIPCHK(hipMemsetAsync(dflag, 0, sizeof(double), s));
-    k_nu_sorted<<<(unsigned)std::min<int64_t>(cdiv(n, 256), 2048), 256, 0, s>>>(dt, n, dflag);
-    k_nu_scalars<<<1, 64, 0, s>>>(ap, freq, dt, n, dsc);
-    HIPCHK(hipGetLastError());
-    double hs[5];
-    HIPCHK(d2h(s, hs, dsc, sizeof(hs)));
     int bad = 0;
     memcpy(&bad, hs + 4, sizeof(int));
     if (bad) return CRIMP_OK;
@@ -1209,7 +1223,8 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* dt, const doub
     int64_t* ctab = nullptr;
     int64_t* cstart = nullptr;
     int64_t* flagged = nullptr;
-    int* nflag = dflag + 1;
+    int* nflag = nullptr;
+    HIPCHK(sc.alloc(&nflag, 1));
     if (any_mfma) {
         HIPCHK(sc.alloc(&U, (size_t)(ubytes / 8)));
         HIPCHK(sc.alloc(&ctab, (size_t)(2 * 8 * nchunk)));
@@ -1345,13 +1360,20 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* dt, const doub
         if (use_gather(pl)) {
             std::vector<int64_t> soff((size_t)nharm);
             int64_t off = 0;
-            for (int k = 1; k <= nharm; ++k) {
-                const int64_t spank = pl.gmax[(size_t)(k - 1)] - pl.gmin[(size_t)(k - 1)] + 1;
-                soff[(size_t)(k - 1)] = off;
-                k_nu_cellstart<<<(unsigned)std::min<int64_t>(cdiv(n, 256), 8192), 256, 0, s>>>(
-                    dt, n, pl.s1, k, pl.gmin[(size_t)(k - 1)], spank, cstart + off);
+            for (int k0 = 1; k0 <= nharm; k0 += kNuCellK) {
+                NuCellArgs ca{};
+                const int nk = std::min(kNuCellK, nharm - k0 + 1);
+                for (int j = 0; j < nk; ++j) {
+                    const int k = k0 + j;
+                    ca.gmin[j] = pl.gmin[(size_t)(k - 1)];
+                    ca.span[j] = pl.gmax[(size_t)(k - 1)] - pl.gmin[(size_t)(k - 1)] + 1;
+                    ca.off[j] = off;
+                    soff[(size_t)(k - 1)] = off;
+                    off += ca.span[j] + 1;
+                }
+                k_nu_cellstart<<<(unsigned)std::min<int64_t>(cdiv(n, 256), 8192), 256, 0, s>>>(t, t0, n, pl.s1, k0, nk,
+                                                                                              ca, cstart);
                 HIPCHK(hipGetLastError());
-                off += spank + 1;
             }
             HIPCHK(span(kNuClsCellStart));
             for (int64_t rb = pl.r0; rb < pl.r1; rb += kNuGatherRows) {
@@ -1363,16 +1385,17 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* dt, const doub
                     occupied(k, &alo, &acnt);
                     const int64_t gbase = (int64_t)alo << ln2, gcount = (int64_t)acnt << ln2;
                     // lanes per cell: enough threads for ~2 rounds of 3 resident waves per SIMD, keeping >= 4
-                    // photons per lane, at most 8
+                    // photons per lane, at most 4 (8 lanes' butterfly costs more than it spreads: config 3 spread
+                    // 0.154 ms at 4 lanes, 0.199 at 8, 0.161 at 2, profiles/r05/ab_lanes.log)
                     const int64_t kspan = pl.gmax[(size_t)(k - 1)] - pl.gmin[(size_t)(k - 1)] + 1;
                     const int64_t ppc = n / std::max<int64_t>(1, std::min<int64_t>(kspan, nfft));
                     int L = 1;
-                    while (L < 8 && gcount * L < (int64_t(1) << 19) && ppc >= 4 * 2 * L) L *= 2;
+                    while (L < 4 && gcount * L < (int64_t(1) << 20) && ppc >= 4 * 2 * L) L *= 2;
                     if (lanes_env > 0) L = lanes_env;  // test hook: CRIMP_NUFFT_LANES=1|2|4|8
                     // per photon and row: premultiplier phase + cis ~ 40 flops, then 2 FMA + 1 multiply per moment
                     g_nu_work[0] += (40.0 + 5.0 * P) * (double)n * nrow;
                     g_nu_work[kNuClsSpread] += 8.0 * (double)n + 16.0 * (double)P * nrow * (double)gcount;
-                    launch_gather(L, twod, gcount, dt, cstart + soff[(size_t)(k - 1)], pl.gmin[(size_t)(k - 1)],
+                    launch_gather(L, twod, gcount, t, t0, cstart + soff[(size_t)(k - 1)], pl.gmin[(size_t)(k - 1)],
                                   pl.gmax[(size_t)(k - 1)], nfft, gbase, pl.s1, pl.fch, pl.fcl,
                                   twod ? c2 + rb : nullptr, nrow, k, P, cis, W, s);
                     HIPCHK(hipGetLastError());
@@ -1403,10 +1426,10 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* dt, const doub
                     g_nu_work[kNuClsSpread] += 8.0 * (double)SL *
                                     (double)(pl.gmax[(size_t)(k0 + kk - 1)] - ps.gmin[kk] + 1 + nchunk);
                 if (twod)
-                    nu_launch_spread<true>(gl, grid, s, dt, n, nchunk, pl.s1, pl.fch, pl.fcl, c2 + rb, nrow, k0, P, dp, cis,
+                    nu_launch_spread<true>(gl, grid, s, t, t0, n, nchunk, pl.s1, pl.fch, pl.fcl, c2 + rb, nrow, k0, P, dp, cis,
                                            U, ctab);
                 else
-                    nu_launch_spread<false>(gl, grid, s, dt, n, nchunk, pl.s1, pl.fch, pl.fcl, c2 + rb, nrow, k0, P, dp,
+                    nu_launch_spread<false>(gl, grid, s, t, t0, n, nchunk, pl.s1, pl.fch, pl.fcl, c2 + rb, nrow, k0, P, dp,
                                             cis, U, ctab);
                 HIPCHK(hipGetLastError());
                 HIPCHK(span(kNuClsSpread));
@@ -1441,7 +1464,7 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* dt, const doub
             cls[evcls[i - 1]] += ms;
             cnt[evcls[i - 1]] += 1.0;  // launches: one per span except the cell starts (one span per nharm launches)
         }
-        cnt[kNuClsCellStart] *= nharm;
+        cnt[kNuClsCellStart] *= (nharm + kNuCellK - 1) / kNuCellK;
         for (hipEvent_t e : ev) (void)hipEventDestroy(e);
         if (g_kernel_times.empty()) g_last_kernel_ms = tot;
         g_kernel_times.push_back(tot);  // then the classes' ms, then their launch counts
@@ -1452,5 +1475,10 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* dt, const doub
     HIPCHK(d2h(s, &nf_h, nflag, sizeof(int)));
     *nfixed = nf_h;
     if (nf_h == 0 || no_fixup) return CRIMP_OK;
+    double *dt = nullptr, *dt2 = nullptr;  // the fix-up's fp64 kernel reads dt (and dt^2) arrays
+    HIPCHK(sc.alloc(&dt, (size_t)n));
+    if (twod) HIPCHK(sc.alloc(&dt2, (size_t)n));
+    k_search_prep<<<(int)std::min<int64_t>(cdiv(n, 256), 4096), 256, 0, s>>>(t, n, t0, dt, dt2);
+    HIPCHK(hipGetLastError());
     return fixup_search(sc, s, dt, dt2, n, freq, nf, c2, twod, nharm, stat, first, flagged, nf_h, out);
 }

@@ -57,14 +57,16 @@ def _as_comm(local, dev):
     return torch.as_tensor(np.asarray(local), dtype=torch.float64, device=dev)
 
 
-def sharded_search(time, freq, nharm=2, stat=0, freq_dot=None, gather="all", compute=None, flags=0, precision=None):
+def sharded_search(time, freq, nharm=2, stat=0, freq_dot=None, gather="all", compute=None, flags=0, precision=None,
+                   t0=None):
     """Z^2 (stat=0) / H (stat=1) over the fd-outer grid, sharded across the process group.
 
     Returns the full power array (gather='all'; a tensor on the rank's device when ``time`` is a device
     tensor, else a numpy array) or ``(best_power, best_flat_index)`` (gather='best'), identical on every rank.
     With the nccl backend the gather runs on the device buffers the search wrote (no host staging).
     ``flags`` and ``precision`` (None | "exact" | "nufft" | "f64", as PeriodSearch) go to the rank's crimp_search
-    call (e.g. FLAG_TIME_KERNELS for bench.py).
+    call (e.g. FLAG_TIME_KERNELS for bench.py). ``t0`` (optional): the reference time (time[0] + time[-1]) / 2 when
+    the caller already holds it, which spares a device read for a device tensor.
     """
     import functools
     import torch
@@ -72,10 +74,12 @@ def sharded_search(time, freq, nharm=2, stat=0, freq_dot=None, gather="all", com
     compute = compute or functools.partial(_gpu_slice, flags=flags, precision=precision)
     as_tensor = isinstance(time, torch.Tensor)
     if as_tensor:
-        t0 = float((time[0] + time[-1]).item()) / 2
+        if t0 is None:
+            t0 = float((time[0] + time[-1]).item()) / 2
         nf = int(freq.numel())
     else:
-        t0 = (time[0] + time[-1]) / 2  # periodsearch.py:54, shared by every shard
+        if t0 is None:
+            t0 = (time[0] + time[-1]) / 2  # periodsearch.py:54, shared by every shard
         nf = int(np.size(freq))
     nfd = 0 if freq_dot is None else int(freq_dot.numel() if isinstance(freq_dot, torch.Tensor) else np.size(freq_dot))
     total = (nfd if nfd else 1) * nf
@@ -86,8 +90,11 @@ def sharded_search(time, freq, nharm=2, stat=0, freq_dot=None, gather="all", com
     loc = _as_comm(local, dev)
     if gather == "best":
         if count:
-            i = torch.argmax(loc)
-            mine = torch.stack([loc[i], (i + first).to(torch.float64)])
+            v, i = torch.max(loc, 0)  # the first maximal index, as np.argmax
+            if dist is None:
+                res = torch.stack([v, i.to(torch.float64)]).cpu().numpy()
+                return float(res[0]), int(res[1]) + first
+            mine = torch.stack([v, (i + first).to(torch.float64)])
         else:
             mine = torch.tensor([-np.inf, float(total)], dtype=torch.float64, device=dev)
         if dist is None:
