@@ -24,6 +24,7 @@ Also reported:
   (interval selection, calcphase, fits, per-interval H-test) from host MJD arrays, with the oracle's fits on all
   allowed host cores as its CPU baseline (a sample, extrapolated) and the fits' VALU roofline;
 * ``config4``: 1e8 photons, 2-D H_20 on a sub-grid of the 1e7-trial grid (131072 trials per GPU), sharded_search;
+  ``config4.nufft``: the WHOLE 1e7-trial grid by precision="nufft" (each rank its 1e7/N slice);
 * ``config2``: ``measureToAs`` on the bundled events, ToAs 35-41, FITS -> table (the reference's published rate).
 The multi-GPU paths are the tested ones (tests/test_distributed_*.py): the search step and the config-4 leg run
 ``sharding.sharded_search(gather="best")``, the ToA leg ``sharding.sharded_toa_fit`` (records all_gathered).
@@ -74,6 +75,7 @@ def parse():
     p.add_argument("--no-config4", action="store_true", help="skip the config-4 (1e8 photons, H_20) leg")
     p.add_argument("--c4-photons", type=int, default=100_000_000)
     p.add_argument("--c4-trials", type=int, default=131072, help="config-4 trials timed per GPU (even)")
+    p.add_argument("--no-nufft-c4", action="store_true", help="skip the whole-grid config-4 NUFFT search")
     return p.parse_args()
 
 
@@ -421,10 +423,40 @@ def config4_leg(a, dev, world, rank):
     el = float(elt.item())
     ops_launch = OPS_PER_EVAL_HARM * 20 * float(n) * count
     ach = ops_launch / (kms * 1e-3) / 1e12
+    nu = None
+    if not a.no_nufft_c4:
+        # the WHOLE config-4 grid (1e5 f x 100 fdot rows = 1e7 trials, N ranks each its 1e7/N slice) by
+        # precision="nufft": the per-GPU workload of BASELINE config 4, timed end to end
+        f_all = torch.as_tensor(f0 + (np.arange(M) - M // 2) / (10.0 * span), device=dev)
+        fd_all = torch.as_tensor(np.linspace(-13.5, -11.5, 100), device=dev)
+        nu_first, nu_count = shard_range(100 * M, world, rank)
+        sharded_search(t, f_all, 20, 1, freq_dot=fd_all, gather="best", precision="nufft")  # untimed
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t1 = time.perf_counter()
+        nb_pow, nb_idx = sharded_search(t, f_all, 20, 1, freq_dot=fd_all, gather="best", precision="nufft")
+        torch.cuda.synchronize()
+        nel = time.perf_counter() - t1
+        elt = torch.tensor([nel], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(elt, op=dist.ReduceOp.MAX)
+        nel = float(elt.item())
+        nplan = N.last_nufft_plan()
+        nrow_, ncol_ = divmod(nb_idx, M)
+        nu = {"evals_per_s": float(n) * 100 * M / nel, "unit": "equivalent photon*trial evals/s (H_20)",
+              "seconds": nel, "trials_total": 100 * M, "trials_per_gpu": nu_count,
+              "search_path": N.load().crimp_last_search_path(), "fp64_fixup_trials": N.load().crimp_last_fixups(),
+              "plan": {"fft_length": nplan[0], "moments": nplan[1], "spread": nplan[2]},
+              "best_power": nb_pow, "best_trial": {"fdot_row": nrow_, "f_index": ncol_},
+              "workload": "config4 WHOLE grid: %.3g photons, H_20, 1e5 f x 100 fdot rows (%d trials per GPU), "
+                          "precision='nufft', sharding.sharded_search(gather='best') over %d rank(s)"
+                          % (n, nu_count, world)}
+        del f_all, fd_all
     del t, f, fd
     torch.cuda.empty_cache()
     row, col = divmod(best_idx, nf)
-    return {"evals_per_s": float(n) * count * world / el, "unit": "photon*trial evals/s (H_20)", "seconds": el,
+    return {"evals_per_s": float(n) * count * world / el, "unit": "photon*trial evals/s (H_20)", "seconds": el, "nufft": nu,
             "kernel_ms": kms, "trials_per_gpu_timed": count, "photons": n, "first_flat_trial": first,
             "fp64_fixup_trials": nfix, "best_power": best_pow, "best_trial": {"fdot_row": row, "f_index": col},
             "photon_generation_s": gen_s,

@@ -304,36 +304,49 @@ __global__ __launch_bounds__(256) void k_nu_gather(const double* __restrict__ tt
     for (int64_t G = gmin + (((g - gmin) % nfft) + nfft) % nfft; G <= gmax; G += nfft) {
         const int64_t i0 = start[G - gmin], i1 = start[G - gmin + 1];
         const double Gd = (double)G;
-        // photon times four iterations ahead (HBM latency is several iterations of one wave)
+        // two photons per iteration (independent chains for the VALU; each one's terms still added in photon
+        // order), their times prefetched two iterations ahead (HBM latency is several iterations of one wave)
         double dn[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) dn[q] = i0 + sub + q * L < i1 ? (tt[i0 + sub + q * L] - t0) : 0.0;
-        for (int64_t i = i0 + sub; i < i1; i += L) {
-            const double d = dn[0];
-            dn[0] = dn[1];
-            dn[1] = dn[2];
-            dn[2] = dn[3];
-            if (i + 4 * L < i1) dn[3] = (tt[i + 4 * L] - t0);
-            const double e = kd * (d * s1) - Gd;
-            const double p1 = nu_frac_prod(fch, fcl, d);
-            double d2 = 0.0, d2e = 0.0;
+        for (int64_t i = i0 + sub; i < i1; i += 2 * L) {
+            const bool hb = i + L < i1;
+            const double da = dn[0], db = hb ? dn[1] : dn[0];  // (no second photon: a finite stand-in, weight 0)
+            dn[0] = dn[2];
+            dn[1] = dn[3];
+            if (i + 4 * L < i1) dn[2] = (tt[i + 4 * L] - t0);
+            if (i + 5 * L < i1) dn[3] = (tt[i + 5 * L] - t0);
+            const double ea = kd * (da * s1) - Gd, eb = kd * (db * s1) - Gd;
+            const double p1a = nu_frac_prod(fch, fcl, da), p1b = nu_frac_prod(fch, fcl, db);
+            double d2a = 0.0, d2ea = 0.0, d2b = 0.0, d2eb = 0.0;
             if (TWOD) {
-                d2 = d * d;
-                d2e = fma(d, d, -d2);
+                d2a = da * da;
+                d2ea = fma(da, da, -d2a);
+                d2b = db * db;
+                d2eb = fma(db, db, -d2b);
             }
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 if (r < nrow) {
-                    double phi = p1;
-                    if (TWOD) phi += nu_frac_c2(c2[r], d2, d2e);
-                    phi -= rint(phi);
-                    const double2 c = nu_cis(stab, nu_frac_k(kd, phi));
-                    double ep = 1.0;
+                    double phia = p1a, phib = p1b;
+                    if (TWOD) {
+                        phia += nu_frac_c2(c2[r], d2a, d2ea);
+                        phib += nu_frac_c2(c2[r], d2b, d2eb);
+                    }
+                    phia -= rint(phia);
+                    phib -= rint(phib);
+                    const double2 ca = nu_cis(stab, nu_frac_k(kd, phia));
+                    double2 cb = nu_cis(stab, nu_frac_k(kd, phib));
+                    if (!hb) cb = make_double2(0.0, 0.0);
+                    double epa = 1.0, epb = 1.0;
 #pragma unroll
                     for (int p = 0; p < PP; ++p) {
-                        ar[r][p] = fma(c.x, ep, ar[r][p]);
-                        ai[r][p] = fma(c.y, ep, ai[r][p]);
-                        ep *= e;
+                        ar[r][p] = fma(ca.x, epa, ar[r][p]);
+                        ai[r][p] = fma(ca.y, epa, ai[r][p]);
+                        ar[r][p] = fma(cb.x, epb, ar[r][p]);
+                        ai[r][p] = fma(cb.y, epb, ai[r][p]);
+                        epa *= ea;
+                        epb *= eb;
                     }
                 }
             }
@@ -602,44 +615,60 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     }
 }
 
-// k_nu_fft_cols for n1 = 256 (two radix-16 stages, 16 columns per block): the same arithmetic as the generic
-// kernel with stage 1 on the columns as loaded into registers (thread (j, cc): rows j + 16 r of column cc) and stage
-// 2's outputs (rows k1 = j + 16 r) twiddled and stored from registers: one LDS write and read instead of six.
-// The inter-pass twiddles are fetched before the barrier.
+// k_nu_fft_cols for n1 = 256 (two radix-16 stages over 16 columns): stage 1 on the columns as loaded into registers
+// (thread (j, cc): rows j + 16 r of column cc), one LDS exchange, stage 2's outputs (rows k1 = j + 16 r) twiddled and
+// stored from registers: one LDS write and read instead of six. Persistent blocks walk the (batch, column block)
+// groups with the next group's rows and twiddle bases loaded during the current one (the kernel is latency-bound at
+// the two waves per SIMD its 64 KB of LDS allow). The inter-pass twiddle w_n^{b k1} = w_n^{b j} (w_n^{16 b})^r: two
+// table values and products over the bits of r (a few ulp, as the tile twiddles).
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_nu_cols256(
-    const double2* __restrict__ X, double2* __restrict__ Y, int lnfft, NuTw T, int alo, int acnt) {
+    const double2* __restrict__ X, double2* __restrict__ Y, int lnfft, NuTw T, int alo, int acnt, int64_t ngroups) {
     extern __shared__ double2 nu_s[];  // [256 rows][16 columns]
     __shared__ NuTile tw;
     nu_tile_init(&tw, 12);
     const int ln2 = lnfft - 8;
     const int64_t nfft = int64_t(1) << lnfft;
     const int cc = threadIdx.x & 15, j = threadIdx.x >> 4;
-    const int64_t b = ((int64_t)blockIdx.x << 4) + cc;
-    const double2* x = X + (int64_t)blockIdx.y * nfft + b;
-    double2* y = Y + (int64_t)blockIdx.y * nfft + b;
-    double2 v[16];
+    const int64_t cpb = int64_t(1) << (ln2 - 4);  // column blocks per batch
+    double2 nv[16], nb, ns;
+    auto fetch = [&](int64_t grp) {  // rows outside [alo, alo + acnt) (mod 256) hold no cell
+        const int64_t b = ((grp % cpb) << 4) + cc;
+        const double2* x = X + (grp / cpb) * nfft + b;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {  // rows outside [alo, alo + acnt) (mod 256) hold no cell
-        const int a = j + 16 * r;
-        v[r] = ((a - alo) & 255) < acnt ? x[(int64_t)a << ln2] : make_double2(0.0, 0.0);
+        for (int r = 0; r < 16; ++r) {
+            const int a = j + 16 * r;
+            nv[r] = ((a - alo) & 255) < acnt ? x[(int64_t)a << ln2] : make_double2(0.0, 0.0);
+        }
+        nb = nu_tw(T, b * (int64_t)j);
+        ns = nu_tw(T, b << 4);
+    };
+    int64_t grp = blockIdx.x;
+    if (grp < ngroups) fetch(grp);
+    __syncthreads();  // tw
+    for (; grp < ngroups; grp += gridDim.x) {
+        double2 v[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = nv[r];
+        const double2 wb = nb, ws = ns;
+        const int64_t b = ((grp % cpb) << 4) + cc;
+        double2* y = Y + (grp / cpb) * nfft + b;
+        if (grp + gridDim.x < ngroups) fetch(grp + gridDim.x);
+        nu_dft16(v);  // stage 1 (Ns = 1)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) nu_s[((j << 4) + r) * 16 + cc] = v[r];
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = nu_s[(j + 16 * r) * 16 + cc];
+        __syncthreads();  // the next group's stage-1 writes reuse the tile
+        nu_twiddle<16>(nu_tw_tile(&tw, j << 4), v);  // w_256^{j r}
+        nu_dft16(v);                                 // stage 2 (Ns = 16): output rows k1 = j + 16 r
+        v[0] = nu_cmul(v[0], wb);
+        nu_twiddle<16>(ws, v);  // v[r] *= (w_n^{16 b})^r
+#pragma unroll
+        for (int r = 1; r < 16; ++r) v[r] = nu_cmul(v[r], wb);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) y[(int64_t)(j + 16 * r) << ln2] = v[r];
     }
-    nu_dft16(v);  // stage 1 (Ns = 1)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) nu_s[((j << 4) + r) * 16 + cc] = v[r];
-    double2 wh[16], wl[16];  // w_n^{b k1}, k1 = j + 16 r, as the table pair nu_tw multiplies
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int64_t m = (b * (int64_t)(j + 16 * r)) & T.mask;
-        wh[r] = T.hi[m >> T.lbits];
-        wl[r] = T.lo[m & ((int64_t(1) << T.lbits) - 1)];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < 16; ++r) v[r] = nu_s[(j + 16 * r) * 16 + cc];
-    nu_twiddle<16>(nu_tw_tile(&tw, j << 4), v);  // w_256^{j r}
-    nu_dft16(v);                                 // stage 2 (Ns = 16): output rows k1 = j + 16 r
-#pragma unroll
-    for (int r = 0; r < 16; ++r) y[(int64_t)(j + 16 * r) << ln2] = nu_cmul(v[r], nu_cmul(wh[r], wl[r]));
 }
 
 // pass 2 (or the only pass): DFT of 2^lr contiguous rows of length 2^ll each, in place
@@ -792,6 +821,90 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
         const int64_t J = k1 + ((int64_t)(t + 256 * q) << ln1);
+        int64_t jc;
+        if (J <= jhi)
+            jc = J;
+        else if (J >= nfft - h)
+            jc = J - nfft;
+        else
+            continue;
+        const int64_t tt = tbase + r * nf + jc;
+        if (tt >= 0 && tt < nbt) CS[tt] = acc[q];
+    }
+}
+
+// k_nu_rows4096_combine with 512 threads and four radix-8 stages (8 elements per thread): two waves per SIMD from
+// one block per CU (the radix-16 form holds 16 elements per thread and runs one). Stage 1 on the loaded row, stage 4's
+// outputs (positions t + 512 r) in registers for the Horner sum, stages 2-3 through two 64 KB tiles whose roles
+// alternate between moments (three barriers per moment); element i at i ^ ((i >> 3) & 7) (stage 1's stride-8
+// writes over all banks). The transform's arithmetic differs from the radix-16 form's in rounding only.
+__device__ __forceinline__ int nu_sw8(int i) { return i ^ ((i >> 3) & 7); }
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k_nu_rows4096_combine8(
+    const double2* __restrict__ X, int lnfft, int P, int nrow, int64_t nf, int64_t jhi, int64_t h, int64_t tbase,
+    int64_t nbt, double2* __restrict__ CS) {
+    extern __shared__ double2 nu_s[];  // [2][4096]
+    __shared__ NuTile tw;
+    nu_tile_init(&tw, 12);
+    const int64_t nfft = int64_t(1) << lnfft;
+    const int ln1 = lnfft - 12;
+    const int64_t k1 = blockIdx.x;
+    const int r = blockIdx.y;
+    const int t = threadIdx.x;
+    const double2* xr = X + (int64_t)r * nfft + (k1 << 12);
+    const int64_t pstride = (int64_t)nrow * nfft;
+    double2 acc[8], nx[8], v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        acc[q] = make_double2(0.0, 0.0);
+        nx[q] = xr[(int64_t)(P - 1) * pstride + t + 512 * q];
+    }
+    const int m2 = (t & 7) << 6, m3 = (t & 63) << 3, m4 = t;  // stage twiddles in units of w_4096
+    const int z2 = ((t >> 3) << 6) + (t & 7), z3 = ((t >> 6) << 9) + (t & 63);  // stage 2 / 3 output bases
+    __syncthreads();                                                             // tw
+    int par = 0;
+    for (int p = P - 1; p >= 0; --p, par ^= 1) {
+        double2* A = nu_s + (par ? 4096 : 0);
+        double2* B = nu_s + (par ? 0 : 4096);
+        const int64_t pn = (int64_t)(p > 0 ? p - 1 : 0) * pstride;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            v[q] = nx[q];
+            nx[q] = xr[pn + t + 512 * q];
+        }
+        nu_dft8(v);  // stage 1 (Ns = 1)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) A[nu_sw8(8 * t + q)] = v[q];
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = A[nu_sw8(t + 512 * q)];
+        nu_twiddle<8>(nu_tw_tile(&tw, m2), v);
+        nu_dft8(v);  // stage 2 (Ns = 8)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) B[nu_sw8(z2 + 8 * q)] = v[q];
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = B[nu_sw8(t + 512 * q)];
+        nu_twiddle<8>(nu_tw_tile(&tw, m3), v);
+        nu_dft8(v);  // stage 3 (Ns = 64)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) A[nu_sw8(z3 + 64 * q)] = v[q];
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = A[nu_sw8(t + 512 * q)];
+        nu_twiddle<8>(nu_tw_tile(&tw, m4), v);
+        nu_dft8(v);  // stage 4 (Ns = 512): output position t + 512 q
+        const double ip = 1.0 / (double)(p + 1);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int64_t J = k1 + ((int64_t)(t + 512 * q) << ln1);
+            const int64_t jc = J <= jhi ? J : J - nfft;
+            const double f = (ldexp((double)jc, -lnfft) * 6.283185307179586476925286766559) * ip;
+            acc[q] = make_double2(fma(-f, acc[q].y, v[q].x), fma(f, acc[q].x, v[q].y));
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const int64_t J = k1 + ((int64_t)(t + 512 * q) << ln1);
         int64_t jc;
         if (J <= jhi)
             jc = J;
@@ -1035,6 +1148,14 @@ static void launch_gather(int L, bool twod, int64_t gcount, const double* tt, do
                                   s);
 }
 
+static int64_t nu_cus() {  // compute units of the current device (persistent grids)
+    int dev = 0, ncu = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        ncu <= 0)
+        ncu = 256;
+    return ncu;
+}
+
 static int64_t nufft_budget() {
     static int64_t b = -1;
     if (b < 0) {
@@ -1191,6 +1312,8 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
     // identity test hook)
     const char* r4_env = getenv("CRIMP_NUFFT_ROWS4096");
     const bool rows4096 = !(r4_env && !strcmp(r4_env, "0"));
+    const char* r8_env = getenv("CRIMP_NUFFT_R8");  // 1: pass 2 of 4096-element rows by k_nu_rows4096_combine8
+    const bool rows_r8 = r8_env && !strcmp(r8_env, "1");
     {  // 128 KB of dynamic LDS for k_nu_rows4096_combine, set once per device
         static std::mutex mu;
         static uint64_t done = 0;
@@ -1199,6 +1322,8 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
         std::lock_guard<std::mutex> lk(mu);
         if (dev >= 64 || !(done >> dev & 1)) {
             HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_nu_rows4096_combine),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kNuTile * (int)sizeof(double2)));
+            HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_nu_rows4096_combine8),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kNuTile * (int)sizeof(double2)));
             if (dev < 64) done |= uint64_t(1) << dev;
         }
@@ -1308,8 +1433,9 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
                 occupied(k, &alo, &acnt);
                 g_nu_work[kNuClsPass1] += plane * ((double)acnt / (double)(int64_t(1) << ln1)) + plane;  // occupied rows in, all out
                 if (ln1 == 8 && rows4096) {
-                    k_nu_cols256<<<dim3((unsigned)(int64_t(1) << (ln2 - 4)), (unsigned)Bp), 256, lds_fft, s>>>(
-                        W, Y, lnfft, T, alo, acnt);
+                    const int64_t ngroups = Bp << (ln2 - 4);
+                    k_nu_cols256<<<(unsigned)std::min<int64_t>(ngroups, 2 * nu_cus()), 256, lds_fft, s>>>(
+                        W, Y, lnfft, T, alo, acnt, ngroups);
                     HIPCHK(hipGetLastError());
                 } else {
                     k_nu_fft_cols<<<dim3((unsigned)(int64_t(1) << (ln2 - lcol)), (unsigned)Bp), 256, lds_fft, s>>>(
@@ -1318,6 +1444,15 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
                 }
                 Zo = Y;
                 HIPCHK(span(kNuClsPass1));
+            }
+            if (fused_combine && ln2 == 12 && rows4096 && rows_r8) {  // 512 threads, radix 8 (A/B: CRIMP_NUFFT_R8)
+                g_nu_work[kNuClsPass2] += plane + 16.0 * (double)nbt;
+                k_nu_rows4096_combine8<<<dim3((unsigned)(int64_t(1) << ln1), (unsigned)nrow), 512, 2 * lds_fft, s>>>(
+                    Zo, lnfft, P, nrow, nf, pl.nseg - 1 - pl.h, pl.h, rb * nf + jbase - (tb0 + first), nbt,
+                    CS + (int64_t)(k - 1) * nbt);
+                HIPCHK(hipGetLastError());
+                HIPCHK(span(kNuClsPass2));
+                return CRIMP_OK;
             }
             if (fused_combine && ln2 == 12 && rows4096) {  // the specialised form for 4096-element rows
                 g_nu_work[kNuClsPass2] += plane + 16.0 * (double)nbt;
