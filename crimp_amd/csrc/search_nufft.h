@@ -1312,8 +1312,10 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
     // identity test hook)
     const char* r4_env = getenv("CRIMP_NUFFT_ROWS4096");
     const bool rows4096 = !(r4_env && !strcmp(r4_env, "0"));
-    const char* r8_env = getenv("CRIMP_NUFFT_R8");  // 1: pass 2 of 4096-element rows by k_nu_rows4096_combine8
-    const bool rows_r8 = r8_env && !strcmp(r8_env, "1");
+    // pass 2 of 4096-element rows by the 512-thread radix-8 kernel (default: 0.178 vs 0.190 ms per config-3 search,
+    // profiles/r05/ab_r8_ilp.log); CRIMP_NUFFT_R8=0 runs the radix-16 form
+    const char* r8_env = getenv("CRIMP_NUFFT_R8");
+    const bool rows_r8 = !(r8_env && !strcmp(r8_env, "0"));
     {  // 128 KB of dynamic LDS for k_nu_rows4096_combine, set once per device
         static std::mutex mu;
         static uint64_t done = 0;
@@ -1445,7 +1447,7 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
                 Zo = Y;
                 HIPCHK(span(kNuClsPass1));
             }
-            if (fused_combine && ln2 == 12 && rows4096 && rows_r8) {  // 512 threads, radix 8 (A/B: CRIMP_NUFFT_R8)
+            if (fused_combine && ln2 == 12 && rows4096 && rows_r8) {  // 512 threads, radix 8
                 g_nu_work[kNuClsPass2] += plane + 16.0 * (double)nbt;
                 k_nu_rows4096_combine8<<<dim3((unsigned)(int64_t(1) << ln1), (unsigned)nrow), 512, 2 * lds_fft, s>>>(
                     Zo, lnfft, P, nrow, nf, pl.nseg - 1 - pl.h, pl.h, rb * nf + jbase - (tb0 + first), nbt,

@@ -183,7 +183,7 @@ def test_nufft_fused_pass2_equals_separate_combine(gpu, monkeypatch):
         monkeypatch.delenv("CRIMP_NUFFT_ROWS4096")
         rel = np.abs(a - c) / np.abs(c)
         assert rel.max() <= 1e-10 and np.median(rel) <= 1e-13, (rel.max(), np.median(rel))
-        monkeypatch.setenv("CRIMP_NUFFT_R8", "1")  # the 512-thread radix-8 row pass
+        monkeypatch.setenv("CRIMP_NUFFT_R8", "0")  # the radix-16 row pass instead of the 512-thread radix-8 one
         d = ops.search(t, t0, f, m, 1, log10_negfdot=fdv, precision="nufft", flags=N.FLAG_NO_FIXUP)
         monkeypatch.delenv("CRIMP_NUFFT_R8")
         rel = np.abs(d - c) / np.abs(c)
