@@ -158,36 +158,37 @@ def test_nufft_unsorted_photons_take_default_path(gpu):
 
 
 def test_nufft_fused_pass2_equals_separate_combine(gpu, monkeypatch):
-    """FFT pass 2 fused with the moments' Horner sum (default) against pass 2 and k_nu_combine as two kernels
-    (CRIMP_NUFFT_FUSED=0): the same arithmetic, so bit-identical powers; and the 4096-row and 256-row-column kernels
-    (k_nu_rows4096_combine, k_nu_cols256) against the generic ones (CRIMP_NUFFT_ROWS4096=0) to rounding --
+    """FFT pass 2 fused with the moments' Horner sum against pass 2 and k_nu_combine as two kernels
+    (CRIMP_NUFFT_FUSED=0), both with the radix-16 row transform (CRIMP_NUFFT_R8=0): the same arithmetic, so
+    bit-identical powers; the default (512-thread radix-8 row pass) and the 4096-row / 256-row-column kernels
+    (k_nu_rows4096_combine*, k_nu_cols256) against the generic ones (CRIMP_NUFFT_ROWS4096=0) to rounding --
     single-pass (n <= 4096) and four-step FFTs, 1-D and 2-D grids."""
     from crimp_amd import ops, _native as N
     from crimp_amd.synth import pulsed_events
     t = pulsed_events(200000, 2.0e5, 3.3, pulsed_frac=0.05, fdot=-2e-11, seed=8)
     t0 = (t[0] + t[-1]) / 2
     fd = np.array([-12.0, -11.0, -10.5])
+
+    def run(**env):
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        z = ops.search(t, t0, f, m, 1, log10_negfdot=fdv, precision="nufft", flags=N.FLAG_NO_FIXUP)
+        for k in env:
+            monkeypatch.delenv(k)
+        return z
+
+    def close(x, y):
+        rel = np.abs(x - y) / np.abs(y)
+        assert rel.max() <= 1e-10 and np.median(rel) <= 1e-13, (rel.max(), np.median(rel))
+
     for f, m, fdv in ((3.3 + np.arange(-700, 701) / 2.0e6, 2, None), (3.3 + np.arange(-40000, 40000) / 2.0e6, 3, None),
                       (3.3 + np.arange(-1500, 1500) / 2.0e6, 5, fd),
                       (3.3 + np.arange(-300000, 300000) / 2.0e7, 2, None)):  # n = 2^20: 256-row columns
-        a = ops.search(t, t0, f, m, 1, log10_negfdot=fdv, precision="nufft", flags=N.FLAG_NO_FIXUP)
-        monkeypatch.setenv("CRIMP_NUFFT_FUSED", "0")
-        b = ops.search(t, t0, f, m, 1, log10_negfdot=fdv, precision="nufft", flags=N.FLAG_NO_FIXUP)
-        monkeypatch.delenv("CRIMP_NUFFT_FUSED")
-        np.testing.assert_array_equal(a, b)
-        # 4096-element rows (n >= 2^13) and 256-row columns (n = 2^20): the specialised kernels against the generic
-        # ones -- the same transforms, pass 1's inter-pass twiddles formed as a base times powers (a few ulp) instead
-        # of one table product
-        monkeypatch.setenv("CRIMP_NUFFT_ROWS4096", "0")
-        c = ops.search(t, t0, f, m, 1, log10_negfdot=fdv, precision="nufft", flags=N.FLAG_NO_FIXUP)
-        monkeypatch.delenv("CRIMP_NUFFT_ROWS4096")
-        rel = np.abs(a - c) / np.abs(c)
-        assert rel.max() <= 1e-10 and np.median(rel) <= 1e-13, (rel.max(), np.median(rel))
-        monkeypatch.setenv("CRIMP_NUFFT_R8", "0")  # the radix-16 row pass instead of the 512-thread radix-8 one
-        d = ops.search(t, t0, f, m, 1, log10_negfdot=fdv, precision="nufft", flags=N.FLAG_NO_FIXUP)
-        monkeypatch.delenv("CRIMP_NUFFT_R8")
-        rel = np.abs(d - c) / np.abs(c)
-        assert rel.max() <= 1e-10 and np.median(rel) <= 1e-13, (rel.max(), np.median(rel))
+        r16 = run(CRIMP_NUFFT_R8="0")
+        np.testing.assert_array_equal(r16, run(CRIMP_NUFFT_R8="0", CRIMP_NUFFT_FUSED="0"))
+        generic = run(CRIMP_NUFFT_ROWS4096="0")
+        close(r16, generic)
+        close(run(), generic)
 
 
 def test_nufft_gather_lane_splits(gpu, monkeypatch):
