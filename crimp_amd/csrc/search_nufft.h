@@ -7,12 +7,14 @@
 // photon by photon: O(N M) per harmonic. On an arithmetic progression f_j = fc + jc delta (jc = j - h, h = nf/2,
 // fc = f_0 + h delta) the sum over trials is a type-1 non-uniform DFT:
 //   A_k(j) = sum_i c_i exp(2 pi i jc u_i / n),   c_i = exp(2 pi i k (fc dt_i + c2 dt_i^2)),   u_i = n k delta dt_i,
-// with n a power of two >= nf. Writing u_i = g_i + e_i (g_i = rint(u_i), |e_i| <= 1/2) and expanding the
-// sub-cell factor exp(2 pi i jc e_i / n) to P terms (Taylor in e_i: "moments"):
-//   A_k(j) = sum_{p<P} (2 pi i jc / n)^p / p! * B_p(jc mod n),   B_p(J) = sum_g b_p[g] exp(2 pi i J g / n),
-//   b_p[g] = sum_{i : g_i = g (mod n)} c_i e_i^p.
-// Per photon the truncation is <= x^P / P! with x = pi |jc| / n (Lagrange remainder of e^{i theta}), so
-// |A_k error| <= N x^P / P! exactly; P <= 16 and n are chosen so that the bound is <= kNuEps at the grid's edge.
+// with n a power of two >= nf. Writing u_i = g_i + e_i (g_i = rint(u_i), |e_i| <= 1/2), the sub-cell factor
+// exp(2 pi i jc e_i / n) = exp(2 i z e_i), z = pi jc / n (|z| <= pi/2), is expanded in Chebyshev polynomials of
+// 2 e_i (Jacobi-Anger; nu_bes): exp(2 i z e) = sum_p eps_p i^p J_p(z) T_p(2e), so with P "moments"
+//   A_k(j) = sum_{p<P} eps_p i^p J_p(z) * B_p(jc mod n),   B_p(J) = sum_g b_p[g] exp(2 pi i J g / n),
+//   b_p[g] = sum_{i : g_i = g (mod n)} c_i T_p(2 e_i).
+// |T_p| <= 1 and |J_p(z)| <= (|z|/2)^p / p!, so |A_k error| <= 2 N sum_{p>=P} (|z|/2)^p / p! < 2.4 N (x/2)^P / P!
+// with x = pi |jc| / n; P and n are chosen so that the bound is <= kNuEps at the grid's edge (16 moments at config 3;
+// a Taylor expansion in e_i, bound N x^P / P!, needs 20).
 // The cost is O(N m P) for the moments plus O(m P n log n) for the FFTs, against O(N M m) for the direct sum.
 //
 // Kernels (one pass = harmonics k0 .. k0+G-1 of up to 8 trial-grid rows):
@@ -25,7 +27,8 @@
 //                 chunks that hold it, in chunk order (deterministic), transposed to batch-major rows.
 //   k_nu_fft_cols, k_nu_fft_rows   four-step FFT (n = n1 n2, Stockham autosort stages of radix 16/8/4/2 in LDS,
 //                 positive exponent); a single row pass for n <= 4096.
-//   k_nu_combine  Horner over the moments at every trial -> (C_k, S_k).
+//   k_nu_combine  the moments' Bessel-weighted sum at every trial -> (C_k, S_k) (fused into the row pass by
+//                 default: k_nu_rows4096_combine8 / k_nu_fft_rows_combine).
 //   k_nu_finalize Z^2 / H in the reference's formula order and the certificate (fix-up list, as the exact path).
 #pragma once
 
@@ -107,6 +110,76 @@ __device__ __forceinline__ double nu_frac_k(double kd, double phi) {
     const double hk = kd * phi;
     const double hl = fma(kd, phi, -hk);
     return (hk - rint(hk)) + hl;
+}
+
+// Chebyshev-Bessel expansion of the moments' phase factor (Jacobi-Anger): for |e| <= 1/2 and theta = 2 pi jc / n,
+//   e^{i theta e} = sum_p eps_p i^p J_p(theta / 2) T_p(2 e),  eps_0 = 1, eps_p = 2,
+// so the spread accumulates Chebyshev moments sum c_i T_p(2 e_i) and the combine weights moment p's transform by
+// eps_p i^p J_p(z), z = pi jc / n (|z| <= pi / 2). Truncating at P moments errs by <= 2 N sum_{p >= P} (|z|/2)^p / p!
+// (< 2.4 N (|z|/2)^P / P! for P >= 4), against N (2|z|)^P / P! for Taylor moments e^p: 20 -> 16 moments at config 3.
+// J_p(z) = (z/2)^p sum_{m < kNuBesM} y^m / (m! (m+p)!), y = -(z/2)^2 (|y| <= 0.617: the omitted terms < 4e-18 of
+// J_p); the coefficients 1 / (m! (m+p)!) come from the host tables (nu_tables), read at uniform indices.
+constexpr int kNuBesP = 26, kNuBesM = 12;
+__device__ __forceinline__ double nu_bes_series(const double* __restrict__ bc, int p, double y) {
+    const double* c = bc + p * kNuBesM;
+    double f = c[kNuBesM - 1];
+#pragma unroll
+    for (int m = kNuBesM - 2; m >= 0; --m) f = fma(f, y, c[m]);
+    return f;  // J_p(z) / (z/2)^p
+}
+// The combine walks the moments from P-1 down to 0 with J_p by the backward recurrence
+// J_p = (2 (p+1) / z) J_p+1 - J_p+2 (stable: J_p is its minimal solution), started from J_P, J_P+1 by the series.
+// z = 0 (jc = 0): J_p = 0 for p > 0 (zero start, 2/z taken as 0) and J_0 = 1 (nu_bes_w).
+struct NuBes {
+    double j1, j2, iz2;  // J_p+1, J_p+2, 2/z
+};
+__device__ __forceinline__ NuBes nu_bes_start(const double* __restrict__ bc, int P, double zh) {
+    double zp = 1.0;
+    for (int p = 0; p < P; ++p) zp *= zh;  // (z/2)^P
+    const double y = -zh * zh;
+    NuBes b;
+    b.j1 = zp * nu_bes_series(bc, P, y);
+    b.j2 = (zp * zh) * nu_bes_series(bc, P + 1, y);
+    b.iz2 = zh != 0.0 ? 1.0 / zh : 0.0;
+    return b;
+}
+// eps_p J_p for moment p (descending calls p = P-1 .. 0), advancing the recurrence
+__device__ __forceinline__ double nu_bes_w(NuBes& b, int p, double zh) {
+    double j = fma((double)(p + 1) * b.iz2, b.j1, -b.j2);
+    b.j2 = b.j1;
+    b.j1 = j;
+    if (p == 0) return zh != 0.0 ? j : 1.0;
+    return 2.0 * j;
+}
+// acc + w i^p v (p uniform)
+__device__ __forceinline__ double2 nu_bes_acc(double2 acc, double w, double2 v, int p) {
+    switch (p & 3) {
+        case 0: return make_double2(fma(w, v.x, acc.x), fma(w, v.y, acc.y));
+        case 1: return make_double2(fma(-w, v.y, acc.x), fma(w, v.x, acc.y));
+        case 2: return make_double2(fma(-w, v.x, acc.x), fma(-w, v.y, acc.y));
+        default: return make_double2(fma(w, v.y, acc.x), fma(-w, v.x, acc.y));
+    }
+}
+// z/2 = (pi/2) jc / n for an FFT output position holding trial offset jc
+__device__ __forceinline__ double nu_zh(int64_t jc, int lnfft) {
+    return ldexp((double)jc, -lnfft) * 1.5707963267948966192313216916398;
+}
+// T_p(u), p < 32, by the doubling ladder (T_2m = 2 T_m^2 - 1, T_2m+1 = 2 T_m T_m+1 - u) -- the MFMA spread's lanes
+// each need one p
+__device__ __forceinline__ double nu_cheb(double u, int p) {
+    double a = 1.0, b = u;  // (T_m, T_m+1), m = 0
+#pragma unroll
+    for (int bit = 4; bit >= 0; --bit) {
+        const double ab = fma(2.0 * a, b, -u);
+        if ((p >> bit) & 1) {
+            b = fma(2.0 * b, b, -1.0);
+            a = ab;
+        } else {
+            a = fma(2.0 * a, a, -1.0);
+            b = ab;
+        }
+    }
+    return a;
 }
 
 __device__ __forceinline__ int64_t nu_readlane64(int64_t v, int lane) {
@@ -208,11 +281,7 @@ __global__ __launch_bounds__(256) void k_nu_spread(const double* __restrict__ tt
                 const double uk = (double)(k0 + kk) * u1;
                 const double gk = rint(uk);
                 const double e = uk - gk;
-                const double e2 = e * e, e4 = e2 * e2, e8 = e4 * e4;
-                double a = (pp & 1) ? e : 1.0;
-                a = (pp & 2) ? a * e2 : a;
-                a = (pp & 4) ? a * e4 : a;
-                a = (pp & 8) ? a * e8 : a;
+                double a = nu_cheb(2.0 * e, pp);  // T_p(2e) (nu_bes)
                 a = (valid && pok) ? a : 0.0;
                 const double b = (valid && rowok) ? (reim ? ck.y : ck.x) : 0.0;
                 const int64_t G64 = (int64_t)gk;
@@ -272,7 +341,7 @@ __global__ __launch_bounds__(256) void k_nu_cellstart(const double* __restrict__
 }
 
 // L lanes per wrapped cell g sum, over its unwrapped cells G = g (mod n) and their photons in time order (lane s
-// takes the cell's photons s, s + L, ...), the moments c_r e^p of rows r < nrow: b_p,r[g] = sum c_{i,r} e_i^p with
+// takes the cell's photons s, s + L, ...), the moments c_r T_p(2e) of rows r < nrow: b_p,r[g] = sum c_{i,r} T_p(2e_i) with
 // c = e^{2 pi i k (fc dt + c2_r dt^2)}, e = k dt s1 - G, in registers; an xor butterfly over the L lanes (a fixed
 // order: deterministic) completes the sums and lane s writes the moments p = s (mod L) to W[p * nrow + r][g].
 // fp64 VALU throughout: per photon, row and harmonic one premultiplier phase and cis, then 3 operations per moment.
@@ -338,15 +407,20 @@ __global__ __launch_bounds__(256) void k_nu_gather(const double* __restrict__ tt
                     const double2 ca = nu_cis(stab, nu_frac_k(kd, phia));
                     double2 cb = nu_cis(stab, nu_frac_k(kd, phib));
                     if (!hb) cb = make_double2(0.0, 0.0);
-                    double epa = 1.0, epb = 1.0;
+                    // Chebyshev moments T_p(2e): T_p+1 = 4e T_p - T_p-1 (nu_bes)
+                    const double ua = 4.0 * ea, ub = 4.0 * eb;
+                    double ta0 = 1.0, ta1 = 2.0 * ea, tb0 = 1.0, tb1 = 2.0 * eb;
 #pragma unroll
                     for (int p = 0; p < PP; ++p) {
-                        ar[r][p] = fma(ca.x, epa, ar[r][p]);
-                        ai[r][p] = fma(ca.y, epa, ai[r][p]);
-                        ar[r][p] = fma(cb.x, epb, ar[r][p]);
-                        ai[r][p] = fma(cb.y, epb, ai[r][p]);
-                        epa *= ea;
-                        epb *= eb;
+                        ar[r][p] = fma(ca.x, ta0, ar[r][p]);
+                        ai[r][p] = fma(ca.y, ta0, ai[r][p]);
+                        ar[r][p] = fma(cb.x, tb0, ar[r][p]);
+                        ai[r][p] = fma(cb.y, tb0, ai[r][p]);
+                        const double ta2 = fma(ua, ta1, -ta0), tb2 = fma(ub, tb1, -tb0);
+                        ta0 = ta1;
+                        ta1 = ta2;
+                        tb0 = tb1;
+                        tb1 = tb2;
                     }
                 }
             }
@@ -692,7 +766,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 constexpr int kNuFusedPer = kNuTile / 256;  // positions per thread
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k_nu_fft_rows_combine(const double2* __restrict__ X, int ll, int lnfft, int P,
                                                              int nrow, int64_t nf, int64_t jhi, int64_t h,
-                                                             int64_t tbase, int64_t nbt, double2* __restrict__ CS) {
+                                                             int64_t tbase, int64_t nbt, const double* __restrict__ bc,
+                                                             double2* __restrict__ CS) {
     extern __shared__ double2 nu_s[];
     __shared__ NuTile tw;
     const int lt = lnfft < 12 ? lnfft : 12;
@@ -702,12 +777,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k
     const int64_t k1 = blockIdx.x;
     const int r = blockIdx.y;
     double2 acc[kNuFusedPer], nx[kNuFusedPer];
+    NuBes bs[kNuFusedPer];
     const double2* xr = X + (int64_t)r * nfft + (k1 << ll);  // moment p's row at xr + p nrow nfft
     const int64_t pstride = (int64_t)nrow * nfft;
 #pragma unroll
     for (int q = 0; q < kNuFusedPer; ++q) {
         acc[q] = make_double2(0.0, 0.0);
         const int e = threadIdx.x + 256 * q;
+        const int64_t J = k1 + ((int64_t)e << ln1);
+        bs[q] = nu_bes_start(bc, P, nu_zh(J <= jhi ? J : J - nfft, lnfft));
         nx[q] = e < L ? xr[(int64_t)(P - 1) * pstride + e] : make_double2(0.0, 0.0);
     }
     for (int p = P - 1; p >= 0; --p) {
@@ -723,7 +801,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k
         }
         __syncthreads();
         nu_fft_lds(nu_s, ll, 0, 1, L, &tw, lt);
-        const double ip = 1.0 / (double)(p + 1);
 #pragma unroll
         for (int q = 0; q < kNuFusedPer; ++q) {
             const int b = threadIdx.x + 256 * q;
@@ -731,9 +808,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k
                 const double2 v = nu_s[b];
                 const int64_t J = k1 + ((int64_t)b << ln1);
                 const int64_t jc = J <= jhi ? J : J - nfft;  // positions between the two ends hold no trial
-                // k_nu_combine's arithmetic exactly: th = (jc 2^-lnfft) 2 pi (exact scaling), f = th fl(1 / (p + 1))
-                const double f = (ldexp((double)jc, -lnfft) * 6.283185307179586476925286766559) * ip;
-                acc[q] = make_double2(fma(-f, acc[q].y, v.x), fma(f, acc[q].x, v.y));
+                // k_nu_combine's arithmetic exactly: eps_p i^p J_p(z), z/2 = (pi/2) jc / n (nu_bes_w)
+                acc[q] = nu_bes_acc(acc[q], nu_bes_w(bs[q], p, nu_zh(jc, lnfft)), v, p);
             }
         }
         __syncthreads();  // the next moment's store overwrites the tile
@@ -764,7 +840,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k
 __device__ __forceinline__ int nu_sw(int i) { return i ^ ((i >> 4) & 15); }
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k_nu_rows4096_combine(
     const double2* __restrict__ X, int lnfft, int P, int nrow, int64_t nf, int64_t jhi, int64_t h, int64_t tbase,
-    int64_t nbt, double2* __restrict__ CS) {
+    int64_t nbt, const double* __restrict__ bc, double2* __restrict__ CS) {
     extern __shared__ double2 nu_s[];  // [2][4096]
     __shared__ NuTile tw;
     nu_tile_init(&tw, 12);
@@ -778,9 +854,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k
     const double2* xr = X + (int64_t)r * nfft + (k1 << 12);
     const int64_t pstride = (int64_t)nrow * nfft;
     double2 acc[16], nx[16], v[16];
+    NuBes bs[16];
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
         acc[q] = make_double2(0.0, 0.0);
+        const int64_t J = k1 + ((int64_t)(t + 256 * q) << ln1);
+        bs[q] = nu_bes_start(bc, P, nu_zh(J <= jhi ? J : J - nfft, lnfft));
         nx[q] = xr[(int64_t)(P - 1) * pstride + t + 256 * q];
     }
     // twiddle indices of this thread's butterflies (units of w_4096): stage 2 w_256^{t & 15}, stage 3 w_4096^t
@@ -809,13 +888,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k
         for (int q = 0; q < 16; ++q) v[q] = B[nu_sw(t + 256 * q)];
         nu_twiddle<16>(nu_tw_tile(&tw, m3), v);
         nu_dft16(v);  // stage 3 (Ns = 256): output position t + 256 q
-        const double ip = 1.0 / (double)(p + 1);
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
             const int64_t J = k1 + ((int64_t)(t + 256 * q) << ln1);
             const int64_t jc = J <= jhi ? J : J - nfft;
-            const double f = (ldexp((double)jc, -lnfft) * 6.283185307179586476925286766559) * ip;
-            acc[q] = make_double2(fma(-f, acc[q].y, v[q].x), fma(f, acc[q].x, v[q].y));
+            acc[q] = nu_bes_acc(acc[q], nu_bes_w(bs[q], p, nu_zh(jc, lnfft)), v[q], p);
         }
     }
 #pragma unroll
@@ -841,7 +918,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k
 __device__ __forceinline__ int nu_sw8(int i) { return i ^ ((i >> 3) & 7); }
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k_nu_rows4096_combine8(
     const double2* __restrict__ X, int lnfft, int P, int nrow, int64_t nf, int64_t jhi, int64_t h, int64_t tbase,
-    int64_t nbt, double2* __restrict__ CS) {
+    int64_t nbt, const double* __restrict__ bc, double2* __restrict__ CS) {
     extern __shared__ double2 nu_s[];  // [2][4096]
     __shared__ NuTile tw;
     nu_tile_init(&tw, 12);
@@ -853,9 +930,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
     const double2* xr = X + (int64_t)r * nfft + (k1 << 12);
     const int64_t pstride = (int64_t)nrow * nfft;
     double2 acc[8], nx[8], v[8];
+    NuBes bs[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
         acc[q] = make_double2(0.0, 0.0);
+        const int64_t J = k1 + ((int64_t)(t + 512 * q) << ln1);
+        bs[q] = nu_bes_start(bc, P, nu_zh(J <= jhi ? J : J - nfft, lnfft));
         nx[q] = xr[(int64_t)(P - 1) * pstride + t + 512 * q];
     }
     const int m2 = (t & 7) << 6, m3 = (t & 63) << 3, m4 = t;  // stage twiddles in units of w_4096
@@ -893,13 +973,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
         for (int q = 0; q < 8; ++q) v[q] = A[nu_sw8(t + 512 * q)];
         nu_twiddle<8>(nu_tw_tile(&tw, m4), v);
         nu_dft8(v);  // stage 4 (Ns = 512): output position t + 512 q
-        const double ip = 1.0 / (double)(p + 1);
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
             const int64_t J = k1 + ((int64_t)(t + 512 * q) << ln1);
             const int64_t jc = J <= jhi ? J : J - nfft;
-            const double f = (ldexp((double)jc, -lnfft) * 6.283185307179586476925286766559) * ip;
-            acc[q] = make_double2(fma(-f, acc[q].y, v[q].x), fma(f, acc[q].x, v[q].y));
+            acc[q] = nu_bes_acc(acc[q], nu_bes_w(bs[q], p, nu_zh(jc, lnfft)), v[q], p);
         }
     }
 #pragma unroll
@@ -918,10 +996,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
 }
 
 // (C_k, S_k) of the trials of one harmonic: position pos = k1 n2 + k2 of the FFT output holds J = k1 + n1 k2
-// (ln1 = 0: natural order); J = jc mod n. Horner over the moments with z = 2 pi i jc / n.
+// (ln1 = 0: natural order); J = jc mod n. The moments' transforms weighted by eps_p i^p J_p(pi jc / n) (nu_bes).
 __global__ __launch_bounds__(256) void k_nu_combine(const double2* __restrict__ Z, int lnfft, int ln1, int P, int nrow,
                                                     int64_t nf, int64_t nseg, int64_t h, int64_t jbase, int64_t row0,
-                                                    int64_t tb0, int64_t nbt, double2* __restrict__ CS) {
+                                                    int64_t tb0, int64_t nbt, const double* __restrict__ bc,
+                                                    double2* __restrict__ CS) {
     const int64_t nfft = int64_t(1) << lnfft;
     const int64_t pos = (int64_t)blockIdx.x * 256 + threadIdx.x;
     const int row = blockIdx.y;
@@ -937,18 +1016,19 @@ __global__ __launch_bounds__(256) void k_nu_combine(const double2* __restrict__ 
         return;
     const int64_t t = (row0 + row) * nf + jbase + jc - tb0;
     if (t < 0 || t >= nbt) return;
-    const double th = ldexp((double)jc, -lnfft) * 6.283185307179586476925286766559;
-    double2 A = Z[((int64_t)(P - 1) * nrow + row) * nfft + pos];
-    for (int p = P - 2; p >= 0; --p) {
-        const double f = th * (1.0 / (double)(p + 1));
+    const double zh = nu_zh(jc, lnfft);
+    double2 A = make_double2(0.0, 0.0);
+    NuBes bs = nu_bes_start(bc, P, zh);
+    for (int p = P - 1; p >= 0; --p) {  // sum_p eps_p i^p J_p(z) B_p (nu_bes_w)
         const double2 b = Z[((int64_t)p * nrow + row) * nfft + pos];
-        A = make_double2(fma(-f, A.y, b.x), fma(f, A.x, b.y));
+        A = nu_bes_acc(A, nu_bes_w(bs, p, zh), b, p);
     }
     CS[t] = A;
 }
 
 // Z^2 / H of trials tb0 .. tb0+nbt-1 (flat, relative to the call's first) from CS[k][t], in the reference's formula
-// order, with the certificate: |A_k error| <= E = N (x^P / P! + kNuRho), x = pi |jc| / n, so Z2_k = (2/N)|A_k|^2
+// order, with the certificate: |A_k error| <= E = N (2.4 (x/2)^P / P! + kNuRho), x = pi |jc| / n (invfact =
+// 2.4 / (2^P P!), nu_trunc), so Z2_k = (2/N)|A_k|^2
 // errs by <= (2/N)(2 |A_k| E + E^2); Z^2 sums them, H = max_k g_k takes the largest bound among the g_k that the
 // errors could lift to the maximum (as k_search_finalize_exact). A trial whose bound exceeds rel |power| goes to the
 // fp64 fix-up list.
@@ -1020,14 +1100,16 @@ enum { kNuClsCellStart, kNuClsSpread, kNuClsMerge, kNuClsPass1, kNuClsPass2, kNu
 // ([1] the spread's bytes; class 0, the cell starts, is not counted)
 static double g_nu_work[kNuCls] = {0, 0, 0, 0, 0, 0, 0};
 
-static double nu_trunc(double x, int P, double* invfact) {  // x^P / P!
+// truncation bound of P Chebyshev moments per unit photon weight at x = pi |jc| / n: 2.4 (x/2)^P / P! (nu_bes);
+// invfact = 2.4 / (2^P P!), so that k_nu_finalize's x^P invfact is the bound
+static double nu_trunc(double x, int P, double* invfact) {
     double f = 1.0, xp = 1.0;
     for (int p = 1; p <= P; ++p) {
-        f *= (double)p;
+        f *= 2.0 * (double)p;
         xp *= x;
     }
-    *invfact = 1.0 / f;
-    return xp / f;
+    *invfact = 2.4 / f;
+    return 2.4 * xp / f;
 }
 
 static int ilog2(int64_t v) {
@@ -1039,7 +1121,7 @@ static int ilog2(int64_t v) {
 // per-call twiddle (w_n^t) and cis tables, fp64 from long double
 // Twiddle (w_n, two-level) and cis tables for n = 2^lnfft, built once per device and n (long double on the host) and
 // kept for the process: a search reuses them without an upload.
-static int nu_tables(Scratch& sc, hipStream_t s, int lnfft, NuTw* T, const double2** cis) {
+static int nu_tables(Scratch& sc, hipStream_t s, int lnfft, NuTw* T, const double2** cis, const double** bc) {
     (void)sc;
     static std::mutex mu;
     static std::map<std::pair<int, int>, double2*> cache;
@@ -1054,7 +1136,7 @@ static int nu_tables(Scratch& sc, hipStream_t s, int lnfft, NuTw* T, const doubl
         if (it != cache.end()) {
             d = it->second;
         } else {
-            std::vector<double2> h((size_t)(nlo + nhi + 1024));
+            std::vector<double2> h((size_t)(nlo + nhi + 1024 + kNuBesP * kNuBesM / 2));
             const long double tp = 6.283185307179586476925286766559L;
             const long double nf = (long double)(int64_t(1) << lnfft);
             for (int64_t i = 0; i < nlo; ++i) {
@@ -1069,6 +1151,15 @@ static int nu_tables(Scratch& sc, hipStream_t s, int lnfft, NuTw* T, const doubl
                 const long double a = tp * (long double)i / 1024.0L;
                 h[(size_t)(nlo + nhi + i)] = make_double2((double)cosl(a), (double)sinl(a));
             }
+            // nu_bes_series coefficients 1 / (m! (m+p)!), [p][m]
+            double* bco = reinterpret_cast<double*>(h.data() + nlo + nhi + 1024);
+            for (int p = 0; p < kNuBesP; ++p)
+                for (int m = 0; m < kNuBesM; ++m) {
+                    long double f = 1.0L;
+                    for (int q = 2; q <= m; ++q) f *= (long double)q;
+                    for (int q = 2; q <= m + p; ++q) f *= (long double)q;
+                    bco[p * kNuBesM + m] = (double)(1.0L / f);
+                }
             HIPCHK(hipMalloc(&d, h.size() * sizeof(double2)));
             HIPCHK(hipMemcpyAsync(d, h.data(), h.size() * sizeof(double2), hipMemcpyHostToDevice, s));
             HIPCHK(hipStreamSynchronize(s));  // h is pageable and local
@@ -1080,6 +1171,7 @@ static int nu_tables(Scratch& sc, hipStream_t s, int lnfft, NuTw* T, const doubl
     T->lbits = lbits;
     T->mask = (int64_t(1) << lnfft) - 1;
     *cis = d + nlo + nhi;
+    *bc = reinterpret_cast<const double*>(d + nlo + nhi + 1024);
     return CRIMP_OK;
 }
 
@@ -1175,7 +1267,7 @@ struct NuPlan {
     std::vector<int64_t> gmin, gmax;                     // unwrapped cells of dt[0], dt[n-1] per harmonic
 };
 
-// n and P: among the powers of two n >= nseg (up to 2^24) whose edge truncation x^P / P! <= kNuEps within P <= pmax
+// n and P: among the powers of two n >= nseg (up to 2^24) whose edge truncation (nu_trunc) <= kNuEps within P <= pmax
 // moments, the one with the least FFT work n P; false when none exists or the photons wrap the grid more than
 // kNuMaxWrap times
 static bool nu_plan(NuPlan* pl, double delta, double f0, double dt0, double dtn, int nharm, int64_t nchunk, int pmax) {
@@ -1407,9 +1499,10 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
     int cur_lnfft = -1;
     NuTw T{};
     const double2* cis = nullptr;
+    const double* bc = nullptr;
     for (const NuPlan& pl : plans) {
         if (pl.lnfft != cur_lnfft) {  // tables for this group's n (a group's first launch follows their upload)
-            const int rc = nu_tables(sc, s, pl.lnfft, &T, &cis);
+            const int rc = nu_tables(sc, s, pl.lnfft, &T, &cis, &bc);
             if (rc) return rc;
             cur_lnfft = pl.lnfft;
         }
@@ -1450,7 +1543,7 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
             if (fused_combine && ln2 == 12 && rows4096 && rows_r8) {  // 512 threads, radix 8
                 g_nu_work[kNuClsPass2] += plane + 16.0 * (double)nbt;
                 k_nu_rows4096_combine8<<<dim3((unsigned)(int64_t(1) << ln1), (unsigned)nrow), 512, 2 * lds_fft, s>>>(
-                    Zo, lnfft, P, nrow, nf, pl.nseg - 1 - pl.h, pl.h, rb * nf + jbase - (tb0 + first), nbt,
+                    Zo, lnfft, P, nrow, nf, pl.nseg - 1 - pl.h, pl.h, rb * nf + jbase - (tb0 + first), nbt, bc,
                     CS + (int64_t)(k - 1) * nbt);
                 HIPCHK(hipGetLastError());
                 HIPCHK(span(kNuClsPass2));
@@ -1459,7 +1552,7 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
             if (fused_combine && ln2 == 12 && rows4096) {  // the specialised form for 4096-element rows
                 g_nu_work[kNuClsPass2] += plane + 16.0 * (double)nbt;
                 k_nu_rows4096_combine<<<dim3((unsigned)(int64_t(1) << ln1), (unsigned)nrow), 256, 2 * lds_fft, s>>>(
-                    Zo, lnfft, P, nrow, nf, pl.nseg - 1 - pl.h, pl.h, rb * nf + jbase - (tb0 + first), nbt,
+                    Zo, lnfft, P, nrow, nf, pl.nseg - 1 - pl.h, pl.h, rb * nf + jbase - (tb0 + first), nbt, bc,
                     CS + (int64_t)(k - 1) * nbt);
                 HIPCHK(hipGetLastError());
                 HIPCHK(span(kNuClsPass2));
@@ -1468,7 +1561,7 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
             if (fused_combine) {  // pass 2 and the moments' Horner sum in one kernel
                 g_nu_work[kNuClsPass2] += plane + 16.0 * (double)nbt;
                 k_nu_fft_rows_combine<<<dim3((unsigned)(int64_t(1) << ln1), (unsigned)nrow), 256, lds_fft, s>>>(
-                    Zo, ln2, lnfft, P, nrow, nf, pl.nseg - 1 - pl.h, pl.h, rb * nf + jbase - (tb0 + first), nbt,
+                    Zo, ln2, lnfft, P, nrow, nf, pl.nseg - 1 - pl.h, pl.h, rb * nf + jbase - (tb0 + first), nbt, bc,
                     CS + (int64_t)(k - 1) * nbt);
                 HIPCHK(hipGetLastError());
                 HIPCHK(span(kNuClsPass2));
@@ -1480,7 +1573,8 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
             HIPCHK(hipGetLastError());
             HIPCHK(span(kNuClsPass2));
             k_nu_combine<<<dim3((unsigned)cdiv(nfft, 256), (unsigned)nrow), 256, 0, s>>>(
-                Zo, lnfft, ln1, P, nrow, nf, pl.nseg, pl.h, jbase, rb, tb0 + first, nbt, CS + (int64_t)(k - 1) * nbt);
+                Zo, lnfft, ln1, P, nrow, nf, pl.nseg, pl.h, jbase, rb, tb0 + first, nbt, bc,
+                CS + (int64_t)(k - 1) * nbt);
             HIPCHK(hipGetLastError());
             HIPCHK(span(kNuClsCombine));
             return CRIMP_OK;
