@@ -54,8 +54,8 @@ PMC_FILE = os.path.join(ROOT, "profiles", "r04", "pmc_traffic.json")
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=5)
-    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--photons", type=int, default=10_000_000)
     p.add_argument("--trials", type=int, default=1_000_000, help="trial frequencies per GPU")
     p.add_argument("--nharm", type=int, default=2)
