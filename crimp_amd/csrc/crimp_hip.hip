@@ -1720,24 +1720,26 @@ static int fixup_search(Scratch& sc, hipStream_t s, const double* dt, const doub
 // (a NUFFT search) the NUFFT's own checks -- photon order and the grid scalars (k_nu_sorted, k_nu_scalars) -- are
 // queued behind it and read back in the same transfer: nu_hs = [delta, f0, dt[0], dt[n-1], unsorted flag].
 static int grid_is_progression(Scratch& sc, hipStream_t s, const double* freq, int64_t nf, double** ap, bool* ok,
-                               const double* nu_t = nullptr, double t0 = 0.0, int64_t n = 0, double* nu_hs = nullptr);
+                               const double* nu_t = nullptr, double t0 = 0.0, int64_t n = 0, double* nu_hs = nullptr,
+                               bool nu_sorted_check = true);
 #include "search_nufft.h"
 static int grid_is_progression(Scratch& sc, hipStream_t s, const double* freq, int64_t nf, double** ap, bool* ok,
-                               const double* nu_t, double t0, int64_t n, double* nu_hs) {
+                               const double* nu_t, double t0, int64_t n, double* nu_hs, bool nu_sorted_check) {
     *ok = false;
     unsigned long long* info = nullptr;
     HIPCHK(sc.alloc(&info, 3 + 6));
     *ap = reinterpret_cast<double*>(info);
     if (nf < 2) return CRIMP_OK;
     HIPCHK(hipMemsetAsync(info, 0, (3 + 6) * sizeof(unsigned long long), s));
-    k_ap_check<<<(unsigned)std::min<int64_t>(cdiv(nf, 256), 128), 256, 0, s>>>(freq, nf, info);
+    k_ap_check<<<(unsigned)std::min<int64_t>(cdiv(nf, 256), 512), 256, 0, s>>>(freq, nf, info);
     HIPCHK(hipGetLastError());
     double h[3 + 5];
     size_t bytes = 3 * sizeof(double);
     if (nu_t) {
         double* dsc = reinterpret_cast<double*>(info + 3);
-        k_nu_sorted<<<(unsigned)std::min<int64_t>(cdiv(n, 256), 2048), 256, 0, s>>>(nu_t, t0, n,
-                                                                                  reinterpret_cast<int*>(dsc + 4));
+        if (nu_sorted_check)
+            k_nu_sorted<<<(unsigned)std::min<int64_t>(cdiv(n, 256), 2048), 256, 0, s>>>(nu_t, t0, n,
+                                                                                      reinterpret_cast<int*>(dsc + 4));
         k_nu_scalars<<<1, 64, 0, s>>>(*ap, freq, nu_t, t0, n, dsc);
         HIPCHK(hipGetLastError());
         bytes = sizeof(h);
@@ -1981,7 +1983,8 @@ extern "C" int crimp_search(const double* t, int64_t n, double t0, const double*
         double nu_hs[5] = {0, 0, 0, 0, 0};
         if (factorised) {
             bool ok = false;
-            int rc = grid_is_progression(sc, s, dfr, nf, &ap, &ok, nufft ? dtm : nullptr, t0, n, nu_hs);
+            int rc = grid_is_progression(sc, s, dfr, nf, &ap, &ok, nufft ? dtm : nullptr, t0, n, nu_hs,
+                                         !nu_gather_form(twod ? nfd : 1));
             if (rc) return rc;
             factorised = ok;
         }

@@ -322,11 +322,18 @@ constexpr int kNuCellK = 4;
 struct NuCellArgs {
     int64_t gmin[kNuCellK], span[kNuCellK], off[kNuCellK];
 };
+// The cell gather's plans take the photon order from here too (no k_nu_sorted pass): a pair out of order sets *bad
+// (the search then takes the default path) and the writes stay inside the tables, which the host zeroes first, so
+// every entry is a photon index in [0, n] whatever the order.
 __global__ __launch_bounds__(256) void k_nu_cellstart(const double* __restrict__ tt, double t0, int64_t n, double s1,
-                                                      int k0, int nk, NuCellArgs a, int64_t* __restrict__ start) {
+                                                      int k0, int nk, NuCellArgs a, int64_t* __restrict__ start,
+                                                      int* __restrict__ bad) {
+    int b = 0;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const double u = (tt[i] - t0) * s1;
-        const double up = i == 0 ? 0.0 : (tt[i - 1] - t0) * s1;
+        const double d = tt[i] - t0, dp = i == 0 ? d : tt[i - 1] - t0;
+        b |= !(dp <= d);
+        const double u = d * s1;
+        const double up = dp * s1;
 #pragma unroll
         for (int j = 0; j < kNuCellK; ++j) {
             if (j >= nk) break;
@@ -334,10 +341,13 @@ __global__ __launch_bounds__(256) void k_nu_cellstart(const double* __restrict__
             const int64_t g = (int64_t)rint(kd * u);
             const int64_t gp = i == 0 ? a.gmin[j] - 1 : (int64_t)rint(kd * up);
             int64_t* st = start + a.off[j];
-            for (int64_t G = gp + 1; G <= g; ++G) st[G - a.gmin[j]] = i;
+            const int64_t lo = gp + 1 > a.gmin[j] ? gp + 1 : a.gmin[j];
+            const int64_t hi = g < a.gmin[j] + a.span[j] - 1 ? g : a.gmin[j] + a.span[j] - 1;
+            for (int64_t G = lo; G <= hi; ++G) st[G - a.gmin[j]] = i;
             if (i == n - 1) st[a.span[j]] = n;
         }
     }
+    if (__any(b) && (threadIdx.x & 63) == 0) atomicOr(bad, 1);
 }
 
 // L lanes per wrapped cell g sum, over its unwrapped cells G = g (mod n) and their photons in time order (lane s
@@ -1315,7 +1325,18 @@ static bool nu_plan(NuPlan* pl, double delta, double f0, double dt0, double dtn,
 // Z^2 / H by NUFFT over trials [first, first + count) of the fd-outer grid (nf trials per row, arithmetic
 // progression with step ap[0]). *applicable = false (nothing computed) for unsorted photons or an out-of-range plan:
 // the caller takes the exact path.
-// hs: [delta, f0, dt[0], dt[n-1], unsorted flag (int bits)] as grid_is_progression read them back.
+// The spread form of a grid of nrows_grid rows: the cell gather for <= kNuGatherRows rows, the MFMA slots otherwise
+// (CRIMP_NUFFT_SPREAD=gather|mfma forces one, a test hook). Decided from the whole grid, so that row shards compute
+// exactly what the whole grid does.
+static bool nu_gather_form(int64_t nrows_grid) {
+    const char* spread_env = getenv("CRIMP_NUFFT_SPREAD");
+    return spread_env && !strcmp(spread_env, "gather")  ? true
+           : spread_env && !strcmp(spread_env, "mfma") ? false
+                                                       : nrows_grid <= kNuGatherRows;
+}
+
+// hs: [delta, f0, dt[0], dt[n-1], unsorted flag (int bits)] as grid_is_progression read them back (the flag only for
+// MFMA-slot plans: a cell-gather plan checks the order in its cell-start pass).
 // t: photon times (seconds), t0 the search's reference time: the kernels form dt = t - t0 as k_search_prep does;
 // dt (and dt^2) arrays are made only for a fix-up.
 static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, int64_t n, const double* freq,
@@ -1332,10 +1353,7 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
     // spread form: the cell gather (VALU, one lane per wrapped cell) for grids of <= kNuGatherRows rows, the MFMA
     // slots otherwise -- decided from the whole grid, so that row shards compute exactly what the whole grid does
     // (CRIMP_NUFFT_SPREAD=gather|mfma forces one, a test hook)
-    const char* spread_env = getenv("CRIMP_NUFFT_SPREAD");
-    const bool gather_grid = spread_env && !strcmp(spread_env, "gather")  ? true
-                             : spread_env && !strcmp(spread_env, "mfma") ? false
-                                                                         : nrows_grid <= kNuGatherRows;
+    const bool gather_grid = nu_gather_form(nrows_grid);
     // row groups: the first row's segment, the full rows between, the last row's segment
     const int64_t r_lo = first / nf, r_hi = (first + count - 1) / nf;
     std::vector<NuPlan> plans;
@@ -1442,8 +1460,8 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
     int64_t* ctab = nullptr;
     int64_t* cstart = nullptr;
     int64_t* flagged = nullptr;
-    int* nflag = nullptr;
-    HIPCHK(sc.alloc(&nflag, 1));
+    int* nflag = nullptr;  // [fix-up count, photons out of order (cell-gather plans)]
+    HIPCHK(sc.alloc(&nflag, 2));
     if (any_mfma) {
         HIPCHK(sc.alloc(&U, (size_t)(ubytes / 8)));
         HIPCHK(sc.alloc(&ctab, (size_t)(2 * 8 * nchunk)));
@@ -1495,7 +1513,7 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
         evcls.push_back(cls);
         return mark();
     };
-    HIPCHK(hipMemsetAsync(nflag, 0, sizeof(int), s));
+    HIPCHK(hipMemsetAsync(nflag, 0, 2 * sizeof(int), s));
     int cur_lnfft = -1;
     NuTw T{};
     const double2* cis = nullptr;
@@ -1591,6 +1609,7 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
         if (use_gather(pl)) {
             std::vector<int64_t> soff((size_t)nharm);
             int64_t off = 0;
+            HIPCHK(hipMemsetAsync(cstart, 0, (size_t)starts_max * sizeof(int64_t), s));
             for (int k0 = 1; k0 <= nharm; k0 += kNuCellK) {
                 NuCellArgs ca{};
                 const int nk = std::min(kNuCellK, nharm - k0 + 1);
@@ -1603,7 +1622,7 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
                     off += ca.span[j] + 1;
                 }
                 k_nu_cellstart<<<(unsigned)std::min<int64_t>(cdiv(n, 256), 8192), 256, 0, s>>>(t, t0, n, pl.s1, k0, nk,
-                                                                                              ca, cstart);
+                                                                                              ca, cstart, nflag + 1);
                 HIPCHK(hipGetLastError());
             }
             HIPCHK(span(kNuClsCellStart));
@@ -1702,8 +1721,14 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
         for (double v : cls) g_kernel_times.push_back(v);
         for (double v : cnt) g_kernel_times.push_back(v);
     }
-    int nf_h = 0;
-    HIPCHK(d2h(s, &nf_h, nflag, sizeof(int)));
+    int fl[2] = {0, 0};
+    HIPCHK(d2h(s, fl, nflag, sizeof(fl)));
+    if (fl[1]) {  // photons out of order (found by the cell starts): nothing computed, the default path runs
+        *applicable = false;
+        g_last_search_path = 0;
+        return CRIMP_OK;
+    }
+    const int nf_h = fl[0];
     *nfixed = nf_h;
     if (nf_h == 0 || no_fixup) return CRIMP_OK;
     double *dt = nullptr, *dt2 = nullptr;  // the fix-up's fp64 kernel reads dt (and dt^2) arrays
