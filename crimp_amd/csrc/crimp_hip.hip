@@ -2504,6 +2504,7 @@ static int toa_fit_impl(const double* x, const int64_t* offsets, int64_t nint, c
         // auxiliary stream and the caller stream's wait for it, dcnt stays held until the histogram has finished
         EventGuard ebin;
         ebin.wait = true;
+        bool hist_pending = false;
         if (rq) {
             HIPCHK(stage_in(sc, rq->edges, (size_t)rq->nbins + 1, dev, &dedg));
             HIPCHK(stage_in(sc, rq->centers, (size_t)rq->nbins, dev, &dcen));
@@ -2511,17 +2512,9 @@ static int toa_fit_impl(const double* x, const int64_t* offsets, int64_t nint, c
             HIPCHK(sc.alloc(&dcnt, (size_t)(nint * rq->nbins)));
             HIPCHK(hipMemsetAsync(dcnt, 0, (size_t)(nint * rq->nbins) * sizeof(unsigned long long), s));
             if (!(flags & CRIMP_FLAG_TIME_KERNELS)) {
-                hipStream_t s1 = aux_stream();
-                if (!s1) return set_err(CRIMP_ERR_HIP, "cannot create the auxiliary stream");
-                EventGuard e0;
-                HIPCHK(hipEventCreateWithFlags(&e0.e, hipEventDisableTiming));
-                HIPCHK(hipEventRecord(e0.e, s));
-                HIPCHK(hipStreamWaitEvent(s1, e0.e, 0));
-                k_binphases<<<dim3((unsigned)nint, (unsigned)bin_splits(hoff[nint], nint)), 64 * kBinWaves, 0, s1>>>(
-                    dx, doff, dedg, rq->nbins, dcnt);
-                HIPCHK(hipGetLastError());
-                HIPCHK(hipEventCreateWithFlags(&ebin.e, hipEventDisableTiming));
-                HIPCHK(hipEventRecord(ebin.e, s1));
+                // launched by launch_hist() once the grid's uploads are queued: launched here, its blocks held every
+                // CU while the uploads' copy kernels waited for one (the grid started ~180 us late, rocprofv3 trace)
+                hist_pending = true;
             } else {
                 k_binphases<<<dim3((unsigned)nint, (unsigned)bin_splits(hoff[nint], nint)), 64 * kBinWaves, 0, s>>>(
                     dx, doff, dedg, rq->nbins, dcnt);
@@ -2820,6 +2813,19 @@ static int toa_fit_impl(const double* x, const int64_t* offsets, int64_t nint, c
             return r2;
         };
         ht.mark("setup");
+        if (hist_pending) {  // redChi2's histogram on the auxiliary stream, beside the grid and the fits
+            hipStream_t s1 = aux_stream();
+            if (!s1) return set_err(CRIMP_ERR_HIP, "cannot create the auxiliary stream");
+            EventGuard e0;
+            HIPCHK(hipEventCreateWithFlags(&e0.e, hipEventDisableTiming));
+            HIPCHK(hipEventRecord(e0.e, s));
+            HIPCHK(hipStreamWaitEvent(s1, e0.e, 0));
+            k_binphases<<<dim3((unsigned)nint, (unsigned)bin_splits(hoff[nint], nint)), 64 * kBinWaves, 0, s1>>>(
+                dx, doff, dedg, rq->nbins, dcnt);
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipEventCreateWithFlags(&ebin.e, hipEventDisableTiming));
+            HIPCHK(hipEventRecord(ebin.e, s1));
+        }
         rc = all(grid_mode);
         if (rc) return rc;
         ht.mark("launch");
