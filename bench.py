@@ -49,6 +49,10 @@ PEAK_VALU_SLOTS = 256 * 4 * 32 * 2.4e9   # fp32 lane-ops/s: 256 CUs x 4 SIMD-32 
 PEAK_F64_OPS = 256 * 64 * 2.4e9          # fp64 FMA-rate lane-ops/s: half the fp32 rate (78.6 TFLOP/s fp64 vector)
 PEAK_F16_TFLOPS = 2500.0                 # MI355X_MICROARCH.md: dense F16/BF16 MFMA ~2.5 PFLOP/s
 PMC_FILE = os.path.join(ROOT, "profiles", "r04", "pmc_traffic.json")
+PMC_NUFFT_FILE = os.path.join(ROOT, "profiles", "r05", "pmc_nufft_traffic.json")
+# the kernel behind each NUFFT class on the config-3 plan (cell gather, n1 = 256 columns, 4096-element rows)
+NUFFT_CLASS_KERNEL = {"cellstart": "k_nu_cellstart", "spread": "k_nu_gather", "pass1": "k_nu_cols256",
+                      "pass2": "k_nu_rows4096_combine8", "finalize": "k_nu_finalize"}
 
 
 def parse():
@@ -589,6 +593,16 @@ def nufft_leg(a, t, t_h, f, rank, M, steps):
                             "peak": PEAK_HBM_GBS, "unit": "GB/s", "work_per_launch": per_launch})
             leg["frac"] = leg["achieved"] / leg["peak"]
         legs[name] = leg
+    # HBM bytes per launch from the tree's PMC pass on this workload (tools/pmc_nufft.sh -> pmc_nufft_traffic.json)
+    try:
+        pm = json.load(open(PMC_NUFFT_FILE))
+        if (pm.get("photons"), pm.get("trials"), pm.get("nharm")) == (a.photons, M, m) and form == "gather":
+            for name, leg in legs.items():
+                kn = pm["kernels"].get(NUFFT_CLASS_KERNEL.get(name, ""), {})
+                if "bytes_per_launch" in kn:
+                    leg["traffic"] = kn["bytes_per_launch"]
+    except (OSError, ValueError, KeyError):
+        pass
     dom = max((k for k in legs if "frac" in legs[k]), key=lambda k: legs[k]["ms"])
     return {"evals_per_s": float(a.photons) * M / wall, "unit": "equivalent photon*trial evals/s (Z^2_%d)" % m,
             "ms_per_search": wall * 1e3, "pipeline_ms": float(sp[0]), "search_path": path, "fp64_fixup_trials": nfix,
@@ -760,10 +774,13 @@ def main():
         else:
             # the NUFFT's per-kernel rooflines from separately timed searches (hipEvent spans per kernel class)
             nu = nufft_leg(a, t, t_h, f, rank, M, max(3, a.steps))
-            rec["roofline"] = dict(nu["roofline"], traffic=None, step_ms=step_ms,
+            rec["roofline"] = dict(nu["roofline"], step_ms=step_ms,
                                    note="dominant kernel class of the NUFFT search (DESIGN.md 5.3): algorithmic "
                                         "work per launch (crimp_last_nufft_work) / mean launch duration (hipEvents "
-                                        "on the library's stream); all classes under `nufft.kernels`")
+                                        "on the library's stream); all classes under `nufft.kernels`; traffic: HBM "
+                                        "bytes per launch, rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (x2 FETCH gfx950 "
+                                        "correction) of the same kernel, profiles/r05/pmc_nufft_traffic.json")
+            rec["roofline"].setdefault("traffic", None)
             rec["nufft"] = nu
             if exact is not None:
                 rec["exact_path"] = exact
