@@ -86,6 +86,19 @@ __device__ __forceinline__ double2 nu_cis(const double2* __restrict__ tab, doubl
     return make_double2(T.x * c - T.y * s, T.x * s + T.y * c);
 }
 
+// e^{2 pi i x}, |x| <= 0.5 (+ a few ulp), from a 2048-entry table (the cell gather keeps it in LDS) and the residual
+// series to degree 4 / 5 (|theta| <= pi/2048: omitted terms < 2e-20)
+__device__ __forceinline__ double2 nu_cis2(const double2* __restrict__ tab, double x) {
+    const double t = rint(x * 2048.0);
+    const double r = fma(t, -1.0 / 2048.0, x);  // exact
+    const double th = r * 6.283185307179586476925286766559;
+    const double t2 = th * th;
+    const double c = fma(t2, fma(t2, 1.0 / 24.0, -0.5), 1.0);
+    const double s = th * fma(t2, fma(t2, 1.0 / 120.0, -1.0 / 6.0), 1.0);
+    const double2 T = tab[((int)t) & 2047];
+    return make_double2(T.x * c - T.y * s, T.x * s + T.y * c);
+}
+
 // frac(a * d) for a = ahi + alo (double-double), as hi part reduced exactly plus the product's rounding error.
 // Contraction off: fused into fma(ahi, d, -rint(p)), the reduction would already hold the rounding error that pe
 // adds again (a phase error of ulp(a d), ~1e-11 cycles at config-3 arguments).
@@ -230,7 +243,7 @@ __global__ __launch_bounds__(256) void k_nu_spread(const double* __restrict__ tt
 #pragma unroll
         for (int kk = 0; kk < G; ++kk) {
             acc[kk] = nu_f64x4{0.0, 0.0, 0.0, 0.0};
-            gcur[kk] = (int64_t)rint((double)(k0 + kk) * u1);
+            gcur[kk] = (int)rint((double)(k0 + kk) * u1);  // cells fit 32 bits (k_nu_cellstart)
             if (lane == 0) ctab[(kk * nchunk + c) * 2] = gcur[kk];  // the chunk's first cell
         }
     }
@@ -284,7 +297,7 @@ __global__ __launch_bounds__(256) void k_nu_spread(const double* __restrict__ tt
                 double a = nu_cheb(2.0 * e, pp);  // T_p(2e) (nu_bes)
                 a = (valid && pok) ? a : 0.0;
                 const double b = (valid && rowok) ? (reim ? ck.y : ck.x) : 0.0;
-                const int64_t G64 = (int64_t)gk;
+                const int64_t G64 = (int)gk;  // cells fit 32 bits (k_nu_cellstart)
                 const int64_t g0 = nu_readlane64(G64, 0), g3 = nu_readlane64(G64, 48);
                 if (g0 == gcur[kk] && g3 == gcur[kk]) {
                     acc[kk] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[kk], 0, 0, 0);
@@ -338,8 +351,9 @@ __global__ __launch_bounds__(256) void k_nu_cellstart(const double* __restrict__
         for (int j = 0; j < kNuCellK; ++j) {
             if (j >= nk) break;
             const double kd = (double)(k0 + j);
-            const int64_t g = (int64_t)rint(kd * u);
-            const int64_t gp = i == 0 ? a.gmin[j] - 1 : (int64_t)rint(kd * up);
+            // cells fit 32 bits (nu_plan: |G| <= 32 n / 2 <= 2^28): one v_cvt_i32_f64, not the int64 conversion
+            const int64_t g = (int)rint(kd * u);
+            const int64_t gp = i == 0 ? a.gmin[j] - 1 : (int)rint(kd * up);
             int64_t* st = start + a.off[j];
             const int64_t lo = gp + 1 > a.gmin[j] ? gp + 1 : a.gmin[j];
             const int64_t hi = g < a.gmin[j] + a.span[j] - 1 ? g : a.gmin[j] + a.span[j] - 1;
@@ -363,8 +377,8 @@ __global__ __launch_bounds__(256) void k_nu_gather(const double* __restrict__ tt
                                                    int64_t gcount, double s1, double fch, double fcl,
                                                    const double* __restrict__ c2row, int nrow, int k, int P,
                                                    const double2* __restrict__ tab, double2* __restrict__ W) {
-    __shared__ double2 stab[1024];  // the cis table (nu_cis), read per photon: LDS, not L2 latency
-    for (int e = threadIdx.x; e < 1024; e += 256) stab[e] = tab[e];
+    __shared__ double2 stab[2048];  // the cis table (nu_cis2), read per photon: LDS, not L2 latency
+    for (int e = threadIdx.x; e < 2048; e += 256) stab[e] = tab[e];
     __syncthreads();
     const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x;
     const int64_t idx = tid / L;
@@ -414,8 +428,8 @@ __global__ __launch_bounds__(256) void k_nu_gather(const double* __restrict__ tt
                     }
                     phia -= rint(phia);
                     phib -= rint(phib);
-                    const double2 ca = nu_cis(stab, nu_frac_k(kd, phia));
-                    double2 cb = nu_cis(stab, nu_frac_k(kd, phib));
+                    const double2 ca = nu_cis2(stab, nu_frac_k(kd, phia));
+                    double2 cb = nu_cis2(stab, nu_frac_k(kd, phib));
                     if (!hb) cb = make_double2(0.0, 0.0);
                     // Chebyshev moments T_p(2e): T_p+1 = 4e T_p - T_p-1 (nu_bes)
                     const double ua = 4.0 * ea, ub = 4.0 * eb;
@@ -1131,7 +1145,8 @@ static int ilog2(int64_t v) {
 // per-call twiddle (w_n^t) and cis tables, fp64 from long double
 // Twiddle (w_n, two-level) and cis tables for n = 2^lnfft, built once per device and n (long double on the host) and
 // kept for the process: a search reuses them without an upload.
-static int nu_tables(Scratch& sc, hipStream_t s, int lnfft, NuTw* T, const double2** cis, const double** bc) {
+static int nu_tables(Scratch& sc, hipStream_t s, int lnfft, NuTw* T, const double2** cis, const double** bc,
+                     const double2** cis2) {
     (void)sc;
     static std::mutex mu;
     static std::map<std::pair<int, int>, double2*> cache;
@@ -1146,7 +1161,7 @@ static int nu_tables(Scratch& sc, hipStream_t s, int lnfft, NuTw* T, const doubl
         if (it != cache.end()) {
             d = it->second;
         } else {
-            std::vector<double2> h((size_t)(nlo + nhi + 1024 + kNuBesP * kNuBesM / 2));
+            std::vector<double2> h((size_t)(nlo + nhi + 1024 + kNuBesP * kNuBesM / 2 + 2048));
             const long double tp = 6.283185307179586476925286766559L;
             const long double nf = (long double)(int64_t(1) << lnfft);
             for (int64_t i = 0; i < nlo; ++i) {
@@ -1170,6 +1185,10 @@ static int nu_tables(Scratch& sc, hipStream_t s, int lnfft, NuTw* T, const doubl
                     for (int q = 2; q <= m + p; ++q) f *= (long double)q;
                     bco[p * kNuBesM + m] = (double)(1.0L / f);
                 }
+            for (int i = 0; i < 2048; ++i) {  // nu_cis2
+                const long double a = tp * (long double)i / 2048.0L;
+                h[(size_t)(nlo + nhi + 1024 + kNuBesP * kNuBesM / 2 + i)] = make_double2((double)cosl(a), (double)sinl(a));
+            }
             HIPCHK(hipMalloc(&d, h.size() * sizeof(double2)));
             HIPCHK(hipMemcpyAsync(d, h.data(), h.size() * sizeof(double2), hipMemcpyHostToDevice, s));
             HIPCHK(hipStreamSynchronize(s));  // h is pageable and local
@@ -1182,6 +1201,7 @@ static int nu_tables(Scratch& sc, hipStream_t s, int lnfft, NuTw* T, const doubl
     T->mask = (int64_t(1) << lnfft) - 1;
     *cis = d + nlo + nhi;
     *bc = reinterpret_cast<const double*>(d + nlo + nhi + 1024);
+    *cis2 = d + nlo + nhi + 1024 + kNuBesP * kNuBesM / 2;
     return CRIMP_OK;
 }
 
@@ -1517,10 +1537,11 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
     int cur_lnfft = -1;
     NuTw T{};
     const double2* cis = nullptr;
+    const double2* cis2 = nullptr;
     const double* bc = nullptr;
     for (const NuPlan& pl : plans) {
         if (pl.lnfft != cur_lnfft) {  // tables for this group's n (a group's first launch follows their upload)
-            const int rc = nu_tables(sc, s, pl.lnfft, &T, &cis, &bc);
+            const int rc = nu_tables(sc, s, pl.lnfft, &T, &cis, &bc, &cis2);
             if (rc) return rc;
             cur_lnfft = pl.lnfft;
         }
@@ -1647,7 +1668,7 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
                     g_nu_work[kNuClsSpread] += 8.0 * (double)n + 16.0 * (double)P * nrow * (double)gcount;
                     launch_gather(L, twod, gcount, t, t0, cstart + soff[(size_t)(k - 1)], pl.gmin[(size_t)(k - 1)],
                                   pl.gmax[(size_t)(k - 1)], nfft, gbase, pl.s1, pl.fch, pl.fcl,
-                                  twod ? c2 + rb : nullptr, nrow, k, P, cis, W, s);
+                                  twod ? c2 + rb : nullptr, nrow, k, P, cis2, W, s);
                     HIPCHK(hipGetLastError());
                     HIPCHK(span(kNuClsSpread));
                     int rc = fft_combine(k, rb, nrow, tb0, nbt);
