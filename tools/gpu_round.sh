@@ -28,13 +28,13 @@ if [[ $STEPS == *smoke* ]]; then
   tail -2 "$OUT/smoke.log"
 fi
 if [[ $STEPS == *bench* ]]; then
-  timeout -k 10 600 python bench.py ${BENCH_ARGS:---steps 3 --warmup 1} > "$OUT/bench.log" 2>&1
+  timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > "$OUT/bench.log" 2>&1
   stop_on_fault $? bench
   tail -1 "$OUT/bench.log"
 fi
 if [[ $STEPS == *prof* ]]; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
-      python bench.py ${PROF_ARGS:---steps 2 --warmup 1 --no-cpu} > "$OUT/prof.log" 2>&1
+      python bench.py ${PROF_ARGS:---steps 20 --warmup 3 --no-cpu --no-toa --no-config2 --no-calcphase --no-config4 --exact-steps 1} > "$OUT/prof.log" 2>&1
   stop_on_fault $? rocprof
   find "$OUT/prof" -name "*stats*" | head
 fi
