@@ -394,21 +394,36 @@ __global__ __launch_bounds__(256) void k_nu_gather(const double* __restrict__ tt
 #pragma unroll
     for (int r = 0; r < R; ++r) c2[r] = (TWOD && r < nrow) ? c2row[r] : 0.0;
     const double kd = (double)k;
-    for (int64_t G = gmin + (((g - gmin) % nfft) + nfft) % nfft; G <= gmax; G += nfft) {
-        const int64_t i0 = start[G - gmin], i1 = start[G - gmin + 1];
+    // the photon times are prefetched raw and unconditionally (indices clamped into the cell, whose stand-ins are
+    // never weighted): a load whose value entered a select or a subtraction at its issue would be waited for there;
+    // the next cell's photon range is loaded during the current cell
+    int64_t G = gmin + (((g - gmin) % nfft) + nfft) % nfft;
+    int64_t ns0 = 0, ns1 = 0;
+    if (G <= gmax) {
+        ns0 = start[G - gmin];
+        ns1 = start[G - gmin + 1];
+    }
+    for (; G <= gmax; G += nfft) {
+        const int64_t i0 = ns0, i1 = ns1;
+        if (G + nfft <= gmax) {
+            ns0 = start[G + nfft - gmin];
+            ns1 = start[G + nfft - gmin + 1];
+        }
+        if (i1 <= i0) continue;  // an empty cell (no clamped load below i0)
         const double Gd = (double)G;
         // two photons per iteration (independent chains for the VALU; each one's terms still added in photon
         // order), their times prefetched two iterations ahead (HBM latency is several iterations of one wave)
+        const int64_t il = i1 - 1;
         double dn[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) dn[q] = i0 + sub + q * L < i1 ? (tt[i0 + sub + q * L] - t0) : 0.0;
+        for (int q = 0; q < 4; ++q) dn[q] = tt[i0 + sub + q * L < il ? i0 + sub + q * L : il];
         for (int64_t i = i0 + sub; i < i1; i += 2 * L) {
             const bool hb = i + L < i1;
-            const double da = dn[0], db = hb ? dn[1] : dn[0];  // (no second photon: a finite stand-in, weight 0)
+            const double da = dn[0] - t0, db = (hb ? dn[1] : dn[0]) - t0;  // (no second photon: a stand-in, weight 0)
             dn[0] = dn[2];
             dn[1] = dn[3];
-            if (i + 4 * L < i1) dn[2] = (tt[i + 4 * L] - t0);
-            if (i + 5 * L < i1) dn[3] = (tt[i + 5 * L] - t0);
+            dn[2] = tt[i + 4 * L < il ? i + 4 * L : il];
+            dn[3] = tt[i + 5 * L < il ? i + 5 * L : il];
             const double ea = kd * (da * s1) - Gd, eb = kd * (db * s1) - Gd;
             const double p1a = nu_frac_prod(fch, fcl, da), p1b = nu_frac_prod(fch, fcl, db);
             double d2a = 0.0, d2ea = 0.0, d2b = 0.0, d2eb = 0.0;
@@ -728,17 +743,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     const int64_t nfft = int64_t(1) << lnfft;
     const int cc = threadIdx.x & 15, j = threadIdx.x >> 4;
     const int64_t cpb = int64_t(1) << (ln2 - 4);  // column blocks per batch
-    double2 nv[16], nb, ns;
+    // the prefetch keeps the twiddle bases as their two table factors each (loaded before the rows) and multiplies
+    // them at use: a product at the fetch would wait for every load issued so far, the rows' included
+    double2 nv[16], tf[4];
     auto fetch = [&](int64_t grp) {  // rows outside [alo, alo + acnt) (mod 256) hold no cell
         const int64_t b = ((grp % cpb) << 4) + cc;
         const double2* x = X + (grp / cpb) * nfft + b;
+        const int64_t lm = (int64_t(1) << T.lbits) - 1, tb = (b * (int64_t)j) & T.mask, ts = (b << 4) & T.mask;
+        tf[0] = T.hi[tb >> T.lbits];
+        tf[1] = T.lo[tb & lm];
+        tf[2] = T.hi[ts >> T.lbits];
+        tf[3] = T.lo[ts & lm];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int a = j + 16 * r;
             nv[r] = ((a - alo) & 255) < acnt ? x[(int64_t)a << ln2] : make_double2(0.0, 0.0);
         }
-        nb = nu_tw(T, b * (int64_t)j);
-        ns = nu_tw(T, b << 4);
     };
     int64_t grp = blockIdx.x;
     if (grp < ngroups) fetch(grp);
@@ -747,7 +767,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
         double2 v[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) v[r] = nv[r];
-        const double2 wb = nb, ws = ns;
+        const double2 wb = nu_cmul(tf[0], tf[1]), ws = nu_cmul(tf[2], tf[3]);  // nu_tw's product
         const int64_t b = ((grp % cpb) << 4) + cc;
         double2* y = Y + (grp / cpb) * nfft + b;
         if (grp + gridDim.x < ngroups) fetch(grp + gridDim.x);
@@ -941,7 +961,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k
 // writes over all banks). The transform's arithmetic differs from the radix-16 form's in rounding only.
 __device__ __forceinline__ int nu_sw8(int i) { return i ^ ((i >> 3) & 7); }
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k_nu_rows4096_combine8(
-    const double2* __restrict__ X, int lnfft, int P, int nrow, int64_t nf, int64_t jhi, int64_t h, int64_t tbase,
+    const double2* X, int lnfft, int P, int nrow, int64_t nf, int64_t jhi, int64_t h, int64_t tbase,
     int64_t nbt, const double* __restrict__ bc, double2* __restrict__ CS) {
     extern __shared__ double2 nu_s[];  // [2][4096]
     __shared__ NuTile tw;
