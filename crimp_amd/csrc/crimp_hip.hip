@@ -1900,6 +1900,87 @@ static int exact_search(Scratch& sc, hipStream_t s, const double* dt, const doub
     return fixup_search(sc, s, dt, dt2, n, freq, nf, c2, twod, nharm, stat, first, flagged, nf_h, out);
 }
 
+// Best trial of a power array, np.argmax semantics (periodsearch.py's callers take the maximum and its index): the
+// largest value, ties to the lowest index, a NaN above every number (the first NaN wins). k_best_blocks reduces
+// grid-stride slices (eight loads in flight per thread) to one candidate per block, k_best_final the candidates.
+struct BestCand {
+    double v;
+    int64_t i;
+};
+__device__ __forceinline__ bool best_better(double v1, int64_t i1, double v2, int64_t i2) {
+    const bool n1 = isnan(v1), n2 = isnan(v2);
+    if (n1 != n2) return n1;
+    if (!n1 && v1 != v2) return v1 > v2;
+    return i1 < i2;
+}
+__device__ __forceinline__ BestCand best_block_reduce(BestCand c) {
+    for (int o = 32; o > 0; o >>= 1) {
+        const double v = __shfl_xor(c.v, o);
+        const int64_t i = __shfl_xor(c.i, o);
+        if (best_better(v, i, c.v, c.i)) c = {v, i};
+    }
+    __shared__ BestCand red[4];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
+    __syncthreads();
+    c = red[0];
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w)
+        if (best_better(red[w].v, red[w].i, c.v, c.i)) c = red[w];
+    return c;
+}
+constexpr int kBestBlocks = 1024;
+__global__ __launch_bounds__(256) void k_best_blocks(const double* __restrict__ x, int64_t n, BestCand* __restrict__ part) {
+    constexpr int U = 8;
+    BestCand c = {-INFINITY, INT64_MAX};
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t j0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j0 < n; j0 += U * stride) {
+        double v[U];
+#pragma unroll
+        for (int q = 0; q < U; ++q) v[q] = x[j0 + q * stride < n ? j0 + q * stride : n - 1];
+#pragma unroll
+        for (int q = 0; q < U; ++q) {
+            const int64_t j = j0 + q * stride;
+            if (j < n && best_better(v[q], j, c.v, c.i)) c = {v[q], j};
+        }
+    }
+    c = best_block_reduce(c);
+    if (threadIdx.x == 0) part[blockIdx.x] = c;
+}
+__global__ __launch_bounds__(256) void k_best_final(const BestCand* __restrict__ part, int nb, double* __restrict__ out) {
+    BestCand c = {-INFINITY, INT64_MAX};
+    for (int b = threadIdx.x; b < nb; b += blockDim.x)
+        if (best_better(part[b].v, part[b].i, c.v, c.i)) c = part[b];
+    c = best_block_reduce(c);
+    if (threadIdx.x == 0) {
+        out[0] = c.v;
+        out[1] = (double)c.i;
+    }
+}
+
+extern "C" int crimp_best(const double* x, int64_t n, double* best, uint32_t flags, void* stream) {
+    ARGCHK(n >= 1, "need at least one value");
+    ARGCHK(x != nullptr && best != nullptr, "null argument");
+    ARGCHK(n <= (int64_t(1) << 53), "n above 2^53 (the index is returned as a double)");
+    const bool dev = flags & CRIMP_FLAG_DEVICE_PTRS;
+    std::lock_guard<std::mutex> lk(g_mutex);
+    hipStream_t s = as_stream(stream);
+    {
+        Scratch sc(s);
+        const double* dx = nullptr;
+        HIPCHK(stage_in(sc, x, (size_t)n, dev, &dx));
+        BestCand* part = nullptr;
+        double* dout = nullptr;
+        HIPCHK(sc.alloc(&part, (size_t)kBestBlocks));
+        HIPCHK(sc.alloc(&dout, 2));
+        const int nb = (int)std::min<int64_t>(cdiv(n, 256 * 8), kBestBlocks);
+        k_best_blocks<<<nb, 256, 0, s>>>(dx, n, part);
+        HIPCHK(hipGetLastError());
+        k_best_final<<<1, 256, 0, s>>>(part, nb, dout);
+        HIPCHK(hipGetLastError());
+        HIPCHK(d2h(s, best, dout, 2 * sizeof(double)));
+    }
+    return finish(s, flags);
+}
+
 extern "C" int crimp_last_search_path(void) { return g_last_search_path; }
 
 extern "C" int crimp_last_nufft_plan(int64_t* fft_length, int32_t* moments, int32_t* gather) {

@@ -120,6 +120,21 @@ def search(t, t0, freq, nharm, stat, log10_negfdot=None, first=0, count=None, ou
     return out
 
 
+def best(x):
+    """(max, index) of a power array with np.argmax semantics (ties to the lowest index, NaN first), one small
+    device reduction and one readback (crimp_best)."""
+    n = int(x.numel() if N._is_torch(x) else np.size(x))
+    if n == 0:
+        raise ValueError("best of an empty array")
+    L = N.load()
+    b = N.Buffers()
+    xp = b.arg(x, np.float64)
+    res = np.zeros(2, dtype=np.float64)
+    with b.device_guard():
+        N.check(L.crimp_best(xp, n, ctypes.c_void_p(res.ctypes.data), b.flags(), b.stream()))
+    return float(res[0]), int(res[1])
+
+
 def search_sets(t, offsets, freq, nharm, stat, flags=0):
     """One-trial Z^2 / H of many photon sets (crimp_search_sets): set i = t[offsets[i]:offsets[i+1]] (seconds) at
     freq[i], each with its own t0 = (first + last)/2. fp64. ``flags`` N.FLAG_ASYNC (device tensors): returns with the

@@ -90,11 +90,19 @@ def sharded_search(time, freq, nharm=2, stat=0, freq_dot=None, gather="all", com
     loc = _as_comm(local, dev)
     if gather == "best":
         if count:
-            v, i = torch.max(loc, 0)  # the first maximal index, as np.argmax
-            if dist is None:
-                res = torch.stack([v, i.to(torch.float64)]).cpu().numpy()
-                return float(res[0]), int(res[1]) + first
-            mine = torch.stack([v, (i + first).to(torch.float64)])
+            if isinstance(local, torch.Tensor) and local.is_cuda:
+                # the rank's best on the device (crimp_best: one reduction, one 16-byte readback)
+                from . import ops
+                bv, bi = ops.best(local)
+                if dist is None:
+                    return bv, bi + first
+                mine = torch.tensor([bv, float(bi + first)], dtype=torch.float64, device=dev)
+            else:
+                v, i = torch.max(loc, 0)  # the first maximal index, as np.argmax
+                if dist is None:
+                    res = torch.stack([v, i.to(torch.float64)]).cpu().numpy()
+                    return float(res[0]), int(res[1]) + first
+                mine = torch.stack([v, (i + first).to(torch.float64)])
         else:
             mine = torch.tensor([-np.inf, float(total)], dtype=torch.float64, device=dev)
         if dist is None:

@@ -150,6 +150,12 @@ int crimp_search(const double* t, int64_t n, double t0, const double* freq, int6
                  const double* log10_negfdot, int64_t nfd, int32_t nharm, int32_t stat, int64_t first,
                  int64_t count, double* out, uint32_t flags, void* stream);
 
+/* Best trial of a power array x[n] (crimp_search's out): best[0] = max, best[1] = its index as a double (exact:
+ * n <= 2^53), np.argmax semantics -- ties to the lowest index, NaN above every number   [the maximum the
+ * reference's callers take of PeriodSearch's powers; sharding.sharded_search(gather='best')]. best is a host
+ * pointer; with CRIMP_FLAG_DEVICE_PTRS x is device memory (else host, staged). One stream sync. */
+int crimp_best(const double* x, int64_t n, double* best, uint32_t flags, void* stream);
+
 /* Many one-trial searches at once: for every set i, PeriodSearch(t[offsets[i]:offsets[i+1]], [freq[i]],
  * nbrHarm).htest() / .ztest()   [periodsearch.py:40-125 as measureToAs.py:210-212 calls it per ToA interval;
  * t0 = (first + last)/2 of each set, :54]. t in seconds; out[nset]. fp64 (the reference's precision). */

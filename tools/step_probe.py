@@ -24,3 +24,9 @@ def best():
     v, i = torch.max(z, 0); return torch.stack([v, i.to(torch.float64)]).cpu().numpy()
 print("max+stack+cpu          %.3f ms" % tm(best))
 print("search+sync only       %.3f ms" % tm(lambda: (ops.search(t, t0, f, 2, 0, out=out, precision="nufft"), torch.cuda.synchronize())))
+print("ops.best alone         %.3f ms" % tm(lambda: ops.best(z)))
+def torch_best():
+    v, i = torch.max(z, 0); return torch.stack([v, i.to(torch.float64)]).cpu().numpy()
+print("search+ops.best        %.3f ms" % tm(lambda: (ops.search(t, t0, f, 2, 0, out=out, precision="nufft"), ops.best(out))))
+print("search+torch best      %.3f ms" % tm(lambda: (ops.search(t, t0, f, 2, 0, out=out, precision="nufft"), torch_best())))
+print("sharded best (again)   %.3f ms" % tm(lambda: sharded_search(t, f, 2, 0, gather="best", precision="nufft", t0=t0)))
