@@ -1731,7 +1731,8 @@ static int grid_is_progression(Scratch& sc, hipStream_t s, const double* freq, i
     *ap = reinterpret_cast<double*>(info);
     if (nf < 2) return CRIMP_OK;
     HIPCHK(hipMemsetAsync(info, 0, (3 + 6) * sizeof(unsigned long long), s));
-    k_ap_check<<<(unsigned)std::min<int64_t>(cdiv(nf, 256), 512), 256, 0, s>>>(freq, nf, info);
+    // 64 blocks (one same-address atomic pair per block): 14.7 us per 1e6-trial grid, 16.3 at 512 blocks
+    k_ap_check<<<(unsigned)std::min<int64_t>(cdiv(nf, 256), 64), 256, 0, s>>>(freq, nf, info);
     HIPCHK(hipGetLastError());
     double h[3 + 5];
     size_t bytes = 3 * sizeof(double);

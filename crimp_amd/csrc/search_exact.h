@@ -900,8 +900,7 @@ __global__ __launch_bounds__(256) void k_ap_check(const double* __restrict__ f, 
     const double f0 = f[0];
     const double d = (f[nf - 1] - f0) / (double)(nf - 1);
     double dev = 0.0, fm = 0.0;
-    // eight grid-stride values per thread per iteration, all loads issued first (clamped indices): the capped grid
-    // left one load in flight per thread, 17 us per 1e6-trial grid, latency-bound
+    // eight grid-stride values per thread per iteration, all loads issued first (clamped indices)
     constexpr int U = 8;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t j0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j0 < nf; j0 += U * stride) {
