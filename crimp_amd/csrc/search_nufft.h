@@ -228,6 +228,11 @@ __global__ __launch_bounds__(256) void k_nu_spread(const double* __restrict__ tt
                                                    int k0, int P, const NuPass* __restrict__ ps,
                                                    const double2* __restrict__ tab, double* __restrict__ U,
                                                    int64_t* __restrict__ ctab) {
+    // the cis table in LDS (read twice per photon and K-group: an L2 round trip each, waited for at once), filled
+    // before any wave leaves
+    __shared__ double2 stab[1024];
+    for (int e = threadIdx.x; e < 1024; e += 256) stab[e] = tab[e];
+    __syncthreads();
     const int lane = threadIdx.x & 63;
     const int64_t c = (int64_t)blockIdx.x * kNuWaves + (threadIdx.x >> 6);
     if (c >= nchunk) return;  // wave-uniform
@@ -269,9 +274,13 @@ __global__ __launch_bounds__(256) void k_nu_spread(const double* __restrict__ tt
             }
         }
     };
+    // past the end: the last photon's time (same cell, zero weight); the next tile's times are loaded (raw) during
+    // the current one
+    double tn = tt[i0 + lane < n ? i0 + lane : n - 1];
     for (int64_t ib = i0; ib < i1; ib += 64) {
-        const int64_t il = ib + lane;
-        const double dv = (tt[il < n ? il : n - 1] - t0);  // past the end: the last photon's time (same cell, zero weight)
+        const double dv = tn - t0;
+        const int64_t il = ib + 64 + lane;
+        tn = tt[il < n ? il : n - 1];
 #pragma unroll 1
         for (int g = 0; g < 16; ++g) {
             if (ib + 4 * g >= i1) break;  // wave-uniform
@@ -284,9 +293,9 @@ __global__ __launch_bounds__(256) void k_nu_spread(const double* __restrict__ tt
                 phi += nu_frac_c2(c2, d2, d2e);
             }
             phi -= rint(phi);
-            const double2 c1 = nu_cis(tab, phi);
+            const double2 c1 = nu_cis(stab, phi);
             double2 ck = c1;
-            if (k0 > 1) ck = nu_cis(tab, nu_frac_k((double)k0, phi));
+            if (k0 > 1) ck = nu_cis(stab, nu_frac_k((double)k0, phi));
             const double u1 = d * s1;
 #pragma unroll
             for (int kk = 0; kk < G; ++kk) {
