@@ -5,11 +5,13 @@ One step = one complete Z^2_2 search of the config-3 workload per GPU: 1e7 synth
 p = 0.1, f0 = 7.123456789 Hz, seed 0, time-sorted as event files are) against 1e6 trial frequencies spaced 1/(10T),
 inputs resident in HBM, followed by the search's one exchange step (every rank's best trial gathered so that all
 ranks agree on the global best, ties -> lowest index). With N ranks each rank searches its own 1e6-trial slice of
-an N*1e6 grid (weak scaling); ``value`` = all ranks' evaluations / max-over-ranks time. The step runs
-``precision="nufft"`` (csrc/search_nufft.h: Taylor-moment NUFFT in fp64, every trial within 1e-6 of the reference
-by its certificate + fp64 fix-up, tests/test_gpu_nufft.py, test_gpu_fullsize.py); ``--precision exact`` times the
-default exact-integer MFMA path instead. "Evaluations" are the photon x trial pairs the reference evaluates
-directly; the NUFFT returns the same per-trial powers without evaluating every pair.
+an N*1e6 grid (weak scaling); ``value`` = all ranks' evaluations / max-over-ranks time. The step is the search call
+without a precision keyword -- what the reference's own ``PeriodSearch(time, freq, 2).ztest()`` reaches: the
+default NUFFT (csrc/search_nufft.h: Chebyshev-moment non-uniform FFT in fp64, every trial within 1e-6 of the
+reference by its truncation-bound certificate + fp64 fix-up, tests/test_gpu_nufft.py, test_gpu_fullsize.py);
+``--precision exact`` times the exact-integer MFMA path instead. The unit says "equivalent": evaluations are the
+photon x trial pairs the reference evaluates directly, and the NUFFT returns the same per-trial powers without
+evaluating every pair (``exact_path`` and ``cpu_baseline`` do evaluate every pair).
 
 Also reported:
 * ``roofline``: the NUFFT's dominant kernel class, its algorithmic work per launch (crimp_last_nufft_work) over the
@@ -24,7 +26,7 @@ Also reported:
   (interval selection, calcphase, fits, per-interval H-test) from host MJD arrays, with the oracle's fits on all
   allowed host cores as its CPU baseline (a sample, extrapolated) and the fits' VALU roofline;
 * ``config4``: 1e8 photons, 2-D H_20 on a sub-grid of the 1e7-trial grid (131072 trials per GPU), sharded_search;
-  ``config4.nufft``: the WHOLE 1e7-trial grid by precision="nufft" (each rank its 1e7/N slice);
+  ``config4.nufft``: the WHOLE 1e7-trial grid by the default search (the NUFFT; each rank its 1e7/N slice);
 * ``config2``: ``measureToAs`` on the bundled events, ToAs 35-41, FITS -> table (the reference's published rate).
 The multi-GPU paths are the tested ones (tests/test_distributed_*.py): the search step and the config-4 leg run
 ``sharding.sharded_search(gather="best")``, the ToA leg ``sharding.sharded_toa_fit`` (records all_gathered).
@@ -65,8 +67,9 @@ def parse():
     p.add_argument("--nharm", type=int, default=2)
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline legs")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
-    p.add_argument("--precision", default="nufft", choices=["nufft", "exact"],
-                   help="the search path of `value` (the other one is timed beside it)")
+    p.add_argument("--precision", default="default", choices=["default", "nufft", "exact"],
+                   help="the search path of `value`: default = no precision keyword (the NUFFT where it applies); "
+                        "the exact path is timed beside it")
     p.add_argument("--exact-steps", type=int, default=3, help="timed steps of the exact-path leg (~0.8 s each)")
     p.add_argument("--no-exact", action="store_true", help="skip the exact-path leg (when value is nufft)")
     p.add_argument("--toa-intervals", type=int, default=1250, help="ToA intervals per GPU (config 5: 1e4 over 8)")
@@ -430,16 +433,16 @@ def config4_leg(a, dev, world, rank):
     nu = None
     if not a.no_nufft_c4:
         # the WHOLE config-4 grid (1e5 f x 100 fdot rows = 1e7 trials, N ranks each its 1e7/N slice) by
-        # precision="nufft": the per-GPU workload of BASELINE config 4, timed end to end
+        # the default search (the NUFFT): the per-GPU workload of BASELINE config 4, timed end to end
         f_all = torch.as_tensor(f0 + (np.arange(M) - M // 2) / (10.0 * span), device=dev)
         fd_all = torch.as_tensor(np.linspace(-13.5, -11.5, 100), device=dev)
         nu_first, nu_count = shard_range(100 * M, world, rank)
-        sharded_search(t, f_all, 20, 1, freq_dot=fd_all, gather="best", precision="nufft")  # untimed
+        sharded_search(t, f_all, 20, 1, freq_dot=fd_all, gather="best")  # untimed
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         t1 = time.perf_counter()
-        nb_pow, nb_idx = sharded_search(t, f_all, 20, 1, freq_dot=fd_all, gather="best", precision="nufft")
+        nb_pow, nb_idx = sharded_search(t, f_all, 20, 1, freq_dot=fd_all, gather="best")
         torch.cuda.synchronize()
         nel = time.perf_counter() - t1
         elt = torch.tensor([nel], dtype=torch.float64, device=dev)
@@ -454,7 +457,7 @@ def config4_leg(a, dev, world, rank):
               "plan": {"fft_length": nplan[0], "moments": nplan[1], "spread": nplan[2]},
               "best_power": nb_pow, "best_trial": {"fdot_row": nrow_, "f_index": ncol_},
               "workload": "config4 WHOLE grid: %.3g photons, H_20, 1e5 f x 100 fdot rows (%d trials per GPU), "
-                          "precision='nufft', sharding.sharded_search(gather='best') over %d rank(s)"
+                          "default precision (NUFFT), sharding.sharded_search(gather='best') over %d rank(s)"
                           % (n, nu_count, world)}
         del f_all, fd_all
     del t, f, fd
@@ -538,7 +541,7 @@ PEAK_F64_TFLOPS = 78.6  # MI355X spec fp64 (vector and matrix); mb_f64 measures 
 
 
 def nufft_leg(a, t, t_h, f, rank, M, steps):
-    """The rank's trial slice by precision="nufft": one untimed search, then ``steps`` timed ones (wall time with the
+    """The rank's trial slice by the default search (the NUFFT): one untimed search, then ``steps`` timed ones (wall time with the
     stream drained, and the library's hipEvent spans: the whole pipeline and each kernel class's time and launches).
     Each class is priced by the algorithmic work the library counted for the plan it chose (crimp_last_nufft_work;
     DESIGN.md section 5.3):
@@ -555,13 +558,13 @@ def nufft_leg(a, t, t_h, f, rank, M, steps):
     from crimp_amd import _native as N
     t0 = (t_h[0] + t_h[-1]) / 2
     out = torch.empty(M, dtype=torch.float64, device=t.device)
-    ops.search(t, t0, f, a.nharm, 0, first=rank * M, count=M, out=out, precision="nufft")
+    ops.search(t, t0, f, a.nharm, 0, first=rank * M, count=M, out=out)
     torch.cuda.synchronize()
     walls, spans = [], []
     for _ in range(steps):
         torch.cuda.synchronize()
         t2 = time.perf_counter()
-        ops.search(t, t0, f, a.nharm, 0, first=rank * M, count=M, out=out, precision="nufft",
+        ops.search(t, t0, f, a.nharm, 0, first=rank * M, count=M, out=out,
                    flags=N.FLAG_TIME_KERNELS)
         torch.cuda.synchronize()
         walls.append(time.perf_counter() - t2)
@@ -736,11 +739,12 @@ def main():
                                      "POP/s, sparse 10.0): frac = matrix-pipe occupancy at 2.4 GHz; traffic: %s" % (
                                          tsrc or "no PMC pass on this workload")}}
 
+    prec = None if a.precision == "default" else a.precision
     el, kern_ms, nfix, (best_pow, best_idx), step_ms, path = timed_steps(
-        a.precision, a.steps, a.warmup, flags=N.FLAG_TIME_KERNELS if a.precision == "exact" else 0)
+        prec, a.steps, a.warmup, flags=N.FLAG_TIME_KERNELS if a.precision == "exact" else 0)
     value = float(a.photons) * M * world * a.steps / el
     exact = None
-    if a.precision == "nufft" and not a.no_exact:
+    if a.precision != "exact" and not a.no_exact:
         e_el, e_kms, e_nfix, e_best, _, _ = timed_steps("exact", a.exact_steps, 1, flags=N.FLAG_TIME_KERNELS)
         exact = exact_record(e_el, e_kms, e_nfix, a.exact_steps)
         exact["best_trial_index"], exact["best_power"] = e_best[1], float(e_best[0])
@@ -749,7 +753,11 @@ def main():
         rec = {
             "metric": "Z^2_2 photon*trial evals/sec (node)",
             "value": value,
-            "unit": "photon*trial evals/s",
+            "unit": "photon*trial evals/s" if a.precision == "exact" else "equivalent photon*trial evals/s",
+            "value_kind": ("direct: every photon x trial pair evaluated" if a.precision == "exact" else
+                           "equivalent: photons x trials / wall time of the NUFFT search, which returns every "
+                           "trial's power (certified within 1e-6 of the reference) without evaluating each pair; "
+                           "exact_path and cpu_baseline evaluate every pair"),
             "n_gpus": world,
             "steps": a.steps,
             "warmup": a.warmup,
@@ -757,7 +765,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f64" if a.precision == "nufft" else
+            "dtype": "f64" if a.precision != "exact" else
                      "int8 digits on i8 MFMA, exact int32/int64 sums (fp64 phase, 2^30 fixed-point cos/sin)",
             "data": "synthetic (seeded Poisson pulsed events, crimp_amd/synth.py)",
             "config": {"workload": "config3: synthetic %d photons x %d trials/GPU, Z^2_%d" % (a.photons, M, a.nharm),

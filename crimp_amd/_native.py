@@ -24,6 +24,7 @@ FLAG_F64 = 256
 FLAG_NO_FIXUP = 1024
 FLAG_ASYNC = 2048
 FLAG_NUFFT = 4096
+FLAG_EXACT = 8192
 
 STAT_Z2 = 0
 STAT_H = 1

@@ -2008,10 +2008,13 @@ extern "C" int crimp_search(const double* t, int64_t n, double t0, const double*
     const int64_t total = (twod ? nfd : 1) * nf;
     ARGCHK(first >= 0 && count >= 0 && first + count <= total, "trial range outside the grid");
     const bool f64 = flags & CRIMP_FLAG_F64;
-    const bool nufft = flags & CRIMP_FLAG_NUFFT;
+    const bool exact_only = flags & CRIMP_FLAG_EXACT;
     ARGCHK(!(flags & CRIMP_FLAG_RETIRED_FAST), "the fp32 fast search path (flag bits 4, 16, 512) was retired: slower and "
                                                 "less precise than the default path");
-    ARGCHK(!(nufft && f64), "CRIMP_FLAG_NUFFT excludes CRIMP_FLAG_F64");
+    ARGCHK(!((flags & CRIMP_FLAG_NUFFT) && f64), "CRIMP_FLAG_NUFFT excludes CRIMP_FLAG_F64");
+    ARGCHK(!(exact_only && (f64 || (flags & CRIMP_FLAG_NUFFT))), "CRIMP_FLAG_EXACT excludes CRIMP_FLAG_F64 and _NUFFT");
+    // the NUFFT is tried first unless a precision flag excludes it (CRIMP_FLAG_NUFFT asks for the default explicitly)
+    const bool nufft = !f64 && !exact_only;
     if (count == 0) return CRIMP_OK;
     std::lock_guard<std::mutex> lk(g_mutex);
     if (flags & CRIMP_FLAG_TIME_KERNELS) {
@@ -2054,34 +2057,34 @@ extern "C" int crimp_search(const double* t, int64_t n, double t0, const double*
 
         // Routing by properties of the whole grid (not of this call's trial range), so that every shard of a
         // sharded search takes the kernel an unsharded search takes:
-        //   default: exact i8 kernel for progressions of >= 256 trials per row and < 2^27 photons, fp64 kernel
-        //            otherwise (a 2-D grid of short rows would fill its 2048-trial tiles with dead columns);
-        //   nufft:   the NUFFT for progressions of >= 64 trials per row (per shard segment) and time-sorted photons,
-        //            the default path otherwise;
+        //   default (and CRIMP_FLAG_NUFFT): the NUFFT for progressions of >= 64 trials per row (per shard segment),
+        //            time-sorted photons and a plan within range (nu_plan); where it declines, the exact rule below;
+        //   exact:   exact i8 kernel for progressions of >= 256 trials per row (any length with FORCE_MFMA), fp64
+        //            kernel otherwise (a 2-D grid of short rows would fill its 2048-trial tiles with dead columns);
         //   f64:     fp64 kernel.
         KernelTimer kt(s, flags & CRIMP_FLAG_TIME_KERNELS);
-        bool factorised = !f64 && (nf >= 256 || (flags & CRIMP_FLAG_FORCE_MFMA) || (nufft && nf >= 64));
+        const bool exact_grid = nf >= 256 || (flags & CRIMP_FLAG_FORCE_MFMA);
+        bool progression = false;
         double* ap = nullptr;
         double nu_hs[5] = {0, 0, 0, 0, 0};
-        if (factorised) {
-            bool ok = false;
-            int rc = grid_is_progression(sc, s, dfr, nf, &ap, &ok, nufft ? dtm : nullptr, t0, n, nu_hs,
+        if (!f64 && (exact_grid || (nufft && nf >= 64))) {
+            int rc = grid_is_progression(sc, s, dfr, nf, &ap, &progression, nufft ? dtm : nullptr, t0, n, nu_hs,
                                          !nu_gather_form(twod ? nfd : 1));
             if (rc) return rc;
-            factorised = ok;
         }
-        if ((flags & CRIMP_FLAG_FORCE_MFMA) && !factorised)
-            return set_err(CRIMP_ERR_ARG, "factorised search not applicable (grid is not an arithmetic progression)");
         int rc = CRIMP_OK;
         bool done = false;
-        if (factorised && nufft) {  // NUFFT; unsorted photons or an out-of-range plan fall through to the exact path
+        if (progression && nufft && nf >= 64) {  // NUFFT; unsorted photons or no plan fall through to the exact rule
             int64_t nfix = 0;
             rc = nufft_search(sc, s, dtm, t0, n, dfr, nf, twod ? nfd : 1, dc2, nu_hs, twod, nharm, stat, first, count,
                               dout, flags & CRIMP_FLAG_TIME_KERNELS, &nfix, (flags & CRIMP_FLAG_NO_FIXUP) != 0, &done);
             if (rc) return rc;
             if (done) g_last_fixups = nfix;
         }
-        if (nufft && !done) HIPCHK(prep());  // the NUFFT did not apply: the default path's kernels read dt
+        const bool factorised = !done && progression && exact_grid;
+        if ((flags & CRIMP_FLAG_FORCE_MFMA) && !done && !factorised)
+            return set_err(CRIMP_ERR_ARG, "factorised search not applicable (grid is not an arithmetic progression)");
+        if (nufft && !done) HIPCHK(prep());  // the NUFFT did not apply: the exact / fp64 kernels read dt
         if (done) {
         } else if (factorised) {
             g_last_search_path = 1;

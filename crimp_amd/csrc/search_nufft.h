@@ -1330,6 +1330,9 @@ struct NuPlan {
 // moments, the one with the least FFT work n P; false when none exists or the photons wrap the grid more than
 // kNuMaxWrap times
 static bool nu_plan(NuPlan* pl, double delta, double f0, double dt0, double dtn, int nharm, int64_t nchunk, int pmax) {
+    // an ascending progression only: with delta < 0 the cells of the later photons come first (s1 < 0) and every
+    // table below would be sized negative (a descending grid takes the exact rule)
+    if (!(delta > 0.0) || !std::isfinite(delta) || !std::isfinite(f0)) return false;
     const int64_t h = pl->nseg / 2;
     pl->h = h;
     int lnfft = 0, P = 0;
@@ -1360,12 +1363,21 @@ static bool nu_plan(NuPlan* pl, double delta, double f0, double dt0, double dtn,
     pl->fcl = ((f0 - (fch - bb)) + (hp - bb)) + hpe;
     // the kernel's arithmetic: rint(k * (dt * s1))
     const double u0 = dt0 * pl->s1, un = dtn * pl->s1;
+    // The kernels convert cells with 32-bit rint (k_nu_spread, k_nu_cellstart, k_nu_gather): every cell of every
+    // harmonic, one FFT length of margin included, must fit an int -- a t0 far from the photons (t0 = 0 with MJD
+    // seconds) can push |G| past 2^31 although the span is small. The plan is declined then (the exact rule runs).
+    const double glim = 2147483647.0 - (double)nfft;
     pl->gmin.assign((size_t)nharm, 0);
     pl->gmax.assign((size_t)nharm, 0);
     (void)nchunk;
     for (int k = 1; k <= nharm; ++k) {
-        pl->gmin[(size_t)(k - 1)] = (int64_t)std::rint((double)k * u0);
-        pl->gmax[(size_t)(k - 1)] = (int64_t)std::rint((double)k * un);
+        const double a = (double)k * u0, b = (double)k * un;
+        if (!(std::fabs(a) < glim && std::fabs(b) < glim)) return false;  // NaN declines too
+        pl->gmin[(size_t)(k - 1)] = (int64_t)std::rint(a);
+        pl->gmax[(size_t)(k - 1)] = (int64_t)std::rint(b);
+        // descending cells (a descending grid, delta < 0, or photons out of order at the ends) would size the
+        // slot and start tables negative: declined
+        if (pl->gmax[(size_t)(k - 1)] < pl->gmin[(size_t)(k - 1)]) return false;
         if ((pl->gmax[(size_t)(k - 1)] - pl->gmin[(size_t)(k - 1)]) / nfft + 1 > kNuMaxWrap) return false;
     }
     return true;

@@ -70,7 +70,7 @@ def _empty_like_input(a, n, b, dtype=np.float64):
 
 
 def search_flags():
-    """Extra search flags from the environment for unmodified callers: CRIMP_PRECISION=f64|nufft, and
+    """Extra search flags from the environment for unmodified callers: CRIMP_PRECISION=exact|nufft|f64, and
     CRIMP_SEARCH=mfma (fail unless a factorised kernel applies)."""
     f = 0
     prec = os.environ.get("CRIMP_PRECISION", "").lower()
@@ -78,7 +78,9 @@ def search_flags():
         f |= N.FLAG_F64
     elif prec == "nufft":
         f |= N.FLAG_NUFFT
-    elif prec not in ("", "exact"):
+    elif prec == "exact":
+        f |= N.FLAG_EXACT
+    elif prec != "":
         raise ValueError("CRIMP_PRECISION must be exact, nufft or f64 (the fp32 'fast' path was retired)")
     if os.environ.get("CRIMP_SEARCH", "").lower() == "mfma":
         f |= N.FLAG_FORCE_MFMA
@@ -86,19 +88,22 @@ def search_flags():
 
 
 PRECISIONS = (None, "exact", "f64", "nufft")
+_PRECISION_FLAGS = {None: 0, "nufft": N.FLAG_NUFFT, "exact": N.FLAG_EXACT, "f64": N.FLAG_F64}
 
 
 def search(t, t0, freq, nharm, stat, log10_negfdot=None, first=0, count=None, out=None, flags=0, precision=None):
     """Z^2 / H over the fd-outer grid; computes flat trials [first, first+count).
-    ``precision``: None/"exact" (default: exact-integer i8 MFMA kernel on progressions, fp64 otherwise, every
-    trial within 1e-6 relative of the reference), "nufft" (non-uniform FFT on progressions of time-sorted photons,
-    the default path otherwise; the same per-trial contract) or "f64" (fp64 kernel everywhere)."""
+    ``precision``: None or "nufft" (default: the non-uniform FFT wherever it applies -- an ascending progression of
+    >= 64 trials per row segment and time-sorted photons --, otherwise the "exact" rule; every trial within 1e-6
+    relative of the reference by its certificate and the fp64 fix-up), "exact" (no NUFFT: the exact-integer i8 MFMA
+    kernel on progressions of >= 256 trials, fp64 otherwise; the default of rounds 1-5) or "f64" (fp64 kernel
+    everywhere). A precision argument takes precedence over CRIMP_PRECISION."""
     if precision not in PRECISIONS:
         raise ValueError("precision must be one of %s (the fp32 'fast' path was retired)" % (PRECISIONS,))
-    if precision == "f64":
-        flags |= N.FLAG_F64
-    elif precision == "nufft":
-        flags |= N.FLAG_NUFFT
+    env = search_flags()
+    if precision is not None:
+        env &= ~(N.FLAG_F64 | N.FLAG_NUFFT | N.FLAG_EXACT)
+    flags |= _PRECISION_FLAGS[precision] | env
     L = N.load()
     b = N.Buffers()
     tp = b.arg(t, np.float64)
@@ -116,7 +121,7 @@ def search(t, t0, freq, nharm, stat, log10_negfdot=None, first=0, count=None, ou
     op = b.arg(out, np.float64, writable=True)
     with b.device_guard():
         N.check(L.crimp_search(tp, n, float(t0), fp, nf, dp, nfd, int(nharm), int(stat), int(first), int(count), op,
-                               b.flags(flags | search_flags()), b.stream()))
+                               b.flags(flags), b.stream()))
     return out
 
 

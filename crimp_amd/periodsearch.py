@@ -9,8 +9,8 @@ Z2pow] plus the matching DataFrame, where ``freq_dot`` holds log10|fdot| of a
 negative fdot (:95). ``twod_htest`` is this package's extension (H-test on the
 same 2-D grid).
 
-All statistics come from ``crimp_search`` (csrc/crimp_hip.hip section 4, the default
-exact kernel in csrc/search_exact.h, the opt-in NUFFT in csrc/search_nufft.h);
+All statistics come from ``crimp_search`` (csrc/crimp_hip.hip section 4: the default
+NUFFT in csrc/search_nufft.h, the exact kernel in csrc/search_exact.h, the fp64 kernel);
 there is no NumPy fallback.
 """
 import numpy as np
@@ -22,15 +22,21 @@ from ._native import STAT_H, STAT_Z2, _is_torch
 class PeriodSearch:
     """``precision`` (keyword, not in the reference):
 
-    * None (default): the exact path -- on arithmetic-progression grids of >= 256 trials per row and < 2^27 photons
-      the i8-MFMA kernel with exact integer sums of 2^30 fixed-point cos/sin (~1e-9 relative per trial), plus an
-      fp64 recomputation of every trial that its 10-sigma error bound cannot place within 1e-6 relative; other
-      grids take the fp64 kernel. Per-trial contract: 1e-6 relative of the reference's fp64 value, except where
-      the reference's own argument rounding is larger (noise-level H at config-4 arguments; DESIGN.md section 8);
-    * "nufft": non-uniform FFT over the progression (time-sorted photons; otherwise the default path): fp64
-      moments of the photons' sub-cell offsets, an fp64 FFT per moment and harmonic, the same per-trial 1e-6
-      certificate and fp64 fix-up as the default path; O(N m + M log M) instead of O(N M m);
-    * "f64": every term in fp64 like the reference (~1e-9 relative on every trial, near-zero bins included)."""
+    * None (default) or "nufft": the non-uniform FFT (csrc/search_nufft.h) wherever it applies -- an ascending
+      arithmetic-progression grid of >= 64 trials per row segment and time-sorted photons (the reference's own
+      ``PeriodSearch(time, freq).ztest()`` on an event list and a ``np.arange``/``linspace`` grid): fp64 Chebyshev
+      moments of the photons' sub-cell offsets, an fp64 FFT per moment and harmonic, O(N m P + M log M) instead of
+      O(N M m); every trial certified within 1e-6 relative of the reference by a worst-case truncation bound, the
+      uncertified ones recomputed in fp64. Where it declines, the "exact" rule below;
+    * "exact": the exact-integer path -- on progressions of >= 256 trials per row the i8-MFMA kernel with exact
+      integer sums of 2^30 fixed-point cos/sin (~1e-9 relative per trial), plus an fp64 recomputation of every trial
+      that its 10-sigma error bound cannot place within 1e-6 relative; other grids take the fp64 kernel (the default
+      of rounds 1-5);
+    * "f64": every term in fp64 like the reference (~1e-9 relative on every trial, near-zero bins included).
+
+    Per-trial contract of every precision: 1e-6 relative of the reference's fp64 value, except where the reference's
+    own argument rounding is larger (noise-level H at config-4 arguments; DESIGN.md section 8);
+    ``crimp_last_search_path()`` tells which kernel ran."""
 
     def __init__(self, time, freq, nbrHarm: int = 2, *, precision=None):
         self.time = time

@@ -16,8 +16,9 @@
  *     and every call returns with that stream drained (host staging copies are
  *     blocking), so results are ready on return -- CRIMP_FLAG_SYNC is accepted and
  *     implied;
- *   - calls are serialised per device (internal mutex); the ctypes layer releases
- *     the GIL around them.
+ *   - calls are serialised process-wide, all devices together (one internal mutex:
+ *     the scratch pool and the measurement hooks are shared); the ctypes layer
+ *     releases the GIL around them, so threads driving different devices queue.
  */
 #ifndef CRIMP_HIP_H
 #define CRIMP_HIP_H
@@ -35,12 +36,16 @@ extern "C" {
 
 #define CRIMP_FLAG_DEVICE_PTRS 1u  /* array arguments are device pointers */
 #define CRIMP_FLAG_SYNC 2u         /* synchronise the stream before returning */
-/* Periodicity-search precision. Default: the exact i8-MFMA kernel on arithmetic-progression grids of >= 256
- * trials (per-term error ~1e-9, integer sums; trials whose 10-sigma bound on those roundings cannot place them within
- * 1e-6 relative are recomputed in fp64 -- crimp_last_fixups()), the fp64 kernel otherwise. Tested within 1e-6 of the
- * reference on every checked trial; the reference's own fp64 argument rounding (~1e-6 of a noise-level H_20) is
- * the floor of any fp64 implementation. */
-#define CRIMP_FLAG_FORCE_MFMA 8u   /* search: fail unless a factorised kernel (exact i8 MFMA or NUFFT) applies */
+/* Periodicity-search precision. Default: the NUFFT (search_nufft.h) on arithmetic-progression grids (ascending)
+ * of >= 64 trials per row segment with time-sorted photons and a plan in range -- every trial certified within 1e-6
+ * relative by a truncation bound, the uncertified ones recomputed in fp64 (crimp_last_fixups()). Where the NUFFT
+ * declines: the exact i8-MFMA kernel on progressions of >= 256 trials (per-term error ~1e-9, integer sums; trials
+ * whose 10-sigma bound cannot place them within 1e-6 relative are recomputed in fp64), the fp64 kernel otherwise.
+ * crimp_last_search_path() says which ran. Tested within 1e-6 of the reference on every checked trial; the
+ * reference's own fp64 argument rounding (~1e-6 of a noise-level H_20) is the floor of any fp64 implementation
+ * (DESIGN.md section 8). */
+#define CRIMP_FLAG_FORCE_MFMA 8u   /* search: fail unless a factorised kernel (NUFFT, or exact i8 MFMA at any row
+                                    * length) applies */
 #define CRIMP_FLAG_TIME_KERNELS 128u /* search / calcphase: time the kernels with hipEvents (crimp_last_kernel_ms) */
 #define CRIMP_FLAG_F64 256u         /* search: fp64 kernel on every grid */
 #define CRIMP_FLAG_NO_FIXUP 1024u   /* search (diagnostic): the exact kernel's / the NUFFT's raw powers, without the
@@ -52,9 +57,10 @@ extern "C" {
 #define CRIMP_FLAG_ASYNC 2048u     /* crimp_search_sets with device pointers: return once the kernel is queued, without
                                      * draining the stream (the caller synchronises it before reading out) */
 
-#define CRIMP_FLAG_NUFFT 4096u     /* search: non-uniform FFT over an arithmetic-progression grid of >= 64 trials per
-                                    * row and time-sorted photons (search_nufft.h; otherwise the default path), every
-                                    * trial certified within 1e-6 relative like the default path, fp64 fix-up included */
+#define CRIMP_FLAG_NUFFT 4096u     /* search: the default routing, asked for explicitly (the NUFFT wherever it applies,
+                                    * the exact rule otherwise); kept for callers of rounds 5 and earlier */
+#define CRIMP_FLAG_EXACT 8192u     /* search: no NUFFT -- the exact i8-MFMA kernel on progressions of >= 256 trials,
+                                    * the fp64 kernel otherwise (the default of rounds 1-5) */
 
 #define CRIMP_STAT_Z2 0 /* Z^2_m  (periodsearch.py:57-71, :73-106) */
 #define CRIMP_STAT_H 1  /* H-test (periodsearch.py:109-125)         */
@@ -143,8 +149,8 @@ int crimp_calcphase(const double* t_mjd, int64_t n, const crimp_timing_model* mo
  * [first, first+count) of it into out[count]. stat = CRIMP_STAT_Z2 or CRIMP_STAT_H (the latter
  * over the 2-D grid is this library's extension). Precision: the CRIMP_FLAG_F64 / _NUFFT notes
  * above; the kernel is chosen from the whole grid (nf, nfd, progression), not from [first, count), so a sharded
- * search computes every trial exactly as an unsharded one -- except that CRIMP_FLAG_NUFFT plans each row segment of
- * [first, count) on its own (a shard of a row is its own progression, so it costs its share): whole rows are
+ * search computes every trial exactly as an unsharded one -- except that the NUFFT (the default) plans each row
+ * segment of [first, count) on its own (a shard of a row is its own progression, so it costs its share): whole rows are
  * bit-identical, a cut row agrees within the plans' ~1e-13 error. */
 int crimp_search(const double* t, int64_t n, double t0, const double* freq, int64_t nf,
                  const double* log10_negfdot, int64_t nfd, int32_t nharm, int32_t stat, int64_t first,

@@ -56,8 +56,11 @@ def _within_1e6_of_reference(got, z64, t_h, f_h, nharm, stat, name, what):
     return e, off.size
 
 
+@pytest.mark.parametrize("precision", ["exact", None])
 @pytest.mark.parametrize("nharm,stat", [(2, 0), (20, 1)])
-def test_certificate_holds_on_correlated_inputs(gpu, nharm, stat):
+def test_certificate_holds_on_correlated_inputs(gpu, nharm, stat, precision):
+    """precision="exact": the exact kernel's statistical certificate; None: the default NUFFT's truncation-bound
+    certificate (crimp_last_search_path() == 2) on the same correlated inputs."""
     import torch
     from crimp_amd import ops, _native as N
     O.set_threads(min(16, os.cpu_count() or 1))
@@ -67,9 +70,10 @@ def test_certificate_holds_on_correlated_inputs(gpu, nharm, stat):
     for name, t_h in inputs.items():
         t = torch.as_tensor(t_h, device=gpu)
         t0 = (t_h[0] + t_h[-1]) / 2
-        z = ops.search(t, t0, f, nharm, stat).cpu().numpy()
+        z = ops.search(t, t0, f, nharm, stat, precision=precision).cpu().numpy()
+        assert N.load().crimp_last_search_path() == (1 if precision == "exact" else 2)
         nfix = N.load().crimp_last_fixups()
-        raw = ops.search(t, t0, f, nharm, stat, flags=N.FLAG_NO_FIXUP).cpu().numpy()
+        raw = ops.search(t, t0, f, nharm, stat, flags=N.FLAG_NO_FIXUP, precision=precision).cpu().numpy()
         z64 = ops.search(t, t0, f, nharm, stat, precision="f64").cpu().numpy()
         e, noff = _within_1e6_of_reference(z, z64, t_h, f_h, nharm, stat, name, "default")
         flagged = z != raw                                   # the fix-up rewrote exactly the flagged trials
@@ -79,8 +83,8 @@ def test_certificate_holds_on_correlated_inputs(gpu, nharm, stat):
                                          "raw kernel on a certified trial")
         assert nfix <= 64, (name, nfix)                      # a kernel regression would flag most trials
         assert int(np.argmax(z)) == int(np.argmax(z64))
-        print("%s m=%d: max rel vs fp64 %.2e (raw certified %.2e), %d checked against the oracle, fix-ups %d" % (
-            name, nharm, e.max(), er.max(), noff, nfix))
+        print("%s %s m=%d: max rel vs fp64 %.2e (raw certified %.2e), %d checked against the oracle, fix-ups %d" % (
+            precision or "default", name, nharm, e.max(), er.max(), noff, nfix))
 
 
 def _run_child(code, env_extra, out):
@@ -100,7 +104,7 @@ def test_fold_path_many_ragged_trial_blocks_2d(gpu):
             "t = torch.as_tensor(t_h, device='cuda'); t0 = (t_h[0] + t_h[-1]) / 2; "
             "f = torch.as_tensor(7.123456789 + (np.arange(3000) - 1500) / 1.0e7, device='cuda'); "
             "fd = torch.as_tensor(np.linspace(-13.0, -11.0, 40), device='cuda'); "
-            "h = ops.search(t, t0, f, 8, 1, log10_negfdot=fd, first=1234, count=100000).cpu().numpy(); "
+            "h = ops.search(t, t0, f, 8, 1, log10_negfdot=fd, first=1234, count=100000, precision='exact').cpu().numpy(); "
             "np.savez(sys.argv[1], h=h)") % (str(__import__("conftest").ROOT))
     with tempfile.TemporaryDirectory() as d:
         a = _run_child(code, {}, os.path.join(d, "a.npz"))
@@ -110,7 +114,8 @@ def test_fold_path_many_ragged_trial_blocks_2d(gpu):
 
 def test_short_rows_2d_route_to_fp64(gpu):
     """A 2-D grid of 2-trial rows (300 rows) would fill 2048-trial tiles with dead columns: it takes the fp64
-    kernel (bit-identical to precision='f64'); 256-trial rows still take the exact kernel."""
+    kernel (bit-identical to precision='f64'); 256-trial rows take the NUFFT by default and the exact kernel with
+    precision='exact'."""
     import torch
     from crimp_amd import ops
     from crimp_amd.synth import pulsed_events
@@ -123,9 +128,13 @@ def test_short_rows_2d_route_to_fp64(gpu):
     z64 = ops.search(t, t0, f2, 2, 0, log10_negfdot=fd, precision="f64").cpu().numpy()
     np.testing.assert_array_equal(z, z64)
     f256 = torch.as_tensor(3.3 + np.arange(256) / 2.0e6, device=gpu)
-    z = ops.search(t, t0, f256, 2, 0, log10_negfdot=fd[:4]).cpu().numpy()
+    from crimp_amd import _native as N
+    assert N.load().crimp_last_search_path() == 0
     z64 = ops.search(t, t0, f256, 2, 0, log10_negfdot=fd[:4], precision="f64").cpu().numpy()
-    assert not np.array_equal(z, z64) and _rel(z, z64).max() <= 1e-6
+    for prec, path in ((None, 2), ("exact", 1)):
+        z = ops.search(t, t0, f256, 2, 0, log10_negfdot=fd[:4], precision=prec).cpu().numpy()
+        assert N.load().crimp_last_search_path() == path
+        assert not np.array_equal(z, z64) and _rel(z, z64).max() <= 1e-6
 
 
 def _sample_template(tm, n, shift, rng):

@@ -26,7 +26,8 @@ def test_config3_full_size(gpu):
     f = torch.as_tensor(f_h, device=gpu)
     t0 = (t_h[0] + t_h[-1]) / 2
     from crimp_amd import _native as N
-    z = ops.search(t, t0, f, 2, 0).cpu().numpy()
+    z = ops.search(t, t0, f, 2, 0, precision="exact").cpu().numpy()
+    assert N.load().crimp_last_search_path() == 1
     # fix-up ceiling: the exact kernel, not the fp64 recomputation, must produce these powers (a kernel regression
     # that the certificate catches would send most trials through the fix-up and still pass the checks below)
     assert N.load().crimp_last_fixups() <= 16
@@ -43,12 +44,13 @@ def test_config3_full_size(gpu):
         z64[w0] = ops.search(t, t0, f, 2, 0, first=w0, count=65536, precision="f64").cpu().numpy()
         assert _rel_err(z[w0:w0 + 65536], z64[w0]).max() <= 1e-6
     # sharding: two halves computed separately equal the whole, bit for bit
-    a = ops.search(t, t0, f, 2, 0, first=0, count=M // 2 + 123).cpu().numpy()
-    b = ops.search(t, t0, f, 2, 0, first=M // 2 + 123, count=M - (M // 2 + 123)).cpu().numpy()
+    a = ops.search(t, t0, f, 2, 0, first=0, count=M // 2 + 123, precision="exact").cpu().numpy()
+    b = ops.search(t, t0, f, 2, 0, first=M // 2 + 123, count=M - (M // 2 + 123), precision="exact").cpu().numpy()
     np.testing.assert_array_equal(np.concatenate([a, b]), z)
-    # the NUFFT over the whole grid: every trial within 1e-6 relative of the exact path (both within 1e-6 of the
-    # reference), same best trial, the sampled oracle trials at plain 1e-6, and its fix-up list small
-    zn = ops.search(t, t0, f, 2, 0, precision="nufft").cpu().numpy()
+    # the default call (the reference's own PeriodSearch(t, f, 2).ztest() reaches it) runs the NUFFT over the whole
+    # grid: every trial within 1e-6 relative of the exact path (both within 1e-6 of the reference), same best
+    # trial, the sampled oracle trials at plain 1e-6, and its fix-up list small
+    zn = ops.search(t, t0, f, 2, 0).cpu().numpy()
     assert N.load().crimp_last_search_path() == 2
     assert N.load().crimp_last_fixups() <= 16
     assert _rel_err(zn, z).max() <= 1e-6
@@ -61,7 +63,7 @@ def test_config3_full_size(gpu):
     assert abs(far.mean() - 4.0) < 0.05
 
 
-@pytest.mark.parametrize("precision", [None, "nufft"])
+@pytest.mark.parametrize("precision", ["exact", None])
 def test_config4_windows_vs_oracle(gpu, precision):
     """Config 4 at plain 1e-6 against the oracle over all 1e8 photons, on contiguous trial windows: 32 noise-level
     trials at the start of the far row (log10|fdot| = -13.5), 32 beside the peak and the peak with its neighbours in
@@ -69,8 +71,8 @@ def test_config4_windows_vs_oracle(gpu, precision):
     its values are committed with checksums of the regenerated photons, tests/golden/gen_config4_windows.py).
     ``ref`` follows the reference's operation order (periodsearch.py:93-98, :118-123); ``true`` is the same formula
     with the argument carried exactly, so ref-vs-true is the reference's own argument rounding (<= 1.6e-7 here).
-    precision="nufft" computes the windows' rows whole (1e5 trials each: a 32-trial range is below the NUFFT's
-    64-trial minimum and would take the default path) and checks the windows cut from them."""
+    The default (NUFFT) computes the windows' rows whole (1e5 trials each: a 32-trial range is below the NUFFT's
+    64-trial minimum and would take the exact rule) and checks the windows cut from them."""
     import os
     import sys
     import torch
@@ -89,31 +91,33 @@ def test_config4_windows_vs_oracle(gpu, precision):
     fd = torch.as_tensor(FD, device=gpu)
     got, nfix, rows = [], 0, {}
     for r, j0, cnt in WINDOWS:
-        if precision == "nufft":
+        if precision is None:
             if r not in rows:
-                rows[r] = ops.search(t, t0, f, 20, 1, log10_negfdot=fd, first=r * M, count=M,
-                                     precision="nufft").cpu().numpy()
+                rows[r] = ops.search(t, t0, f, 20, 1, log10_negfdot=fd, first=r * M, count=M).cpu().numpy()
                 assert N.load().crimp_last_search_path() == 2
                 nfix += N.load().crimp_last_fixups()
             got.append(rows[r][j0:j0 + cnt])
             continue
-        got.append(ops.search(t, t0, f, 20, 1, log10_negfdot=fd, first=r * M + j0, count=cnt).cpu().numpy())
+        got.append(ops.search(t, t0, f, 20, 1, log10_negfdot=fd, first=r * M + j0, count=cnt,
+                              precision="exact").cpu().numpy())
+        assert N.load().crimp_last_search_path() == 1
         nfix += N.load().crimp_last_fixups()
     h = np.concatenate(got)
     assert _rel_err(h, fx["ref"]).max() <= 1e-6          # measured 2.6e-7 (profiles/r03/config4_windows.json)
     assert _rel_err(h, fx["true"]).max() <= 1e-6         # measured 1.4e-7
     assert np.median(_rel_err(h, fx["ref"])) <= 1e-7
     assert int(np.argmax(h)) == int(np.argmax(fx["ref"]))
-    assert nfix <= (8 if precision is None else 64)     # nufft: fix-ups over two whole rows of 1e5 trials
+    assert nfix <= (8 if precision == "exact" else 64)  # default: fix-ups over two whole rows of 1e5 trials
 
 
-def test_config4_full_photon_count_h20(gpu):
+@pytest.mark.parametrize("precision", ["exact", None])
+def test_config4_full_photon_count_h20(gpu, precision):
     """1e8 photons with fdot, 2-D H-test m=20 on a 3 x 8192 trial sub-grid (the full 1e7-trial grid runs sharded
     on 8 GPUs in the bench configuration) whose rows include both ends of config 4's log10|fdot| range: oracle over
     all photons on 8 sampled trials (plain per-trial relative error), and every fd row computed as its own trial
-    range bit-identical to the whole grid."""
+    range bit-identical to the whole grid (the exact path; the default NUFFT with its MFMA-slot spread)."""
     import torch
-    from crimp_amd import ops
+    from crimp_amd import ops, _native as N
     from crimp_amd.synth import pulsed_events
     n, span, f0, fdot = 100_000_000, 1.0e7, 7.123456789, -1.0e-12
     t_h = pulsed_events(n, span, f0, pulsed_frac=0.05, fdot=fdot, seed=1)
@@ -125,12 +129,13 @@ def test_config4_full_photon_count_h20(gpu):
     f = torch.as_tensor(f_h, device=gpu)
     fdd = torch.as_tensor(fd, device=gpu)
     t0 = (t_h[0] + t_h[-1]) / 2
-    hf = ops.search(t, t0, f, 20, 1, log10_negfdot=fdd).cpu().numpy()
+    hf = ops.search(t, t0, f, 20, 1, log10_negfdot=fdd, precision=precision).cpu().numpy()
+    assert N.load().crimp_last_search_path() == (1 if precision == "exact" else 2)
     h = hf.reshape(3, M)
     r, j = np.unravel_index(int(np.argmax(h)), h.shape)
     assert r == 1 and j == M // 2                              # fdot = -1e-12 -> log10 = -12, f0 at index M/2
     for row in range(3):                                       # row-sharded, as 3 ranks would compute it
-        hr = ops.search(t, t0, f, 20, 1, log10_negfdot=fdd, first=row * M, count=M).cpu().numpy()
+        hr = ops.search(t, t0, f, 20, 1, log10_negfdot=fdd, first=row * M, count=M, precision=precision).cpu().numpy()
         np.testing.assert_array_equal(hr, h[row])
     rng = np.random.default_rng(4)
     sample = [(1, M // 2), (1, M // 2 + 1), (0, 100), (2, M - 1)] + [(int(a), int(b)) for a, b in
@@ -171,10 +176,10 @@ def test_trial_blocks_and_fixup(gpu, monkeypatch):
     t = torch.as_tensor(t_h, device=gpu)
     f = torch.as_tensor(f_h, device=gpu)
     t0 = (t_h[0] + t_h[-1]) / 2
-    h = ops.search(t, t0, f, 20, 1).cpu().numpy()
+    h = ops.search(t, t0, f, 20, 1, precision="exact").cpu().numpy()
     assert int(np.argmax(h)) == M // 2
     monkeypatch.setenv("CRIMP_SEARCH_BUDGET_MB", "4")
-    hb = ops.search(t, t0, f, 20, 1).cpu().numpy()
+    hb = ops.search(t, t0, f, 20, 1, precision="exact").cpu().numpy()
     np.testing.assert_array_equal(hb, h)
     idx = np.array([0, 450_000, 450_559, 450_560, 450_561, M - 1])
     hr = O.search(t_h, f_h[idx], 20, stat="h")
@@ -186,7 +191,7 @@ def test_trial_blocks_and_fixup(gpu, monkeypatch):
     code = ("import sys, numpy as np; sys.path.insert(0, %r); from crimp_amd import ops, _native as N; "
             "from crimp_amd.synth import pulsed_events; t = pulsed_events(200000, 2.0e5, 7.123456789, "
             "pulsed_frac=0.05, seed=4); f = 7.123456789 + np.arange(-1024, 1024) / 2.0e6; t0 = (t[0] + t[-1]) / 2; "
-            "z = ops.search(t, t0, f, 2, 0); nfix = N.load().crimp_last_fixups(); "
+            "z = ops.search(t, t0, f, 2, 0, precision='exact'); nfix = N.load().crimp_last_fixups(); "
             "z64 = ops.search(t, t0, f, 2, 0, precision='f64'); np.savez(sys.argv[1], z=z, z64=z64, nfix=nfix)") % (
         str(__import__("conftest").ROOT))
     import tempfile
@@ -370,10 +375,11 @@ def test_cauchy_vonmises_blocks_1e5(gpu):
             _fit_vs_oracle(r, i, xs[i], E[i], tm)
 
 
-def test_exact_vs_f64_every_trial(gpu):
-    """The per-trial contract on every trial of larger grids, near-zero powers included: the default (exact +
-    fix-up) path against the fp64 path (itself within 1e-8 of the reference's outputs), 1e6 photons, Z^2_4 over
-    16384 trials and 2-D H_20 over 2 x 8192 trials."""
+@pytest.mark.parametrize("precision", ["exact", None])
+def test_exact_vs_f64_every_trial(gpu, precision):
+    """The per-trial contract on every trial of larger grids, near-zero powers included: the exact (+ fix-up) path
+    and the default (NUFFT + fix-up) against the fp64 path (itself within 1e-8 of the reference's outputs), 1e6
+    photons, Z^2_4 over 16384 trials and 2-D H_20 over 2 x 8192 trials."""
     import torch
     from crimp_amd import ops, _native as N
     from crimp_amd.synth import pulsed_events
@@ -381,11 +387,12 @@ def test_exact_vs_f64_every_trial(gpu):
     t = torch.as_tensor(t_h, device=gpu)
     t0 = (t_h[0] + t_h[-1]) / 2
     f = torch.as_tensor(7.123456789 + (np.arange(16384) - 8192) / 1.0e7, device=gpu)
-    z = ops.search(t, t0, f, 4, 0).cpu().numpy()
+    z = ops.search(t, t0, f, 4, 0, precision=precision).cpu().numpy()
+    assert N.load().crimp_last_search_path() == (1 if precision == "exact" else 2)
     z64 = ops.search(t, t0, f, 4, 0, precision="f64").cpu().numpy()
     assert _rel_err(z, z64).max() <= 1e-6
     fd = torch.as_tensor(np.array([-12.0, -11.0]), device=gpu)
-    h = ops.search(t, t0, f[4096:12288], 20, 1, log10_negfdot=fd).cpu().numpy()
+    h = ops.search(t, t0, f[4096:12288], 20, 1, log10_negfdot=fd, precision=precision).cpu().numpy()
     nfix = N.load().crimp_last_fixups()
     h64 = ops.search(t, t0, f[4096:12288], 20, 1, log10_negfdot=fd, precision="f64").cpu().numpy()
     assert _rel_err(h, h64).max() <= 1e-6
@@ -403,13 +410,15 @@ def test_exact_many_harmonics_and_ragged_partitions(gpu):
     t = torch.as_tensor(t_h, device=gpu)
     t0 = (t_h[0] + t_h[-1]) / 2
     f = torch.as_tensor(3.3 + (np.arange(1000) - 500) / 2.0e6, device=gpu)
-    h = ops.search(t, t0, f, 64, 1).cpu().numpy()
+    h = ops.search(t, t0, f, 64, 1, precision="exact").cpu().numpy()
     h64 = ops.search(t, t0, f, 64, 1, precision="f64").cpu().numpy()
     assert _rel_err(h, h64).max() <= 1e-6
+    hd = ops.search(t, t0, f, 64, 1).cpu().numpy()   # the default (NUFFT) at 64 harmonics
+    assert _rel_err(hd, h64).max() <= 1e-6
     fd = torch.as_tensor(np.array([-13.0, -12.0, -11.0]), device=gpu)
-    whole = ops.search(t, t0, f, 2, 0, log10_negfdot=fd).cpu().numpy()
+    whole = ops.search(t, t0, f, 2, 0, log10_negfdot=fd, precision="exact").cpu().numpy()
     cuts = [0, 1, 999, 1500, 2047, 2100, 3000]
-    parts = [ops.search(t, t0, f, 2, 0, log10_negfdot=fd, first=a, count=b - a).cpu().numpy()
+    parts = [ops.search(t, t0, f, 2, 0, log10_negfdot=fd, first=a, count=b - a, precision="exact").cpu().numpy()
              for a, b in zip(cuts[:-1], cuts[1:])]
     np.testing.assert_array_equal(np.concatenate(parts), whole)
 
@@ -429,13 +438,13 @@ def test_exact_path_above_2_27_photons(gpu):
     t0 = float((t[0] + t[-1]).item()) / 2
     for nn in (n, (1 << 27) - 1):
         tt = t[:nn]
-        z = ops.search(tt, t0, f, 2, 0).cpu().numpy()
+        z = ops.search(tt, t0, f, 2, 0, precision="exact").cpu().numpy()
         assert N.load().crimp_last_search_path() == 1
         assert N.load().crimp_last_fixups() <= 8
         z64 = ops.search(tt, t0, f, 2, 0, precision="f64").cpu().numpy()
         assert _rel_err(z, z64).max() <= 1e-6
         assert not np.array_equal(z, z64)       # a different (exact) kernel ran
-        zn = ops.search(tt, t0, f, 2, 0, precision="nufft").cpu().numpy()
+        zn = ops.search(tt, t0, f, 2, 0).cpu().numpy()   # the default
         assert N.load().crimp_last_search_path() == 2
         assert _rel_err(zn, z64).max() <= 1e-6
 
@@ -456,9 +465,9 @@ def test_exact_long_splits_fold_path_bit_identical(gpu):
         "import torch; t_h = pulsed_events(4000000, 1.0e6, 7.123456789, pulsed_frac=0.05, seed=6); "
         "t = torch.as_tensor(t_h, device='cuda'); t0 = (t_h[0] + t_h[-1]) / 2; "
         "f = torch.as_tensor(7.123456789 + np.arange(-1000000, 1000000) / 1.0e7, device='cuda'); "
-        "z = ops.search(t, t0, f, 3, 0).cpu().numpy(); "
+        "z = ops.search(t, t0, f, 3, 0, precision='exact').cpu().numpy(); "
         "fd = torch.as_tensor(np.array([-13.0, -12.0]), device='cuda'); "
-        "h = ops.search(t, t0, f[:524288], 8, 1, log10_negfdot=fd).cpu().numpy(); "
+        "h = ops.search(t, t0, f[:524288], 8, 1, log10_negfdot=fd, precision='exact').cpu().numpy(); "
         "np.savez(sys.argv[1], z=z, h=h)") % (str(__import__("conftest").ROOT))
     with tempfile.TemporaryDirectory() as d:
         res = []

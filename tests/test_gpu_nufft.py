@@ -1,7 +1,8 @@
-"""precision="nufft" (csrc/search_nufft.h) through the C-ABI: the non-uniform-FFT Z^2 / H search against the
-reference's goldens and the oracle at the default path's per-trial contract (plain 1e-6 relative, best trial
-exact), its raw powers (fix-up off) against the fp64 kernel, determinism, row sharding, and the routes it leaves
-to the default path (unsorted photons, short or non-uniform grids). Full-size configs: tests/test_gpu_fullsize.py."""
+"""The NUFFT (csrc/search_nufft.h; the default search path, also asked for by precision="nufft") through the C-ABI:
+the non-uniform-FFT Z^2 / H search against the reference's goldens and the oracle at the per-trial contract (plain
+1e-6 relative, best trial exact), its raw powers (fix-up off) against the fp64 kernel, determinism, row sharding,
+and the inputs it declines to the exact rule (unsorted photons, short, non-uniform or descending grids, cells beyond
+32 bits). Full-size configs: tests/test_gpu_fullsize.py."""
 import numpy as np
 import pytest
 
@@ -144,7 +145,12 @@ def test_nufft_deterministic_and_row_shards(gpu):
     assert np.median(np.abs(cut - full) / np.abs(full)) <= 1e-12
 
 
-def test_nufft_unsorted_photons_take_default_path(gpu):
+@pytest.mark.parametrize("precision", [None, "nufft"])
+def test_nufft_unsorted_photons_take_default_path(gpu, precision):
+    """Unsorted photons: the NUFFT declines and the exact rule runs -- the exact kernel on a 512-trial progression,
+    the fp64 kernel on a 128-trial one (rows of < 256 trials never take the exact kernel, whichever precision was
+    asked for; bit-identical to precision="f64")."""
+    from crimp_amd import ops
     from crimp_amd.periodsearch import PeriodSearch
     from crimp_amd.synth import pulsed_events
     t = pulsed_events(50000, 5.0e4, 2.5, pulsed_frac=0.2, seed=3)
@@ -152,9 +158,52 @@ def test_nufft_unsorted_photons_take_default_path(gpu):
     rng = np.random.default_rng(0)
     tp = t[rng.permutation(t.size)]
     tp[0], tp[-1] = t[0], t[-1]  # same t0
-    z = PeriodSearch(tp, f, 2, precision="nufft").ztest()
+    z = PeriodSearch(tp, f, 2, precision=precision).ztest()
     assert _path() == 1
     close_rel(z, O.search(tp, f, 2))
+    z = PeriodSearch(tp, f[:128], 2, precision=precision).ztest()
+    assert _path() == 0
+    t0 = (tp[0] + tp[-1]) / 2
+    np.testing.assert_array_equal(z, ops.search(tp, t0, f[:128], 2, 0, precision="f64"))
+    close_rel(z, O.search(tp, f[:128], 2))
+
+
+@pytest.mark.parametrize("precision", [None, "nufft"])
+def test_nufft_declines_descending_grid(gpu, precision):
+    """A descending progression (delta < 0, accepted by the progression check) would size the NUFFT's cell tables
+    negative: the plan declines it and the exact kernel runs, within 1e-6 of the oracle on every trial (1-D Z^2_2
+    and 2-D H_3)."""
+    from crimp_amd.periodsearch import PeriodSearch
+    from crimp_amd.synth import pulsed_events
+    t = pulsed_events(100000, 1.0e5, 3.0, pulsed_frac=0.1, seed=19)
+    f = np.flip(3.0 + np.arange(-512, 512) / 1.0e6)
+    z = PeriodSearch(t, f, 2, precision=precision).ztest()
+    assert _path() == 1
+    zr = O.search(t, f, 2)
+    assert int(np.argmax(z)) == int(np.argmax(zr))
+    close_rel(z, zr)
+    fd = np.array([-12.0, -11.0])
+    a = PeriodSearch(t, f[256:768], 3, precision=precision).twod_htest(fd)[0][:, 2]
+    assert _path() == 1
+    close_rel(a, O.search(t, f[256:768], 3, freq_dot=fd, stat="h"))
+
+
+def test_nufft_declines_cells_beyond_32_bits(gpu):
+    """The kernels convert cells with 32-bit rint: a reference time far from the photons (t0 = 0 for photons near
+    5e9 s) puts the cells of a 4096-trial grid at 2e-4 Hz steps past 2^31 although the photons span only 3 wraps of
+    the FFT. The plan declines (the exact kernel runs, bit-identical to precision="exact" with the same t0); with
+    the photons' midpoint as t0 the same grid takes the NUFFT. (1-D Z^2 does not depend on t0.)"""
+    from crimp_amd import ops
+    rng = np.random.default_rng(23)
+    t = np.sort(5.0e9 + rng.uniform(0.0, 1.0e4, 20000))
+    f = 1.0 + np.arange(4096) * 2.0e-4
+    z0 = ops.search(t, 0.0, f, 2, 0)
+    assert _path() == 1
+    np.testing.assert_array_equal(z0, ops.search(t, 0.0, f, 2, 0, precision="exact"))
+    tm = (t[0] + t[-1]) / 2
+    zm = ops.search(t, tm, f, 2, 0)
+    assert _path() == 2
+    close_rel(zm, ops.search(t, tm, f, 2, 0, precision="f64"))
 
 
 def test_nufft_fused_pass2_equals_separate_combine(gpu, monkeypatch):

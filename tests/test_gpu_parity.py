@@ -1,9 +1,10 @@
 """HIP path (through the C-ABI) against the oracle and the reference's golden vectors.
 
 Tolerances (BASELINE.json north_star): Z^2/H powers within 1e-6 relative PER TRIAL (plain relative error,
-no scale floor: ``close_rel``) for the default search path (exact-integer i8 MFMA kernel, fp64 kernel on
-other grids) and the fp64 path; best-trial index bit-exact; ToA phase shifts within 1e-4 cycles;
-calcphase within 1e-9 cycles; LL within 1e-9 relative (fp64 kernel). precision="nufft": tests/test_gpu_nufft.py.
+no scale floor: ``close_rel``) for the default search path (the NUFFT where it applies, else the exact rule),
+precision="exact" (exact-integer i8 MFMA kernel, fp64 kernel on other grids) and the fp64 path; best-trial index
+bit-exact; ToA phase shifts within 1e-4 cycles; calcphase within 1e-9 cycles; LL within 1e-9 relative (fp64
+kernel). NUFFT internals (raw powers, plans, row shards): tests/test_gpu_nufft.py.
 """
 import json
 import math
@@ -27,53 +28,61 @@ def close_rel(got, ref, rtol=RTOL):
     return err.max()
 
 
-def test_z2_h_config1_golden(gpu):
-    """Config 1 (default path: the exact kernel on the 400-trial progression, 20 launches for H_20)."""
+@pytest.mark.parametrize("precision,path", [(None, 2), ("exact", 1)])
+def test_z2_h_config1_golden(gpu, precision, path):
+    """Config 1 through the reference's own call, PeriodSearch(time, freq, m).ztest() / .htest() / .twod_ztest(): the
+    default reaches the NUFFT (crimp_last_search_path() == 2) on the 400-trial progression of the 1E 2259 events;
+    precision="exact" the exact kernel (20 launches for H_20)."""
     from crimp_amd.periodsearch import PeriodSearch
+    from crimp_amd import _native as N
     g = gold("periodsearch_1e2259.npz")
-    z = PeriodSearch(g["time"], g["freq"], 2).ztest()
+    z = PeriodSearch(g["time"], g["freq"], 2, precision=precision).ztest()
+    assert N.load().crimp_last_search_path() == path
     assert int(np.argmax(z)) == 200
     close_rel(z, g["z2_m2"])
-    h = PeriodSearch(g["time"], g["freq"], 20).htest()
+    h = PeriodSearch(g["time"], g["freq"], 20, precision=precision).htest()
+    assert N.load().crimp_last_search_path() == path
     assert int(np.argmax(h)) == 200
     close_rel(h, g["h_m20"])
-    arr, df = PeriodSearch(g["time"], g["fsub"], 2).twod_ztest(g["fd"])
+    arr, df = PeriodSearch(g["time"], g["fsub"], 2, precision=precision).twod_ztest(g["fd"])
     np.testing.assert_array_equal(arr[:, :2], g["z2d_m2"][:, :2])
     close_rel(arr[:, 2], g["z2d_m2"][:, 2])
     assert list(df.columns) == ["Freq", "Freq_dot", "Z2pow"]
 
 
-def test_search_synthetic_golden_and_edges(gpu):
+@pytest.mark.parametrize("precision", [None, "exact"])
+def test_search_synthetic_golden_and_edges(gpu, precision):
     from crimp_amd.periodsearch import PeriodSearch
     g = gold("periodsearch_synth.npz")
     t, f = g["time"], g["freq"]
+    P = precision
     for m in (1, 2, 3, 5):
-        z = PeriodSearch(t, f, m).ztest()
+        z = PeriodSearch(t, f, m, precision=P).ztest()
         close_rel(z, g["z_m%d" % m])
         assert np.argmax(z) == np.argmax(g["z_m%d" % m])
     for m in (1, 5, 20):
-        close_rel(PeriodSearch(t, f, m).htest(), g["h_m%d" % m])
-    close_rel(PeriodSearch(t, f[64:128], 2).twod_ztest(g["fd"])[0][:, 2], g["z2d_m2"][:, 2])
-    close_rel(PeriodSearch(t, f[64:128], 3).twod_ztest(g["fd"])[0][:, 2], g["z2d_m3"][:, 2])
-    close_rel(PeriodSearch(g["time_perm"], g["freq_nu"], 2).ztest(), g["z_nonuniform_m2"])
-    close_rel(PeriodSearch(g["time_perm"], g["freq_nu"], 4).htest(), g["h_nonuniform_m4"])
-    close_rel(PeriodSearch(t[:1], f[:8], 2).ztest(), g["z_n1"])
-    close_rel(PeriodSearch(t[:2], f[:8], 2).ztest(), g["z_n2"])
-    close_rel(PeriodSearch(t[:2], f[:8], 3).htest(), g["h_n2"])
-    close_rel(PeriodSearch(t, f[100:101], 2).ztest(), g["z_m1trial"])
-    assert PeriodSearch(t, f[:0], 2).ztest().size == 0
+        close_rel(PeriodSearch(t, f, m, precision=P).htest(), g["h_m%d" % m])
+    close_rel(PeriodSearch(t, f[64:128], 2, precision=P).twod_ztest(g["fd"])[0][:, 2], g["z2d_m2"][:, 2])
+    close_rel(PeriodSearch(t, f[64:128], 3, precision=P).twod_ztest(g["fd"])[0][:, 2], g["z2d_m3"][:, 2])
+    close_rel(PeriodSearch(g["time_perm"], g["freq_nu"], 2, precision=P).ztest(), g["z_nonuniform_m2"])
+    close_rel(PeriodSearch(g["time_perm"], g["freq_nu"], 4, precision=P).htest(), g["h_nonuniform_m4"])
+    close_rel(PeriodSearch(t[:1], f[:8], 2, precision=P).ztest(), g["z_n1"])
+    close_rel(PeriodSearch(t[:2], f[:8], 2, precision=P).ztest(), g["z_n2"])
+    close_rel(PeriodSearch(t[:2], f[:8], 3, precision=P).htest(), g["h_n2"])
+    close_rel(PeriodSearch(t, f[100:101], 2, precision=P).ztest(), g["z_m1trial"])
+    assert PeriodSearch(t, f[:0], 2, precision=P).ztest().size == 0
     with pytest.raises(IndexError):
-        PeriodSearch(t[:0], f, 2)
+        PeriodSearch(t[:0], f, 2, precision=P)
 
 
-@pytest.mark.parametrize("mode", ["exact", "f64", "nufft"])
+@pytest.mark.parametrize("mode", ["default", "exact", "f64", "nufft"])
 def test_search_vs_oracle_larger(gpu, mode):
     """Every search path on 2e5 photons x 2048 trials (Z^2_2) and a 3 x 1024 2-D grid (H_3): per trial within 1e-6
     relative; best trial exact."""
     from crimp_amd.periodsearch import PeriodSearch
     from crimp_amd.synth import pulsed_events
     from crimp_amd import _native as N
-    prec = {"exact": None, "f64": "f64", "nufft": "nufft"}[mode]
+    prec = {"default": None, "exact": "exact", "f64": "f64", "nufft": "nufft"}[mode]
     check = close_rel
     t = pulsed_events(200000, 2.0e5, 7.123456789, pulsed_frac=0.05, seed=4)
     f = 7.123456789 + (np.arange(-1024, 1024) / (10 * 2.0e5))
@@ -86,8 +95,7 @@ def test_search_vs_oracle_larger(gpu, mode):
     ar = O.search(t, f[512:1536], 3, freq_dot=fd, stat="h")
     assert int(np.argmax(a)) == int(np.argmax(ar))
     check(a, ar)
-    if mode == "exact":
-        assert N.load().crimp_last_fixups() >= 0
+    assert N.load().crimp_last_search_path() == {"default": 2, "exact": 1, "f64": 0, "nufft": 2}[mode]
 
 
 def test_search_f64_strict_relative_vs_reference_goldens(gpu):
@@ -132,7 +140,9 @@ def test_search_f64_larger_vs_oracle(gpu):
 
 
 def test_search_sharded_ranges_equal_full(gpu):
-    """A search split into flat-trial ranges (what each rank computes) equals the unsplit search."""
+    """precision="exact": a search split into flat-trial ranges (what each rank computes) equals the unsplit search
+    bit for bit (integer totals); the default (NUFFT) split at row edges is bit-identical too, a cut row agrees within
+    its plans' error."""
     from crimp_amd import ops
     from crimp_amd.synth import pulsed_events
     t = pulsed_events(50000, 1.0e5, 3.0, pulsed_frac=0.1, seed=9)
@@ -140,16 +150,24 @@ def test_search_sharded_ranges_equal_full(gpu):
     fd = np.array([-12.0, -11.0])
     t0 = (t[0] + t[-1]) / 2
     from crimp_amd import _native as N
-    full = ops.search(t, t0, f, 2, 0, log10_negfdot=fd)
+    full = ops.search(t, t0, f, 2, 0, log10_negfdot=fd, precision="exact")
     # the exact kernel, not its fp64 fix-up, must produce these (a broken exact kernel is hidden by a fix-up of
     # every trial; at 5e4 photons and powers ~1 the error bound flags none)
     assert N.load().crimp_last_fixups() <= 12
-    parts = [ops.search(t, t0, f, 2, 0, log10_negfdot=fd, first=a, count=b - a)
+    parts = [ops.search(t, t0, f, 2, 0, log10_negfdot=fd, first=a, count=b - a, precision="exact")
              for a, b in ((0, 333), (333, 901), (901, 1200))]
     np.testing.assert_array_equal(np.concatenate(parts), full)
+    dfull = ops.search(t, t0, f, 2, 0, log10_negfdot=fd)
+    assert N.load().crimp_last_search_path() == 2
+    drows = [ops.search(t, t0, f, 2, 0, log10_negfdot=fd, first=a, count=600) for a in (0, 600)]
+    np.testing.assert_array_equal(np.concatenate(drows), dfull)
+    dparts = [ops.search(t, t0, f, 2, 0, log10_negfdot=fd, first=a, count=b - a)
+              for a, b in ((0, 333), (333, 901), (901, 1200))]
+    close_rel(np.concatenate(dparts), dfull, 1e-6)
+    close_rel(dfull, full, 1e-6)
     for twod in (None, fd):  # raw exact-kernel powers (fix-up off) within the kernel's error model of fp64
         ref = ops.search(t, t0, f, 2, 0, log10_negfdot=twod, precision="f64")
-        z = ops.search(t, t0, f, 2, 0, log10_negfdot=twod, flags=N.FLAG_NO_FIXUP)
+        z = ops.search(t, t0, f, 2, 0, log10_negfdot=twod, flags=N.FLAG_NO_FIXUP, precision="exact")
         close_rel(z, ref, 1e-6)
 
 
