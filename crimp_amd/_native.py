@@ -25,6 +25,8 @@ FLAG_NO_FIXUP = 1024
 FLAG_ASYNC = 2048
 FLAG_NUFFT = 4096
 FLAG_EXACT = 8192
+FLAG_TIME_DAYS = 16384
+FLAG_FOLD_RADIANS = 32768
 
 STAT_Z2 = 0
 STAT_H = 1
@@ -58,7 +60,8 @@ class Template(ctypes.Structure):
 EXPORTS = ("crimp_version", "crimp_last_error", "crimp_last_kernel_ms", "crimp_last_kernel_times", "crimp_last_fixups",
            "crimp_last_search_path", "crimp_last_nufft_plan", "crimp_last_nufft_work", "crimp_last_toa_grid_norms", "crimp_last_toa_grid_fast", "crimp_release_scratch",
            "crimp_device_count", "crimp_calcphase", "crimp_search", "crimp_best", "crimp_search_sets", "crimp_toa_points",
-           "crimp_toa_grid", "crimp_toa_fit", "crimp_toa_redchi2", "crimp_toa_fit_redchi2", "crimp_toa_shape_points", "crimp_binphases")
+           "crimp_toa_grid", "crimp_toa_fit", "crimp_toa_redchi2", "crimp_toa_fit_redchi2", "crimp_toa_shape_points", "crimp_binphases",
+           "crimp_is_sorted", "crimp_select_intervals", "crimp_gather_ranges")
 
 _lib = None
 _lock = threading.Lock()
@@ -97,6 +100,9 @@ def load(require_device=True):
             L.crimp_toa_fit.argtypes = [P, P, i64, ctypes.POINTER(Template), P, ctypes.c_double, i32, i32, P, u32, P]
             L.crimp_toa_shape_points.argtypes = [P, P, i64, ctypes.POINTER(Template), P, P, P, P, i64, P, u32, P]
             L.crimp_binphases.argtypes = [P, P, i64, P, i32, P, u32, P]
+            L.crimp_is_sorted.argtypes = [P, i64, ctypes.POINTER(i32), u32, P]
+            L.crimp_select_intervals.argtypes = [P, i64, P, P, i64, P, P, P, u32, P]
+            L.crimp_gather_ranges.argtypes = [P, i64, P, P, i64, P, u32, P]
             L.crimp_toa_redchi2.argtypes = [P, P, i64, ctypes.POINTER(Template), P, P, P, P, i32, i32, P, u32, P]
             L.crimp_toa_fit_redchi2.argtypes = [P, P, i64, ctypes.POINTER(Template), P, ctypes.c_double, i32, i32, P, P,
                                                 i32, i32, P, P, u32, P]

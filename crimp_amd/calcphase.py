@@ -52,8 +52,12 @@ class Phases:
         return self._run(PART_GLITCH)
 
     def waves(self):
-        if not any(k.startswith("WAVE") for k in self.timModParam):
-            return 0  # calcphase.py:136 returns the scalar 0 without waves
+        # calcphase.py:135-149: the harmonics are WAVE1 .. WAVE(n-2) of the n WAVE* keys (WAVEEPOCH and WAVE_OM
+        # among them); with none -- no WAVE* key at all, or only the epoch and OM -- the loop adds nothing and the
+        # reference returns the scalar 0 * F0 (KeyError without F0, as there)
+        nharm = sum(1 for k in self.timModParam if k.startswith("WAVE")) - 2
+        if nharm <= 0:
+            return 0 * self.timModParam["F0"]
         return self._run(PART_WAVES)
 
 

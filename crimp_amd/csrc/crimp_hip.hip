@@ -351,7 +351,7 @@ __device__ __forceinline__ double cp_one(const CPModel* __restrict__ M, double t
 // for a 4096-block grid-stride loop with 1, 2 or 4 loads in flight per thread (profiles/r1_s4/calcphase_ab.log).
 __global__ __launch_bounds__(256) void k_calcphase_vec(const double2* __restrict__ t, int64_t npair,
                                                        const CPModel Mv, double2* __restrict__ total,
-                                                       double2* __restrict__ folded) {
+                                                       double2* __restrict__ folded, double fscale) {
     const CPModel* M = &Mv;  // the model rides in the kernel arguments (no upload, no copy to the stack)
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < npair; i += (int64_t)gridDim.x * blockDim.x) {
         const double2 tv = t[i];
@@ -361,8 +361,8 @@ __global__ __launch_bounds__(256) void k_calcphase_vec(const double2* __restrict
         total[i] = tot;
         if (folded) {
             double2 fo;
-            fo.x = tot.x - floor(tot.x);
-            fo.y = tot.y - floor(tot.y);
+            fo.x = (tot.x - floor(tot.x)) * fscale;  // fscale 1 (cycles) or 2 pi (measureToAs.py:195, :200)
+            fo.y = (tot.y - floor(tot.y)) * fscale;
             folded[i] = fo;
         }
     }
@@ -370,12 +370,12 @@ __global__ __launch_bounds__(256) void k_calcphase_vec(const double2* __restrict
 
 __global__ __launch_bounds__(256) void k_calcphase_scalar(const double* __restrict__ t, int64_t n,
                                                           const CPModel Mv, double* __restrict__ total,
-                                                          double* __restrict__ folded) {
+                                                          double* __restrict__ folded, double fscale) {
     const CPModel* M = &Mv;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const double tot = cp_one(M, t[i]);
         total[i] = tot;
-        if (folded) folded[i] = tot - floor(tot);
+        if (folded) folded[i] = (tot - floor(tot)) * fscale;
     }
 }
 
@@ -1375,12 +1375,14 @@ constexpr int kSetBlock = 256;
 __global__ __launch_bounds__(kSetBlock) void k_search_sets(const double* __restrict__ t,
                                                            const int64_t* __restrict__ offsets,
                                                            const double* __restrict__ freq, int m, int stat,
-                                                           double* __restrict__ out) {
+                                                           double tscale, double* __restrict__ out) {
+#pragma clang fp contract(off)  // t * tscale rounded before the subtraction, as the host's TIME_toa * 86400
     __shared__ double red[kSetBlock / 64][16];
     const int64_t set = blockIdx.x;
     const int64_t a = offsets[set], b = offsets[set + 1];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const double t0 = (t[a] + t[b - 1]) / 2;
+    // tscale 1 (seconds) or 86400 (days: the reference's TIME_toa * 86400, measureToAs.py:211, in the same multiply)
+    const double t0 = (t[a] * tscale + t[b - 1] * tscale) / 2;
     const double f = freq[set];
     const double w = 2.0 / (double)(b - a);
     double zsum = 0.0, cum = 0.0, best = -INFINITY;
@@ -1390,7 +1392,7 @@ __global__ __launch_bounds__(kSetBlock) void k_search_sets(const double* __restr
 #pragma unroll
         for (int k = 0; k < 8; ++k) C[k] = S[k] = 0.0;
         for (int64_t i = a + tid; i < b; i += kSetBlock) {
-            const double ph = f * (t[i] - t0);
+            const double ph = f * (t[i] * tscale - t0);
             double s1, c1, s, c;
             sincospi(2.0 * (ph - rint(ph)), &s1, &c1);
             if (k0 == 1) {
@@ -1593,11 +1595,15 @@ extern "C" int crimp_calcphase(const double* t_mjd, int64_t n, const crimp_timin
         const int blocks = (int)std::min<int64_t>(cdiv(vec ? n / 2 : n, 256), int64_t(1) << 20);
         KernelTimer kt(s, flags & CRIMP_FLAG_TIME_KERNELS);
         kt.start();
+        // CRIMP_FLAG_FOLD_RADIANS: the folded phase times 2 pi, the host's `folded * (2 * np.pi)` of the Cauchy and
+        // von Mises fits (measureToAs.py:195, :200) in the same fp64 multiply
+        const double fscale = (flags & CRIMP_FLAG_FOLD_RADIANS) ? 2.0 * 3.141592653589793 : 1.0;
         if (vec)
             k_calcphase_vec<<<blocks, 256, 0, s>>>(reinterpret_cast<const double2*>(dt), n / 2, hm,
-                                                     reinterpret_cast<double2*>(dtot), reinterpret_cast<double2*>(dfol));
+                                                     reinterpret_cast<double2*>(dtot), reinterpret_cast<double2*>(dfol),
+                                                     fscale);
         else
-            k_calcphase_scalar<<<blocks, 256, 0, s>>>(dt, n, hm, dtot, dfol);
+            k_calcphase_scalar<<<blocks, 256, 0, s>>>(dt, n, hm, dtot, dfol, fscale);
         HIPCHK(hipGetLastError());
         kt.stop();
         HIPCHK(copy_back(s, total, dtot, (size_t)n, dev));
@@ -2135,7 +2141,8 @@ extern "C" int crimp_search_sets(const double* t, const int64_t* offsets, int64_
         HIPCHK(stage_in(sc, offsets, (size_t)nset + 1, dev, &doff));
         HIPCHK(stage_in(sc, freq, (size_t)nset, dev, &df));
         HIPCHK(stage_out(sc, out, (size_t)nset, dev, &dout));
-        k_search_sets<<<(unsigned)nset, kSetBlock, 0, s>>>(dt, doff, df, nharm, stat, dout);
+        k_search_sets<<<(unsigned)nset, kSetBlock, 0, s>>>(dt, doff, df, nharm, stat,
+                                                           (flags & CRIMP_FLAG_TIME_DAYS) ? 86400.0 : 1.0, dout);
         HIPCHK(hipGetLastError());
         HIPCHK(copy_back(s, out, dout, (size_t)nset, dev));
         // CRIMP_FLAG_ASYNC: with device pointers the call stages nothing and takes no scratch block (a block handed
@@ -3231,6 +3238,162 @@ extern "C" int crimp_binphases(const double* x, const int64_t* offsets, int64_t 
             dx, doff, de, nbins, reinterpret_cast<unsigned long long*>(dc));
         HIPCHK(hipGetLastError());
         HIPCHK(copy_back(s, counts, dc, (size_t)(nint * nbins), dev));
+    }
+    return finish(s, flags);
+}
+
+// ============================================================== 7. interval selection (measureToAs.py:168-182)
+// The photons of a ToA interval are TIME[(TIME >= start) & (TIME <= end)] (measureToAs.py:173-174); on time-sorted
+// photons (event files are) that is the range [lower_bound(start), upper_bound(end)) -- two binary searches per
+// interval instead of a pass over all photons per interval. crimp_is_sorted decides which applies.
+__global__ __launch_bounds__(256) void k_unsorted(const double* __restrict__ t, int64_t n, int* __restrict__ flag) {
+    constexpr int U = 4;  // pairs per thread and sweep, loads issued together
+    int b = 0;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 + 1 < n; i0 += U * stride) {
+        double a[U], c[U];
+#pragma unroll
+        for (int q = 0; q < U; ++q) {
+            const int64_t i = i0 + q * stride;
+            a[q] = t[i + 1 < n ? i : 0];
+            c[q] = t[i + 1 < n ? i + 1 : 0];
+        }
+#pragma unroll
+        for (int q = 0; q < U; ++q)
+            if (i0 + q * stride + 1 < n) b |= !(a[q] <= c[q]);  // a NaN is out of order, as np.all(T[1:] >= T[:-1])
+    }
+    if (__any(b) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
+}
+
+// lo[i] = first photon with t >= starts[i] (np.searchsorted side="left"), count[i] = photons up to the last with
+// t <= ends[i] (side="right") less lo[i], at least 0; first_last[2i], [2i+1] = t of the interval's first and last
+// photon (NaN when it holds none). A NaN bound selects nothing, as the reference's mask.
+__global__ __launch_bounds__(256) void k_select_intervals(const double* __restrict__ t, int64_t n,
+                                                          const double* __restrict__ starts,
+                                                          const double* __restrict__ ends, int64_t nint,
+                                                          int64_t* __restrict__ lo, int64_t* __restrict__ count,
+                                                          double* __restrict__ first_last) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nint) return;
+    const double s = starts[i], e = ends[i];
+    int64_t a = 0, b = n;
+    while (a < b) {  // lower bound of s
+        const int64_t m = (a + b) >> 1;
+        if (t[m] < s) a = m + 1; else b = m;
+    }
+    const int64_t l = a;
+    b = n;
+    while (a < b) {  // upper bound of e, from l
+        const int64_t m = (a + b) >> 1;
+        if (t[m] <= e) a = m + 1; else b = m;
+    }
+    const int64_t c = (s == s && e == e && a > l) ? a - l : 0;
+    lo[i] = l;
+    count[i] = c;
+    if (first_last) {
+        first_last[2 * i] = c > 0 ? t[l] : NAN;
+        first_last[2 * i + 1] = c > 0 ? t[l + c - 1] : NAN;
+    }
+}
+
+// out[offsets[i] + j] = t[lo[i] + j], j < offsets[i+1] - offsets[i]: the intervals' photons concatenated
+__global__ __launch_bounds__(256) void k_gather_ranges(const double* __restrict__ t, const int64_t* __restrict__ lo,
+                                                       const int64_t* __restrict__ offsets, double* __restrict__ out) {
+    const int64_t i = blockIdx.x;
+    const int64_t o = offsets[i], len = offsets[i + 1] - o;
+    const double* src = t + lo[i];
+    for (int64_t j = threadIdx.x; j < len; j += blockDim.x) out[o + j] = src[j];
+}
+
+extern "C" int crimp_is_sorted(const double* t, int64_t n, int32_t* unsorted, uint32_t flags, void* stream) {
+    ARGCHK(n >= 0, "n < 0");
+    ARGCHK(unsorted != nullptr && (t != nullptr || n == 0), "null argument");
+    *unsorted = 0;
+    if (n < 2) return CRIMP_OK;
+    const bool dev = flags & CRIMP_FLAG_DEVICE_PTRS;
+    std::lock_guard<std::mutex> lk(g_mutex);
+    hipStream_t s = as_stream(stream);
+    {
+        Scratch sc(s);
+        const double* dt = nullptr;
+        int* dflag = nullptr;
+        HIPCHK(stage_in(sc, t, (size_t)n, dev, &dt));
+        HIPCHK(sc.alloc(&dflag, 1));
+        HIPCHK(hipMemsetAsync(dflag, 0, sizeof(int), s));
+        k_unsorted<<<(unsigned)std::min<int64_t>(cdiv(n, 256 * 4), 2048), 256, 0, s>>>(dt, n, dflag);
+        HIPCHK(hipGetLastError());
+        int h = 0;
+        HIPCHK(d2h(s, &h, dflag, sizeof(int)));
+        *unsorted = h ? 1 : 0;
+    }
+    return finish(s, flags);
+}
+
+extern "C" int crimp_select_intervals(const double* t, int64_t n, const double* starts, const double* ends,
+                                      int64_t nint, int64_t* lo, int64_t* count, double* first_last, uint32_t flags,
+                                      void* stream) {
+    ARGCHK(n >= 0 && nint >= 0, "negative size");
+    ARGCHK((t != nullptr || n == 0) && (nint == 0 || (starts && ends && lo && count)), "null argument");
+    if (nint == 0) return CRIMP_OK;
+    const bool dev = flags & CRIMP_FLAG_DEVICE_PTRS;
+    std::lock_guard<std::mutex> lk(g_mutex);
+    hipStream_t s = as_stream(stream);
+    {
+        Scratch sc(s);
+        const double *dt = nullptr, *ds = nullptr, *de = nullptr;
+        int64_t *dlo = nullptr, *dc = nullptr;
+        double* dfl = nullptr;
+        HIPCHK(stage_in(sc, t, (size_t)n, dev, &dt));
+        HIPCHK(stage_in(sc, starts, (size_t)nint, dev, &ds));
+        HIPCHK(stage_in(sc, ends, (size_t)nint, dev, &de));
+        HIPCHK(stage_out(sc, lo, (size_t)nint, dev, &dlo));
+        HIPCHK(stage_out(sc, count, (size_t)nint, dev, &dc));
+        if (first_last) HIPCHK(stage_out(sc, first_last, (size_t)(2 * nint), dev, &dfl));
+        k_select_intervals<<<(unsigned)cdiv(nint, 256), 256, 0, s>>>(dt, n, ds, de, nint, dlo, dc, dfl);
+        HIPCHK(hipGetLastError());
+        HIPCHK(copy_back(s, lo, dlo, (size_t)nint, dev));
+        HIPCHK(copy_back(s, count, dc, (size_t)nint, dev));
+        if (first_last) HIPCHK(copy_back(s, first_last, dfl, (size_t)(2 * nint), dev));
+    }
+    return finish(s, flags);
+}
+
+extern "C" int crimp_gather_ranges(const double* t, int64_t n, const int64_t* lo, const int64_t* offsets,
+                                   int64_t nint, double* out, uint32_t flags, void* stream) {
+    ARGCHK(n >= 0 && nint >= 0, "negative size");
+    ARGCHK(nint <= 2147483647LL, "too many intervals");
+    ARGCHK(nint == 0 || (t && lo && offsets && out), "null argument");
+    if (nint == 0) return CRIMP_OK;
+    const bool dev = flags & CRIMP_FLAG_DEVICE_PTRS;
+    std::lock_guard<std::mutex> lk(g_mutex);
+    hipStream_t s = as_stream(stream);
+    // the ranges are checked on the host against the photon array before any copy is queued
+    std::vector<int64_t> hlo((size_t)nint), hoff((size_t)nint + 1);
+    if (dev) {
+        HIPCHK(d2h(s, hlo.data(), lo, (size_t)nint * sizeof(int64_t)));
+        HIPCHK(d2h(s, hoff.data(), offsets, ((size_t)nint + 1) * sizeof(int64_t)));
+    } else {
+        std::memcpy(hlo.data(), lo, (size_t)nint * sizeof(int64_t));
+        std::memcpy(hoff.data(), offsets, ((size_t)nint + 1) * sizeof(int64_t));
+    }
+    ARGCHK(hoff[0] == 0, "offsets[0] must be 0");
+    for (int64_t i = 0; i < nint; ++i) {
+        const int64_t len = hoff[(size_t)i + 1] - hoff[(size_t)i];
+        ARGCHK(len >= 0 && hlo[(size_t)i] >= 0 && hlo[(size_t)i] + len <= n, "a range lies outside the photon array");
+    }
+    const int64_t total = hoff[(size_t)nint];
+    {
+        Scratch sc(s);
+        const double* dt = nullptr;
+        const int64_t *dlo = nullptr, *doff = nullptr;
+        double* dout = nullptr;
+        HIPCHK(stage_in(sc, t, (size_t)n, dev, &dt));
+        HIPCHK(stage_in(sc, lo, (size_t)nint, dev, &dlo));
+        HIPCHK(stage_in(sc, offsets, (size_t)nint + 1, dev, &doff));
+        HIPCHK(stage_out(sc, out, (size_t)total, dev, &dout));
+        k_gather_ranges<<<(unsigned)nint, 256, 0, s>>>(dt, dlo, doff, dout);
+        HIPCHK(hipGetLastError());
+        HIPCHK(copy_back(s, out, dout, (size_t)total, dev));
     }
     return finish(s, flags);
 }

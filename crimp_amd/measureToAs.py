@@ -18,12 +18,12 @@ import time
 
 import numpy as np
 
-from .calcphase import calcphase
+from .calcphase import Phases
 from .ephemTmjd import ephemTmjd
 from .eventfile import EvtFileOps
 from .logging_utils import configure_logging, get_logger
 from . import ops
-from ._native import STAT_H
+from ._native import FLAG_TIME_DAYS, STAT_H
 from .readPPtemplate import readPPtemplate
 from .readtimingmodel import ReadTimingModel
 from .timfile import phshiftTotimfile
@@ -188,23 +188,19 @@ def measure_intervals(TIMEMJD, timMod, tempModPP, starts, ends, exposures, phShi
         if res is not None:
             return res
     T = _device_times(TIMEMJD)
-    if T is not None and (T.numel() < 2 or bool((T[1:] >= T[:-1]).all())):
-        lo = torch.searchsorted(T, torch.as_tensor(starts, device=T.device), right=False)
-        hi = torch.maximum(torch.searchsorted(T, torch.as_tensor(ends, device=T.device), right=True), lo)
-        n = (hi - lo).cpu().numpy()
+    if T is not None and ops.is_sorted(T):
+        # time-sorted photons on the device: two binary searches per interval (crimp_select_intervals), the
+        # intervals' photons gathered by crimp_gather_ranges -- torch holds the buffers only
+        lo, n, first, last = ops.select_intervals(T, starts, ends)
         offs = np.concatenate([[0], np.cumsum(n)]).astype(np.int64)
         if np.any(n <= 0):  # measureToAs.py:182 reads TIME_toa[-1] of every interval
             raise IndexError("index -1 is out of bounds for axis 0 with size 0 (a ToA interval holds no photons)")
-        offs_d = torch.as_tensor(offs, device=T.device)
-        if n.size == 1 or bool((lo[1:] == hi[:-1]).all()):
+        if n.size == 1 or np.all(lo[1:] == lo[:-1] + n[:-1]):
             # consecutive intervals with no photon between them (ToA intervals tiling an observation): their
             # concatenation is a slice of the time array, no copy
             allt = T[int(lo[0]):int(lo[0]) + int(offs[-1])]
         else:
-            rel = torch.arange(int(offs[-1]), device=T.device, dtype=torch.int64)
-            seg = torch.repeat_interleave(torch.arange(n.size, device=T.device), torch.as_tensor(n, device=T.device))
-            allt = T[lo[seg] + (rel - offs_d[seg])]
-        first, last = allt[offs_d[:-1]], allt[offs_d[1:] - 1]
+            allt = ops.gather_ranges(T, lo, offs)
     else:
         allt, offs = select_intervals(TIMEMJD if T is None else T.cpu().numpy(), starts, ends)
         if np.any(np.diff(offs) <= 0):
@@ -212,11 +208,8 @@ def measure_intervals(TIMEMJD, timMod, tempModPP, starts, ends, exposures, phShi
         first, last = allt[offs[:-1]], allt[offs[1:] - 1]
         if T is not None:
             allt = torch.as_tensor(allt, device=T.device)
-    mids = ((last - first) / 2) + first                 # measureToAs.py:182
-    mids = mids.cpu().numpy() if hasattr(mids, "cpu") else np.asarray(mids)
-    _, folded = calcphase(allt, tm)
-    if model in ("cauchy", "vonmises"):
-        folded = folded * (2 * np.pi)                  # :195, :200
+    mids = ((last - first) / 2) + first                 # measureToAs.py:182 (host NumPy)
+    folded = _folded(allt, tm, model)
     E = np.asarray(exposures, dtype=np.float64)
     if readvaryparam:
         res = VaryParamFitter(folded, offs, E, tmpl, phShiftRes, nbrBins, vary_amps=bool(varyAmps)).fit(
@@ -224,17 +217,30 @@ def measure_intervals(TIMEMJD, timMod, tempModPP, starts, ends, exposures, phShi
     else:
         res = ToAFitter(folded, offs, E, tmpl, phShiftRes, nbrBins).fit(brutemin=brutemin, vary_amps=bool(varyAmps))
     freqs = np.atleast_1d(ephemTmjd(mids, tm)["freqAtTmjd"])          # :210
+    # :211-212, one trial per interval; TIME_toa * 86400 formed in the kernel (CRIMP_FLAG_TIME_DAYS)
     if hasattr(allt, "device"):
-        hp = ops.search_sets(allt * 86400, torch.as_tensor(offs, device=allt.device),
-                             torch.as_tensor(freqs, dtype=torch.float64, device=allt.device), 5, STAT_H).cpu().numpy()
+        hp = ops.search_sets(allt, torch.as_tensor(offs, device=allt.device),
+                             torch.as_tensor(freqs, dtype=torch.float64, device=allt.device), 5, STAT_H,
+                             flags=FLAG_TIME_DAYS).cpu().numpy()
     else:
-        hp = ops.search_sets(allt * 86400, offs, freqs, 5, STAT_H)   # :211-212, one trial per interval
+        hp = ops.search_sets(allt, offs, freqs, 5, STAT_H, flags=FLAG_TIME_DAYS)
     res["ToA_mid"] = mids
     res["htestPow"] = np.asarray(hp)
     return res
 
 
 _HTEST_STREAMS = {}
+
+
+def _folded(allt, tm, model):
+    """The folded phases of the selected photons (measureToAs.py:186-200): calcphase's cycle fold, in radians for the
+    Cauchy and von Mises templates -- the host's `folded * (2 * np.pi)` formed in the kernel (CRIMP_FLAG_FOLD_RADIANS,
+    the same fp64 multiply)."""
+    from ._native import FLAG_FOLD_RADIANS
+    ph = Phases(allt, tm)
+    _, folded = ops.calcphase(ph.timeMJD, ph.timModParam,
+                              flags=FLAG_FOLD_RADIANS if model in ("cauchy", "vonmises") else 0)
+    return folded
 
 
 def _fit_block(allt, offs, mids, tm, tmpl, model, E, phShiftRes, nbrBins, varyAmps, brutemin):
@@ -246,7 +252,6 @@ def _fit_block(allt, offs, mids, tm, tmpl, model, E, phShiftRes, nbrBins, varyAm
     from ._native import FLAG_ASYNC
     dev = allt.device
     freqs = np.atleast_1d(ephemTmjd(mids, tm)["freqAtTmjd"])          # :210
-    ts = allt * 86400
     offs_d = torch.as_tensor(offs, device=dev)
     freqs_d = torch.as_tensor(freqs, dtype=torch.float64, device=dev)
     side = _HTEST_STREAMS.get(dev.index)
@@ -254,13 +259,11 @@ def _fit_block(allt, offs, mids, tm, tmpl, model, E, phShiftRes, nbrBins, varyAm
         side = _HTEST_STREAMS[dev.index] = torch.cuda.Stream(device=dev)
     cur = torch.cuda.current_stream(dev)
     side.wait_stream(cur)
-    with torch.cuda.stream(side):
-        hp_d = ops.search_sets(ts, offs_d, freqs_d, 5, STAT_H, flags=FLAG_ASYNC)   # :211-212, one trial per interval
-    for t_ in (ts, offs_d, freqs_d, hp_d):
+    with torch.cuda.stream(side):  # :211-212, one trial per interval, TIME_toa * 86400 in the kernel
+        hp_d = ops.search_sets(allt, offs_d, freqs_d, 5, STAT_H, flags=FLAG_ASYNC | FLAG_TIME_DAYS)
+    for t_ in (allt, offs_d, freqs_d, hp_d):
         t_.record_stream(side)
-    _, folded = calcphase(allt, tm)
-    if model in ("cauchy", "vonmises"):
-        folded = folded * (2 * np.pi)                  # :195, :200
+    folded = _folded(allt, tm, model)
     res = ToAFitter(folded, offs, E, tmpl, phShiftRes, nbrBins).fit(brutemin=brutemin, vary_amps=bool(varyAmps))
     cur.wait_stream(side)
     res["ToA_mid"] = mids
@@ -341,8 +344,7 @@ def _measure_pipelined(TIMEMJD, tm, tmpl, model, starts, ends, exposures, phShif
     sys.setswitchinterval(1e-4)
     th.start()
     cur = torch.cuda.current_stream(dev)
-    ok = torch.ones((), dtype=torch.bool, device=dev)
-    prev_last = None
+    ok = True
     parts = []
     try:
         for b0, b1 in blocks:
@@ -352,21 +354,16 @@ def _measure_pipelined(TIMEMJD, tm, tmpl, model, starts, ends, exposures, phShif
             d, ev, a = item
             cur.wait_event(ev)
             d.record_stream(cur)
-            if d.numel() > 1:
-                ok &= (d[1:] >= d[:-1]).all()
-            if prev_last is not None:
-                ok &= d[0] >= prev_last
-            prev_last = d[-1]
+            # the block's photons in order on the device (crimp_is_sorted); the joins between blocks and the photons
+            # no block uploads were checked on the host (_gaps_sorted)
+            ok = ok and ops.is_sorted(d)
             nb = n[b0:b1]
             offs = np.concatenate([[0], np.cumsum(nb)]).astype(np.int64)
             rel_lo = lo[b0:b1] - a
             if np.all(rel_lo[1:] == rel_lo[:-1] + nb[:-1]):   # consecutive intervals: one slice, no copy
                 allt = d[int(rel_lo[0]):int(rel_lo[0]) + int(offs[-1])]
             else:
-                seg = torch.repeat_interleave(torch.arange(nb.size, device=dev), torch.as_tensor(nb, device=dev))
-                rel = torch.arange(int(offs[-1]), device=dev, dtype=torch.int64)
-                offs_d = torch.as_tensor(offs, device=dev)
-                allt = d[torch.as_tensor(rel_lo, device=dev)[seg] + (rel - offs_d[seg])]
+                allt = ops.gather_ranges(d, rel_lo, offs)
             first = t[lo[b0:b1]]
             last = t[lo[b0:b1] + nb - 1]
             mids = ((last - first) / 2) + first                 # measureToAs.py:182
@@ -384,7 +381,7 @@ def _measure_pipelined(TIMEMJD, tm, tmpl, model, starts, ends, exposures, phShif
                 pass
         th.join()
         sys.setswitchinterval(switch)
-    if not bool(ok):
+    if not ok:
         return None
     out = {k: np.concatenate([np.atleast_1d(np.asarray(p[k])) for p in parts]) for k in parts[0]}
     if trace is not None:

@@ -324,3 +324,77 @@ def binphases_counts(x, offsets, edges):
     with b.device_guard():
         N.check(L.crimp_binphases(xp, op, nint, ep, nb, cp, b.flags(), b.stream()))
     return out.reshape(nint, nb)
+
+
+def is_sorted(t):
+    """True when the times are non-decreasing (crimp_is_sorted; a NaN counts as out of order), as
+    np.all(t[1:] >= t[:-1])."""
+    L = N.load()
+    b = N.Buffers()
+    tp = b.arg(t, np.float64)
+    n = int(t.numel() if N._is_torch(t) else np.size(t))
+    flag = ctypes.c_int32(0)
+    with b.device_guard():
+        N.check(L.crimp_is_sorted(tp, n, ctypes.byref(flag), b.flags(), b.stream()))
+    return flag.value == 0
+
+
+def select_intervals(t, starts, ends):
+    """(lo, count, first, last) per interval on time-sorted photons t (crimp_select_intervals): the photons
+    t[lo : lo + count] are those of the reference's mask (t >= start) & (t <= end) (measureToAs.py:173-174), first /
+    last their first and last time (NaN for an empty interval). Host NumPy arrays out; t stays where it is (a device
+    tensor is searched on the device, the bounds go up with it)."""
+    L = N.load()
+    b = N.Buffers()
+    tp = b.arg(t, np.float64)
+    n = int(t.numel() if N._is_torch(t) else np.size(t))
+    starts = np.ascontiguousarray(starts, dtype=np.float64).reshape(-1)
+    ends = np.ascontiguousarray(ends, dtype=np.float64).reshape(-1)
+    if starts.size != ends.size:
+        raise ValueError("starts and ends differ in length")
+    nint = int(starts.size)
+    if b.device:
+        import torch
+        sd = torch.as_tensor(starts, device=t.device)
+        ed = torch.as_tensor(ends, device=t.device)
+        outi = torch.empty(2 * nint, dtype=torch.int64, device=t.device)
+        outf = torch.empty(2 * nint, dtype=torch.float64, device=t.device)
+        args = (b.arg(sd, np.float64), b.arg(ed, np.float64), b.arg(outi[:nint], np.int64, writable=True),
+                b.arg(outi[nint:], np.int64, writable=True), b.arg(outf, np.float64, writable=True))
+    else:
+        outi = np.empty(2 * nint, dtype=np.int64)
+        outf = np.empty(2 * nint, dtype=np.float64)
+        args = (b.arg(starts, np.float64), b.arg(ends, np.float64), ctypes.c_void_p(outi.ctypes.data),
+                ctypes.c_void_p(outi[nint:].ctypes.data), ctypes.c_void_p(outf.ctypes.data))
+    with b.device_guard():
+        N.check(L.crimp_select_intervals(tp, n, args[0], args[1], nint, args[2], args[3], args[4], b.flags(),
+                                         b.stream()))
+    if N._is_torch(outi):
+        outi, outf = outi.cpu().numpy(), outf.cpu().numpy()
+    return outi[:nint].copy(), outi[nint:].copy(), outf[0::2].copy(), outf[1::2].copy()
+
+
+def gather_ranges(t, lo, offsets):
+    """The photons t[lo[i] : lo[i] + (offsets[i+1] - offsets[i])] of every interval, concatenated (crimp_gather_ranges);
+    same placement as t (a device tensor in, a device tensor out)."""
+    L = N.load()
+    b = N.Buffers()
+    tp = b.arg(t, np.float64)
+    n = int(t.numel() if N._is_torch(t) else np.size(t))
+    lo = np.ascontiguousarray(lo, dtype=np.int64).reshape(-1)
+    offsets = np.ascontiguousarray(offsets, dtype=np.int64).reshape(-1)
+    nint = int(lo.size)
+    if offsets.size != nint + 1:
+        raise ValueError("offsets needs one entry more than lo")
+    total = int(offsets[-1]) if nint else 0
+    out = _empty_like_input(t, total, b)
+    if b.device:
+        import torch
+        lp = b.arg(torch.as_tensor(lo, device=t.device), np.int64)
+        op = b.arg(torch.as_tensor(offsets, device=t.device), np.int64)
+    else:
+        lp, op = b.arg(lo, np.int64), b.arg(offsets, np.int64)
+    outp = b.arg(out, np.float64, writable=True)
+    with b.device_guard():
+        N.check(L.crimp_gather_ranges(tp, n, lp, op, nint, outp, b.flags(), b.stream()))
+    return out

@@ -62,6 +62,11 @@ extern "C" {
 #define CRIMP_FLAG_EXACT 8192u     /* search: no NUFFT -- the exact i8-MFMA kernel on progressions of >= 256 trials,
                                     * the fp64 kernel otherwise (the default of rounds 1-5) */
 
+#define CRIMP_FLAG_TIME_DAYS 16384u    /* crimp_search_sets: t in days (MJD); the kernel forms t * 86400 seconds as
+                                        * measureToAs.py:211 does on the host (the same fp64 multiply) */
+#define CRIMP_FLAG_FOLD_RADIANS 32768u /* crimp_calcphase: the folded phase times 2 pi (radians), the host's
+                                        * `folded * (2 * np.pi)` of measureToAs.py:195, :200 in the same multiply */
+
 #define CRIMP_STAT_Z2 0 /* Z^2_m  (periodsearch.py:57-71, :73-106) */
 #define CRIMP_STAT_H 1  /* H-test (periodsearch.py:109-125)         */
 
@@ -238,6 +243,20 @@ int crimp_toa_fit_redchi2(const double* x, const int64_t* offsets, int64_t nint,
  * np.histogram(x, bins=edges) semantics with edges[nbins+1] (numpy.linspace). counts[i*nbins+b]. */
 int crimp_binphases(const double* x, const int64_t* offsets, int64_t nint, const double* edges, int32_t nbins,
                     int64_t* counts, uint32_t flags, void* stream);
+
+/* Interval selection of measureToAs (measureToAs.py:168-182): TIME[(TIME >= start) & (TIME <= end)] per ToA interval
+ * (:173-174) and its first / last photon (ToA_mid, :182).
+ * crimp_is_sorted: *unsorted = 1 if some t[i+1] < t[i] (or a NaN), else 0 (host int; t host or device per flags).
+ * crimp_select_intervals: on time-sorted t, lo[i] = np.searchsorted(t, starts[i], "left"), count[i] =
+ *   max(np.searchsorted(t, ends[i], "right") - lo[i], 0) (0 for a NaN bound), first_last[2i], [2i+1] = the
+ *   interval's first and last time (NaN if empty; may be NULL) -- the mask's photons on sorted times.
+ * crimp_gather_ranges: out[offsets[i] + j] = t[lo[i] + j] for j < offsets[i+1] - offsets[i] (offsets[0] = 0; every
+ *   range inside t[0, n)): the intervals' photons concatenated, as measureToAs.py's per-interval selections. */
+int crimp_is_sorted(const double* t, int64_t n, int32_t* unsorted, uint32_t flags, void* stream);
+int crimp_select_intervals(const double* t, int64_t n, const double* starts, const double* ends, int64_t nint,
+                           int64_t* lo, int64_t* count, double* first_last, uint32_t flags, void* stream);
+int crimp_gather_ranges(const double* t, int64_t n, const int64_t* lo, const int64_t* offsets, int64_t nint,
+                        double* out, uint32_t flags, void* stream);
 
 #ifdef __cplusplus
 }

@@ -385,3 +385,17 @@ def test_add_column_rewrites_events_table(tmp_path):
         add_column(p, "EVENTS", "PHASE", ph)
     with pytest.raises(ValueError):
         add_column(p, "EVENTS", "PHASE2", ph[:5])
+
+
+def test_phases_waves_scalar_without_wave_harmonics():
+    """Phases.waves() without WAVEj terms returns the reference's scalar 0 * F0 (calcphase.py:135-149): no WAVE*
+    key at all, or only WAVEEPOCH and WAVE_OM (the harmonic loop runs over len(WAVE*) - 2 = 0 terms). No GPU call."""
+    from crimp_amd.calcphase import Phases
+    t = 58000.0 + np.arange(4.0)
+    for tm in ({"PEPOCH": 58000.0, "F0": 0.5},
+               {"PEPOCH": 58000.0, "F0": 0.5, "WAVEEPOCH": 58000.0, "WAVE_OM": 0.01}):
+        w = Phases(t, tm).waves()
+        assert np.ndim(w) == 0 and w == 0.0 and isinstance(w, float)
+    with pytest.raises(KeyError):  # as the reference, which reads F0 for the normalisation
+        Phases(t, {"PEPOCH": 58000.0}).waves()
+
