@@ -59,7 +59,7 @@ class Template(ctypes.Structure):
 
 EXPORTS = ("crimp_version", "crimp_last_error", "crimp_last_kernel_ms", "crimp_last_kernel_times", "crimp_last_fixups",
            "crimp_last_search_path", "crimp_last_nufft_plan", "crimp_last_nufft_work", "crimp_last_toa_grid_norms", "crimp_last_toa_grid_fast", "crimp_release_scratch",
-           "crimp_device_count", "crimp_calcphase", "crimp_search", "crimp_best", "crimp_search_sets", "crimp_toa_points",
+           "crimp_device_count", "crimp_calcphase", "crimp_search", "crimp_search_best", "crimp_best", "crimp_search_sets", "crimp_toa_points",
            "crimp_toa_grid", "crimp_toa_fit", "crimp_toa_redchi2", "crimp_toa_fit_redchi2", "crimp_toa_shape_points", "crimp_binphases",
            "crimp_is_sorted", "crimp_select_intervals", "crimp_gather_ranges")
 
@@ -95,6 +95,7 @@ def load(require_device=True):
             L.crimp_search.argtypes = [P, i64, ctypes.c_double, P, i64, P, i64, i32, i32, i64, i64, P, u32, P]
             L.crimp_search_sets.argtypes = [P, P, i64, P, i32, i32, P, u32, P]
             L.crimp_best.argtypes = [P, i64, P, u32, P]
+            L.crimp_search_best.argtypes = [P, i64, ctypes.c_double, P, i64, P, i64, i32, i32, i64, i64, P, P, u32, P]
             L.crimp_toa_points.argtypes = [P, P, i64, ctypes.POINTER(Template), P, P, P, i64, P, u32, P]
             L.crimp_toa_grid.argtypes = [P, P, i64, ctypes.POINTER(Template), P, i64, P, i64, P, P, u32, P]
             L.crimp_toa_fit.argtypes = [P, P, i64, ctypes.POINTER(Template), P, ctypes.c_double, i32, i32, P, u32, P]

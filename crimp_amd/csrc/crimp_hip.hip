@@ -1721,10 +1721,79 @@ static int fixup_search(Scratch& sc, hipStream_t s, const double* dt, const doub
     return CRIMP_OK;
 }
 
-// Arithmetic-progression check of the (device) frequency grid: 16 ulp of max|f| (k_ap_check). Writes delta
-// into ap[0] on the device (read by the factorised kernels) and returns whether the grid qualifies. With nu_dt
-// (a NUFFT search) the NUFFT's own checks -- photon order and the grid scalars (k_nu_sorted, k_nu_scalars) -- are
-// queued behind it and read back in the same transfer: nu_hs = [delta, f0, dt[0], dt[n-1], unsorted flag].
+// Best trial of a power array, np.argmax semantics (periodsearch.py's callers take the maximum and its index): the
+// largest value, ties to the lowest index, a NaN above every number (the first NaN wins). k_best_blocks reduces
+// grid-stride slices (eight loads in flight per thread) to one candidate per block, k_best_final the candidates.
+struct BestCand {
+    double v;
+    int64_t i;
+};
+__device__ __forceinline__ bool best_better(double v1, int64_t i1, double v2, int64_t i2) {
+    const bool n1 = isnan(v1), n2 = isnan(v2);
+    if (n1 != n2) return n1;
+    if (!n1 && v1 != v2) return v1 > v2;
+    return i1 < i2;
+}
+__device__ __forceinline__ BestCand best_block_reduce(BestCand c) {
+    for (int o = 32; o > 0; o >>= 1) {
+        const double v = __shfl_xor(c.v, o);
+        const int64_t i = __shfl_xor(c.i, o);
+        if (best_better(v, i, c.v, c.i)) c = {v, i};
+    }
+    __shared__ BestCand red[4];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
+    __syncthreads();
+    c = red[0];
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w)
+        if (best_better(red[w].v, red[w].i, c.v, c.i)) c = red[w];
+    return c;
+}
+constexpr int kBestBlocks = 1024;
+__global__ __launch_bounds__(256) void k_best_blocks(const double* __restrict__ x, int64_t n, BestCand* __restrict__ part) {
+    constexpr int U = 8;
+    BestCand c = {-INFINITY, INT64_MAX};
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t j0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j0 < n; j0 += U * stride) {
+        double v[U];
+#pragma unroll
+        for (int q = 0; q < U; ++q) v[q] = x[j0 + q * stride < n ? j0 + q * stride : n - 1];
+#pragma unroll
+        for (int q = 0; q < U; ++q) {
+            const int64_t j = j0 + q * stride;
+            if (j < n && best_better(v[q], j, c.v, c.i)) c = {v[q], j};
+        }
+    }
+    c = best_block_reduce(c);
+    if (threadIdx.x == 0) part[blockIdx.x] = c;
+}
+__global__ __launch_bounds__(256) void k_best_final(const BestCand* __restrict__ part, int nb, double* __restrict__ out) {
+    BestCand c = {-INFINITY, INT64_MAX};
+    for (int b = threadIdx.x; b < nb; b += blockDim.x)
+        if (best_better(part[b].v, part[b].i, c.v, c.i)) c = part[b];
+    c = best_block_reduce(c);
+    if (threadIdx.x == 0) {
+        out[0] = c.v;
+        out[1] = (double)c.i;
+    }
+}
+
+// the best trial of x[n] (device) into dout[0..1] (device): k_best_blocks + k_best_final on the stream, no sync
+static int launch_best(Scratch& sc, hipStream_t s, const double* x, int64_t n, double* dout) {
+    BestCand* part = nullptr;
+    HIPCHK(sc.alloc(&part, (size_t)kBestBlocks));
+    const int nb = (int)std::min<int64_t>(cdiv(n, 256 * 8), kBestBlocks);
+    k_best_blocks<<<nb, 256, 0, s>>>(x, n, part);
+    HIPCHK(hipGetLastError());
+    k_best_final<<<1, 256, 0, s>>>(part, nb, dout);
+    HIPCHK(hipGetLastError());
+    return CRIMP_OK;
+}
+
+// Arithmetic-progression check of the (device) frequency grid: 16 ulp of max|f| (k_ap_check, k_ap_final). Writes
+// delta into ap[0] on the device (read by the factorised kernels) and returns whether the grid qualifies. With nu_t
+// (a NUFFT search) the NUFFT's own checks -- photon order (k_nu_sorted, MFMA-slot plans only) and the plan's
+// scalars (k_ap_final) -- are queued with it and read back in the same transfer: nu_hs = [delta, f0, dt[0],
+// dt[n-1], unsorted flag]. No memset: k_ap_check zeroes the order flag, k_ap_final writes the rest.
 static int grid_is_progression(Scratch& sc, hipStream_t s, const double* freq, int64_t nf, double** ap, bool* ok,
                                const double* nu_t = nullptr, double t0 = 0.0, int64_t n = 0, double* nu_hs = nullptr,
                                bool nu_sorted_check = true);
@@ -1732,26 +1801,23 @@ static int grid_is_progression(Scratch& sc, hipStream_t s, const double* freq, i
 static int grid_is_progression(Scratch& sc, hipStream_t s, const double* freq, int64_t nf, double** ap, bool* ok,
                                const double* nu_t, double t0, int64_t n, double* nu_hs, bool nu_sorted_check) {
     *ok = false;
-    unsigned long long* info = nullptr;
-    HIPCHK(sc.alloc(&info, 3 + 6));
-    *ap = reinterpret_cast<double*>(info);
+    // info: [delta, max deviation, max |f|, NUFFT: delta, f_0, dt[0], dt[n-1], order flag (int bits)], then the
+    // block partials of k_ap_check
+    double* info = nullptr;
+    HIPCHK(sc.alloc(&info, 8 + 2 * kApBlocks));
+    *ap = info;
     if (nf < 2) return CRIMP_OK;
-    HIPCHK(hipMemsetAsync(info, 0, (3 + 6) * sizeof(unsigned long long), s));
-    // 64 blocks (one same-address atomic pair per block): 14.7 us per 1e6-trial grid, 16.3 at 512 blocks
-    k_ap_check<<<(unsigned)std::min<int64_t>(cdiv(nf, 256), 64), 256, 0, s>>>(freq, nf, info);
+    double2* part = reinterpret_cast<double2*>(info + 8);
+    int* order = reinterpret_cast<int*>(info + 7);
+    const int nb = (int)std::min<int64_t>(cdiv(nf, 256 * 8), kApBlocks);
+    k_ap_check<<<nb, 256, 0, s>>>(freq, nf, part, nu_t ? order : nullptr);
     HIPCHK(hipGetLastError());
-    double h[3 + 5];
-    size_t bytes = 3 * sizeof(double);
-    if (nu_t) {
-        double* dsc = reinterpret_cast<double*>(info + 3);
-        if (nu_sorted_check)
-            k_nu_sorted<<<(unsigned)std::min<int64_t>(cdiv(n, 256), 2048), 256, 0, s>>>(nu_t, t0, n,
-                                                                                      reinterpret_cast<int*>(dsc + 4));
-        k_nu_scalars<<<1, 64, 0, s>>>(*ap, freq, nu_t, t0, n, dsc);
-        HIPCHK(hipGetLastError());
-        bytes = sizeof(h);
-    }
-    HIPCHK(d2h(s, h, info, bytes));
+    if (nu_t && nu_sorted_check)
+        k_nu_sorted<<<(unsigned)std::min<int64_t>(cdiv(n, 256), 2048), 256, 0, s>>>(nu_t, t0, n, order);
+    k_ap_final<<<1, 256, 0, s>>>(freq, nf, part, nb, info, nu_t, t0, n, info + 3);
+    HIPCHK(hipGetLastError());
+    double h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    HIPCHK(d2h(s, h, info, (nu_t ? 8 : 3) * sizeof(double)));
     *ok = std::isfinite(h[0]) && h[0] != 0.0 && h[1] <= 16.0 * 2.220446049250313e-16 * h[2];
     if (nu_t) std::memcpy(nu_hs, h + 3, 5 * sizeof(double));
     return CRIMP_OK;
@@ -1907,62 +1973,6 @@ static int exact_search(Scratch& sc, hipStream_t s, const double* dt, const doub
     return fixup_search(sc, s, dt, dt2, n, freq, nf, c2, twod, nharm, stat, first, flagged, nf_h, out);
 }
 
-// Best trial of a power array, np.argmax semantics (periodsearch.py's callers take the maximum and its index): the
-// largest value, ties to the lowest index, a NaN above every number (the first NaN wins). k_best_blocks reduces
-// grid-stride slices (eight loads in flight per thread) to one candidate per block, k_best_final the candidates.
-struct BestCand {
-    double v;
-    int64_t i;
-};
-__device__ __forceinline__ bool best_better(double v1, int64_t i1, double v2, int64_t i2) {
-    const bool n1 = isnan(v1), n2 = isnan(v2);
-    if (n1 != n2) return n1;
-    if (!n1 && v1 != v2) return v1 > v2;
-    return i1 < i2;
-}
-__device__ __forceinline__ BestCand best_block_reduce(BestCand c) {
-    for (int o = 32; o > 0; o >>= 1) {
-        const double v = __shfl_xor(c.v, o);
-        const int64_t i = __shfl_xor(c.i, o);
-        if (best_better(v, i, c.v, c.i)) c = {v, i};
-    }
-    __shared__ BestCand red[4];
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
-    __syncthreads();
-    c = red[0];
-    for (int w = 1; w < (int)(blockDim.x >> 6); ++w)
-        if (best_better(red[w].v, red[w].i, c.v, c.i)) c = red[w];
-    return c;
-}
-constexpr int kBestBlocks = 1024;
-__global__ __launch_bounds__(256) void k_best_blocks(const double* __restrict__ x, int64_t n, BestCand* __restrict__ part) {
-    constexpr int U = 8;
-    BestCand c = {-INFINITY, INT64_MAX};
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t j0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j0 < n; j0 += U * stride) {
-        double v[U];
-#pragma unroll
-        for (int q = 0; q < U; ++q) v[q] = x[j0 + q * stride < n ? j0 + q * stride : n - 1];
-#pragma unroll
-        for (int q = 0; q < U; ++q) {
-            const int64_t j = j0 + q * stride;
-            if (j < n && best_better(v[q], j, c.v, c.i)) c = {v[q], j};
-        }
-    }
-    c = best_block_reduce(c);
-    if (threadIdx.x == 0) part[blockIdx.x] = c;
-}
-__global__ __launch_bounds__(256) void k_best_final(const BestCand* __restrict__ part, int nb, double* __restrict__ out) {
-    BestCand c = {-INFINITY, INT64_MAX};
-    for (int b = threadIdx.x; b < nb; b += blockDim.x)
-        if (best_better(part[b].v, part[b].i, c.v, c.i)) c = part[b];
-    c = best_block_reduce(c);
-    if (threadIdx.x == 0) {
-        out[0] = c.v;
-        out[1] = (double)c.i;
-    }
-}
-
 extern "C" int crimp_best(const double* x, int64_t n, double* best, uint32_t flags, void* stream) {
     ARGCHK(n >= 1, "need at least one value");
     ARGCHK(x != nullptr && best != nullptr, "null argument");
@@ -1974,15 +1984,10 @@ extern "C" int crimp_best(const double* x, int64_t n, double* best, uint32_t fla
         Scratch sc(s);
         const double* dx = nullptr;
         HIPCHK(stage_in(sc, x, (size_t)n, dev, &dx));
-        BestCand* part = nullptr;
         double* dout = nullptr;
-        HIPCHK(sc.alloc(&part, (size_t)kBestBlocks));
         HIPCHK(sc.alloc(&dout, 2));
-        const int nb = (int)std::min<int64_t>(cdiv(n, 256 * 8), kBestBlocks);
-        k_best_blocks<<<nb, 256, 0, s>>>(dx, n, part);
-        HIPCHK(hipGetLastError());
-        k_best_final<<<1, 256, 0, s>>>(part, nb, dout);
-        HIPCHK(hipGetLastError());
+        const int rc = launch_best(sc, s, dx, n, dout);
+        if (rc) return rc;
         HIPCHK(d2h(s, best, dout, 2 * sizeof(double)));
     }
     return finish(s, flags);
@@ -2002,9 +2007,28 @@ extern "C" int crimp_last_nufft_work(double* work, int32_t cap) {
     return kNuCls;
 }
 
+static int search_impl(const double* t, int64_t n, double t0, const double* freq, int64_t nf,
+                       const double* log10_negfdot, int64_t nfd, int32_t nharm, int32_t stat, int64_t first,
+                       int64_t count, double* out, uint32_t flags, void* stream, double* best);
+
 extern "C" int crimp_search(const double* t, int64_t n, double t0, const double* freq, int64_t nf,
                             const double* log10_negfdot, int64_t nfd, int32_t nharm, int32_t stat, int64_t first,
                             int64_t count, double* out, uint32_t flags, void* stream) {
+    return search_impl(t, n, t0, freq, nf, log10_negfdot, nfd, nharm, stat, first, count, out, flags, stream, nullptr);
+}
+
+extern "C" int crimp_search_best(const double* t, int64_t n, double t0, const double* freq, int64_t nf,
+                                 const double* log10_negfdot, int64_t nfd, int32_t nharm, int32_t stat, int64_t first,
+                                 int64_t count, double* out, double* best, uint32_t flags, void* stream) {
+    ARGCHK(best != nullptr, "null argument");
+    ARGCHK(count >= 1, "the best trial of an empty range");
+    ARGCHK(count <= (int64_t(1) << 53), "count above 2^53 (the index is returned as a double)");
+    return search_impl(t, n, t0, freq, nf, log10_negfdot, nfd, nharm, stat, first, count, out, flags, stream, best);
+}
+
+static int search_impl(const double* t, int64_t n, double t0, const double* freq, int64_t nf,
+                       const double* log10_negfdot, int64_t nfd, int32_t nharm, int32_t stat, int64_t first,
+                       int64_t count, double* out, uint32_t flags, void* stream, double* best) {
     ARGCHK(n >= 1, "need at least one photon (periodsearch.py:54 reads time[0], time[-1])");
     ARGCHK(nf >= 1, "need at least one trial frequency");
     ARGCHK(nharm >= 1 && nharm <= 256, "nbrHarm must be in 1..256");
@@ -2079,11 +2103,12 @@ extern "C" int crimp_search(const double* t, int64_t n, double t0, const double*
             if (rc) return rc;
         }
         int rc = CRIMP_OK;
-        bool done = false;
+        bool done = false, best_done = false;
         if (progression && nufft && nf >= 64) {  // NUFFT; unsorted photons or no plan fall through to the exact rule
             int64_t nfix = 0;
             rc = nufft_search(sc, s, dtm, t0, n, dfr, nf, twod ? nfd : 1, dc2, nu_hs, twod, nharm, stat, first, count,
-                              dout, flags & CRIMP_FLAG_TIME_KERNELS, &nfix, (flags & CRIMP_FLAG_NO_FIXUP) != 0, &done);
+                              dout, flags & CRIMP_FLAG_TIME_KERNELS, &nfix, (flags & CRIMP_FLAG_NO_FIXUP) != 0, &done,
+                              best, &best_done);
             if (rc) return rc;
             if (done) g_last_fixups = nfix;
         }
@@ -2104,6 +2129,13 @@ extern "C" int crimp_search(const double* t, int64_t n, double t0, const double*
                                false, &kt);
         }
         if (rc) return rc;
+        if (best && !best_done) {  // the exact / fp64 paths, or a NUFFT whose fix-up rewrote powers after its read-back
+            double* db = nullptr;
+            HIPCHK(sc.alloc(&db, 2));
+            rc = launch_best(sc, s, dout, count, db);
+            if (rc) return rc;
+            HIPCHK(d2h(s, best, db, 2 * sizeof(double)));
+        }
         HIPCHK(copy_back(s, out, dout, (size_t)count, dev));
     }
     return finish(s, flags);

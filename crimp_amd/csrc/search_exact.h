@@ -894,13 +894,15 @@ __global__ __launch_bounds__(256) void k_search_finalize_exact(const long long* 
 }
 
 // arithmetic-progression check on the device: |f_j - (f_0 + j delta)| <= 16 ulp(max|f|), delta from the ends.
-// info[0] = delta, info[1] = max deviation (as bits: non-negative doubles order as integers), info[2] = max |f|.
-__global__ __launch_bounds__(256) void k_ap_check(const double* __restrict__ f, int64_t nf,
-                                                  unsigned long long* __restrict__ info) {
+// Each block writes its (max deviation, max |f|) to part[blockIdx] (plain stores: same-address atomics from every
+// block serialise at L2); k_ap_final reduces them. One pass of eight loads in flight per thread over up to
+// kApBlocks blocks: the whole 8 MB of a 1e6-trial grid is in flight at once (64 blocks with a loop: 14.7 us).
+constexpr int kApBlocks = 1024;
+__global__ __launch_bounds__(256) void k_ap_check(const double* __restrict__ f, int64_t nf, double2* __restrict__ part,
+                                                  int* __restrict__ zero) {
     const double f0 = f[0];
     const double d = (f[nf - 1] - f0) / (double)(nf - 1);
     double dev = 0.0, fm = 0.0;
-    // eight grid-stride values per thread per iteration, all loads issued first (clamped indices)
     constexpr int U = 8;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t j0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j0 < nf; j0 += U * stride) {
@@ -920,7 +922,6 @@ __global__ __launch_bounds__(256) void k_ap_check(const double* __restrict__ f, 
         dev = fmax(dev, __shfl_xor(dev, o));
         fm = fmax(fm, __shfl_xor(fm, o));
     }
-    // one atomic pair per block (same-address atomics from every wave serialise at L2)
     __shared__ double red[2][4];
     if ((threadIdx.x & 63) == 0) {
         red[0][threadIdx.x >> 6] = dev;
@@ -930,8 +931,43 @@ __global__ __launch_bounds__(256) void k_ap_check(const double* __restrict__ f, 
     if (threadIdx.x == 0) {
         dev = fmax(fmax(red[0][0], red[0][1]), fmax(red[0][2], red[0][3]));
         fm = fmax(fmax(red[1][0], red[1][1]), fmax(red[1][2], red[1][3]));
-        atomicMax(&info[1], (unsigned long long)__double_as_longlong(dev));
-        atomicMax(&info[2], (unsigned long long)__double_as_longlong(fm));
+        part[blockIdx.x] = make_double2(dev, fm);
+        if (blockIdx.x == 0 && zero) *zero = 0;  // the NUFFT's order flag (k_nu_sorted ORs into it afterwards)
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) info[0] = (unsigned long long)__double_as_longlong(d);
+}
+
+// info[0] = delta, info[1] = max deviation, info[2] = max |f| (doubles); with tt (a NUFFT search) also the plan's
+// scalars nu[0..3] = delta, f_0, t[0] - t0, t[n-1] - t0 -- one read-back for all of them.
+__global__ __launch_bounds__(256) void k_ap_final(const double* __restrict__ f, int64_t nf,
+                                                  const double2* __restrict__ part, int nb, double* __restrict__ info,
+                                                  const double* __restrict__ tt, double t0, int64_t n,
+                                                  double* __restrict__ nu) {
+    double dev = 0.0, fm = 0.0;
+    for (int b = threadIdx.x; b < nb; b += blockDim.x) {
+        dev = fmax(dev, part[b].x);
+        fm = fmax(fm, part[b].y);
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        dev = fmax(dev, __shfl_xor(dev, o));
+        fm = fmax(fm, __shfl_xor(fm, o));
+    }
+    __shared__ double red[2][4];
+    if ((threadIdx.x & 63) == 0) {
+        red[0][threadIdx.x >> 6] = dev;
+        red[1][threadIdx.x >> 6] = fm;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const double f0 = f[0];
+        const double d = (f[nf - 1] - f0) / (double)(nf - 1);
+        info[0] = d;
+        info[1] = fmax(fmax(red[0][0], red[0][1]), fmax(red[0][2], red[0][3]));
+        info[2] = fmax(fmax(red[1][0], red[1][1]), fmax(red[1][2], red[1][3]));
+        if (tt) {
+            nu[0] = d;
+            nu[1] = f0;
+            nu[2] = tt[0] - t0;
+            nu[3] = tt[n - 1] - t0;
+        }
+    }
 }

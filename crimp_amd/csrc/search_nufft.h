@@ -209,17 +209,6 @@ __global__ __launch_bounds__(256) void k_nu_sorted(const double* __restrict__ tt
     if (__any(b) && (threadIdx.x & 63) == 0) atomicOr(bad, 1);
 }
 
-// host-side scalars of the plan in one read-back: delta, f_0, dt[0], dt[n-1]
-__global__ void k_nu_scalars(const double* __restrict__ ap, const double* __restrict__ freq,
-                             const double* __restrict__ tt, double t0, int64_t n, double* __restrict__ out) {
-    if (threadIdx.x == 0) {
-        out[0] = ap[0];
-        out[1] = freq[0];
-        out[2] = (tt[0] - t0);
-        out[3] = (tt[n - 1] - t0);
-    }
-}
-
 // Moments of harmonics k0 .. k0+G-1 for rows [0, nrow) of the pass (c2row points at the pass's first row).
 // Lane l: photon q = l >> 4 of the K-group, A row (moment) p = l & 15, B column col = l & 15 = 2 row + (re/im).
 template <int G, bool TWOD>
@@ -347,27 +336,43 @@ struct NuCellArgs {
 // The cell gather's plans take the photon order from here too (no k_nu_sorted pass): a pair out of order sets *bad
 // (the search then takes the default path) and the writes stay inside the tables, which the host zeroes first, so
 // every entry is a photon index in [0, n] whatever the order.
+// Four photons per thread and sweep, their loads (and their predecessors', L1 hits) issued together: one load per
+// iteration left the pass latency-bound at ~2 TB/s (35-44 us per 80 MB at config 3).
+constexpr int kNuCellU = 4;
 __global__ __launch_bounds__(256) void k_nu_cellstart(const double* __restrict__ tt, double t0, int64_t n, double s1,
                                                       int k0, int nk, NuCellArgs a, int64_t* __restrict__ start,
                                                       int* __restrict__ bad) {
     int b = 0;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const double d = tt[i] - t0, dp = i == 0 ? d : tt[i - 1] - t0;
-        b |= !(dp <= d);
-        const double u = d * s1;
-        const double up = dp * s1;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < n; i0 += kNuCellU * stride) {
+        double cur[kNuCellU], prv[kNuCellU];
 #pragma unroll
-        for (int j = 0; j < kNuCellK; ++j) {
-            if (j >= nk) break;
-            const double kd = (double)(k0 + j);
-            // cells fit 32 bits (nu_plan: |G| <= 32 n / 2 <= 2^28): one v_cvt_i32_f64, not the int64 conversion
-            const int64_t g = (int)rint(kd * u);
-            const int64_t gp = i == 0 ? a.gmin[j] - 1 : (int)rint(kd * up);
-            int64_t* st = start + a.off[j];
-            const int64_t lo = gp + 1 > a.gmin[j] ? gp + 1 : a.gmin[j];
-            const int64_t hi = g < a.gmin[j] + a.span[j] - 1 ? g : a.gmin[j] + a.span[j] - 1;
-            for (int64_t G = lo; G <= hi; ++G) st[G - a.gmin[j]] = i;
-            if (i == n - 1) st[a.span[j]] = n;
+        for (int q = 0; q < kNuCellU; ++q) {
+            const int64_t i = i0 + q * stride, ic = i < n ? i : n - 1;
+            cur[q] = tt[ic];
+            prv[q] = tt[ic > 0 ? ic - 1 : 0];
+        }
+#pragma unroll
+        for (int q = 0; q < kNuCellU; ++q) {
+            const int64_t i = i0 + q * stride;
+            if (i >= n) break;
+            const double d = cur[q] - t0, dp = i == 0 ? d : prv[q] - t0;
+            b |= !(dp <= d);
+            const double u = d * s1;
+            const double up = dp * s1;
+#pragma unroll
+            for (int j = 0; j < kNuCellK; ++j) {
+                if (j >= nk) break;
+                const double kd = (double)(k0 + j);
+                // cells fit 32 bits (nu_plan checks |G| + n < 2^31): one v_cvt_i32_f64, not the int64 conversion
+                const int64_t g = (int)rint(kd * u);
+                const int64_t gp = i == 0 ? a.gmin[j] - 1 : (int)rint(kd * up);
+                int64_t* st = start + a.off[j];
+                const int64_t lo = gp + 1 > a.gmin[j] ? gp + 1 : a.gmin[j];
+                const int64_t hi = g < a.gmin[j] + a.span[j] - 1 ? g : a.gmin[j] + a.span[j] - 1;
+                for (int64_t G = lo; G <= hi; ++G) st[G - a.gmin[j]] = i;
+                if (i == n - 1) st[a.span[j]] = n;
+            }
         }
     }
     if (__any(b) && (threadIdx.x & 63) == 0) atomicOr(bad, 1);
@@ -1403,8 +1408,10 @@ static bool nu_gather_form(int64_t nrows_grid) {
 static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, int64_t n, const double* freq,
                         int64_t nf, int64_t nrows_grid, const double* c2, const double* hs, bool twod, int nharm,
                         int stat, int64_t first,
-                        int64_t count, double* out, bool timed, int64_t* nfixed, bool no_fixup, bool* applicable) {
+                        int64_t count, double* out, bool timed, int64_t* nfixed, bool no_fixup, bool* applicable,
+                        double* best, bool* best_done) {
     *applicable = false;
+    *best_done = false;
     *nfixed = 0;
     int bad = 0;
     memcpy(&bad, hs + 4, sizeof(int));
@@ -1521,8 +1528,10 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
     int64_t* ctab = nullptr;
     int64_t* cstart = nullptr;
     int64_t* flagged = nullptr;
-    int* nflag = nullptr;  // [fix-up count, photons out of order (cell-gather plans)]
-    HIPCHK(sc.alloc(&nflag, 2));
+    // [fix-up count, photons out of order (cell-gather plans), -, -, best power, best index (as doubles)]: read back
+    // in one transfer at the end
+    int* nflag = nullptr;
+    HIPCHK(sc.alloc(&nflag, 8));
     if (any_mfma) {
         HIPCHK(sc.alloc(&U, (size_t)(ubytes / 8)));
         HIPCHK(sc.alloc(&ctab, (size_t)(2 * 8 * nchunk)));
@@ -1683,7 +1692,7 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
                     soff[(size_t)(k - 1)] = off;
                     off += ca.span[j] + 1;
                 }
-                k_nu_cellstart<<<(unsigned)std::min<int64_t>(cdiv(n, 256), 8192), 256, 0, s>>>(t, t0, n, pl.s1, k0, nk,
+                k_nu_cellstart<<<(unsigned)std::min<int64_t>(cdiv(n, 256 * kNuCellU), 8192), 256, 0, s>>>(t, t0, n, pl.s1, k0, nk,
                                                                                               ca, cstart, nflag + 1);
                 HIPCHK(hipGetLastError());
             }
@@ -1783,8 +1792,13 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
         for (double v : cls) g_kernel_times.push_back(v);
         for (double v : cnt) g_kernel_times.push_back(v);
     }
-    int fl[2] = {0, 0};
-    HIPCHK(d2h(s, fl, nflag, sizeof(fl)));
+    // the best trial of the powers (crimp_search_best) rides on the same read-back; valid unless a fix-up follows
+    if (best) {
+        const int rc = launch_best(sc, s, out, count, reinterpret_cast<double*>(nflag + 4));
+        if (rc) return rc;
+    }
+    int fl[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    HIPCHK(d2h(s, fl, nflag, (best ? 8 : 2) * sizeof(int)));
     if (fl[1]) {  // photons out of order (found by the cell starts): nothing computed, the default path runs
         *applicable = false;
         g_last_search_path = 0;
@@ -1792,6 +1806,10 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
     }
     const int nf_h = fl[0];
     *nfixed = nf_h;
+    if (best && (nf_h == 0 || no_fixup)) {
+        std::memcpy(best, fl + 4, 2 * sizeof(double));
+        *best_done = true;
+    }
     if (nf_h == 0 || no_fixup) return CRIMP_OK;
     double *dt = nullptr, *dt2 = nullptr;  // the fix-up's fp64 kernel reads dt (and dt^2) arrays
     HIPCHK(sc.alloc(&dt, (size_t)n));

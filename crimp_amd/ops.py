@@ -98,6 +98,17 @@ def search(t, t0, freq, nharm, stat, log10_negfdot=None, first=0, count=None, ou
     relative of the reference by its certificate and the fp64 fix-up), "exact" (no NUFFT: the exact-integer i8 MFMA
     kernel on progressions of >= 256 trials, fp64 otherwise; the default of rounds 1-5) or "f64" (fp64 kernel
     everywhere). A precision argument takes precedence over CRIMP_PRECISION."""
+    return _search(t, t0, freq, nharm, stat, log10_negfdot, first, count, out, flags, precision, False)
+
+
+def search_best(t, t0, freq, nharm, stat, log10_negfdot=None, first=0, count=None, out=None, flags=0,
+                precision=None):
+    """``search`` and the best trial of its powers in one call (crimp_search_best): (out, best power, index within
+    the computed range), np.argmax semantics; a NUFFT search reads the best back with its fix-up count."""
+    return _search(t, t0, freq, nharm, stat, log10_negfdot, first, count, out, flags, precision, True)
+
+
+def _search(t, t0, freq, nharm, stat, log10_negfdot, first, count, out, flags, precision, want_best):
     if precision not in PRECISIONS:
         raise ValueError("precision must be one of %s (the fp32 'fast' path was retired)" % (PRECISIONS,))
     env = search_flags()
@@ -119,10 +130,16 @@ def search(t, t0, freq, nharm, stat, log10_negfdot=None, first=0, count=None, ou
     if out is None:
         out = _empty_like_input(t, count, b)
     op = b.arg(out, np.float64, writable=True)
+    if not want_best:
+        with b.device_guard():
+            N.check(L.crimp_search(tp, n, float(t0), fp, nf, dp, nfd, int(nharm), int(stat), int(first), int(count),
+                                   op, b.flags(flags), b.stream()))
+        return out
+    res = np.zeros(2, dtype=np.float64)
     with b.device_guard():
-        N.check(L.crimp_search(tp, n, float(t0), fp, nf, dp, nfd, int(nharm), int(stat), int(first), int(count), op,
-                               b.flags(flags), b.stream()))
-    return out
+        N.check(L.crimp_search_best(tp, n, float(t0), fp, nf, dp, nfd, int(nharm), int(stat), int(first), int(count),
+                                    op, ctypes.c_void_p(res.ctypes.data), b.flags(flags), b.stream()))
+    return out, float(res[0]), int(res[1])
 
 
 def best(x):

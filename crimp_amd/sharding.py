@@ -39,13 +39,14 @@ def _device_for_backend(dist):
     return torch.device("cpu")
 
 
-def _gpu_slice(time, t0, freq, nharm, stat, freq_dot, first, count, flags=0, precision=None):
+def _gpu_slice(time, t0, freq, nharm, stat, freq_dot, first, count, flags=0, precision=None, best=False):
     from . import ops
     import torch
     if isinstance(time, torch.Tensor) and freq_dot is not None and not isinstance(freq_dot, torch.Tensor):
         freq_dot = torch.as_tensor(np.asarray(freq_dot, dtype=np.float64), device=time.device)
-    return ops.search(time, t0, freq, nharm, stat, log10_negfdot=freq_dot, first=first, count=count, flags=flags,
-                      precision=precision)
+    fn = ops.search_best if best else ops.search
+    return fn(time, t0, freq, nharm, stat, log10_negfdot=freq_dot, first=first, count=count, flags=flags,
+              precision=precision)
 
 
 def _as_comm(local, dev):
@@ -71,6 +72,7 @@ def sharded_search(time, freq, nharm=2, stat=0, freq_dot=None, gather="all", com
     import functools
     import torch
     dist, world, rank = _dist()
+    custom = compute is not None
     compute = compute or functools.partial(_gpu_slice, flags=flags, precision=precision)
     as_tensor = isinstance(time, torch.Tensor)
     if as_tensor:
@@ -84,16 +86,25 @@ def sharded_search(time, freq, nharm=2, stat=0, freq_dot=None, gather="all", com
     nfd = 0 if freq_dot is None else int(freq_dot.numel() if isinstance(freq_dot, torch.Tensor) else np.size(freq_dot))
     total = (nfd if nfd else 1) * nf
     first, count = shard_range(total, world, rank)
-    local = compute(time, t0, freq, nharm, stat, freq_dot, first, count)
+    rank_best = None
+    if gather == "best" and count and not custom and as_tensor and time.is_cuda:
+        # the rank's search and its best trial in one call (crimp_search_best: a NUFFT search reads the best back
+        # with its fix-up count)
+        local, bv_, bi_ = _gpu_slice(time, t0, freq, nharm, stat, freq_dot, first, count, flags=flags,
+                                     precision=precision, best=True)
+        rank_best = (bv_, bi_)
+    else:
+        local = compute(time, t0, freq, nharm, stat, freq_dot, first, count)
     dev = _device_for_backend(dist) if dist is not None else (
         local.device if isinstance(local, torch.Tensor) else torch.device("cpu"))
     loc = _as_comm(local, dev)
     if gather == "best":
         if count:
-            if isinstance(local, torch.Tensor) and local.is_cuda:
-                # the rank's best on the device (crimp_best: one reduction, one 16-byte readback)
+            if rank_best is not None or (isinstance(local, torch.Tensor) and local.is_cuda):
+                # the rank's best on the device (crimp_search_best, or crimp_best: one reduction, one 16-byte
+                # readback)
                 from . import ops
-                bv, bi = ops.best(local)
+                bv, bi = rank_best if rank_best is not None else ops.best(local)
                 if dist is None:
                     return bv, bi + first
                 mine = torch.tensor([bv, float(bi + first)], dtype=torch.float64, device=dev)

@@ -161,6 +161,14 @@ int crimp_search(const double* t, int64_t n, double t0, const double* freq, int6
                  const double* log10_negfdot, int64_t nfd, int32_t nharm, int32_t stat, int64_t first,
                  int64_t count, double* out, uint32_t flags, void* stream);
 
+/* crimp_search and the best trial of its powers in one call: out[count] as crimp_search, best[0] = the largest of
+ * out, best[1] = its index within [first, first+count) as a double (np.argmax semantics, as crimp_best), best a host
+ * pointer. A NUFFT search reads the best trial back with its fix-up count (one stream sync less than crimp_search +
+ * crimp_best; sharding.sharded_search(gather='best')). */
+int crimp_search_best(const double* t, int64_t n, double t0, const double* freq, int64_t nf,
+                      const double* log10_negfdot, int64_t nfd, int32_t nharm, int32_t stat, int64_t first,
+                      int64_t count, double* out, double* best, uint32_t flags, void* stream);
+
 /* Best trial of a power array x[n] (crimp_search's out): best[0] = max, best[1] = its index as a double (exact:
  * n <= 2^53), np.argmax semantics -- ties to the lowest index, NaN above every number   [the maximum the
  * reference's callers take of PeriodSearch's powers; sharding.sharded_search(gather='best')]. best is a host
