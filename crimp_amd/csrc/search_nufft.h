@@ -42,7 +42,7 @@ constexpr int kNuGatherMaxP = 24;  // moments of the cell-gather spread (registe
 constexpr int kNuMergeG = 16;      // wrapped cells per merge block
 constexpr int kNuMaxWrap = 32;     // unwrapped cells per wrapped cell (span of the photons over n)
 constexpr int kNuTile = 4096;      // complex elements per FFT block (64 KB of LDS), 16 per thread
-constexpr double kNuEps = 1e-14;   // truncation bound per photon at the grid's edge
+constexpr double kNuEps = 5e-14;   // truncation bound per photon at the grid's edge (below the rounding term kNuRho)
 // Rounding bound per photon for the certificate, in units of |A_k|'s scale N: c_i (cis table + fp64 polynomial,
 // angle-addition over <= 8 harmonics: ~20 ulp), the MFMA's fp64 accumulation over <= 256 K-groups per cell run
 // (<= 256 ulp of the run's sum of |terms|, each <= 1), the merge, the FFT (~3 log2 n ulp) and Horner (e^x ulp):
@@ -974,9 +974,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k
 // alternate between moments (three barriers per moment); element i at i ^ ((i >> 3) & 7) (stage 1's stride-8
 // writes over all banks). The transform's arithmetic differs from the radix-16 form's in rounding only.
 __device__ __forceinline__ int nu_sw8(int i) { return i ^ ((i >> 3) & 7); }
+// Moment chunks: the launch transforms moments plo .. P-1 (X holds their planes only, beta = (p - plo) nrow + r) and,
+// with accum, adds its partial sum to the CS an earlier chunk (moments above P) wrote -- the sum over moments is
+// linear, and each chunk starts the Bessel recurrence at its own top (nu_bes_start(P)).
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k_nu_rows4096_combine8(
-    const double2* X, int lnfft, int P, int nrow, int64_t nf, int64_t jhi, int64_t h, int64_t tbase,
-    int64_t nbt, const double* __restrict__ bc, double2* __restrict__ CS) {
+    const double2* X, int lnfft, int P, int plo, int accum, int nrow, int64_t nf, int64_t jhi, int64_t h,
+    int64_t tbase, int64_t nbt, const double* __restrict__ bc, double2* __restrict__ CS) {
     extern __shared__ double2 nu_s[];  // [2][4096]
     __shared__ NuTile tw;
     nu_tile_init(&tw, 12);
@@ -993,17 +996,22 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
     for (int q = 0; q < 8; ++q) {
         acc[q] = make_double2(0.0, 0.0);
         const int64_t J = k1 + ((int64_t)(t + 512 * q) << ln1);
+        if (accum) {  // the earlier chunk's sum at this position's trial (positions without a trial keep 0)
+            const int64_t jc = J <= jhi ? J : J - nfft;
+            const int64_t tt = tbase + r * nf + jc;
+            if ((J <= jhi || J >= nfft - h) && tt >= 0 && tt < nbt) acc[q] = CS[tt];
+        }
         bs[q] = nu_bes_start(bc, P, nu_zh(J <= jhi ? J : J - nfft, lnfft));
-        nx[q] = xr[(int64_t)(P - 1) * pstride + t + 512 * q];
+        nx[q] = xr[(int64_t)(P - 1 - plo) * pstride + t + 512 * q];
     }
     const int m2 = (t & 7) << 6, m3 = (t & 63) << 3, m4 = t;  // stage twiddles in units of w_4096
     const int z2 = ((t >> 3) << 6) + (t & 7), z3 = ((t >> 6) << 9) + (t & 63);  // stage 2 / 3 output bases
     __syncthreads();                                                             // tw
     int par = 0;
-    for (int p = P - 1; p >= 0; --p, par ^= 1) {
+    for (int p = P - 1; p >= plo; --p, par ^= 1) {
         double2* A = nu_s + (par ? 4096 : 0);
         double2* B = nu_s + (par ? 0 : 4096);
-        const int64_t pn = (int64_t)(p > 0 ? p - 1 : 0) * pstride;
+        const int64_t pn = (int64_t)(p > plo ? p - 1 - plo : 0) * pstride;
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
             v[q] = nx[q];
@@ -1312,6 +1320,14 @@ static int64_t nu_cus() {  // compute units of the current device (persistent gr
     return ncu;
 }
 
+// Moments per pass-1 / pass-2 chunk of the radix-8 row path (CRIMP_NUFFT_PCHUNK, an A/B hook; 0 or above P: one
+// chunk, the whole moment set)
+static int nu_pchunk() {  // read per call (tests switch it within one process)
+    const char* e = getenv("CRIMP_NUFFT_PCHUNK");
+    const int c = e ? atoi(e) : 4;
+    return c > 0 ? c : (1 << 20);
+}
+
 static int64_t nufft_budget() {
     static int64_t b = -1;
     if (b < 0) {
@@ -1611,6 +1627,42 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
         auto fft_combine = [&](int k, int64_t rb, int nrow, int64_t tb0, int64_t nbt) -> int {
             const int64_t Bp = (int64_t)P * nrow;
             const double plane = 16.0 * (double)Bp * (double)nfft;  // one complex FFT buffer of the batch
+            if (fused_combine && ln2 == 12 && rows4096 && rows_r8) {
+                // moment chunks of <= pchunk: pass 1 and pass 2 of a chunk in turn, the chunk's pass-1 output (16
+                // pchunk nrow n bytes: 64 MB at config 3) still in the Infinity Cache when pass 2 reads it
+                int alo = 0, acnt = 0;
+                if (ln1 > 0) occupied(k, &alo, &acnt);
+                const int pc = std::max(1, std::min(nu_pchunk(), P));
+                for (int phi = P; phi > 0; phi -= pc) {
+                    const int plo = std::max(0, phi - pc);
+                    const int64_t Bc = (int64_t)(phi - plo) * nrow;
+                    const double cplane = 16.0 * (double)Bc * (double)nfft;
+                    const double2* Win = W + (int64_t)plo * nrow * nfft;
+                    const double2* Zo = Win;
+                    if (ln1 > 0) {
+                        g_nu_work[kNuClsPass1] += cplane * ((double)acnt / (double)(int64_t(1) << ln1)) + cplane;
+                        if (ln1 == 8) {
+                            const int64_t ngroups = Bc << (ln2 - 4);
+                            k_nu_cols256<<<(unsigned)std::min<int64_t>(ngroups, 2 * nu_cus()), 256, lds_fft, s>>>(
+                                Win, Y, lnfft, T, alo, acnt, ngroups);
+                        } else {
+                            k_nu_fft_cols<<<dim3((unsigned)(int64_t(1) << (ln2 - lcol)), (unsigned)Bc), 256, lds_fft,
+                                            s>>>(Win, Y, lnfft, ln1, lcol, T, alo, acnt);
+                        }
+                        HIPCHK(hipGetLastError());
+                        Zo = Y;
+                        HIPCHK(span(kNuClsPass1));
+                    }
+                    g_nu_work[kNuClsPass2] += cplane + 16.0 * (double)nbt * (phi < P ? 2.0 : 1.0);
+                    k_nu_rows4096_combine8<<<dim3((unsigned)(int64_t(1) << ln1), (unsigned)nrow), 512, 2 * lds_fft,
+                                             s>>>(Zo, lnfft, phi, plo, phi < P ? 1 : 0, nrow, nf, pl.nseg - 1 - pl.h,
+                                                  pl.h, rb * nf + jbase - (tb0 + first), nbt, bc,
+                                                  CS + (int64_t)(k - 1) * nbt);
+                    HIPCHK(hipGetLastError());
+                    HIPCHK(span(kNuClsPass2));
+                }
+                return CRIMP_OK;
+            }
             double2* Zo = W;
             if (ln1 > 0) {
                 int alo = 0, acnt = 0;
@@ -1628,15 +1680,6 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
                 }
                 Zo = Y;
                 HIPCHK(span(kNuClsPass1));
-            }
-            if (fused_combine && ln2 == 12 && rows4096 && rows_r8) {  // 512 threads, radix 8
-                g_nu_work[kNuClsPass2] += plane + 16.0 * (double)nbt;
-                k_nu_rows4096_combine8<<<dim3((unsigned)(int64_t(1) << ln1), (unsigned)nrow), 512, 2 * lds_fft, s>>>(
-                    Zo, lnfft, P, nrow, nf, pl.nseg - 1 - pl.h, pl.h, rb * nf + jbase - (tb0 + first), nbt, bc,
-                    CS + (int64_t)(k - 1) * nbt);
-                HIPCHK(hipGetLastError());
-                HIPCHK(span(kNuClsPass2));
-                return CRIMP_OK;
             }
             if (fused_combine && ln2 == 12 && rows4096) {  // the specialised form for 4096-element rows
                 g_nu_work[kNuClsPass2] += plane + 16.0 * (double)nbt;

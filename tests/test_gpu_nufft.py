@@ -264,3 +264,26 @@ def test_nufft_gather_lane_splits(gpu, monkeypatch):
     monkeypatch.setenv("CRIMP_NUFFT_LANES", "3")
     with pytest.raises(Exception):
         ops.search(t, t0, f, 2, 1, precision="nufft")
+
+
+def test_nufft_moment_chunks_agree(gpu, monkeypatch):
+    """The radix-8 row path runs the moments in chunks (CRIMP_NUFFT_PCHUNK, default 4: pass 1 and pass 2 of one chunk
+    in turn, each chunk adding its part of the moment sum to the trials' harmonic sums): chunks of 1, 3, 4 and all P
+    moments agree to rounding (the chunks restart the Bessel recurrence from their own series values) -- a 1-D
+    2^20-point plan (256-row columns) and a 2-D 2^17-point plan (generic columns), raw powers (fix-up off)."""
+    from crimp_amd import ops, _native as N
+    from crimp_amd.synth import pulsed_events
+    t = pulsed_events(300_000, 2.0e5, 3.3, pulsed_frac=0.05, fdot=-2e-11, seed=13)
+    t0 = (t[0] + t[-1]) / 2
+    cases = ((3.3 + np.arange(-300000, 300000) / 2.0e7, 2, None), (3.3 + np.arange(-40000, 40000) / 2.0e6, 3,
+                                                                    np.array([-12.0, -11.0, -10.5])))
+    for f, m, fdv in cases:
+        got = {}
+        for pc in ("0", "1", "3", "4"):
+            monkeypatch.setenv("CRIMP_NUFFT_PCHUNK", pc)
+            got[pc] = ops.search(t, t0, f, m, 1, log10_negfdot=fdv, flags=N.FLAG_NO_FIXUP)
+            assert _path() == 2
+        for pc in ("1", "3", "4"):
+            rel = np.abs(got[pc] - got["0"]) / np.abs(got["0"])
+            assert rel.max() <= 1e-10 and np.median(rel) <= 1e-13, (pc, rel.max(), np.median(rel))
+        close_rel(got["4"], ops.search(t, t0, f, m, 1, log10_negfdot=fdv, precision="f64"), 1e-6)
