@@ -1320,11 +1320,13 @@ static int64_t nu_cus() {  // compute units of the current device (persistent gr
     return ncu;
 }
 
-// Moments per pass-1 / pass-2 chunk of the radix-8 row path (CRIMP_NUFFT_PCHUNK, an A/B hook; 0 or above P: one
-// chunk, the whole moment set)
-static int nu_pchunk() {  // read per call (tests switch it within one process)
+// Moments per pass-1 / pass-2 chunk of the radix-8 row path (CRIMP_NUFFT_PCHUNK, an A/B hook read per call; unset, 0
+// or above P: one chunk, the whole moment set). Chunks meant the chunk's pass-1 output to be read back from the
+// Infinity Cache; measured slower at every size (config 3 pass 1 + pass 2: 0.265 ms whole, 0.352 at 8 moments, 0.527
+// at 4, 0.874 at 2; profiles/r06/ab_pchunk.log), so the default is one chunk.
+static int nu_pchunk() {
     const char* e = getenv("CRIMP_NUFFT_PCHUNK");
-    const int c = e ? atoi(e) : 4;
+    const int c = e ? atoi(e) : 0;
     return c > 0 ? c : (1 << 20);
 }
 
@@ -1628,8 +1630,7 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
             const int64_t Bp = (int64_t)P * nrow;
             const double plane = 16.0 * (double)Bp * (double)nfft;  // one complex FFT buffer of the batch
             if (fused_combine && ln2 == 12 && rows4096 && rows_r8) {
-                // moment chunks of <= pchunk: pass 1 and pass 2 of a chunk in turn, the chunk's pass-1 output (16
-                // pchunk nrow n bytes: 64 MB at config 3) still in the Infinity Cache when pass 2 reads it
+                // moment chunks of <= nu_pchunk() (default: all P moments in one): pass 1 and pass 2 of a chunk in turn
                 int alo = 0, acnt = 0;
                 if (ln1 > 0) occupied(k, &alo, &acnt);
                 const int pc = std::max(1, std::min(nu_pchunk(), P));
