@@ -2,6 +2,8 @@
 against the oracle on a sample of trials computed over ALL photons (plain per-trial relative error), plus
 size-independent properties (injected signal found at its trial, trial partitions bit-identical to the
 whole, NUFFT vs exact path agreement on every trial, the chi^2_4 noise mean). Tolerances as tests/test_gpu_parity.py."""
+import math
+
 import numpy as np
 import pytest
 
@@ -272,23 +274,44 @@ def test_config5_toas_vs_oracle(gpu):
     for i in sample:
         _fit_vs_oracle(r, i, xh[oh[i]:oh[i + 1]], E[i], tm)
     assert margins[ties[0]] < 1e-5       # the sample did include a near-tie of the lattice
-    _every_interval_vs_oracle_profile(r, xh, oh, E, tm)
+    clipped = _every_interval_vs_oracle_profile(r, xh, oh, E, tm)
+    print("config 5 per GPU: %d clipped scan positions checked" % clipped)
 
 
-def _every_interval_vs_oracle_profile(r, xh, oh, E, tm, ph_shift_res=1000):
+def _scan_position(phi, side, k, step, pb, fourier):
+    """phShift of the reference's 1-sigma scan at its k-th step on one side (measureToAs.py:330-376 as O.fit_toa
+    restates it, lmfit's clip-to-bound semantics): the target phi + side k step clipped to the phShift bounds
+    +-pb; for Fourier templates a step taken while the previous one sat on +-pi moves that bound to the target
+    (the scan then walks past +-pi), for Cauchy / von Mises the scan stays on the bound."""
+    pmin, pmax, cur = -pb, pb, phi
+    for kk in range(1, k + 1):
+        target = phi + side * kk * step
+        if fourier:
+            if side < 0 and kk > 1 and cur <= -math.pi:
+                pmin = target
+            if side > 0 and kk > 1 and cur >= math.pi:
+                pmax = target
+        cur = min(max(target, pmin), pmax)
+    return cur
+
+
+def _every_interval_vs_oracle_profile(r, xh, oh, E, tm, ph_shift_res=1000, workers=None):
     """Every interval of a device fit against the oracle's fp64 extended likelihood (templatemodels.py:98-121), a
     few likelihood passes each instead of a whole oracle fit (measureToAs.py:320-376):
     * optimum: at the device's (norm, phShift) the profile's Newton step -g_phi / (H_pp - H_pn^2 / H_nn) is below
       1e-6 cycles and the norm's -g_n / H_nn below 1e-9 of the norm (the device optimum is the oracle's);
     * 1-sigma scan: with k* = kk - 1 the scan step the reported bound kk * step + step / 2 implies on each side, the
-      norm-profiled LL at phShift -+ (k* - 1) step lies within 0.5 chi2_1(0.6827) = 0.500021713558733 of LLmax and
-      at -+ k* step beyond it -- the crossing is exactly where the device reported it (lmfit's clip to the phShift
-      bounds at +-pi as the oracle's fit_toa; the phShiftRes / 2 cap excepted)."""
+      norm-profiled LL at the scan's step k* - 1 lies within 0.5 chi2_1(0.6827) = 0.500021713558733 of LLmax and at
+      step k* beyond it -- the crossing is exactly where the device reported it. The scan's positions follow lmfit's
+      clip to the phShift bounds (_scan_position: the intervals whose scan reaches +-pi are checked on the clipped
+      and bound-moving steps, not skipped); a scan that reached the phShiftRes / 2 cap is checked inside up to it."""
     import math
     import os
     from concurrent.futures import ThreadPoolExecutor
     thr = 0.500021713558733
     tarr = O.template_arrays(tm)
+    fourier = str(tm["model"]).lower() == "fourier"
+    pb = math.pi if fourier else 1.5 * math.pi
     n0 = float(tm["norm"]["value"])
     lo, hi = n0 / 100.0, 500.0
     step = 2 * math.pi / ph_shift_res
@@ -299,40 +322,70 @@ def _every_interval_vs_oracle_profile(r, xh, oh, E, tm, ph_shift_res=1000):
         o = O.toa_eval(x, E[i], tarr, n, phi)
         heff = o[5] - o[4] * o[4] / o[3]
         step_phi = -(o[2] - o[4] * o[1] / o[3]) / heff  # profile Newton step (norm re-maximised)
-        if abs(phi) >= math.pi - 1e-9 and step_phi * phi > 0:
+        if abs(phi) >= pb - 1e-9 and step_phi * phi > 0:
             wphi = 0.0  # the maximum lies past the phShift bound: the bounded fit stops there (lmfit's bounds)
         else:
             wphi = abs(step_phi) / (2 * math.pi)
         wn = abs(o[1] / o[3]) / n if lo < n < hi else 0.0
         llmax = O._profile_norm(x, E[i], tarr, phi, lo, hi, n)[1][0]
-        bad = []
+        bad, clipped = [], 0
         for side, bound in ((-1, r["phShi_LL"][i]), (1, r["phShi_UL"][i])):
             kk = int(round((bound - step / 2) / step))
             kstar = kk - 1
-            if kstar + 1 > ph_shift_res / 2:
-                continue                                       # capped scan
-            if abs(phi) + (kstar + 1) * step >= math.pi:
-                continue      # the scan reached +-pi: lmfit's clip-to-bound steps (tests/test_gpu_scan_edges.py)
-            for k, inside in ((kstar - 1, True), (kstar, False)):
+            capped = kstar + 1 > ph_shift_res / 2
+            checks = [(kstar - 1, True)] if capped else [(kstar - 1, True), (kstar, False)]
+            for k, inside in checks:
                 if k < 1:
                     continue
-                p = min(max(phi + side * k * step, -math.pi), math.pi)
+                p = _scan_position(phi, side, k, step, pb, fourier)
+                clipped += p != phi + side * k * step
                 _, ok = O._profile_norm(x, E[i], tarr, p, lo, hi, n)
                 diff = llmax - ok[0]
                 if not ((diff <= thr) if inside else (diff > thr)):
                     bad.append((i, side, k, kstar, diff))
-        return wphi, wn, bad
+        return wphi, wn, bad, clipped
 
-    workers = max(1, min(16, len(os.sched_getaffinity(0))))
+    workers = workers or max(1, min(16, len(os.sched_getaffinity(0))))
     with ThreadPoolExecutor(workers) as ex:
         res = list(ex.map(one, range(len(E))))
-    bad = [b for _, _, bb in res for b in bb]
+    bad = [b for _, _, bb, _ in res for b in bb]
     assert not bad, bad[:5]
-    iphi = int(np.argmax([w for w, _, _ in res]))
-    inrm = int(np.argmax([w for _, w, _ in res]))
+    iphi = int(np.argmax([w for w, _, _, _ in res]))
+    inrm = int(np.argmax([w for _, w, _, _ in res]))
     worst_phi, worst_n = res[iphi][0], res[inrm][1]
     assert worst_phi <= 1e-6, (iphi, worst_phi, float(r["phShi"][iphi]), float(r["norm"][iphi]))
     assert worst_n <= 1e-9, (inrm, worst_n, float(r["phShi"][inrm]), float(r["norm"][inrm]))
+    return sum(c for _, _, _, c in res)
+
+
+@pytest.mark.timeout(900)
+def test_config5_whole_every_interval_vs_oracle(gpu):
+    """The whole of config 5 on one GPU -- 1e4 intervals x 1e5 photons, bench.py's toa_full_config5 workload (seed
+    12) -- every interval against the oracle's profile likelihood as above, the bound-adjacent intervals included
+    (their scans replayed with lmfit's clip-to-bound steps)."""
+    import os
+    import torch
+    from crimp_amd.readPPtemplate import readPPtemplate
+    from crimp_amd.synth import template_intervals_torch
+    from crimp_amd.toafit import ToAFitter
+    from conftest import gpath
+    O.set_threads(1)
+    tm = readPPtemplate(gpath("1e2259_template.txt"))
+    K = sum(1 for k in tm if k.startswith("amp_"))
+    amps = [tm["amp_%d" % j]["value"] for j in range(1, K + 1)]
+    phs = [tm["ph_%d" % j]["value"] for j in range(1, K + 1)]
+    x, off, E, shifts = template_intervals_torch(10_000, 100_000, tm["norm"]["value"], amps, phs, seed=12, device=gpu)
+    r = ToAFitter(x, off, E, tm).fit(brutemin=True)
+    d = np.angle(np.exp(1j * (r["phShi"] - shifts)))
+    assert np.sqrt(np.mean(d ** 2)) / (2 * np.pi) < 5e-3
+    xh, oh = x.cpu().numpy(), off.cpu().numpy()
+    del x
+    torch.cuda.empty_cache()
+    near = int(np.sum(np.abs(r["phShi"]) + 60 * 2 * np.pi / 1000 >= np.pi))
+    clipped = _every_interval_vs_oracle_profile(r, xh, oh, E, tm, workers=max(1, min(16, len(os.sched_getaffinity(0)))))
+    print("config 5 whole: %d intervals, %d fitted within 60 scan steps of +-pi, %d clipped scan positions checked"
+          % (len(E), near, clipped))
+    assert near > 0 and clipped > 0  # the bound-adjacent intervals were checked, not skipped
 
 
 def _sample_template(tm, n, shift, rng):
