@@ -40,19 +40,26 @@ def _correlated_inputs():
 
 def _within_1e6_of_reference(got, z64, t_h, f_h, nharm, stat, name, what):
     """Every trial within 1e-6 relative of the fp64 path or, where it is not, of the oracle in the reference's
-    operation order. At m = 20 two fp64 evaluations with different argument roundings (the reference's
-    2 pi k f dt, the fp64 kernel's angle additions, the exact kernel's f_j dt) differ by ~2^-53 of the k = 20
-    argument per term, which moves a noise-level H by up to ~1e-6 (duplicated photons double it coherently):
-    there the reference itself is the yardstick. Measured (tools/diag_cert.py): duplicated photons, H_20, trial
-    7429: exact 4.9e-7 from the reference, the fp64 kernel 1.7e-6 from the exact path, the reference 2.5e-6 from
-    the exact-argument value."""
+    operation order (``ref``). At m = 20 two fp64 evaluations with different argument roundings (the reference's
+    2 pi k f dt, the fp64 kernel's angle additions, the exact kernel's f_j dt, the NUFFT's f_0 + j delta model of
+    the grid, whose values deviate from the array's by a few ulp) differ by ~2^-53 of the k = 20 argument per term,
+    which moves a noise-level H by up to ~1e-6 where H = Z^2_m - 4 (m - 1) cancels (duplicated photons double it
+    coherently): there the reference itself is that far from the exact-argument value (``true``, the same formula
+    with the argument carried exactly), and the contract is DESIGN.md section 8's exception -- the device as close to
+    ``true`` as the reference is, plus 1e-6. Measured (tools/diag_cert.py, tools/diag_nufft_harm.py,
+    profiles/r06/diag_nufft_harm_duplicated.log): duplicated photons, H_20, trial 7429, H = Z^2_20 - 76 = 0.4985
+    (153x cancellation): the reference 2.5e-6 from ``true``, the exact path 1.8e-6, the NUFFT 1.1e-6, the fp64
+    kernel 8.6e-8."""
     e = _rel(got, z64)
     off = np.flatnonzero(e > 1e-6)
     assert off.size <= 32, (name, what, off.size)
     if off.size:
         ref = O.search(t_h, f_h[off], nharm, stat="h" if stat else "z2")
         er = _rel(got[off], ref)
-        assert er.max() <= 1e-6, (name, what, er.max(), int(off[er.argmax()]))
+        tru = O.search(t_h, f_h[off], nharm, stat="h" if stat else "z2", exact_argument=True)
+        exc = np.abs(got[off] - tru) <= np.abs(ref - tru) + 1e-6 * np.abs(tru)
+        ok = (er <= 1e-6) | ((_rel(ref, tru) > 1e-6) & exc)
+        assert ok.all(), (name, what, er[~ok], _rel(ref, tru)[~ok], int(off[~ok][0]))
     return e, off.size
 
 
