@@ -338,13 +338,18 @@ struct NuCellArgs {
 // every entry is a photon index in [0, n] whatever the order.
 // Four photons per thread and sweep, their loads (and their predecessors', L1 hits) issued together: one load per
 // iteration left the pass latency-bound at ~2 TB/s (35-44 us per 80 MB at config 3).
+// A block that finds a pair out of order among its 256 photons writes nothing for them: on sorted photons every
+// block is clean and the tables complete; on unsorted ones the search is discarded anyway (*bad), and a skipped
+// block cannot run a long write loop for a backward-then-forward jump (the gathers never read the tables then).
 constexpr int kNuCellU = 4;
 __global__ __launch_bounds__(256) void k_nu_cellstart(const double* __restrict__ tt, double t0, int64_t n, double s1,
                                                       int k0, int nk, NuCellArgs a, int64_t* __restrict__ start,
                                                       int* __restrict__ bad) {
     int b = 0;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < n; i0 += kNuCellU * stride) {
+    // block-uniform loop bound (the barrier of __syncthreads_or below)
+    for (int64_t i0b = (int64_t)blockIdx.x * blockDim.x; i0b < n; i0b += kNuCellU * stride) {
+        const int64_t i0 = i0b + threadIdx.x;
         double cur[kNuCellU], prv[kNuCellU];
 #pragma unroll
         for (int q = 0; q < kNuCellU; ++q) {
@@ -355,9 +360,11 @@ __global__ __launch_bounds__(256) void k_nu_cellstart(const double* __restrict__
 #pragma unroll
         for (int q = 0; q < kNuCellU; ++q) {
             const int64_t i = i0 + q * stride;
-            if (i >= n) break;
+            const bool valid = i < n;
             const double d = cur[q] - t0, dp = i == 0 ? d : prv[q] - t0;
-            b |= !(dp <= d);
+            const int ooo = valid && !(dp <= d);
+            b |= ooo;
+            if (__syncthreads_or(ooo) || !valid) continue;
             const double u = d * s1;
             const double up = dp * s1;
 #pragma unroll
@@ -384,21 +391,41 @@ __global__ __launch_bounds__(256) void k_nu_cellstart(const double* __restrict__
 // order: deterministic) completes the sums and lane s writes the moments p = s (mod L) to W[p * nrow + r][g].
 // fp64 VALU throughout: per photon, row and harmonic one premultiplier phase and cis, then 3 operations per moment.
 // L > 1 spreads a cell's photons over several lanes when cells are dense (many photons per cell, few cells).
+// One launch serves up to kNuGatherSet harmonics (NuGatherSet: block ranges, cells, lanes per cell and W plane of
+// each): the harmonics of a search share the launch's waves, so its last round of blocks is not one harmonic's tail
+// (config 3 ran two launches of 1.7 and 3.4 rounds of resident waves).
 constexpr int kNuGatherRows = 2;
-template <int R, bool TWOD, int L, int PP>  // PP >= P moments accumulated unconditionally (no per-moment selects)
-__global__ __launch_bounds__(256) void k_nu_gather(const double* __restrict__ tt, double t0, const int64_t* __restrict__ start,
-                                                   int64_t gmin, int64_t gmax, int64_t nfft, int64_t gbase,
-                                                   int64_t gcount, double s1, double fch, double fcl,
-                                                   const double* __restrict__ c2row, int nrow, int k, int P,
-                                                   const double2* __restrict__ tab, double2* __restrict__ W) {
+constexpr int kNuGatherSet = 8;
+struct NuGatherSet {
+    int nk;
+    int k[kNuGatherSet], lanes_log2[kNuGatherSet];
+    int64_t blk0[kNuGatherSet + 1];                       // first block of each harmonic, then the total
+    int64_t gmin[kNuGatherSet], gmax[kNuGatherSet], gbase[kNuGatherSet], gcount[kNuGatherSet];
+    int64_t soff[kNuGatherSet], woff[kNuGatherSet];       // the harmonic's start table and W planes
+};
+template <int R, bool TWOD, int PP>  // PP >= P moments accumulated unconditionally (no per-moment selects)
+__global__ __launch_bounds__(256) void k_nu_gather(const double* __restrict__ tt, double t0,
+                                                   const int64_t* __restrict__ startb, int64_t nfft, double s1,
+                                                   double fch, double fcl, const double* __restrict__ c2row, int nrow,
+                                                   int P, const NuGatherSet S, const int* __restrict__ bad,
+                                                   const double2* __restrict__ tab, double2* __restrict__ Wb) {
+    // photons out of order (the cell starts found it): the start tables are not filled (nothing zeroes them), so no
+    // lane may read them; the search's results are discarded and the default path runs
+    if (*bad) return;
     __shared__ double2 stab[2048];  // the cis table (nu_cis2), read per photon: LDS, not L2 latency
     for (int e = threadIdx.x; e < 2048; e += 256) stab[e] = tab[e];
     __syncthreads();
-    const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const int64_t idx = tid / L;
-    const int sub = (int)(tid % L);
-    if (idx >= gcount) return;  // whole L-groups leave together (L divides 64); no barrier below
-    const int64_t g = (gbase + idx) & (nfft - 1);  // the FFT's occupied rows only (nu_occupied)
+    int j = 0;  // this block's harmonic (block-uniform)
+    while (j + 1 < S.nk && (int64_t)blockIdx.x >= S.blk0[j + 1]) ++j;
+    const int ll = S.lanes_log2[j], L = 1 << ll;
+    const int64_t tid = ((int64_t)blockIdx.x - S.blk0[j]) * 256 + threadIdx.x;
+    const int64_t idx = tid >> ll;
+    const int sub = (int)(tid & (L - 1));
+    if (idx >= S.gcount[j]) return;  // whole L-groups leave together (L divides 64); no barrier below
+    const int64_t gmin = S.gmin[j], gmax = S.gmax[j];
+    const int64_t* __restrict__ start = startb + S.soff[j];
+    double2* __restrict__ W = Wb + S.woff[j];
+    const int64_t g = (S.gbase[j] + idx) & (nfft - 1);  // the FFT's occupied rows only (nu_occupied)
     double ar[R][PP], ai[R][PP];
 #pragma unroll
     for (int r = 0; r < R; ++r)
@@ -407,7 +434,7 @@ __global__ __launch_bounds__(256) void k_nu_gather(const double* __restrict__ tt
     double c2[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) c2[r] = (TWOD && r < nrow) ? c2row[r] : 0.0;
-    const double kd = (double)k;
+    const double kd = (double)S.k[j];
     // the photon times are prefetched raw and unconditionally (indices clamped into the cell, whose stand-ins are
     // never weighted): a load whose value entered a select or a subtraction at its issue would be waited for there;
     // the next cell's photon range is loaded during the current cell
@@ -479,8 +506,7 @@ __global__ __launch_bounds__(256) void k_nu_gather(const double* __restrict__ tt
             }
         }
     }
-#pragma unroll
-    for (int o = L / 2; o > 0; o >>= 1)
+    for (int o = L / 2; o > 0; o >>= 1)  // block-uniform L
 #pragma unroll
         for (int r = 0; r < R; ++r)
 #pragma unroll
@@ -493,7 +519,7 @@ __global__ __launch_bounds__(256) void k_nu_gather(const double* __restrict__ tt
     for (int r = 0; r < R; ++r)
 #pragma unroll
         for (int p = 0; p < PP; ++p)
-            if (r < nrow && p < P && (p % L) == sub)
+            if (r < nrow && p < P && (p & (L - 1)) == sub)
                 W[((int64_t)p * nrow + r) * nfft + g] = make_double2(ar[r][p], ai[r][p]);
 }
 
@@ -1276,40 +1302,30 @@ static void nu_launch_spread(int G, dim3 grid, hipStream_t s, const double* tt, 
 
 // Budget of the NUFFT path's device buffers (CRIMP_NUFFT_BUDGET_MB, default 6144): slots, FFT ping-pong, sums.
 template <int R, bool TWOD>
-static void launch_gather_r(int L, int64_t gcount, const double* tt, double t0, const int64_t* start, int64_t gmin,
-                            int64_t gmax,
-                            int64_t nfft, int64_t gbase, double s1, double fch, double fcl, const double* c2, int nrow,
-                            int k, int P, const double2* tab, double2* W, hipStream_t s) {
-    const dim3 grid((unsigned)cdiv(gcount * L, 256));
-#define NU_GATHER(LL, PPP) k_nu_gather<R, TWOD, LL, PPP><<<grid, 256, 0, s>>>(tt, t0, start, gmin, gmax, nfft, gbase, \
-                                                                              gcount, s1, fch, fcl, c2, nrow, k, P, tab, W)
-#define NU_GATHER_L(PPP)              \
-    switch (L) {                      \
-        case 8: NU_GATHER(8, PPP); break; \
-        case 4: NU_GATHER(4, PPP); break; \
-        case 2: NU_GATHER(2, PPP); break; \
-        default: NU_GATHER(1, PPP); break; \
-    }
-    if (P <= 16) {
-        NU_GATHER_L(16)
+static void launch_gather_r(int64_t blocks, const double* tt, double t0, const int64_t* start, int64_t nfft, double s1,
+                            double fch, double fcl, const double* c2, int nrow, int P, const NuGatherSet& S,
+                            const int* bad, const double2* tab, double2* W, hipStream_t s) {
+    const dim3 grid((unsigned)blocks);
+#define NU_GATHER(PPP) \
+    k_nu_gather<R, TWOD, PPP><<<grid, 256, 0, s>>>(tt, t0, start, nfft, s1, fch, fcl, c2, nrow, P, S, bad, tab, W)
+    if (P <= 15) {
+        NU_GATHER(15);
+    } else if (P <= 16) {
+        NU_GATHER(16);
     } else if (P <= 20) {
-        NU_GATHER_L(20)
+        NU_GATHER(20);
     } else {
-        NU_GATHER_L(kNuGatherMaxP)
+        NU_GATHER(kNuGatherMaxP);
     }
-#undef NU_GATHER_L
 #undef NU_GATHER
 }
-static void launch_gather(int L, bool twod, int64_t gcount, const double* tt, double t0, const int64_t* start,
-                          int64_t gmin,
-                          int64_t gmax, int64_t nfft, int64_t gbase, double s1, double fch, double fcl,
-                          const double* c2, int nrow, int k, int P, const double2* tab, double2* W, hipStream_t s) {
+static void launch_gather(bool twod, int64_t blocks, const double* tt, double t0, const int64_t* start, int64_t nfft,
+                          double s1, double fch, double fcl, const double* c2, int nrow, int P, const NuGatherSet& S,
+                          const int* bad, const double2* tab, double2* W, hipStream_t s) {
     if (twod)
-        launch_gather_r<kNuGatherRows, true>(L, gcount, tt, t0, start, gmin, gmax, nfft, gbase, s1, fch, fcl, c2, nrow, k,
-                                             P, tab, W, s);
+        launch_gather_r<kNuGatherRows, true>(blocks, tt, t0, start, nfft, s1, fch, fcl, c2, nrow, P, S, bad, tab, W, s);
     else
-        launch_gather_r<1, false>(L, gcount, tt, t0, start, gmin, gmax, nfft, gbase, s1, fch, fcl, c2, nrow, k, P, tab, W,
-                                  s);
+        launch_gather_r<1, false>(blocks, tt, t0, start, nfft, s1, fch, fcl, c2, nrow, P, S, bad, tab, W, s);
 }
 
 static int64_t nu_cus() {  // compute units of the current device (persistent grids)
@@ -1479,7 +1495,13 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
         nfmax = std::max<int64_t>(nfmax, int64_t(1) << pl.lnfft);
         nrow_all = std::max<int64_t>(nrow_all, nrow_max);
     }
-    const int64_t fixed_bytes = 2 * Bmax * 16 + csmax * 16;
+    // cell-gather grids gather up to kNuGatherSet harmonics per launch, each into its own W planes
+    int gw = 1;
+    if (gather_grid) {
+        gw = std::min(nharm, kNuGatherSet);
+        while (gw > 1 && (gw + 1) * Bmax * 16 + csmax * 16 > nufft_budget()) --gw;
+    }
+    const int64_t fixed_bytes = (gw + 1) * Bmax * 16 + csmax * 16;
     std::vector<std::pair<int, int>> passes;  // (k0, harmonics) of each spread pass, harmonics a power of two
     int64_t ubytes = 0;
     for (int G = 8;; G /= 2) {  // G >= 2
@@ -1555,7 +1577,7 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
         HIPCHK(sc.alloc(&ctab, (size_t)(2 * 8 * nchunk)));
     }
     if (starts_max > 0) HIPCHK(sc.alloc(&cstart, (size_t)starts_max));
-    HIPCHK(sc.alloc(&W, (size_t)Bmax));
+    HIPCHK(sc.alloc(&W, (size_t)(Bmax * gw)));
     HIPCHK(sc.alloc(&Y, (size_t)Bmax));
     HIPCHK(sc.alloc(&CS, (size_t)csmax));
     HIPCHK(sc.alloc(&flagged, (size_t)count));
@@ -1626,7 +1648,7 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
         auto occupied = [&](int k, int* alo, int* acnt) {
             nu_occupied(pl.gmin[(size_t)(k - 1)], pl.gmax[(size_t)(k - 1)], lnfft, ln1, alo, acnt);
         };
-        auto fft_combine = [&](int k, int64_t rb, int nrow, int64_t tb0, int64_t nbt) -> int {
+        auto fft_combine = [&](int k, int64_t rb, int nrow, int64_t tb0, int64_t nbt, double2* W) -> int {
             const int64_t Bp = (int64_t)P * nrow;
             const double plane = 16.0 * (double)Bp * (double)nfft;  // one complex FFT buffer of the batch
             if (fused_combine && ln2 == 12 && rows4096 && rows_r8) {
@@ -1724,7 +1746,8 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
         if (use_gather(pl)) {
             std::vector<int64_t> soff((size_t)nharm);
             int64_t off = 0;
-            HIPCHK(hipMemsetAsync(cstart, 0, (size_t)starts_max * sizeof(int64_t), s));
+            // no zeroing of the start tables: on time-sorted photons every entry is written (each cell's first
+            // photon writes it), and on unsorted ones the gathers read none of them (k_nu_gather exits on *bad)
             for (int k0 = 1; k0 <= nharm; k0 += kNuCellK) {
                 NuCellArgs ca{};
                 const int nk = std::min(kNuCellK, nharm - k0 + 1);
@@ -1745,28 +1768,46 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
                 const int nrow = (int)std::min<int64_t>(kNuGatherRows, pl.r1 - rb);
                 const int64_t tb0 = std::max<int64_t>(first, rb * nf) - first;
                 const int64_t nbt = std::min<int64_t>(first + count, (rb + nrow) * nf) - first - tb0;
-                for (int k = 1; k <= nharm; ++k) {
-                    int alo = 0, acnt = 0;
-                    occupied(k, &alo, &acnt);
-                    const int64_t gbase = (int64_t)alo << ln2, gcount = (int64_t)acnt << ln2;
-                    // lanes per cell: enough threads for ~2 rounds of 3 resident waves per SIMD, keeping >= 4
-                    // photons per lane, at most 4 (8 lanes' butterfly costs more than it spreads: config 3 spread
-                    // 0.154 ms at 4 lanes, 0.199 at 8, 0.161 at 2, profiles/r05/ab_lanes.log)
-                    const int64_t kspan = pl.gmax[(size_t)(k - 1)] - pl.gmin[(size_t)(k - 1)] + 1;
-                    const int64_t ppc = n / std::max<int64_t>(1, std::min<int64_t>(kspan, nfft));
-                    int L = 1;
-                    while (L < 4 && gcount * L < (int64_t(1) << 20) && ppc >= 4 * 2 * L) L *= 2;
-                    if (lanes_env > 0) L = lanes_env;  // test hook: CRIMP_NUFFT_LANES=1|2|4|8
-                    // per photon and row: premultiplier phase + cis ~ 40 flops, then 2 FMA + 1 multiply per moment
-                    g_nu_work[0] += (40.0 + 5.0 * P) * (double)n * nrow;
-                    g_nu_work[kNuClsSpread] += 8.0 * (double)n + 16.0 * (double)P * nrow * (double)gcount;
-                    launch_gather(L, twod, gcount, t, t0, cstart + soff[(size_t)(k - 1)], pl.gmin[(size_t)(k - 1)],
-                                  pl.gmax[(size_t)(k - 1)], nfft, gbase, pl.s1, pl.fch, pl.fcl,
-                                  twod ? c2 + rb : nullptr, nrow, k, P, cis2, W, s);
+                for (int k0 = 1; k0 <= nharm; k0 += gw) {
+                    NuGatherSet S{};
+                    S.nk = std::min(gw, nharm - k0 + 1);
+                    int64_t blocks = 0;
+                    for (int jj = 0; jj < S.nk; ++jj) {
+                        const int k = k0 + jj;
+                        int alo = 0, acnt = 0;
+                        occupied(k, &alo, &acnt);
+                        const int64_t gbase = (int64_t)alo << ln2, gcount = (int64_t)acnt << ln2;
+                        // lanes per cell: enough threads for ~2 rounds of 3 resident waves per SIMD, keeping >= 4
+                        // photons per lane, at most 4 (8 lanes' butterfly costs more than it spreads: config 3
+                        // spread 0.154 ms at 4 lanes, 0.199 at 8, 0.161 at 2, profiles/r05/ab_lanes.log)
+                        const int64_t kspan = pl.gmax[(size_t)(k - 1)] - pl.gmin[(size_t)(k - 1)] + 1;
+                        const int64_t ppc = n / std::max<int64_t>(1, std::min<int64_t>(kspan, nfft));
+                        int L = 1;
+                        while (L < 4 && gcount * L < (int64_t(1) << 20) && ppc >= 4 * 2 * L) L *= 2;
+                        if (lanes_env > 0) L = lanes_env;  // test hook: CRIMP_NUFFT_LANES=1|2|4|8
+                        S.k[jj] = k;
+                        S.lanes_log2[jj] = L == 8 ? 3 : L == 4 ? 2 : L == 2 ? 1 : 0;
+                        S.blk0[jj] = blocks;
+                        blocks += cdiv(gcount * L, 256);
+                        S.gmin[jj] = pl.gmin[(size_t)(k - 1)];
+                        S.gmax[jj] = pl.gmax[(size_t)(k - 1)];
+                        S.gbase[jj] = gbase;
+                        S.gcount[jj] = gcount;
+                        S.soff[jj] = soff[(size_t)(k - 1)];
+                        S.woff[jj] = (int64_t)jj * Bmax;
+                        // per photon and row: premultiplier phase + cis ~ 40 flops, then 2 FMA + 1 multiply per moment
+                        g_nu_work[0] += (40.0 + 5.0 * P) * (double)n * nrow;
+                        g_nu_work[kNuClsSpread] += 8.0 * (double)n + 16.0 * (double)P * nrow * (double)gcount;
+                    }
+                    S.blk0[S.nk] = blocks;
+                    launch_gather(twod, blocks, t, t0, cstart, nfft, pl.s1, pl.fch, pl.fcl, twod ? c2 + rb : nullptr,
+                                  nrow, P, S, nflag + 1, cis2, W, s);
                     HIPCHK(hipGetLastError());
                     HIPCHK(span(kNuClsSpread));
-                    int rc = fft_combine(k, rb, nrow, tb0, nbt);
-                    if (rc) return rc;
+                    for (int jj = 0; jj < S.nk; ++jj) {
+                        int rc = fft_combine(k0 + jj, rb, nrow, tb0, nbt, W + (int64_t)jj * Bmax);
+                        if (rc) return rc;
+                    }
                 }
                 int rc = finalize(tb0, nbt);
                 if (rc) return rc;
@@ -1810,7 +1851,7 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
                         nfft, gbase, gcount, W);
                     HIPCHK(hipGetLastError());
                     HIPCHK(span(kNuClsMerge));
-                    int rc = fft_combine(k, rb, nrow, tb0, nbt);
+                    int rc = fft_combine(k, rb, nrow, tb0, nbt, W);
                     if (rc) return rc;
                 }
             }
