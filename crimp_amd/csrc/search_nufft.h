@@ -336,53 +336,56 @@ struct NuCellArgs {
 // The cell gather's plans take the photon order from here too (no k_nu_sorted pass): a pair out of order sets *bad
 // (the search then takes the default path) and the writes stay inside the tables, which the host zeroes first, so
 // every entry is a photon index in [0, n] whatever the order.
-// Four photons per thread and sweep, their loads (and their predecessors', L1 hits) issued together: one load per
-// iteration left the pass latency-bound at ~2 TB/s (35-44 us per 80 MB at config 3).
-// A block that finds a pair out of order among its 256 photons writes nothing for them: on sorted photons every
+// Two photons per thread (one 16-byte load when t is 16-byte aligned, VEC), a grid covering the photons (no loop): the
+// predecessor of a pair's first photon is the previous lane's second one (a shuffle; lane 0 loads it). A loop of
+// 8-byte loads (one or four per iteration) ran at ~2 TB/s (35-43 us per 80 MB at config 3).
+// A block that finds a pair out of order among its 512 photons writes nothing for them: on sorted photons every
 // block is clean and the tables complete; on unsorted ones the search is discarded anyway (*bad), and a skipped
 // block cannot run a long write loop for a backward-then-forward jump (the gathers never read the tables then).
-constexpr int kNuCellU = 4;
+template <bool VEC>
 __global__ __launch_bounds__(256) void k_nu_cellstart(const double* __restrict__ tt, double t0, int64_t n, double s1,
                                                       int k0, int nk, NuCellArgs a, int64_t* __restrict__ start,
                                                       int* __restrict__ bad) {
-    int b = 0;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    // block-uniform loop bound (the barrier of __syncthreads_or below)
-    for (int64_t i0b = (int64_t)blockIdx.x * blockDim.x; i0b < n; i0b += kNuCellU * stride) {
-        const int64_t i0 = i0b + threadIdx.x;
-        double cur[kNuCellU], prv[kNuCellU];
+    const int64_t pr = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // pair: photons 2 pr, 2 pr + 1
+    const int64_t i0 = 2 * pr;
+    double x0, x1;
+    if (VEC && i0 + 1 < n) {
+        const double2 v = reinterpret_cast<const double2*>(tt)[pr];
+        x0 = v.x;
+        x1 = v.y;
+    } else {
+        x0 = tt[i0 < n ? i0 : n - 1];
+        x1 = tt[i0 + 1 < n ? i0 + 1 : n - 1];
+    }
+    const int lane = threadIdx.x & 63;
+    double xp = __shfl_up(x1, 1, 64);
+    if (lane == 0) xp = tt[i0 > 0 ? i0 - 1 : 0];
+    double d[2] = {x0 - t0, x1 - t0};
+    const double dp0 = i0 == 0 ? d[0] : xp - t0;
+    const bool v0 = i0 < n, v1 = i0 + 1 < n;
+    const int ooo = (v0 && !(dp0 <= d[0])) || (v1 && !(d[0] <= d[1]));
+    if (__any(ooo) && lane == 0) atomicOr(bad, 1);
+    if (__syncthreads_or(ooo)) return;
 #pragma unroll
-        for (int q = 0; q < kNuCellU; ++q) {
-            const int64_t i = i0 + q * stride, ic = i < n ? i : n - 1;
-            cur[q] = tt[ic];
-            prv[q] = tt[ic > 0 ? ic - 1 : 0];
-        }
+    for (int q = 0; q < 2; ++q) {
+        const int64_t i = i0 + q;
+        if (i >= n) break;
+        const double u = d[q] * s1;
+        const double up = (q == 0 ? dp0 : d[0]) * s1;
 #pragma unroll
-        for (int q = 0; q < kNuCellU; ++q) {
-            const int64_t i = i0 + q * stride;
-            const bool valid = i < n;
-            const double d = cur[q] - t0, dp = i == 0 ? d : prv[q] - t0;
-            const int ooo = valid && !(dp <= d);
-            b |= ooo;
-            if (__syncthreads_or(ooo) || !valid) continue;
-            const double u = d * s1;
-            const double up = dp * s1;
-#pragma unroll
-            for (int j = 0; j < kNuCellK; ++j) {
-                if (j >= nk) break;
-                const double kd = (double)(k0 + j);
-                // cells fit 32 bits (nu_plan checks |G| + n < 2^31): one v_cvt_i32_f64, not the int64 conversion
-                const int64_t g = (int)rint(kd * u);
-                const int64_t gp = i == 0 ? a.gmin[j] - 1 : (int)rint(kd * up);
-                int64_t* st = start + a.off[j];
-                const int64_t lo = gp + 1 > a.gmin[j] ? gp + 1 : a.gmin[j];
-                const int64_t hi = g < a.gmin[j] + a.span[j] - 1 ? g : a.gmin[j] + a.span[j] - 1;
-                for (int64_t G = lo; G <= hi; ++G) st[G - a.gmin[j]] = i;
-                if (i == n - 1) st[a.span[j]] = n;
-            }
+        for (int j = 0; j < kNuCellK; ++j) {
+            if (j >= nk) break;
+            const double kd = (double)(k0 + j);
+            // cells fit 32 bits (nu_plan checks |G| + n < 2^31): one v_cvt_i32_f64, not the int64 conversion
+            const int64_t g = (int)rint(kd * u);
+            const int64_t gp = i == 0 ? a.gmin[j] - 1 : (int)rint(kd * up);
+            int64_t* st = start + a.off[j];
+            const int64_t lo = gp + 1 > a.gmin[j] ? gp + 1 : a.gmin[j];
+            const int64_t hi = g < a.gmin[j] + a.span[j] - 1 ? g : a.gmin[j] + a.span[j] - 1;
+            for (int64_t G = lo; G <= hi; ++G) st[G - a.gmin[j]] = i;
+            if (i == n - 1) st[a.span[j]] = n;
         }
     }
-    if (__any(b) && (threadIdx.x & 63) == 0) atomicOr(bad, 1);
 }
 
 // L lanes per wrapped cell g sum, over its unwrapped cells G = g (mod n) and their photons in time order (lane s
@@ -1759,8 +1762,11 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
                     soff[(size_t)(k - 1)] = off;
                     off += ca.span[j] + 1;
                 }
-                k_nu_cellstart<<<(unsigned)std::min<int64_t>(cdiv(n, 256 * kNuCellU), 8192), 256, 0, s>>>(t, t0, n, pl.s1, k0, nk,
-                                                                                              ca, cstart, nflag + 1);
+                const unsigned cb = (unsigned)cdiv(cdiv(n, 2), 256);
+                if ((reinterpret_cast<uintptr_t>(t) & 15u) == 0)
+                    k_nu_cellstart<true><<<cb, 256, 0, s>>>(t, t0, n, pl.s1, k0, nk, ca, cstart, nflag + 1);
+                else
+                    k_nu_cellstart<false><<<cb, 256, 0, s>>>(t, t0, n, pl.s1, k0, nk, ca, cstart, nflag + 1);
                 HIPCHK(hipGetLastError());
             }
             HIPCHK(span(kNuClsCellStart));
@@ -1771,19 +1777,25 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
                 for (int k0 = 1; k0 <= nharm; k0 += gw) {
                     NuGatherSet S{};
                     S.nk = std::min(gw, nharm - k0 + 1);
-                    int64_t blocks = 0;
+                    int64_t blocks = 0, set_cells = 0;  // the set's occupied cells (threads at one lane per cell)
+                    for (int jj = 0; jj < S.nk; ++jj) {
+                        int alo = 0, acnt = 0;
+                        occupied(k0 + jj, &alo, &acnt);
+                        set_cells += (int64_t)acnt << ln2;
+                    }
                     for (int jj = 0; jj < S.nk; ++jj) {
                         const int k = k0 + jj;
                         int alo = 0, acnt = 0;
                         occupied(k, &alo, &acnt);
                         const int64_t gbase = (int64_t)alo << ln2, gcount = (int64_t)acnt << ln2;
-                        // lanes per cell: enough threads for ~2 rounds of 3 resident waves per SIMD, keeping >= 4
-                        // photons per lane, at most 4 (8 lanes' butterfly costs more than it spreads: config 3
-                        // spread 0.154 ms at 4 lanes, 0.199 at 8, 0.161 at 2, profiles/r05/ab_lanes.log)
+                        // lanes per cell: doubled (up to 4) while the launch's threads stay <= 2^20 -- counted over
+                        // every harmonic of the set at the doubled lanes -- and each lane keeps >= 8 photons (config
+                        // 3, both harmonics in one launch: 0.099 ms at 2 lanes, 0.108 at 4, 0.143 at 8,
+                        // profiles/r06/ab_gather_lanes.log)
                         const int64_t kspan = pl.gmax[(size_t)(k - 1)] - pl.gmin[(size_t)(k - 1)] + 1;
                         const int64_t ppc = n / std::max<int64_t>(1, std::min<int64_t>(kspan, nfft));
                         int L = 1;
-                        while (L < 4 && gcount * L < (int64_t(1) << 20) && ppc >= 4 * 2 * L) L *= 2;
+                        while (L < 4 && set_cells * 2 * L <= (int64_t(1) << 20) && ppc >= 4 * 2 * L) L *= 2;
                         if (lanes_env > 0) L = lanes_env;  // test hook: CRIMP_NUFFT_LANES=1|2|4|8
                         S.k[jj] = k;
                         S.lanes_log2[jj] = L == 8 ? 3 : L == 4 ? 2 : L == 2 ? 1 : 0;
