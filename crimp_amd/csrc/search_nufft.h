@@ -336,56 +336,72 @@ struct NuCellArgs {
 // The cell gather's plans take the photon order from here too (no k_nu_sorted pass): a pair out of order sets *bad
 // (the search then takes the default path) and the writes stay inside the tables, which the host zeroes first, so
 // every entry is a photon index in [0, n] whatever the order.
-// Two photons per thread (one 16-byte load when t is 16-byte aligned, VEC), a grid covering the photons (no loop): the
-// predecessor of a pair's first photon is the previous lane's second one (a shuffle; lane 0 loads it). A loop of
-// 8-byte loads (one or four per iteration) ran at ~2 TB/s (35-43 us per 80 MB at config 3).
-// A block that finds a pair out of order among its 512 photons writes nothing for them: on sorted photons every
-// block is clean and the tables complete; on unsorted ones the search is discarded anyway (*bad), and a skipped
-// block cannot run a long write loop for a backward-then-forward jump (the gathers never read the tables then).
+// Photon pairs (one 16-byte load when t is 16-byte aligned, VEC), kNuCellU pairs per thread and sweep with their
+// loads issued together, over at most 2048 blocks: the predecessor of a pair's first photon is the previous lane's
+// second one (a shuffle; lane 0 loads it). One 8-byte load per iteration ran at ~2 TB/s, and one pair per thread
+// over a grid covering the photons (19.5k short blocks at config 3) was bound by the workgroup dispatch: 35-43 us per
+// 80 MB either way.
+// A block that finds a pair out of order among its photons of a sweep writes nothing for them: on sorted photons
+// every block is clean and the tables complete; on unsorted ones the search is discarded anyway (*bad), and a
+// skipped block cannot run a long write loop for a backward-then-forward jump (the gathers never read the tables).
+constexpr int kNuCellU = 4;
 template <bool VEC>
 __global__ __launch_bounds__(256) void k_nu_cellstart(const double* __restrict__ tt, double t0, int64_t n, double s1,
                                                       int k0, int nk, NuCellArgs a, int64_t* __restrict__ start,
                                                       int* __restrict__ bad) {
-    const int64_t pr = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // pair: photons 2 pr, 2 pr + 1
-    const int64_t i0 = 2 * pr;
-    double x0, x1;
-    if (VEC && i0 + 1 < n) {
-        const double2 v = reinterpret_cast<const double2*>(tt)[pr];
-        x0 = v.x;
-        x1 = v.y;
-    } else {
-        x0 = tt[i0 < n ? i0 : n - 1];
-        x1 = tt[i0 + 1 < n ? i0 + 1 : n - 1];
-    }
+    const int64_t npair = (n + 1) / 2, stride = (int64_t)gridDim.x * blockDim.x;
     const int lane = threadIdx.x & 63;
-    double xp = __shfl_up(x1, 1, 64);
-    if (lane == 0) xp = tt[i0 > 0 ? i0 - 1 : 0];
-    double d[2] = {x0 - t0, x1 - t0};
-    const double dp0 = i0 == 0 ? d[0] : xp - t0;
-    const bool v0 = i0 < n, v1 = i0 + 1 < n;
-    const int ooo = (v0 && !(dp0 <= d[0])) || (v1 && !(d[0] <= d[1]));
-    if (__any(ooo) && lane == 0) atomicOr(bad, 1);
-    if (__syncthreads_or(ooo)) return;
+    int b = 0;
+    // block-uniform loop bound (the barrier of __syncthreads_or below)
+    for (int64_t p0b = (int64_t)blockIdx.x * blockDim.x; p0b < npair; p0b += kNuCellU * stride) {
+        double x0[kNuCellU], x1[kNuCellU], xl[kNuCellU];
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const int64_t i = i0 + q;
-        if (i >= n) break;
-        const double u = d[q] * s1;
-        const double up = (q == 0 ? dp0 : d[0]) * s1;
+        for (int q = 0; q < kNuCellU; ++q) {
+            const int64_t pr = p0b + threadIdx.x + q * stride, i0 = 2 * pr;
+            if (VEC && i0 + 1 < n) {
+                const double2 v = reinterpret_cast<const double2*>(tt)[pr];
+                x0[q] = v.x;
+                x1[q] = v.y;
+            } else {
+                x0[q] = tt[i0 < n ? i0 : n - 1];
+                x1[q] = tt[i0 + 1 < n ? i0 + 1 : n - 1];
+            }
+            xl[q] = tt[i0 > 0 && i0 - 1 < n ? i0 - 1 : 0];  // lane 0's predecessor (others: an L1 hit, unused)
+        }
 #pragma unroll
-        for (int j = 0; j < kNuCellK; ++j) {
-            if (j >= nk) break;
-            const double kd = (double)(k0 + j);
-            // cells fit 32 bits (nu_plan checks |G| + n < 2^31): one v_cvt_i32_f64, not the int64 conversion
-            const int64_t g = (int)rint(kd * u);
-            const int64_t gp = i == 0 ? a.gmin[j] - 1 : (int)rint(kd * up);
-            int64_t* st = start + a.off[j];
-            const int64_t lo = gp + 1 > a.gmin[j] ? gp + 1 : a.gmin[j];
-            const int64_t hi = g < a.gmin[j] + a.span[j] - 1 ? g : a.gmin[j] + a.span[j] - 1;
-            for (int64_t G = lo; G <= hi; ++G) st[G - a.gmin[j]] = i;
-            if (i == n - 1) st[a.span[j]] = n;
+        for (int q = 0; q < kNuCellU; ++q) {
+            const int64_t i0 = 2 * (p0b + threadIdx.x + q * stride);
+            double xp = __shfl_up(x1[q], 1, 64);
+            if (lane == 0) xp = xl[q];
+            const double d0 = x0[q] - t0, d1 = x1[q] - t0;
+            const double dp0 = i0 == 0 ? d0 : xp - t0;
+            const bool v0 = i0 < n, v1 = i0 + 1 < n;
+            const int ooo = (v0 && !(dp0 <= d0)) || (v1 && !(d0 <= d1));
+            b |= ooo;
+            if (__syncthreads_or(ooo)) continue;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int64_t i = i0 + h;
+                if (i >= n) break;
+                const double u = (h == 0 ? d0 : d1) * s1;
+                const double up = (h == 0 ? dp0 : d0) * s1;
+#pragma unroll
+                for (int j = 0; j < kNuCellK; ++j) {
+                    if (j >= nk) break;
+                    const double kd = (double)(k0 + j);
+                    // cells fit 32 bits (nu_plan checks |G| + n < 2^31): one v_cvt_i32_f64, not the int64 one
+                    const int64_t g = (int)rint(kd * u);
+                    const int64_t gp = i == 0 ? a.gmin[j] - 1 : (int)rint(kd * up);
+                    int64_t* st = start + a.off[j];
+                    const int64_t lo = gp + 1 > a.gmin[j] ? gp + 1 : a.gmin[j];
+                    const int64_t hi = g < a.gmin[j] + a.span[j] - 1 ? g : a.gmin[j] + a.span[j] - 1;
+                    for (int64_t G = lo; G <= hi; ++G) st[G - a.gmin[j]] = i;
+                    if (i == n - 1) st[a.span[j]] = n;
+                }
+            }
         }
     }
+    if (__any(b) && lane == 0) atomicOr(bad, 1);
 }
 
 // L lanes per wrapped cell g sum, over its unwrapped cells G = g (mod n) and their photons in time order (lane s
@@ -1762,7 +1778,7 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
                     soff[(size_t)(k - 1)] = off;
                     off += ca.span[j] + 1;
                 }
-                const unsigned cb = (unsigned)cdiv(cdiv(n, 2), 256);
+                const unsigned cb = (unsigned)std::min<int64_t>(cdiv(cdiv(n, 2), 256 * kNuCellU), 2048);
                 if ((reinterpret_cast<uintptr_t>(t) & 15u) == 0)
                     k_nu_cellstart<true><<<cb, 256, 0, s>>>(t, t0, n, pl.s1, k0, nk, ca, cstart, nflag + 1);
                 else
