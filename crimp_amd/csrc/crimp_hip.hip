@@ -1796,10 +1796,11 @@ static int launch_best(Scratch& sc, hipStream_t s, const double* x, int64_t n, d
 // dt[n-1], unsorted flag]. No memset: k_ap_check zeroes the order flag, k_ap_final writes the rest.
 static int grid_is_progression(Scratch& sc, hipStream_t s, const double* freq, int64_t nf, double** ap, bool* ok,
                                const double* nu_t = nullptr, double t0 = 0.0, int64_t n = 0, double* nu_hs = nullptr,
-                               bool nu_sorted_check = true);
+                               bool nu_sorted_check = true, int* nuflags = nullptr, const NuExpect* ex = nullptr);
 #include "search_nufft.h"
 static int grid_is_progression(Scratch& sc, hipStream_t s, const double* freq, int64_t nf, double** ap, bool* ok,
-                               const double* nu_t, double t0, int64_t n, double* nu_hs, bool nu_sorted_check) {
+                               const double* nu_t, double t0, int64_t n, double* nu_hs, bool nu_sorted_check,
+                               int* nuflags, const NuExpect* ex) {
     *ok = false;
     // info: [delta, max deviation, max |f|, NUFFT: delta, f_0, dt[0], dt[n-1], order flag (int bits)], then the
     // block partials of k_ap_check
@@ -1814,8 +1815,13 @@ static int grid_is_progression(Scratch& sc, hipStream_t s, const double* freq, i
     HIPCHK(hipGetLastError());
     if (nu_t && nu_sorted_check)
         k_nu_sorted<<<(unsigned)std::min<int64_t>(cdiv(n, 256), 2048), 256, 0, s>>>(nu_t, t0, n, order);
-    k_ap_final<<<1, 256, 0, s>>>(freq, nf, part, nb, info, nu_t, t0, n, info + 3);
+    NuExpect none{};
+    k_ap_final<<<1, 256, 0, s>>>(freq, nf, part, nb, info, nu_t, t0, n, info + 3, order, ex ? *ex : none, nuflags);
     HIPCHK(hipGetLastError());
+    if (ex && ex->on) {  // a cached NUFFT plan runs on: no read-back, the device checks the plan (nuflags[1])
+        *ok = true;
+        return CRIMP_OK;
+    }
     double h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     HIPCHK(d2h(s, h, info, (nu_t ? 8 : 3) * sizeof(double)));
     *ok = std::isfinite(h[0]) && h[0] != 0.0 && h[1] <= 16.0 * 2.220446049250313e-16 * h[2];
@@ -2097,20 +2103,55 @@ static int search_impl(const double* t, int64_t n, double t0, const double* freq
         bool progression = false;
         double* ap = nullptr;
         double nu_hs[5] = {0, 0, 0, 0, 0};
-        if (!f64 && (exact_grid || (nufft && nf >= 64))) {
-            int rc = grid_is_progression(sc, s, dfr, nf, &ap, &progression, nufft ? dtm : nullptr, t0, n, nu_hs,
-                                         !nu_gather_form(twod ? nfd : 1));
-            if (rc) return rc;
-        }
         int rc = CRIMP_OK;
         bool done = false, best_done = false;
-        if (progression && nufft && nf >= 64) {  // NUFFT; unsorted photons or no plan fall through to the exact rule
-            int64_t nfix = 0;
-            rc = nufft_search(sc, s, dtm, t0, n, dfr, nf, twod ? nfd : 1, dc2, nu_hs, twod, nharm, stat, first, count,
-                              dout, flags & CRIMP_FLAG_TIME_KERNELS, &nfix, (flags & CRIMP_FLAG_NO_FIXUP) != 0, &done,
-                              best, &best_done);
+        const bool nu_try = nufft && nf >= 64;
+        int* nuflags = nullptr;  // the NUFFT's device flags (fix-up count, photon order / plan check, best trial)
+        if (nu_try) HIPCHK(sc.alloc(&nuflags, 8));
+        const bool gather_form = nu_gather_form(twod ? nfd : 1);
+        // A repeated search over the same buffers reuses its last plan (nu_spec_find): the progression check and
+        // the plan's scalars are recomputed on the device and compared there (k_ap_final), every NUFFT kernel that
+        // reads photon-derived tables exits if they differ, and the host, reading the result flags anyway at the
+        // end, redoes the search from a fresh plan -- one host round trip per search instead of two.
+        NuSpecKey key{};
+        bool spec_mismatch = false;
+        if (nu_try && !f64) {
+            key = nu_spec_key(dtm, n, t0, dfr, nf, twod ? nfd : 0, nharm, first, count, gather_form);
+            NuExpect ex{};
+            if (nu_spec_find(key, nu_hs)) {
+                for (int q = 0; q < 4; ++q) ex.v[q] = nu_hs[q];
+                ex.on = 1;
+                ex.check_order = gather_form ? 0 : 1;
+                rc = grid_is_progression(sc, s, dfr, nf, &ap, &progression, dtm, t0, n, nu_hs, !gather_form, nuflags,
+                                         &ex);
+                if (rc) return rc;
+                int64_t nfix = 0;
+                rc = nufft_search(sc, s, dtm, t0, n, dfr, nf, twod ? nfd : 1, dc2, nu_hs, twod, nharm, stat, first,
+                                  count, dout, flags & CRIMP_FLAG_TIME_KERNELS, &nfix,
+                                  (flags & CRIMP_FLAG_NO_FIXUP) != 0, &done, best, &best_done, nuflags, &spec_mismatch);
+                if (rc) return rc;
+                if (done) g_last_fixups = nfix;
+                if (spec_mismatch) nu_spec_drop(key);
+                // not done and no mismatch: photons out of order under a still-valid progression (the exact rule)
+            }
+        }
+        if (!done && (!progression || spec_mismatch) && !f64 && (exact_grid || nu_try)) {
+            progression = false;
+            rc = grid_is_progression(sc, s, dfr, nf, &ap, &progression, nufft ? dtm : nullptr, t0, n, nu_hs,
+                                     !gather_form, nuflags, nullptr);
             if (rc) return rc;
-            if (done) g_last_fixups = nfix;
+            if (progression && nu_try) {  // NUFFT; unsorted photons or no plan fall through to the exact rule
+                int64_t nfix = 0;
+                bool mm = false;
+                rc = nufft_search(sc, s, dtm, t0, n, dfr, nf, twod ? nfd : 1, dc2, nu_hs, twod, nharm, stat, first,
+                                  count, dout, flags & CRIMP_FLAG_TIME_KERNELS, &nfix,
+                                  (flags & CRIMP_FLAG_NO_FIXUP) != 0, &done, best, &best_done, nuflags, &mm);
+                if (rc) return rc;
+                if (done) {
+                    g_last_fixups = nfix;
+                    nu_spec_store(key, nu_hs);
+                }
+            }
         }
         const bool factorised = !done && progression && exact_grid;
         if ((flags & CRIMP_FLAG_FORCE_MFMA) && !done && !factorised)

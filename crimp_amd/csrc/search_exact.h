@@ -937,11 +937,20 @@ __global__ __launch_bounds__(256) void k_ap_check(const double* __restrict__ f, 
 }
 
 // info[0] = delta, info[1] = max deviation, info[2] = max |f| (doubles); with tt (a NUFFT search) also the plan's
-// scalars nu[0..3] = delta, f_0, t[0] - t0, t[n-1] - t0 -- one read-back for all of them.
+// scalars nu[0..3] = delta, f_0, t[0] - t0, t[n-1] - t0 -- one read-back for all of them -- and the NUFFT's flags
+// nuflags[0] = 0 (fix-up count), nuflags[1] = 0, or 2 when the search runs a cached plan (ex.on) whose scalars, photon
+// order (order, MFMA-slot plans) or progression no longer hold: every NUFFT kernel that reads photon-derived tables
+// then exits, and the host redoes the search from a fresh plan.
+struct NuExpect {
+    double v[4];       // delta, f_0, t[0] - t0, t[n-1] - t0 the cached plan was made from
+    int on;            // a cached plan is running
+    int check_order;   // its spread reads photons in order (k_nu_sorted ran into *order)
+};
 __global__ __launch_bounds__(256) void k_ap_final(const double* __restrict__ f, int64_t nf,
                                                   const double2* __restrict__ part, int nb, double* __restrict__ info,
                                                   const double* __restrict__ tt, double t0, int64_t n,
-                                                  double* __restrict__ nu) {
+                                                  double* __restrict__ nu, const int* __restrict__ order,
+                                                  NuExpect ex, int* __restrict__ nuflags) {
     double dev = 0.0, fm = 0.0;
     for (int b = threadIdx.x; b < nb; b += blockDim.x) {
         dev = fmax(dev, part[b].x);
@@ -960,14 +969,27 @@ __global__ __launch_bounds__(256) void k_ap_final(const double* __restrict__ f, 
     if (threadIdx.x == 0) {
         const double f0 = f[0];
         const double d = (f[nf - 1] - f0) / (double)(nf - 1);
+        dev = fmax(fmax(red[0][0], red[0][1]), fmax(red[0][2], red[0][3]));
+        fm = fmax(fmax(red[1][0], red[1][1]), fmax(red[1][2], red[1][3]));
         info[0] = d;
-        info[1] = fmax(fmax(red[0][0], red[0][1]), fmax(red[0][2], red[0][3]));
-        info[2] = fmax(fmax(red[1][0], red[1][1]), fmax(red[1][2], red[1][3]));
+        info[1] = dev;
+        info[2] = fm;
         if (tt) {
+            const double a0 = tt[0] - t0, a1 = tt[n - 1] - t0;
             nu[0] = d;
             nu[1] = f0;
-            nu[2] = tt[0] - t0;
-            nu[3] = tt[n - 1] - t0;
+            nu[2] = a0;
+            nu[3] = a1;
+            if (nuflags) {
+                int m = 0;
+                if (ex.on) {
+                    const bool ok = isfinite(d) && d != 0.0 && dev <= 16.0 * 2.220446049250313e-16 * fm;
+                    m = !(ok && d == ex.v[0] && f0 == ex.v[1] && a0 == ex.v[2] && a1 == ex.v[3] &&
+                          (!ex.check_order || *order == 0));
+                }
+                nuflags[0] = 0;
+                nuflags[1] = m ? 2 : 0;
+            }
         }
     }
 }

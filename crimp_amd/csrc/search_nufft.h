@@ -216,7 +216,8 @@ __global__ __launch_bounds__(256) void k_nu_spread(const double* __restrict__ tt
                                                    double fch, double fcl, const double* __restrict__ c2row, int nrow,
                                                    int k0, int P, const NuPass* __restrict__ ps,
                                                    const double2* __restrict__ tab, double* __restrict__ U,
-                                                   int64_t* __restrict__ ctab) {
+                                                   int64_t* __restrict__ ctab, const int* __restrict__ bad) {
+    if (*bad) return;  // photons out of order or a cached plan that no longer holds (k_ap_final)
     // the cis table in LDS (read twice per photon and K-group: an L2 round trip each, waited for at once), filled
     // before any wave leaves
     __shared__ double2 stab[1024];
@@ -349,6 +350,7 @@ template <bool VEC>
 __global__ __launch_bounds__(256) void k_nu_cellstart(const double* __restrict__ tt, double t0, int64_t n, double s1,
                                                       int k0, int nk, NuCellArgs a, int64_t* __restrict__ start,
                                                       int* __restrict__ bad) {
+    if (*bad) return;  // a cached plan that no longer holds (k_ap_final): no table is written
     const int64_t npair = (n + 1) / 2, stride = (int64_t)gridDim.x * blockDim.x;
     const int lane = threadIdx.x & 63;
     int b = 0;
@@ -546,7 +548,8 @@ __global__ __launch_bounds__(256) void k_nu_gather(const double* __restrict__ tt
 __global__ __launch_bounds__(256) void k_nu_merge(const double* __restrict__ U, int64_t SL,
                                                   const int64_t* __restrict__ ctab, int64_t nchunk, int64_t gmin,
                                                   int64_t gmax, int64_t nfft, int64_t gbase, int64_t gcount,
-                                                  double2* __restrict__ W) {
+                                                  double2* __restrict__ W, const int* __restrict__ bad) {
+    if (*bad) return;  // the spread did not run (k_nu_spread): its slots and cell table are not written
     __shared__ int64_t rs[kNuMergeG][kNuMaxWrap];
     __shared__ int rc[kNuMergeG][kNuMaxWrap];
     __shared__ int nr[kNuMergeG];
@@ -1312,9 +1315,9 @@ template <bool TWOD>
 static void nu_launch_spread(int G, dim3 grid, hipStream_t s, const double* tt, double t0, int64_t n, int64_t nchunk,
                              double s1,
                              double fch, double fcl, const double* c2, int nrow, int k0, int P, const NuPass* ps,
-                             const double2* tab, double* U, int64_t* ctab) {
+                             const double2* tab, double* U, int64_t* ctab, const int* bad) {
 #define CRIMP_NS(GG) \
-    k_nu_spread<GG, TWOD><<<grid, 256, 0, s>>>(tt, t0, n, nchunk, s1, fch, fcl, c2, nrow, k0, P, ps, tab, U, ctab)
+    k_nu_spread<GG, TWOD><<<grid, 256, 0, s>>>(tt, t0, n, nchunk, s1, fch, fcl, c2, nrow, k0, P, ps, tab, U, ctab, bad)
     if (G == 8) CRIMP_NS(8); else if (G == 4) CRIMP_NS(4); else CRIMP_NS(2);
 #undef CRIMP_NS
 }
@@ -1458,14 +1461,79 @@ static bool nu_gather_form(int64_t nrows_grid) {
 // MFMA-slot plans: a cell-gather plan checks the order in its cell-start pass).
 // t: photon times (seconds), t0 the search's reference time: the kernels form dt = t - t0 as k_search_prep does;
 // dt (and dt^2) arrays are made only for a fix-up.
+// A search's last plan, keyed by its buffers and shape (crimp_search reuses it on the next identical call; the device
+// re-checks its scalars, k_ap_final). Up to 16 entries, the oldest dropped first.
+struct NuSpecKey {
+    const void* t;
+    const void* f;
+    int64_t n, nf, nfd, first, count;
+    double t0;
+    int nharm, dev, gather;
+    bool operator==(const NuSpecKey& o) const {
+        return t == o.t && f == o.f && n == o.n && nf == o.nf && nfd == o.nfd && first == o.first &&
+               count == o.count && t0 == o.t0 && nharm == o.nharm && dev == o.dev && gather == o.gather;
+    }
+};
+struct NuSpecEntry {
+    NuSpecKey key;
+    double hs[5];
+};
+static std::vector<NuSpecEntry> g_nu_spec;
+static bool nu_spec_disabled() {  // CRIMP_NUFFT_PLAN_CACHE=0: every search reads its plan back (A/B hook)
+    const char* e = getenv("CRIMP_NUFFT_PLAN_CACHE");
+    return e && !strcmp(e, "0");
+}
+static NuSpecKey nu_spec_key(const double* t, int64_t n, double t0, const double* f, int64_t nf, int64_t nfd,
+                             int nharm, int64_t first, int64_t count, bool gather) {
+    NuSpecKey k{};
+    k.t = t;
+    k.f = f;
+    k.n = n;
+    k.nf = nf;
+    k.nfd = nfd;
+    k.first = first;
+    k.count = count;
+    k.t0 = t0;
+    k.nharm = nharm;
+    k.gather = gather ? 1 : 0;
+    (void)hipGetDevice(&k.dev);
+    return k;
+}
+static bool nu_spec_find(const NuSpecKey& k, double* hs) {
+    if (nu_spec_disabled()) return false;
+    for (const NuSpecEntry& e : g_nu_spec)
+        if (e.key == k) {
+            std::memcpy(hs, e.hs, sizeof(e.hs));
+            return true;
+        }
+    return false;
+}
+static void nu_spec_drop(const NuSpecKey& k) {
+    for (size_t i = 0; i < g_nu_spec.size(); ++i)
+        if (g_nu_spec[i].key == k) {
+            g_nu_spec.erase(g_nu_spec.begin() + (std::ptrdiff_t)i);
+            return;
+        }
+}
+static void nu_spec_store(const NuSpecKey& k, const double* hs) {
+    if (nu_spec_disabled()) return;
+    nu_spec_drop(k);
+    if (g_nu_spec.size() >= 16) g_nu_spec.erase(g_nu_spec.begin());
+    NuSpecEntry e;
+    e.key = k;
+    std::memcpy(e.hs, hs, sizeof(e.hs));
+    g_nu_spec.push_back(e);
+}
+
 static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, int64_t n, const double* freq,
                         int64_t nf, int64_t nrows_grid, const double* c2, const double* hs, bool twod, int nharm,
                         int stat, int64_t first,
                         int64_t count, double* out, bool timed, int64_t* nfixed, bool no_fixup, bool* applicable,
-                        double* best, bool* best_done) {
+                        double* best, bool* best_done, int* nflag, bool* mismatch) {
     *applicable = false;
     *best_done = false;
     *nfixed = 0;
+    *mismatch = false;
     int bad = 0;
     memcpy(&bad, hs + 4, sizeof(int));
     if (bad) return CRIMP_OK;
@@ -1587,10 +1655,8 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
     int64_t* ctab = nullptr;
     int64_t* cstart = nullptr;
     int64_t* flagged = nullptr;
-    // [fix-up count, photons out of order (cell-gather plans), -, -, best power, best index (as doubles)]: read back
-    // in one transfer at the end
-    int* nflag = nullptr;
-    HIPCHK(sc.alloc(&nflag, 8));
+    // nflag: [fix-up count, photons out of order (1; cell-gather plans) or a cached plan no longer valid (2), -, -,
+    // best power, best index (as doubles)], zeroed or set by k_ap_final, read back in one transfer at the end
     if (any_mfma) {
         HIPCHK(sc.alloc(&U, (size_t)(ubytes / 8)));
         HIPCHK(sc.alloc(&ctab, (size_t)(2 * 8 * nchunk)));
@@ -1642,7 +1708,6 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
         evcls.push_back(cls);
         return mark();
     };
-    HIPCHK(hipMemsetAsync(nflag, 0, 2 * sizeof(int), s));
     int cur_lnfft = -1;
     NuTw T{};
     const double2* cis = nullptr;
@@ -1861,10 +1926,10 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
                                     (double)(pl.gmax[(size_t)(k0 + kk - 1)] - ps.gmin[kk] + 1 + nchunk);
                 if (twod)
                     nu_launch_spread<true>(gl, grid, s, t, t0, n, nchunk, pl.s1, pl.fch, pl.fcl, c2 + rb, nrow, k0, P, dp, cis,
-                                           U, ctab);
+                                           U, ctab, nflag + 1);
                 else
                     nu_launch_spread<false>(gl, grid, s, t, t0, n, nchunk, pl.s1, pl.fch, pl.fcl, c2 + rb, nrow, k0, P, dp,
-                                            cis, U, ctab);
+                                            cis, U, ctab, nflag + 1);
                 HIPCHK(hipGetLastError());
                 HIPCHK(span(kNuClsSpread));
                 for (int kk = 0; kk < gl && k0 + kk <= nharm; ++kk) {
@@ -1876,7 +1941,7 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
                                     16.0 * (double)P * nrow * (double)gcount;
                     k_nu_merge<<<(unsigned)cdiv(gcount, kNuMergeG), 256, (size_t)kNuMergeG * SL * sizeof(double), s>>>(
                         U + ps.ubase[kk], SL, ctab + 2 * kk * nchunk, nchunk, ps.gmin[kk], pl.gmax[(size_t)(k - 1)],
-                        nfft, gbase, gcount, W);
+                        nfft, gbase, gcount, W, nflag + 1);
                     HIPCHK(hipGetLastError());
                     HIPCHK(span(kNuClsMerge));
                     int rc = fft_combine(k, rb, nrow, tb0, nbt, W);
@@ -1912,8 +1977,9 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
     }
     int fl[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     HIPCHK(d2h(s, fl, nflag, (best ? 8 : 2) * sizeof(int)));
-    if (fl[1]) {  // photons out of order (found by the cell starts): nothing computed, the default path runs
-        *applicable = false;
+    if (fl[1]) {  // photons out of order (found by the cell starts), or a cached plan that no longer holds (2):
+        *applicable = false;  // nothing computed, the default path (or a fresh plan) runs
+        *mismatch = fl[1] == 2;
         g_last_search_path = 0;
         return CRIMP_OK;
     }

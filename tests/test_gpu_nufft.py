@@ -287,3 +287,46 @@ def test_nufft_moment_chunks_agree(gpu, monkeypatch):
             rel = np.abs(got[pc] - got["0"]) / np.abs(got["0"])
             assert rel.max() <= 1e-10 and np.median(rel) <= 1e-13, (pc, rel.max(), np.median(rel))
         close_rel(got["4"], ops.search(t, t0, f, m, 1, log10_negfdot=fdv, precision="f64"), 1e-6)
+
+
+@pytest.mark.parametrize("rows", [1, 3])
+def test_nufft_plan_cache_revalidated_on_device(gpu, rows, monkeypatch):
+    """A repeated search over the same device buffers reuses its last plan without reading the plan's scalars back
+    (the device re-checks them, k_ap_final). Changing the buffers in place between calls -- the photons shifted,
+    the grid rescaled, two photons swapped (unsorted), the grid made non-uniform -- must give exactly what a search
+    without the cache gives (CRIMP_NUFFT_PLAN_CACHE=0), kernel family included: the cell-gather form (1 row) and the
+    MFMA-slot form (3 rows)."""
+    import torch
+    from crimp_amd import ops
+    from crimp_amd.synth import pulsed_events
+    t_h = pulsed_events(200_000, 2.0e5, 3.3, pulsed_frac=0.05, fdot=-2e-11, seed=17)
+    f_h = 3.3 + np.arange(-1000, 1000) / 2.0e6
+    fd = None if rows == 1 else torch.as_tensor(np.linspace(-12.0, -10.5, rows), device=gpu)
+    t = torch.as_tensor(t_h, device=gpu)
+    f = torch.as_tensor(f_h, device=gpu)
+    t0 = (t_h[0] + t_h[-1]) / 2
+
+    def run(cache):
+        if cache:
+            monkeypatch.delenv("CRIMP_NUFFT_PLAN_CACHE", raising=False)
+        else:
+            monkeypatch.setenv("CRIMP_NUFFT_PLAN_CACHE", "0")
+        z = ops.search(t, t0, f, 3, 1, log10_negfdot=fd).cpu().numpy()
+        return z, _path()
+
+    first, p1 = run(True)
+    again, p2 = run(True)        # the cached plan, revalidated on the device
+    assert p1 == p2 == 2
+    np.testing.assert_array_equal(again, first)
+    edits = [("shift photons", lambda: t.add_(0.37)),
+             ("rescale grid", lambda: f.mul_(1.0 + 1e-7)),
+             ("swap two photons", lambda: t.__setitem__(slice(1000, 1002), t[1000:1002].flip(0).clone())),
+             ("restore order", lambda: t.copy_(torch.sort(t).values)),
+             ("non-uniform grid", lambda: f.__setitem__(7, f[7] + 1e-9))]
+    for name, edit in edits:
+        run(True)                 # the plan of the current buffers is cached
+        edit()
+        got, pg = run(True)       # the stale plan: detected on the device, recomputed
+        ref, pr = run(False)
+        assert pg == pr, (name, pg, pr)
+        np.testing.assert_array_equal(got, ref, err_msg=name)
