@@ -602,6 +602,62 @@ __global__ __launch_bounds__(256) void k_nu_merge(const double* __restrict__ U, 
     }
 }
 
+// Power and error bound of one trial from its harmonic sums: CS[k * nbt + t] for k < m, except that with lastv the
+// last harmonic's sum is the register value `last` (the fused row pass, k_nu_rows4096_combine8). The same operations
+// in the same order either way, so the fused and separate finalize give identical powers and flags.
+__device__ __forceinline__ void nu_power(const double2* __restrict__ CS, int64_t nbt, int64_t t, int m, int stat,
+                                         double nph, double E, bool lastv, double2 last, double* pout,
+                                         double* eout) {
+    const double w = 2.0 / nph;
+    auto zk = [&](int k, double* amag) {
+        const double2 a = (lastv && k == m - 1) ? last : CS[(int64_t)k * nbt + t];
+        const double z = a.x * a.x + a.y * a.y;
+        *amag = sqrt(z);
+        return z;
+    };
+    double p, err;
+    if (stat == CRIMP_STAT_Z2) {
+        double zsum = 0.0, eb = 0.0, am;
+        for (int k = 0; k < m; ++k) {
+            zsum += zk(k, &am);
+            eb += 2.0 * am * E + E * E;
+        }
+        p = zsum * w;
+        err = eb * w;
+    } else {
+        double cum = 0.0, best = -INFINITY, ebest = 0.0, eacc = 0.0, am;
+        for (int k = 0; k < m; ++k) {
+            const double z = zk(k, &am);
+            cum += z * w;
+            eacc += (2.0 * am * E + E * E) * w;
+            const double v = cum - 4.0 * (double)k;
+            if (v > best) {
+                best = v;
+                ebest = eacc;
+            }
+        }
+        p = best;
+        err = ebest;
+        cum = 0.0;
+        eacc = 0.0;
+        for (int k = 0; k < m; ++k) {
+            const double z = zk(k, &am);
+            cum += z * w;
+            eacc += (2.0 * am * E + E * E) * w;
+            if (cum - 4.0 * (double)k + eacc >= best - ebest) err = fmax(err, eacc);
+        }
+    }
+    *pout = p;
+    *eout = err;
+}
+// E = N (x^P invfact + kNuRho) at trial offset jc (nu_trunc)
+__device__ __forceinline__ double nu_err_bound(int64_t jc, int64_t nfft, int P, double invfact, double nph) {
+    const double x = 3.14159265358979323846 * fabs((double)jc) / (double)nfft;
+    double xp = 1.0;
+    for (int p = 0; p < P; ++p) xp *= x;
+    return nph * (xp * invfact + kNuRho);
+}
+
 // ---- FFT: DFTs of radix 2..16 in registers (X_k = sum_j x_j w_R^{+jk}, natural order) ----
 __device__ __forceinline__ void nu_dft2(double2* v) {
     const double2 a = v[0], b = v[1];
@@ -1025,9 +1081,24 @@ __device__ __forceinline__ int nu_sw8(int i) { return i ^ ((i >> 3) & 7); }
 // Moment chunks: the launch transforms moments plo .. P-1 (X holds their planes only, beta = (p - plo) nrow + r) and,
 // with accum, adds its partial sum to the CS an earlier chunk (moments above P) wrote -- the sum over moments is
 // linear, and each chunk starts the Bessel recurrence at its own top (nu_bes_start(P)).
+// The last harmonic's launch may finalize (NuFinal.on): its sums stay in registers and each trial's power and
+// certificate are formed there from the earlier harmonics' CS (nu_power), the fix-up list appended, and the block's
+// best trial (np.argmax semantics) written to best_part for k_best_final -- no CS write, no finalize launch, no
+// reduction pass over the powers.
+struct NuFinal {
+    int on, m, stat, Pc;           // Pc: the plan's moments (the certificate), P of the launch may be a chunk's top
+    double nph, invfact, rel;
+    int64_t tb0;                   // out index of the batch's trial 0
+    double* out;
+    int* nflag;
+    int64_t* flagged;
+    BestCand* best_part;           // per-block best (nullable)
+    int64_t best_base;
+    const double2* CS0;            // harmonic 0's sums of the batch (stride nbt)
+};
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k_nu_rows4096_combine8(
     const double2* X, int lnfft, int P, int plo, int accum, int nrow, int64_t nf, int64_t jhi, int64_t h,
-    int64_t tbase, int64_t nbt, const double* __restrict__ bc, double2* __restrict__ CS) {
+    int64_t tbase, int64_t nbt, const double* __restrict__ bc, double2* __restrict__ CS, const NuFinal F) {
     extern __shared__ double2 nu_s[];  // [2][4096]
     __shared__ NuTile tw;
     nu_tile_init(&tw, 12);
@@ -1094,6 +1165,24 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
             acc[q] = nu_bes_acc(acc[q], nu_bes_w(bs[q], p, nu_zh(jc, lnfft)), v[q], p);
         }
     }
+    if (!F.on) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int64_t J = k1 + ((int64_t)(t + 512 * q) << ln1);
+            int64_t jc;
+            if (J <= jhi)
+                jc = J;
+            else if (J >= nfft - h)
+                jc = J - nfft;
+            else
+                continue;
+            const int64_t tt = tbase + r * nf + jc;
+            if (tt >= 0 && tt < nbt) CS[tt] = acc[q];
+        }
+        return;
+    }
+    // fused finalize (k_nu_finalize's arithmetic, the last harmonic from registers)
+    BestCand bc_ = {-INFINITY, INT64_MAX};
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
         const int64_t J = k1 + ((int64_t)(t + 512 * q) << ln1);
@@ -1105,7 +1194,28 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
         else
             continue;
         const int64_t tt = tbase + r * nf + jc;
-        if (tt >= 0 && tt < nbt) CS[tt] = acc[q];
+        if (tt < 0 || tt >= nbt) continue;
+        double p, err;
+        nu_power(F.CS0, nbt, tt, F.m, F.stat, F.nph, nu_err_bound(jc, nfft, F.Pc, F.invfact, F.nph), true, acc[q], &p,
+                 &err);
+        F.out[F.tb0 + tt] = p;
+        if (!(err <= F.rel * fabs(p))) F.flagged[atomicAdd(F.nflag, 1)] = F.tb0 + tt;
+        if (best_better(p, F.tb0 + tt, bc_.v, bc_.i)) bc_ = {p, F.tb0 + tt};
+    }
+    if (!F.best_part) return;
+    for (int o = 32; o > 0; o >>= 1) {
+        const double v = __shfl_xor(bc_.v, o);
+        const int64_t i = __shfl_xor(bc_.i, o);
+        if (best_better(v, i, bc_.v, bc_.i)) bc_ = {v, i};
+    }
+    __syncthreads();  // the tiles are free: the wave candidates go to LDS
+    BestCand* red = reinterpret_cast<BestCand*>(nu_s);
+    if ((t & 63) == 0) red[t >> 6] = bc_;
+    __syncthreads();
+    if (t == 0) {
+        for (int w = 1; w < 8; ++w)
+            if (best_better(red[w].v, red[w].i, bc_.v, bc_.i)) bc_ = red[w];
+        F.best_part[F.best_base + (int64_t)blockIdx.y * gridDim.x + blockIdx.x] = bc_;
     }
 }
 
@@ -1155,49 +1265,9 @@ __global__ __launch_bounds__(256) void k_nu_finalize(const double2* __restrict__
     if (t >= nbt) return;
     const int64_t flat = tb0 + t + first;
     const int64_t jc = flat % nf - jbase;
-    const double x = 3.14159265358979323846 * fabs((double)jc) / (double)nfft;
-    double xp = 1.0;
-    for (int p = 0; p < P; ++p) xp *= x;
-    const double E = nph * (xp * invfact + kNuRho);
-    const double w = 2.0 / nph;
-    auto zk = [&](int k, double* amag) {
-        const double2 a = CS[(int64_t)k * nbt + t];
-        const double z = a.x * a.x + a.y * a.y;
-        *amag = sqrt(z);
-        return z;
-    };
     double p, err;
-    if (stat == CRIMP_STAT_Z2) {
-        double zsum = 0.0, eb = 0.0, am;
-        for (int k = 0; k < m; ++k) {
-            zsum += zk(k, &am);
-            eb += 2.0 * am * E + E * E;
-        }
-        p = zsum * w;
-        err = eb * w;
-    } else {
-        double cum = 0.0, best = -INFINITY, ebest = 0.0, eacc = 0.0, am;
-        for (int k = 0; k < m; ++k) {
-            const double z = zk(k, &am);
-            cum += z * w;
-            eacc += (2.0 * am * E + E * E) * w;
-            const double v = cum - 4.0 * (double)k;
-            if (v > best) {
-                best = v;
-                ebest = eacc;
-            }
-        }
-        p = best;
-        err = ebest;
-        cum = 0.0;
-        eacc = 0.0;
-        for (int k = 0; k < m; ++k) {
-            const double z = zk(k, &am);
-            cum += z * w;
-            eacc += (2.0 * am * E + E * E) * w;
-            if (cum - 4.0 * (double)k + eacc >= best - ebest) err = fmax(err, eacc);
-        }
-    }
+    nu_power(CS, nbt, t, m, stat, nph, nu_err_bound(jc, nfft, P, invfact, nph), false, make_double2(0.0, 0.0), &p,
+             &err);
     out[tb0 + t] = p;
     if (!(err <= rel * fabs(p))) flagged[atomicAdd(nflag, 1)] = tb0 + t;
 }
@@ -1366,6 +1436,13 @@ static int nu_pchunk() {
     const char* e = getenv("CRIMP_NUFFT_PCHUNK");
     const int c = e ? atoi(e) : 0;
     return c > 0 ? c : (1 << 20);
+}
+
+// CRIMP_NUFFT_FINAL=separate: the k_nu_finalize launch after every row batch instead of the fused finalize (A/B and
+// identity test hook, read per call)
+static bool nu_final_separate() {
+    const char* e = getenv("CRIMP_NUFFT_FINAL");
+    return e && !strcmp(e, "separate");
 }
 
 static int64_t nufft_budget() {
@@ -1666,6 +1743,14 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
     HIPCHK(sc.alloc(&Y, (size_t)Bmax));
     HIPCHK(sc.alloc(&CS, (size_t)csmax));
     HIPCHK(sc.alloc(&flagged, (size_t)count));
+    // per-block best trials of the fused finalize (k_nu_rows4096_combine8 blocks of every row batch)
+    BestCand* best_part = nullptr;
+    int64_t best_count = 0, separate_batches = 0;
+    if (best) {
+        int64_t nb = 0;
+        for (const NuPlan& pl : plans) nb += (pl.r1 - pl.r0) * (int64_t(1) << std::max(0, pl.lnfft - 12));
+        HIPCHK(sc.alloc(&best_part, (size_t)std::max<int64_t>(nb, 1)));
+    }
     // every MFMA (group, row batch, pass)'s slot table, uploaded once before the launches
     std::vector<NuPass> hps;
     for (const NuPlan& pl : plans) {
@@ -1732,6 +1817,9 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
         auto occupied = [&](int k, int* alo, int* acnt) {
             nu_occupied(pl.gmin[(size_t)(k - 1)], pl.gmax[(size_t)(k - 1)], lnfft, ln1, alo, acnt);
         };
+        // fused finalize: the last harmonic's row pass forms the powers (NuFinal), for the 4096-row radix-8 path
+        const bool fuse_final = fused_combine && ln2 == 12 && rows4096 && rows_r8 && !nu_final_separate();
+        bool final_done = false;  // set by fft_combine when it finalized the batch
         auto fft_combine = [&](int k, int64_t rb, int nrow, int64_t tb0, int64_t nbt, double2* W) -> int {
             const int64_t Bp = (int64_t)P * nrow;
             const double plane = 16.0 * (double)Bp * (double)nfft;  // one complex FFT buffer of the batch
@@ -1760,11 +1848,33 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
                         Zo = Y;
                         HIPCHK(span(kNuClsPass1));
                     }
-                    g_nu_work[kNuClsPass2] += cplane + 16.0 * (double)nbt * (phi < P ? 2.0 : 1.0);
+                    NuFinal F{};
+                    if (fuse_final && k == nharm && plo == 0) {
+                        F.on = 1;
+                        F.m = nharm;
+                        F.stat = stat;
+                        F.Pc = P;
+                        F.nph = (double)n;
+                        F.invfact = pl.invfact;
+                        F.rel = fixup_rel();
+                        F.tb0 = tb0;
+                        F.out = out;
+                        F.nflag = nflag;
+                        F.flagged = flagged;
+                        F.best_part = best ? best_part : nullptr;
+                        F.best_base = best_count;
+                        F.CS0 = CS;
+                        best_count += (int64_t(1) << ln1) * nrow;
+                        final_done = true;
+                    }
+                    // bytes: the chunk's planes; CS read by a later chunk and written, or (fused finalize) the
+                    // earlier harmonics' sums read and the powers written
+                    g_nu_work[kNuClsPass2] += cplane + (F.on ? (16.0 * (nharm - 1) + 8.0) * (double)nbt
+                                                             : 16.0 * (double)nbt * (phi < P ? 2.0 : 1.0));
                     k_nu_rows4096_combine8<<<dim3((unsigned)(int64_t(1) << ln1), (unsigned)nrow), 512, 2 * lds_fft,
                                              s>>>(Zo, lnfft, phi, plo, phi < P ? 1 : 0, nrow, nf, pl.nseg - 1 - pl.h,
                                                   pl.h, rb * nf + jbase - (tb0 + first), nbt, bc,
-                                                  CS + (int64_t)(k - 1) * nbt);
+                                                  CS + (int64_t)(k - 1) * nbt, F);
                     HIPCHK(hipGetLastError());
                     HIPCHK(span(kNuClsPass2));
                 }
@@ -1902,6 +2012,11 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
                         if (rc) return rc;
                     }
                 }
+                if (final_done) {
+                    final_done = false;
+                    continue;
+                }
+                ++separate_batches;
                 int rc = finalize(tb0, nbt);
                 if (rc) return rc;
             }
@@ -1948,6 +2063,11 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
                     if (rc) return rc;
                 }
             }
+            if (final_done) {
+                final_done = false;
+                continue;
+            }
+            ++separate_batches;
             int rc = finalize(tb0, nbt);
             if (rc) return rc;
         }
@@ -1972,8 +2092,13 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
     }
     // the best trial of the powers (crimp_search_best) rides on the same read-back; valid unless a fix-up follows
     if (best) {
-        const int rc = launch_best(sc, s, out, count, reinterpret_cast<double*>(nflag + 4));
-        if (rc) return rc;
+        if (separate_batches == 0 && best_count > 0) {  // every batch finalized in its row pass: reduce their blocks
+            k_best_final<<<1, 256, 0, s>>>(best_part, (int)best_count, reinterpret_cast<double*>(nflag + 4));
+            HIPCHK(hipGetLastError());
+        } else {
+            const int rc = launch_best(sc, s, out, count, reinterpret_cast<double*>(nflag + 4));
+            if (rc) return rc;
+        }
     }
     int fl[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     HIPCHK(d2h(s, fl, nflag, (best ? 8 : 2) * sizeof(int)));

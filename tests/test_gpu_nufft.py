@@ -330,3 +330,50 @@ def test_nufft_plan_cache_revalidated_on_device(gpu, rows, monkeypatch):
         ref, pr = run(False)
         assert pg == pr, (name, pg, pr)
         np.testing.assert_array_equal(got, ref, err_msg=name)
+
+
+def test_nufft_fused_finalize_identical(gpu, monkeypatch):
+    """The last harmonic's row pass forms the powers, certificate and per-block best trials itself (NuFinal); the
+    separate k_nu_finalize launch (CRIMP_NUFFT_FINAL=separate) gives the same powers bit for bit, the same fix-up count
+    and the same best trial -- Z^2 and H, 1-D (cell gather) and 3-row 2-D (MFMA slots) grids, a forced fix-up of many
+    trials included (CRIMP_FIXUP_REL in a child process)."""
+    import os
+    import subprocess
+    import sys
+    import tempfile
+    from crimp_amd import ops, _native as N
+    from crimp_amd.synth import pulsed_events
+    from conftest import ROOT
+    t = pulsed_events(300_000, 2.0e5, 3.3, pulsed_frac=0.05, fdot=-2e-11, seed=21)
+    t0 = (t[0] + t[-1]) / 2
+    for f, m, stat, fdv in ((3.3 + np.arange(-300000, 300000) / 2.0e7, 2, 0, None),
+                            (3.3 + np.arange(-300000, 300000) / 2.0e7, 5, 1, None),
+                            (3.3 + np.arange(-40000, 40000) / 2.0e6, 3, 1, np.array([-12.0, -11.0, -10.5]))):
+        res = {}
+        for mode in ("fused", "separate"):
+            if mode == "separate":
+                monkeypatch.setenv("CRIMP_NUFFT_FINAL", "separate")
+            else:
+                monkeypatch.delenv("CRIMP_NUFFT_FINAL", raising=False)
+            z, bv, bi = ops.search_best(t, t0, f, m, stat, log10_negfdot=fdv)
+            res[mode] = (z, bv, bi, N.load().crimp_last_fixups(), _path())
+        a, b = res["fused"], res["separate"]
+        np.testing.assert_array_equal(a[0], b[0])
+        assert a[1:] == b[1:] and a[4] == 2
+        assert a[2] == int(np.argmax(a[0])) and a[1] == a[0].max()
+    code = ("import sys, os, numpy as np; sys.path.insert(0, %r); from crimp_amd import ops, _native as N; "
+            "from crimp_amd.synth import pulsed_events; t = pulsed_events(300000, 2.0e5, 3.3, pulsed_frac=0.05, "
+            "seed=21); f = 3.3 + np.arange(-300000, 300000) / 2.0e7; t0 = (t[0] + t[-1]) / 2; out = {}\\n"
+            "for mode in ('fused', 'separate'):\\n"
+            "    os.environ['CRIMP_NUFFT_FINAL'] = mode\\n"
+            "    z, bv, bi = ops.search_best(t, t0, f, 3, 1); out[mode] = (z, bv, bi, N.load().crimp_last_fixups())\\n"
+            "np.savez(sys.argv[1], za=out['fused'][0], zb=out['separate'][0], "
+            "ma=np.array(out['fused'][1:]), mb=np.array(out['separate'][1:]))") % ROOT
+    with tempfile.TemporaryDirectory() as d:
+        outp = os.path.join(d, "f.npz")
+        subprocess.run([sys.executable, "-c", code, outp], check=True, timeout=300,
+                       env=dict(os.environ, CRIMP_FIXUP_REL="1e-9"))
+        r = np.load(outp)
+    np.testing.assert_array_equal(r["za"], r["zb"])
+    np.testing.assert_array_equal(r["ma"], r["mb"])
+    assert r["ma"][2] > 100  # fix-ups ran (the best trial was then recomputed after them)

@@ -45,10 +45,12 @@ def raw():
                            None, 0, 2, 0, 0, out.numel(), ctypes.c_void_p(out.data_ptr()), N.FLAG_DEVICE_PTRS, stream))
 
 
+ARGS = (ctypes.c_void_p(t.data_ptr()), t.numel(), t0, ctypes.c_void_p(f.data_ptr()), f.numel(), None, 0, 2, 0, 0,
+        out.numel(), ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(res.ctypes.data), N.FLAG_DEVICE_PTRS, stream)
+
+
 def raw_best():
-    N.check(L.crimp_search_best(ctypes.c_void_p(t.data_ptr()), t.numel(), t0, ctypes.c_void_p(f.data_ptr()),
-                                f.numel(), None, 0, 2, 0, 0, out.numel(), ctypes.c_void_p(out.data_ptr()),
-                                ctypes.c_void_p(res.ctypes.data), N.FLAG_DEVICE_PTRS, stream))
+    N.check(L.crimp_search_best(*ARGS))
 
 
 rows = [("ops.search out=given", lambda: ops.search(t, t0, f, 2, 0, out=out)),
@@ -58,6 +60,8 @@ rows = [("ops.search out=given", lambda: ops.search(t, t0, f, 2, 0, out=out)),
         ("ops.search + ops.best", lambda: (ops.search(t, t0, f, 2, 0, out=out), ops.best(out))),
         ("ops.search_best", lambda: ops.search_best(t, t0, f, 2, 0, out=out)),
         ("sharded_search best (bench step)", lambda: sharded_search(t, f, 2, 0, gather="best", t0=t0)),
+        ("raw best, plan cache off", lambda: (os.environ.__setitem__("CRIMP_NUFFT_PLAN_CACHE", "0"), raw_best(),
+                                              os.environ.pop("CRIMP_NUFFT_PLAN_CACHE"))),
         ("ops.best alone", lambda: ops.best(out))]
 for name, fn in rows:
     print("%-34s %.3f ms" % (name, tm(fn)), flush=True)
