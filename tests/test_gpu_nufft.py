@@ -363,10 +363,10 @@ def test_nufft_fused_finalize_identical(gpu, monkeypatch):
         assert a[2] == int(np.argmax(a[0])) and a[1] == a[0].max()
     code = ("import sys, os, numpy as np; sys.path.insert(0, %r); from crimp_amd import ops, _native as N; "
             "from crimp_amd.synth import pulsed_events; t = pulsed_events(300000, 2.0e5, 3.3, pulsed_frac=0.05, "
-            "seed=21); f = 3.3 + np.arange(-300000, 300000) / 2.0e7; t0 = (t[0] + t[-1]) / 2; out = {}\\n"
-            "for mode in ('fused', 'separate'):\\n"
-            "    os.environ['CRIMP_NUFFT_FINAL'] = mode\\n"
-            "    z, bv, bi = ops.search_best(t, t0, f, 3, 1); out[mode] = (z, bv, bi, N.load().crimp_last_fixups())\\n"
+            "seed=21); f = 3.3 + np.arange(-300000, 300000) / 2.0e7; t0 = (t[0] + t[-1]) / 2; out = {}\n"
+            "for mode in ('fused', 'separate'):\n"
+            "    os.environ['CRIMP_NUFFT_FINAL'] = mode\n"
+            "    z, bv, bi = ops.search_best(t, t0, f, 3, 1); out[mode] = (z, bv, bi, N.load().crimp_last_fixups())\n"
             "np.savez(sys.argv[1], za=out['fused'][0], zb=out['separate'][0], "
             "ma=np.array(out['fused'][1:]), mb=np.array(out['separate'][1:]))") % ROOT
     with tempfile.TemporaryDirectory() as d:
