@@ -62,6 +62,8 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--settle", type=float, default=0.3,
+                   help="seconds of untimed steps before the warmup steps (GPU clocks back at steady state)")
     p.add_argument("--photons", type=int, default=10_000_000)
     p.add_argument("--trials", type=int, default=1_000_000, help="trial frequencies per GPU")
     p.add_argument("--nharm", type=int, default=2)
@@ -691,6 +693,14 @@ def main():
         def step():
             return sharded_search(t, f, a.nharm, 0, gather="best", flags=flags, precision=precision, t0=t0_h)
 
+        # clock settle (untimed): the step repeated for a.settle seconds before the W warmup steps -- after the
+        # seconds of host-side setup the GPU's clocks have dropped, and a short timed window would measure the
+        # ramp, not the steady state a search service runs at (20 steps after 3 warmups: 0.49 vs 0.43-0.44 ms per
+        # step in a loop that had run for a while, profiles/r06/clock_settle.log)
+        t_s = time.perf_counter()
+        while time.perf_counter() - t_s < a.settle:
+            step()
+            torch.cuda.synchronize()
         for _ in range(warmup):
             step()
         torch.cuda.synchronize()
