@@ -755,29 +755,6 @@ __device__ __forceinline__ void nu_twiddle(double2 w, double2* v) {
     }
 }
 
-// the products w^r (r = 1 .. R-1) exactly as nu_twiddle forms them (so a stage multiplied by a table of them is
-// bit-identical to one that forms them per use)
-template <int R>
-__device__ __forceinline__ void nu_twiddle_powers(double2 w, double2* out) {
-    double2 b[4];
-    b[0] = w;
-#pragma unroll
-    for (int i = 1; i < 4; ++i)
-        if ((1 << i) < R) b[i] = nu_cmul(b[i - 1], b[i - 1]);
-#pragma unroll
-    for (int r = 1; r < R; ++r) {
-        double2 wr = make_double2(1.0, 0.0);
-        bool first = true;
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-            if (r & (1 << i)) {
-                wr = first ? b[i] : nu_cmul(wr, b[i]);
-                first = false;
-            }
-        out[r] = wr;
-    }
-}
-
 // One Stockham autosort stage of radix R over 2^lc transforms of length 2^ll held in LDS at s[a*sa + cc*sc]:
 // butterfly (j, cc) reads x[j + r L/R], twiddles by w_{Ns R}^{(j mod Ns) r}, and writes
 // y[(j / Ns) Ns R + (j mod Ns) + r Ns]. 16 / R butterflies per thread (a tile holds <= 16 elements per thread).
@@ -1124,10 +1101,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
     int64_t tbase, int64_t nbt, const double* __restrict__ bc, double2* __restrict__ CS, const NuFinal F) {
     extern __shared__ double2 nu_s[];  // [2][4096]
     __shared__ NuTile tw;
-    // stage 2 and 3 twiddles w^r of the 8 and 64 distinct thread classes (t & 7, t & 63), formed once per block:
-    // the per-moment bit products of nu_twiddle were a third of the pass's VALU work (stage 4's 512 classes stay
-    // per use)
-    __shared__ double2 T2[8][8], T3[64][8];
     nu_tile_init(&tw, 12);
     const int64_t nfft = int64_t(1) << lnfft;
     const int ln1 = lnfft - 12;
@@ -1150,14 +1123,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
         bs[q] = nu_bes_start(bc, P, nu_zh(J <= jhi ? J : J - nfft, lnfft));
         nx[q] = xr[(int64_t)(P - 1 - plo) * pstride + t + 512 * q];
     }
-    const int m4 = t;  // stage 4 twiddle in units of w_4096 (stages 2, 3: the tables)
+    const int m2 = (t & 7) << 6, m3 = (t & 63) << 3, m4 = t;  // stage twiddles in units of w_4096
     const int z2 = ((t >> 3) << 6) + (t & 7), z3 = ((t >> 6) << 9) + (t & 63);  // stage 2 / 3 output bases
     __syncthreads();                                                             // tw
-    if (t < 8) nu_twiddle_powers<8>(nu_tw_tile(&tw, t << 6), T2[t]);
-    else if (t >= 64 && t < 128) nu_twiddle_powers<8>(nu_tw_tile(&tw, (t - 64) << 3), T3[t - 64]);
-    __syncthreads();  // T2, T3
-    const double2* w2 = T2[t & 7];
-    const double2* w3 = T3[t & 63];
     int par = 0;
     for (int p = P - 1; p >= plo; --p, par ^= 1) {
         double2* A = nu_s + (par ? 4096 : 0);
@@ -1174,16 +1142,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
         __syncthreads();
 #pragma unroll
         for (int q = 0; q < 8; ++q) v[q] = A[nu_sw8(t + 512 * q)];
-#pragma unroll
-        for (int q = 1; q < 8; ++q) v[q] = nu_cmul(v[q], w2[q]);
+        nu_twiddle<8>(nu_tw_tile(&tw, m2), v);
         nu_dft8(v);  // stage 2 (Ns = 8)
 #pragma unroll
         for (int q = 0; q < 8; ++q) B[nu_sw8(z2 + 8 * q)] = v[q];
         __syncthreads();
 #pragma unroll
         for (int q = 0; q < 8; ++q) v[q] = B[nu_sw8(t + 512 * q)];
-#pragma unroll
-        for (int q = 1; q < 8; ++q) v[q] = nu_cmul(v[q], w3[q]);
+        nu_twiddle<8>(nu_tw_tile(&tw, m3), v);
         nu_dft8(v);  // stage 3 (Ns = 64)
 #pragma unroll
         for (int q = 0; q < 8; ++q) A[nu_sw8(z3 + 64 * q)] = v[q];
