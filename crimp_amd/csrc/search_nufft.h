@@ -195,6 +195,28 @@ __device__ __forceinline__ double nu_cheb(double u, int p) {
     return a;
 }
 
+// T_p(x) = x^(p & 1) Q_p(x^2) with Q_p's monomial coefficients (exact integers), p < 16: the MFMA spread's lane
+// evaluates its own T_p by a degree-7 Horner in y = x^2 (9 fp64 operations; the doubling ladder nu_cheb took ~30
+// plus selects). |x| <= 1, so the rounding is at most ~sum |c| ulp: 2e-11 absolute for T_15, whose weight in the
+// combine is |2 J_15(pi/2)| < 3e-14 (nu_bes); ~1e-15 for the p <= 4 moments that carry the sums.
+__constant__ double kNuChebMono[16][8] = {
+    {1.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0},
+    {1.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0},
+    {-1.0, 2.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0},
+    {-3.0, 4.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0},
+    {1.0, -8.0, 8.0, 0.0, 0.0, 0.0, 0.0, 0.0},
+    {5.0, -20.0, 16.0, 0.0, 0.0, 0.0, 0.0, 0.0},
+    {-1.0, 18.0, -48.0, 32.0, 0.0, 0.0, 0.0, 0.0},
+    {-7.0, 56.0, -112.0, 64.0, 0.0, 0.0, 0.0, 0.0},
+    {1.0, -32.0, 160.0, -256.0, 128.0, 0.0, 0.0, 0.0},
+    {9.0, -120.0, 432.0, -576.0, 256.0, 0.0, 0.0, 0.0},
+    {-1.0, 50.0, -400.0, 1120.0, -1280.0, 512.0, 0.0, 0.0},
+    {-11.0, 220.0, -1232.0, 2816.0, -2816.0, 1024.0, 0.0, 0.0},
+    {1.0, -72.0, 840.0, -3584.0, 6912.0, -6144.0, 2048.0, 0.0},
+    {13.0, -364.0, 2912.0, -9984.0, 16640.0, -13312.0, 4096.0, 0.0},
+    {-1.0, 98.0, -1568.0, 9408.0, -26880.0, 39424.0, -28672.0, 8192.0},
+    {-15.0, 560.0, -6048.0, 28800.0, -70400.0, 92160.0, -61440.0, 16384.0}};
+
 __device__ __forceinline__ int64_t nu_readlane64(int64_t v, int lane) {
     const int lo = __builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)v, lane);
     const int hi = __builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), lane);
@@ -229,6 +251,10 @@ __global__ __launch_bounds__(256) void k_nu_spread(const double* __restrict__ tt
     const int q = lane >> 4, col = lane & 15, prow = col >> 1, reim = col & 1, pp = lane & 15;
     const bool rowok = prow < nrow, pok = pp < P;
     const double c2 = (TWOD && rowok) ? c2row[prow] : 0.0;
+    double cm[8];  // this lane's T_pp in monomials of (2e)^2 (kNuChebMono)
+#pragma unroll
+    for (int m = 0; m < 8; ++m) cm[m] = kNuChebMono[pp][m];
+    const bool odd = pp & 1;
     const int64_t i0 = c * kNuCW, i1 = i0 + kNuCW < n ? i0 + kNuCW : n;
     const int64_t SL = 2 * (int64_t)P * nrow;  // doubles per slot: [p][row][re, im]
     nu_f64x4 acc[G];
@@ -293,7 +319,11 @@ __global__ __launch_bounds__(256) void k_nu_spread(const double* __restrict__ tt
                 const double uk = (double)(k0 + kk) * u1;
                 const double gk = rint(uk);
                 const double e = uk - gk;
-                double a = nu_cheb(2.0 * e, pp);  // T_p(2e) (nu_bes)
+                const double x = 2.0 * e, y = x * x;  // T_p(2e) (nu_bes) by Horner in y
+                double a = cm[7];
+#pragma unroll
+                for (int m = 6; m >= 0; --m) a = fma(a, y, cm[m]);
+                if (odd) a *= x;
                 a = (valid && pok) ? a : 0.0;
                 const double b = (valid && rowok) ? (reim ? ck.y : ck.x) : 0.0;
                 const int64_t G64 = (int)gk;  // cells fit 32 bits (k_nu_cellstart)
