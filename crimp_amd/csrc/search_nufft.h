@@ -251,25 +251,26 @@ __global__ __launch_bounds__(256) void k_nu_spread(const double* __restrict__ tt
     const int q = lane >> 4, col = lane & 15, prow = col >> 1, reim = col & 1, pp = lane & 15;
     const bool rowok = prow < nrow, pok = pp < P;
     const double c2 = (TWOD && rowok) ? c2row[prow] : 0.0;
-    double cm[8];  // this lane's T_pp in monomials of (2e)^2 (kNuChebMono)
+    double cm[8];  // this lane's T_pp in monomials of (2e)^2 (kNuChebMono); rows p >= P of D are never stored
 #pragma unroll
     for (int m = 0; m < 8; ++m) cm[m] = kNuChebMono[pp][m];
     const bool odd = pp & 1;
+    (void)pok;
     const int64_t i0 = c * kNuCW, i1 = i0 + kNuCW < n ? i0 + kNuCW : n;
     const int64_t SL = 2 * (int64_t)P * nrow;  // doubles per slot: [p][row][re, im]
     nu_f64x4 acc[G];
-    int64_t gcur[G];
+    int gcur[G];  // cells fit 32 bits (nu_plan: |G| + n < 2^31)
     {
         const double u1 = (tt[i0] - t0) * s1;
 #pragma unroll
         for (int kk = 0; kk < G; ++kk) {
             acc[kk] = nu_f64x4{0.0, 0.0, 0.0, 0.0};
-            gcur[kk] = (int)rint((double)(k0 + kk) * u1);  // cells fit 32 bits (k_nu_cellstart)
+            gcur[kk] = (int)rint((double)(k0 + kk) * u1);
             if (lane == 0) ctab[(kk * nchunk + c) * 2] = gcur[kk];  // the chunk's first cell
         }
     }
     auto flush = [&](int kk) {
-        const int64_t slot = gcur[kk] - ps->gmin[kk] + c;
+        const int64_t slot = (int64_t)gcur[kk] - ps->gmin[kk] + c;
         double* const base = U + ps->ubase[kk] + slot * SL;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -312,10 +313,15 @@ __global__ __launch_bounds__(256) void k_nu_spread(const double* __restrict__ tt
             const double2 c1 = nu_cis(stab, phi);
             double2 ck = c1;
             if (k0 > 1) ck = nu_cis(stab, nu_frac_k((double)k0, phi));
+            // this lane's B column as the real part of cl: c for re lanes, (-i) c for im lanes; zero for a photon
+            // past the chunk's end or a row beyond the pass (products by c1 keep it zero, and A needs no mask:
+            // its rows p >= P are never stored). One select per K-group instead of per harmonic.
+            double2 cl = reim ? make_double2(ck.y, -ck.x) : ck;
+            if (!(valid && rowok)) cl = make_double2(0.0, 0.0);
             const double u1 = d * s1;
 #pragma unroll
             for (int kk = 0; kk < G; ++kk) {
-                if (kk > 0) ck = nu_cmul(ck, c1);
+                if (kk > 0) cl = nu_cmul(cl, c1);
                 const double uk = (double)(k0 + kk) * u1;
                 const double gk = rint(uk);
                 const double e = uk - gk;
@@ -324,23 +330,22 @@ __global__ __launch_bounds__(256) void k_nu_spread(const double* __restrict__ tt
 #pragma unroll
                 for (int m = 6; m >= 0; --m) a = fma(a, y, cm[m]);
                 if (odd) a *= x;
-                a = (valid && pok) ? a : 0.0;
-                const double b = (valid && rowok) ? (reim ? ck.y : ck.x) : 0.0;
-                const int64_t G64 = (int)gk;  // cells fit 32 bits (k_nu_cellstart)
-                const int64_t g0 = nu_readlane64(G64, 0), g3 = nu_readlane64(G64, 48);
+                const double b = cl.x;
+                const int G32 = (int)gk;  // 32-bit cells and read-lanes
+                const int g0 = __builtin_amdgcn_readlane(G32, 0), g3 = __builtin_amdgcn_readlane(G32, 48);
                 if (g0 == gcur[kk] && g3 == gcur[kk]) {
                     acc[kk] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[kk], 0, 0, 0);
                 } else {
                     // the K-group crosses cells: photons of the current cell first, then each later cell in turn
-                    const int64_t g1 = nu_readlane64(G64, 16), g2 = nu_readlane64(G64, 32);
+                    const int g1 = __builtin_amdgcn_readlane(G32, 16), g2 = __builtin_amdgcn_readlane(G32, 32);
                     for (;;) {
                         if (g0 <= gcur[kk]) {
-                            const double am = (G64 == gcur[kk]) ? a : 0.0;
+                            const double am = (G32 == gcur[kk]) ? a : 0.0;
                             acc[kk] = __builtin_amdgcn_mfma_f64_16x16x4f64(am, b, acc[kk], 0, 0, 0);
                         }
                         if (g3 == gcur[kk]) break;
                         flush(kk);
-                        const int64_t nx = g0 > gcur[kk] ? g0 : g1 > gcur[kk] ? g1 : g2 > gcur[kk] ? g2 : g3;
+                        const int nx = g0 > gcur[kk] ? g0 : g1 > gcur[kk] ? g1 : g2 > gcur[kk] ? g2 : g3;
                         if (nx > gcur[kk] + 1) zero_gap(kk, gcur[kk], nx);
                         gcur[kk] = nx;
                     }
