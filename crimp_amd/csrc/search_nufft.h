@@ -49,9 +49,10 @@ constexpr double kNuEps = 5e-14;   // truncation bound per photon at the grid's 
 // < 4e-14 N; kept at 1e-13 N.
 constexpr double kNuRho = 1e-13;
 
+constexpr int kNuPassMax = 10;  // harmonics per MFMA spread pass (k_nu_spread<G>, G <= 10)
 struct NuPass {          // one spread pass: the slot array of each harmonic k0 + kk
-    int64_t gmin[8];     // unwrapped cell of dt[0]
-    int64_t ubase[8];    // offset (doubles) of the harmonic's slots in U
+    int64_t gmin[kNuPassMax];   // unwrapped cell of dt[0]
+    int64_t ubase[kNuPassMax];  // offset (doubles) of the harmonic's slots in U
 };
 
 struct NuTw {            // w_n^t = hi[t >> lbits] * lo[t & (2^lbits - 1)], t in [0, n)
@@ -1423,7 +1424,8 @@ static void nu_launch_spread(int G, dim3 grid, hipStream_t s, const double* tt, 
                              const double2* tab, double* U, int64_t* ctab, const int* bad) {
 #define CRIMP_NS(GG) \
     k_nu_spread<GG, TWOD><<<grid, 256, 0, s>>>(tt, t0, n, nchunk, s1, fch, fcl, c2, nrow, k0, P, ps, tab, U, ctab, bad)
-    if (G == 8) CRIMP_NS(8); else if (G == 4) CRIMP_NS(4); else CRIMP_NS(2);
+    if (G == 10) CRIMP_NS(10); else if (G == 8) CRIMP_NS(8); else if (G == 6) CRIMP_NS(6); else if (G == 4) CRIMP_NS(4);
+    else CRIMP_NS(2);
 #undef CRIMP_NS
 }
 
@@ -1703,12 +1705,21 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
     const int64_t fixed_bytes = (gw + 1) * Bmax * 16 + csmax * 16;
     std::vector<std::pair<int, int>> passes;  // (k0, harmonics) of each spread pass, harmonics a power of two
     int64_t ubytes = 0;
-    for (int G = 8;; G /= 2) {  // G >= 2
+    // harmonics per MFMA spread pass: the largest size in {10, 8, 6, 4, 2} (<= Gmax) the remaining harmonics fill,
+    // allowing one past nharm (its cells are planned, nu_plan(nharm + 1)): H_20 runs as 10 + 10 (two photon passes;
+    // 8 + 8 + 4 paid the per-photon phase and cis three times)
+    for (int Gmax = 10;; Gmax = Gmax == 10 ? 8 : Gmax / 2) {  // Gmax >= 2
+        const int G = Gmax;
         passes.clear();
         ubytes = 0;
         for (int k0 = 1; k0 <= nharm;) {
-            const int g = std::min(G, nharm - k0 + 1);
-            const int gl = g >= 8 ? 8 : g >= 4 ? 4 : 2;  // (a single last harmonic rides with the one past nharm)
+            const int rem = nharm - k0 + 1;
+            int gl = 2;
+            for (int cand : {10, 8, 6, 4, 2})
+                if (cand <= G && cand <= rem + 1) {
+                    gl = cand;
+                    break;
+                }
             for (const NuPlan& pl : plans) {
                 const int64_t SLmax = 2 * (int64_t)pl.P * std::min<int64_t>(kNuRows, pl.r1 - pl.r0);
                 int64_t sl = 0;
@@ -1771,7 +1782,7 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
     // best power, best index (as doubles)], zeroed or set by k_ap_final, read back in one transfer at the end
     if (any_mfma) {
         HIPCHK(sc.alloc(&U, (size_t)(ubytes / 8)));
-        HIPCHK(sc.alloc(&ctab, (size_t)(2 * 8 * nchunk)));
+        HIPCHK(sc.alloc(&ctab, (size_t)(2 * kNuPassMax * nchunk)));
     }
     if (starts_max > 0) HIPCHK(sc.alloc(&cstart, (size_t)starts_max));
     HIPCHK(sc.alloc(&W, (size_t)(Bmax * gw)));
