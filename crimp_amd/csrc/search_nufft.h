@@ -378,14 +378,14 @@ struct NuCellArgs {
 // second one (a shuffle; lane 0 loads it). One 8-byte load per iteration ran at ~2 TB/s, and one pair per thread
 // over a grid covering the photons (19.5k short blocks at config 3) was bound by the workgroup dispatch: 35-43 us per
 // 80 MB either way.
-// A block that finds a pair out of order among its photons of a sweep writes nothing for them: on sorted photons
-// every block is clean and the tables complete; on unsorted ones the search is discarded anyway (*bad), and a
-// skipped block cannot run a long write loop for a backward-then-forward jump (the gathers never read the tables).
+// A wave that finds a pair out of order among its photons of a sweep writes nothing for them: on sorted photons
+// every wave is clean and the tables complete; on unsorted ones the search is discarded anyway (*bad), and a
+// skipped wave cannot run a long write loop for a backward-then-forward jump (the gathers never read the tables).
 constexpr int kNuCellU = 4;
 template <bool VEC>
 __global__ __launch_bounds__(256) void k_nu_cellstart(const double* __restrict__ tt, double t0, int64_t n, double s1,
                                                       int k0, int nk, NuCellArgs a, int64_t* __restrict__ start,
-                                                      int* __restrict__ bad) {
+                                                      int* __restrict__ bad, int mode) {
     if (*bad) return;  // a cached plan that no longer holds (k_ap_final): no table is written
     const int64_t npair = (n + 1) / 2, stride = (int64_t)gridDim.x * blockDim.x;
     const int lane = threadIdx.x & 63;
@@ -404,7 +404,8 @@ __global__ __launch_bounds__(256) void k_nu_cellstart(const double* __restrict__
                 x0[q] = tt[i0 < n ? i0 : n - 1];
                 x1[q] = tt[i0 + 1 < n ? i0 + 1 : n - 1];
             }
-            xl[q] = tt[i0 > 0 && i0 - 1 < n ? i0 - 1 : 0];  // lane 0's predecessor (others: an L1 hit, unused)
+            xl[q] = 0.0;
+            if (lane == 0) xl[q] = tt[i0 > 0 && i0 - 1 < n ? i0 - 1 : 0];  // the wave's first predecessor
         }
 #pragma unroll
         for (int q = 0; q < kNuCellU; ++q) {
@@ -416,7 +417,10 @@ __global__ __launch_bounds__(256) void k_nu_cellstart(const double* __restrict__
             const bool v0 = i0 < n, v1 = i0 + 1 < n;
             const int ooo = (v0 && !(dp0 <= d0)) || (v1 && !(d0 <= d1));
             b |= ooo;
-            if (__syncthreads_or(ooo)) continue;
+            if (mode == 1) continue;  // A/B probe: loads and order check only (the search is then discarded)
+            // a wave that holds a pair out of order writes nothing for its photons (a vote, no block barrier: the
+            // barrier cost a quarter of the pass; mode 2, A/B: the lanes' own pairs only)
+            if (mode == 2 ? ooo : __any(ooo)) continue;
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const int64_t i = i0 + h;
@@ -440,6 +444,7 @@ __global__ __launch_bounds__(256) void k_nu_cellstart(const double* __restrict__
         }
     }
     if (__any(b) && lane == 0) atomicOr(bad, 1);
+    if (mode == 1 && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(bad, 1);  // the probe's tables are not written
 }
 
 // L lanes per wrapped cell g sum, over its unwrapped cells G = g (mod n) and their photons in time order (lane s
@@ -2000,10 +2005,14 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
                     off += ca.span[j] + 1;
                 }
                 const unsigned cb = (unsigned)std::min<int64_t>(cdiv(cdiv(n, 2), 256 * kNuCellU), 2048);
+                // CRIMP_NUFFT_CS_MODE (A/B probe of the pass's cost): 1 = loads and order check only (the search is
+                // discarded), 2 = no block barrier; 0 = the pass
+                const char* csm = getenv("CRIMP_NUFFT_CS_MODE");
+                const int cs_mode = csm ? atoi(csm) : 0;
                 if ((reinterpret_cast<uintptr_t>(t) & 15u) == 0)
-                    k_nu_cellstart<true><<<cb, 256, 0, s>>>(t, t0, n, pl.s1, k0, nk, ca, cstart, nflag + 1);
+                    k_nu_cellstart<true><<<cb, 256, 0, s>>>(t, t0, n, pl.s1, k0, nk, ca, cstart, nflag + 1, cs_mode);
                 else
-                    k_nu_cellstart<false><<<cb, 256, 0, s>>>(t, t0, n, pl.s1, k0, nk, ca, cstart, nflag + 1);
+                    k_nu_cellstart<false><<<cb, 256, 0, s>>>(t, t0, n, pl.s1, k0, nk, ca, cstart, nflag + 1, cs_mode);
                 HIPCHK(hipGetLastError());
             }
             HIPCHK(span(kNuClsCellStart));
