@@ -51,7 +51,7 @@ PEAK_VALU_SLOTS = 256 * 4 * 32 * 2.4e9   # fp32 lane-ops/s: 256 CUs x 4 SIMD-32 
 PEAK_F64_OPS = 256 * 64 * 2.4e9          # fp64 FMA-rate lane-ops/s: half the fp32 rate (78.6 TFLOP/s fp64 vector)
 PEAK_F16_TFLOPS = 2500.0                 # MI355X_MICROARCH.md: dense F16/BF16 MFMA ~2.5 PFLOP/s
 PMC_FILE = os.path.join(ROOT, "profiles", "r04", "pmc_traffic.json")
-PMC_NUFFT_FILE = os.path.join(ROOT, "profiles", "r05", "pmc_nufft_traffic.json")
+PMC_NUFFT_FILE = os.path.join(ROOT, "profiles", "r06", "pmc_nufft_traffic.json")
 # the kernel behind each NUFFT class on the config-3 plan (cell gather, n1 = 256 columns, 4096-element rows)
 NUFFT_CLASS_KERNEL = {"cellstart": "k_nu_cellstart", "spread": "k_nu_gather", "pass1": "k_nu_cols256",
                       "pass2": "k_nu_rows4096_combine8", "finalize": "k_nu_finalize"}
@@ -553,7 +553,8 @@ def nufft_leg(a, t, t_h, f, rank, M, steps):
       pass1    HBM: the FFT's column pass reading the occupied rows and writing all (k_nu_cols256 / k_nu_fft_cols);
       pass2    HBM: the row pass fused with the Horner sum over moments, reading all and writing one complex sum per
                trial and harmonic (k_nu_rows4096_combine / k_nu_fft_rows_combine);
-      finalize HBM: the harmonic sums read, the powers written (k_nu_finalize).
+      finalize HBM: the harmonic sums read, the powers written (k_nu_finalize; absent when the last harmonic's
+               pass 2 finalizes, the default, whose extra bytes pass2 then counts).
     The cell starts (k_nu_cellstart) are timed but not priced."""
     import torch
     from crimp_amd import ops
@@ -575,7 +576,7 @@ def nufft_leg(a, t, t_h, f, rank, M, steps):
     nfix = N.load().crimp_last_fixups()
     wall = float(np.mean(walls))
     sp = np.mean(np.array(spans), axis=0)  # total, then 7 class sums (ms), then 7 launch counts
-    n, P, form = N.last_nufft_plan()  # search_nufft.h nu_plan: least n P with x^P/P! <= 1e-14, x = pi (M/2) / n
+    n, P, form = N.last_nufft_plan()  # search_nufft.h nu_plan: least n P with 2.4 (x/2)^P/P! <= 5e-14, x = pi (M/2) / n
     w = N.last_nufft_work()
     m = a.nharm
     work = {"spread": (w["spread_flops"], "fp64"), "merge": (w["merge_bytes"], "hbm"), "pass1": (w["pass1_bytes"], "hbm"),
@@ -792,7 +793,7 @@ def main():
                                         "work per launch (crimp_last_nufft_work) / mean launch duration (hipEvents "
                                         "on the library's stream); all classes under `nufft.kernels`; traffic: HBM "
                                         "bytes per launch, rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (x2 FETCH gfx950 "
-                                        "correction) of the same kernel, profiles/r05/pmc_nufft_traffic.json")
+                                        "correction) of the same kernel, profiles/r06/pmc_nufft_traffic.json")
             rec["roofline"].setdefault("traffic", None)
             rec["nufft"] = nu
             if exact is not None:
