@@ -1115,10 +1115,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k
 
 // k_nu_rows4096_combine with 512 threads and four radix-8 stages (8 elements per thread): two waves per SIMD from
 // one block per CU (the radix-16 form holds 16 elements per thread and runs one). Stage 1 on the loaded row, stage 4's
-// outputs (positions t + 512 r) in registers for the Horner sum, stages 2-3 through two 64 KB tiles whose roles
-// alternate between moments (three barriers per moment); element i at i ^ ((i >> 3) & 7) (stage 1's stride-8
-// writes over all banks). The transform's arithmetic differs from the radix-16 form's in rounding only.
-__device__ __forceinline__ int nu_sw8(int i) { return i ^ ((i >> 3) & 7); }
+// outputs (positions t + 512 r) in registers for the moment sum, stages 2-3 through two padded 72 KB tiles whose
+// roles alternate between moments (three barriers per moment). The transform's arithmetic differs from the radix-16
+// form's in rounding only. Measured (profiles/r06/ab_p2_probes.log, config 3): without its loads the pass takes 0.90
+// of its time, without its LDS exchanges 0.85, without the transform's arithmetic 0.81, without both 0.69 -- the
+// loads, exchanges and arithmetic of one block per CU overlap little; 30 % fewer VALU instructions (below) or a second
+// moment's loads in flight moved it by 1-2 %, rows of 2048 with two blocks per CU by 9 % (pass 1 then needs 512-row
+// columns), an L2 touch of the rows two moments ahead cost 12 % (profiles/r06/ab_p2_l2prefetch_rejected.log).
 // Moment chunks: the launch transforms moments plo .. P-1 (X holds their planes only, beta = (p - plo) nrow + r) and,
 // with accum, adds its partial sum to the CS an earlier chunk (moments above P) wrote -- the sum over moments is
 // linear, and each chunk starts the Bessel recurrence at its own top (nu_bes_start(P)).
@@ -1137,79 +1140,18 @@ struct NuFinal {
     int64_t best_base;
     const double2* CS0;            // harmonic 0's sums of the batch (stride nbt)
 };
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k_nu_rows4096_combine8(
-    const double2* X, int lnfft, int P, int plo, int accum, int nrow, int64_t nf, int64_t jhi, int64_t h,
-    int64_t tbase, int64_t nbt, const double* __restrict__ bc, double2* __restrict__ CS, const NuFinal F) {
-    extern __shared__ double2 nu_s[];  // [2][4096]
-    __shared__ NuTile tw;
-    nu_tile_init(&tw, 12);
-    const int64_t nfft = int64_t(1) << lnfft;
-    const int ln1 = lnfft - 12;
-    const int64_t k1 = blockIdx.x;
-    const int r = blockIdx.y;
+// The row pass's epilogue: each position's sum to CS (F.on == 0), or (fused finalize, k_nu_finalize's arithmetic
+// with the last harmonic from registers) each trial's power, the fix-up list and the block's best trial. Position
+// q of thread t is t + TPB q of the row.
+template <int TPB, int NP>
+__device__ __forceinline__ void nu_rows_epilogue(const double2 (&acc)[NP], int64_t k1, int ln1, int64_t nfft,
+                                                 int64_t jhi, int64_t h, int64_t tbase, int r, int64_t nf, int64_t nbt,
+                                                 double2* __restrict__ CS, const NuFinal& F, double2* lds) {
     const int t = threadIdx.x;
-    const double2* xr = X + (int64_t)r * nfft + (k1 << 12);
-    const int64_t pstride = (int64_t)nrow * nfft;
-    double2 acc[8], nx[8], v[8];
-    NuBes bs[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        acc[q] = make_double2(0.0, 0.0);
-        const int64_t J = k1 + ((int64_t)(t + 512 * q) << ln1);
-        if (accum) {  // the earlier chunk's sum at this position's trial (positions without a trial keep 0)
-            const int64_t jc = J <= jhi ? J : J - nfft;
-            const int64_t tt = tbase + r * nf + jc;
-            if ((J <= jhi || J >= nfft - h) && tt >= 0 && tt < nbt) acc[q] = CS[tt];
-        }
-        bs[q] = nu_bes_start(bc, P, nu_zh(J <= jhi ? J : J - nfft, lnfft));
-        nx[q] = xr[(int64_t)(P - 1 - plo) * pstride + t + 512 * q];
-    }
-    const int m2 = (t & 7) << 6, m3 = (t & 63) << 3, m4 = t;  // stage twiddles in units of w_4096
-    const int z2 = ((t >> 3) << 6) + (t & 7), z3 = ((t >> 6) << 9) + (t & 63);  // stage 2 / 3 output bases
-    __syncthreads();                                                             // tw
-    int par = 0;
-    for (int p = P - 1; p >= plo; --p, par ^= 1) {
-        double2* A = nu_s + (par ? 4096 : 0);
-        double2* B = nu_s + (par ? 0 : 4096);
-        const int64_t pn = (int64_t)(p > plo ? p - 1 - plo : 0) * pstride;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            v[q] = nx[q];
-            nx[q] = xr[pn + t + 512 * q];
-        }
-        nu_dft8(v);  // stage 1 (Ns = 1)
-#pragma unroll
-        for (int q = 0; q < 8; ++q) A[nu_sw8(8 * t + q)] = v[q];
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < 8; ++q) v[q] = A[nu_sw8(t + 512 * q)];
-        nu_twiddle<8>(nu_tw_tile(&tw, m2), v);
-        nu_dft8(v);  // stage 2 (Ns = 8)
-#pragma unroll
-        for (int q = 0; q < 8; ++q) B[nu_sw8(z2 + 8 * q)] = v[q];
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < 8; ++q) v[q] = B[nu_sw8(t + 512 * q)];
-        nu_twiddle<8>(nu_tw_tile(&tw, m3), v);
-        nu_dft8(v);  // stage 3 (Ns = 64)
-#pragma unroll
-        for (int q = 0; q < 8; ++q) A[nu_sw8(z3 + 64 * q)] = v[q];
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < 8; ++q) v[q] = A[nu_sw8(t + 512 * q)];
-        nu_twiddle<8>(nu_tw_tile(&tw, m4), v);
-        nu_dft8(v);  // stage 4 (Ns = 512): output position t + 512 q
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const int64_t J = k1 + ((int64_t)(t + 512 * q) << ln1);
-            const int64_t jc = J <= jhi ? J : J - nfft;
-            acc[q] = nu_bes_acc(acc[q], nu_bes_w(bs[q], p, nu_zh(jc, lnfft)), v[q], p);
-        }
-    }
     if (!F.on) {
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const int64_t J = k1 + ((int64_t)(t + 512 * q) << ln1);
+        for (int q = 0; q < NP; ++q) {
+            const int64_t J = k1 + ((int64_t)(t + TPB * q) << ln1);
             int64_t jc;
             if (J <= jhi)
                 jc = J;
@@ -1222,11 +1164,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
         }
         return;
     }
-    // fused finalize (k_nu_finalize's arithmetic, the last harmonic from registers)
     BestCand bc_ = {-INFINITY, INT64_MAX};
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        const int64_t J = k1 + ((int64_t)(t + 512 * q) << ln1);
+    for (int q = 0; q < NP; ++q) {
+        const int64_t J = k1 + ((int64_t)(t + TPB * q) << ln1);
         int64_t jc;
         if (J <= jhi)
             jc = J;
@@ -1250,14 +1191,140 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
         if (best_better(v, i, bc_.v, bc_.i)) bc_ = {v, i};
     }
     __syncthreads();  // the tiles are free: the wave candidates go to LDS
-    BestCand* red = reinterpret_cast<BestCand*>(nu_s);
+    BestCand* red = reinterpret_cast<BestCand*>(lds);
     if ((t & 63) == 0) red[t >> 6] = bc_;
     __syncthreads();
     if (t == 0) {
-        for (int w = 1; w < 8; ++w)
+        for (int w = 1; w < TPB / 64; ++w)
             if (best_better(red[w].v, red[w].i, bc_.v, bc_.i)) bc_ = red[w];
         F.best_part[F.best_base + (int64_t)blockIdx.y * gridDim.x + blockIdx.x] = bc_;
     }
+}
+
+// The moment sum is carried in a rotating frame: S_p = sum_{p' >= p} eps_p' i^p' J_p'(z) v_p' as T_p = i^-p S_p,
+// T_p = i T_p+1 + w_p v_p -- the product by i an exact swap and negation folded into the two fmas, no per-moment
+// select of i^p -- and the Bessel recurrence as 2 J (exact), so w_p = 2 J_p is the state itself (p > 0). Every rounding
+// is that of nu_bes_w / nu_bes_acc, so the sums are those of the direct form bit for bit, in ~30 % fewer VALU
+// instructions. Two moments per loop iteration: the register arrays alternate between the moment in use and the next
+// one's loads, the tiles between their roles (no copies). Rows by buffer loads (one offset register, the element
+// offsets in a scalar register); tile element i at i + i / 8, so that every stage's element offsets are compile-time
+// constants and its accesses a base plus immediates: 221 VGPRs, no spills (the xor swizzle's per-lane store addresses
+// took 256 and spilled). Stride-8 stores stay conflict-free; some reads of a 16-lane group meet 2-way.
+struct NuRot {
+    double j1, j2, iz2;  // 2 J_p+1, 2 J_p+2 (the next moment's), 2 / z
+};
+constexpr size_t kNuRowsLds = 2 * (4096 + 512) * sizeof(double2);  // k_nu_rows4096_combine8: two padded tiles
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k_nu_rows4096_combine8(
+    const double2* X, int lnfft, int P, int plo, int accum, int nrow, int64_t nf, int64_t jhi, int64_t h,
+    int64_t tbase, int64_t nbt, const double* __restrict__ bc, double2* __restrict__ CS, const NuFinal F) {
+    constexpr int N = 4096, TPB = 512, NT = N + N / 8;
+    extern __shared__ double2 nu_s[];  // [2][NT]
+    __shared__ NuTile tw;
+    nu_tile_init(&tw, 12);
+    const int64_t nfft = int64_t(1) << lnfft;
+    const int ln1 = lnfft - 12;
+    const int64_t k1 = blockIdx.x;
+    const int r = blockIdx.y;
+    const int t = threadIdx.x;
+    const double2* xr = X + (int64_t)r * nfft + (k1 << 12);
+    const int64_t pstride = (int64_t)nrow * nfft;
+    auto load_row = [&](int pm, double2 (&dst)[8]) {  // moment pm's row: elements t + 512 q
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc((void*)(xr + (int64_t)pm * pstride), (short)0, N * 16, 0x00020000);
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            dst[q] = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rs, t * 16, TPB * 16 * q, 0));
+    };
+    double2 acc[8], xa[8], xb[8];
+    NuRot bs[8];
+    // the frame at the top moment: T_P = i^-P S_P (S_P: an earlier chunk's sum at this position's trial, else 0)
+    const int rP = P & 3;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        double2 a0 = make_double2(0.0, 0.0);
+        const int64_t J = k1 + ((int64_t)(t + TPB * q) << ln1);
+        const int64_t jc = J <= jhi ? J : J - nfft;
+        if (accum) {
+            const int64_t tt = tbase + r * nf + jc;
+            if ((J <= jhi || J >= nfft - h) && tt >= 0 && tt < nbt) a0 = CS[tt];
+        }
+        acc[q] = rP == 0 ? a0 : rP == 1 ? make_double2(a0.y, -a0.x) : rP == 2 ? make_double2(-a0.x, -a0.y)
+                                                                        : make_double2(-a0.y, a0.x);
+        const NuBes b0 = nu_bes_start(bc, P, nu_zh(jc, lnfft));
+        bs[q] = {2.0 * b0.j1, 2.0 * b0.j2, b0.iz2};
+    }
+    load_row(P - 1 - plo, xa);
+    const int m2 = (t & 7) << 6, m3 = (t & 63) << 3, m4 = t;  // stage twiddles in units of w_4096
+    const int z2 = ((t >> 3) << 6) + (t & 7), z3 = ((t >> 6) << 9) + (t & 63);  // stage 2 / 3 output bases
+    // padded bases: element e = base + offset lands at e + e / 8 = (base + base / 8) + (offset + offset / 8) for these
+    const int w1 = 9 * t, w2 = z2 + (z2 >> 3), w3 = z3 + (z3 >> 3), rd = t + (t >> 3);
+    __syncthreads();  // tw
+    // one moment: v (its row) through the four stages, moment p - 1's loads into nv, then the sum
+    auto moment = [&](auto LAST, int p, double2 (&v)[8], double2 (&nv)[8], double2* A, double2* B) {
+        constexpr bool last = decltype(LAST)::value;  // p == 0: w_0 = J_0 (1 where z = 0)
+        if (p > plo) load_row(p - 1 - plo, nv);
+        nu_dft8(v);  // stage 1 (Ns = 1)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) A[w1 + q] = v[q];
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = A[rd + 576 * q];
+        nu_twiddle<8>(nu_tw_tile(&tw, m2), v);
+        nu_dft8(v);  // stage 2 (Ns = 8)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) B[w2 + 9 * q] = v[q];
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = B[rd + 576 * q];
+        nu_twiddle<8>(nu_tw_tile(&tw, m3), v);
+        nu_dft8(v);  // stage 3 (Ns = 64)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) A[w3 + 72 * q] = v[q];
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = A[rd + 576 * q];
+        nu_twiddle<8>(nu_tw_tile(&tw, m4), v);
+        nu_dft8(v);  // stage 4 (Ns = 512): output position t + 512 q
+        const double pp1 = (double)(p + 1);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const double j = fma(pp1 * bs[q].iz2, bs[q].j1, -bs[q].j2);  // 2 J_p
+            bs[q].j2 = bs[q].j1;
+            bs[q].j1 = j;
+            double w = j;
+            // w_0 = J_0, and 1 at z = 0: trial offset jc = J = 0, position 0 of row 0
+            if constexpr (last) w = (q == 0 && k1 == 0 && t == 0) ? 1.0 : 0.5 * j;
+            acc[q] = make_double2(fma(w, v[q].x, -acc[q].y), fma(w, v[q].y, acc[q].x));  // i T + w v
+        }
+    };
+    // moments P-1 .. max(plo, 1) two per iteration (the first alone when their count is odd), then moment 0
+    const int pend = plo > 0 ? plo : 1;
+    int p = P - 1;
+    double2* TA = nu_s;
+    double2* TB = nu_s + NT;
+    if (p >= pend && ((p - pend + 1) & 1)) {
+        moment(std::false_type(), p, xa, xb, TA, TB);
+        --p;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) xa[q] = xb[q];
+        double2* tt = TA;
+        TA = TB;
+        TB = tt;
+    }
+    for (; p >= pend; p -= 2) {
+        moment(std::false_type(), p, xa, xb, TA, TB);
+        moment(std::false_type(), p - 1, xb, xa, TB, TA);
+    }
+    if (plo == 0) moment(std::true_type(), 0, xa, xb, TA, TB);
+    // back to S = i^plo T
+    const int rl = plo & 3;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const double2 a = acc[q];
+        acc[q] = rl == 0 ? a : rl == 1 ? make_double2(-a.y, a.x) : rl == 2 ? make_double2(-a.x, -a.y)
+                                                                : make_double2(a.y, -a.x);
+    }
+    nu_rows_epilogue<TPB, 8>(acc, k1, ln1, nfft, jhi, h, tbase, r, nf, nbt, CS, F, nu_s);
 }
 
 // (C_k, S_k) of the trials of one harmonic: position pos = k1 n2 + k2 of the FFT output holds J = k1 + n1 k2
@@ -1759,7 +1826,7 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
             HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_nu_rows4096_combine),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kNuTile * (int)sizeof(double2)));
             HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_nu_rows4096_combine8),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kNuTile * (int)sizeof(double2)));
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)kNuRowsLds));
             if (dev < 64) done |= uint64_t(1) << dev;
         }
     }
@@ -1922,7 +1989,11 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
                     // earlier harmonics' sums read and the powers written
                     g_nu_work[kNuClsPass2] += cplane + (F.on ? (16.0 * (nharm - 1) + 8.0) * (double)nbt
                                                              : 16.0 * (double)nbt * (phi < P ? 2.0 : 1.0));
-                    k_nu_rows4096_combine8<<<dim3((unsigned)(int64_t(1) << ln1), (unsigned)nrow), 512, 2 * lds_fft,
+#define CRIMP_P2(PR)                                                                                               \
+    k_nu_rows4096_combine8<PR><<<dim3((unsigned)(int64_t(1) << ln1), (unsigned)nrow), 512, 2 * lds_fft, s>>>(     \
+        Zo, lnfft, phi, plo, phi < P ? 1 : 0, nrow, nf, pl.nseg - 1 - pl.h, pl.h, rb * nf + jbase - (tb0 + first),  \
+        nbt, bc, CS + (int64_t)(k - 1) * nbt, F)
+                    k_nu_rows4096_combine8<<<dim3((unsigned)(int64_t(1) << ln1), (unsigned)nrow), 512, kNuRowsLds,
                                              s>>>(Zo, lnfft, phi, plo, phi < P ? 1 : 0, nrow, nf, pl.nseg - 1 - pl.h,
                                                   pl.h, rb * nf + jbase - (tb0 + first), nbt, bc,
                                                   CS + (int64_t)(k - 1) * nbt, F);

@@ -27,6 +27,7 @@ variants = [v for v in os.environ.get("VARIANTS", "").split(";")]
 keys = sorted({kv.split("=")[0] for v in variants for kv in v.split(",") if kv})
 res = {v: [] for v in variants}
 dig = {}
+zs = {}
 for rnd in range(int(os.environ.get("REPS", 5)) + 1):
     for v in variants:
         for k in keys:
@@ -43,8 +44,12 @@ for rnd in range(int(os.environ.get("REPS", 5)) + 1):
         sp = N.last_kernel_times()[:15]
         if rnd > 0:
             res[v].append([el * 1e3] + sp[:8])
-        dig[v] = hashlib.sha1(z.cpu().numpy().tobytes()).hexdigest()[:12]
-print("%-32s %8s %8s | %s | digest" % ("variant", "wall", "pipe", " ".join("%8s" % c for c in N.NUFFT_CLASSES)))
+        zs[v] = z.cpu().numpy()
+        dig[v] = hashlib.sha1(zs[v].tobytes()).hexdigest()[:12]
+print("%-32s %8s %8s | %s | digest  max-rel-vs-first" % ("variant", "wall", "pipe",
+                                                          " ".join("%8s" % c for c in N.NUFFT_CLASSES)))
+z0 = zs[variants[0]]
 for v in variants:
     a = np.mean(np.array(res[v]), axis=0)
-    print("%-32s %8.3f %8.3f | %s | %s" % (v or "(default)", a[0], a[1], " ".join("%8.4f" % x for x in a[2:9]), dig[v]))
+    print("%-32s %8.3f %8.3f | %s | %s %.2e" % (v or "(default)", a[0], a[1], " ".join("%8.4f" % x for x in a[2:9]),
+                                                dig[v], float(np.max(np.abs(zs[v] - z0) / np.abs(z0)))))
