@@ -28,7 +28,7 @@
 //   k_nu_fft_cols, k_nu_fft_rows   four-step FFT (n = n1 n2, Stockham autosort stages of radix 16/8/4/2 in LDS,
 //                 positive exponent); a single row pass for n <= 4096.
 //   k_nu_combine  the moments' Bessel-weighted sum at every trial -> (C_k, S_k) (fused into the row pass by
-//                 default: k_nu_rows4096_combine8 / k_nu_fft_rows_combine).
+//                 default: k_nu_rows_combine8 / k_nu_fft_rows_combine).
 //   k_nu_finalize Z^2 / H in the reference's formula order and the certificate (fix-up list, as the exact path).
 #pragma once
 
@@ -644,7 +644,7 @@ __global__ __launch_bounds__(256) void k_nu_merge(const double* __restrict__ U, 
 }
 
 // Power and error bound of one trial from its harmonic sums: CS[k * nbt + t] for k < m, except that with lastv the
-// last harmonic's sum is the register value `last` (the fused row pass, k_nu_rows4096_combine8). The same operations
+// last harmonic's sum is the register value `last` (the fused row pass, k_nu_rows_combine8). The same operations
 // in the same order either way, so the fused and separate finalize give identical powers and flags.
 __device__ __forceinline__ void nu_power(const double2* __restrict__ CS, int64_t nbt, int64_t t, int m, int stat,
                                          double nph, double E, bool lastv, double2 last, double* pout,
@@ -948,6 +948,114 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     }
 }
 
+// k_nu_fft_cols for n1 = 512 (n = 512 n2; CRIMP_NUFFT_ROW2048=1): groups of 8 columns (NC = 1: 128 VGPRs, two blocks
+// per CU; 16 columns at 248 VGPRs and one block measured 10 % slower), 512 threads (column cc = t & 7, j = t >> 3),
+// three radix-8 Stockham stages over rows j + 64 q (8 elements per thread and column: rows as loaded, stage 3's outputs
+// k1 = j + 64 q stored from registers), two exchanges through a [512 rows][8 columns] tile (conflict-free without a
+// swizzle: 8 consecutive lanes hold 8 consecutive columns). Persistent blocks, the next group's occupied rows loaded
+// during the current one; rows by buffer loads and stores (one offset register); the inter-pass twiddle
+// w_n^{b k1} = w_n^{b j} (w_n^{64 b})^q as in k_nu_cols256.
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k_nu_cols512(
+    const double2* __restrict__ X, double2* __restrict__ Y, int lnfft, NuTw T, int alo, int acnt, int64_t ngroups) {
+    constexpr int NC = 1, C = 8;
+    extern __shared__ double2 nu_s[];  // [512 rows][C columns]
+    __shared__ NuTile tw;
+    nu_tile_init(&tw, 9);
+    const int ln2 = lnfft - 9;
+    const int64_t nfft = int64_t(1) << lnfft;
+    const int cc = threadIdx.x & 7, j = threadIdx.x >> 3;
+    const int64_t cpb = int64_t(1) << (ln2 - 3);  // column groups per batch
+    double2 nv[NC][8], tf[NC][4];
+    const int voff = ((j << ln2) + cc) * 16;  // row offsets 64 q n2 16 B and column offsets 8 c 16 B: scalar
+    auto fetch = [&](int64_t grp) {  // rows outside [alo, alo + acnt) (mod 512) hold no cell
+        const int64_t b0 = (grp % cpb) * C;
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(X + (grp / cpb) * nfft + b0), (short)0, (int)(16 << lnfft), 0x00020000);
+        const int64_t lm = (int64_t(1) << T.lbits) - 1;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const int64_t b = b0 + cc + 8 * c, tb = (b * (int64_t)j) & T.mask, ts = (b << 6) & T.mask;
+            tf[c][0] = T.hi[tb >> T.lbits];
+            tf[c][1] = T.lo[tb & lm];
+            tf[c][2] = T.hi[ts >> T.lbits];
+            tf[c][3] = T.lo[ts & lm];
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const bool occ = ((j + 64 * q - alo) & 511) < acnt;
+#pragma unroll
+            for (int c = 0; c < NC; ++c)
+                nv[c][q] = occ ? __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(
+                                                                 rs, voff, ((64 * q << ln2) + 8 * c) * 16, 0))
+                               : make_double2(0.0, 0.0);
+        }
+    };
+    int64_t grp = blockIdx.x;
+    if (grp < ngroups) fetch(grp);
+    const int m2 = (j & 7) << 3;  // stage-2 twiddle w_64^{(j & 7) q} in units of w_512; stage 3: w_512^{j q}
+    const int z2 = ((j >> 3) << 6) + (j & 7);
+    __syncthreads();  // tw
+    typedef unsigned int nu_u4 __attribute__((ext_vector_type(4)));
+    for (; grp < ngroups; grp += gridDim.x) {
+        double2 v[NC][8], wb[NC], ws[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) v[c][q] = nv[c][q];
+            wb[c] = nu_cmul(tf[c][0], tf[c][1]);
+            ws[c] = nu_cmul(tf[c][2], tf[c][3]);
+        }
+        const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(Y + (grp / cpb) * nfft + (grp % cpb) * C), (short)0, (int)(16 << lnfft), 0x00020000);
+        if (grp + gridDim.x < ngroups) fetch(grp + gridDim.x);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            nu_dft8(v[c]);  // stage 1 (Ns = 1): row 8 j + q
+#pragma unroll
+            for (int q = 0; q < 8; ++q) nu_s[((j << 3) + q) * C + cc + 8 * c] = v[c][q];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) v[c][q] = nu_s[(j + 64 * q) * C + cc + 8 * c];
+        }
+        __syncthreads();  // the stage-2 writes reuse the tile
+        const double2 t2 = nu_tw_tile(&tw, m2);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            nu_twiddle<8>(t2, v[c]);
+            nu_dft8(v[c]);  // stage 2 (Ns = 8): row z2 + 8 q
+#pragma unroll
+            for (int q = 0; q < 8; ++q) nu_s[(z2 + 8 * q) * C + cc + 8 * c] = v[c][q];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) v[c][q] = nu_s[(j + 64 * q) * C + cc + 8 * c];
+        }
+        __syncthreads();  // the next group's stage-1 writes reuse the tile
+        const double2 t3 = nu_tw_tile(&tw, j);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            nu_twiddle<8>(t3, v[c]);
+            nu_dft8(v[c]);  // stage 3 (Ns = 64): output row k1 = j + 64 q
+            v[c][0] = nu_cmul(v[c][0], wb[c]);
+            nu_twiddle<8>(ws[c], v[c]);  // v[q] *= (w_n^{64 b})^q
+#pragma unroll
+            for (int q = 1; q < 8; ++q) v[c][q] = nu_cmul(v[c][q], wb[c]);
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+#pragma unroll
+            for (int c = 0; c < NC; ++c)
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(nu_u4, v[c][q]), ry, voff,
+                                                       ((64 * q << ln2) + 8 * c) * 16, 0);
+        }
+    }
+}
+
 // pass 2 (or the only pass): DFT of 2^lr contiguous rows of length 2^ll each, in place
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_nu_fft_rows(double2* __restrict__ X, int ll, int lr, int lnfft) {
     extern __shared__ double2 nu_s[];
@@ -1213,22 +1321,29 @@ __device__ __forceinline__ void nu_rows_epilogue(const double2 (&acc)[NP], int64
 struct NuRot {
     double j1, j2, iz2;  // 2 J_p+1, 2 J_p+2 (the next moment's), 2 / z
 };
-constexpr size_t kNuRowsLds = 2 * (4096 + 512) * sizeof(double2);  // k_nu_rows4096_combine8: two padded tiles
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k_nu_rows4096_combine8(
+// dynamic LDS of k_nu_rows_combine8<LN2>: two padded tiles
+constexpr size_t nu_rows_lds(int ln2) { return 2 * ((size_t(1) << ln2) + (size_t(1) << (ln2 - 3))) * sizeof(double2); }
+// LN2 = 12: rows of 4096, 512 threads, four radix-8 stages (Ns = 1, 8, 64, 512). LN2 = 11: rows of 2048 (n = 2^20:
+// columns of 512, k_nu_cols512), 256 threads, one radix-4 stage (butterflies t and t + 1024 on v[0, 2, 4, 6] and
+// v[1, 3, 5, 7]) then three radix-8 (Ns = 4, 32, 256): half the LDS and threads, two blocks per CU.
+template <int LN2>
+__global__ __launch_bounds__(1 << (LN2 - 3)) __attribute__((amdgpu_waves_per_eu(2))) void k_nu_rows_combine8(
     const double2* X, int lnfft, int P, int plo, int accum, int nrow, int64_t nf, int64_t jhi, int64_t h,
     int64_t tbase, int64_t nbt, const double* __restrict__ bc, double2* __restrict__ CS, const NuFinal F) {
-    constexpr int N = 4096, TPB = 512, NT = N + N / 8;
+    constexpr int N = 1 << LN2, TPB = N / 8, NT = N + N / 8;
+    constexpr int Ns2 = LN2 == 12 ? 8 : 4, Ns3 = 8 * Ns2;
+    static_assert(LN2 == 11 || LN2 == 12, "rows of 2048 or 4096");
     extern __shared__ double2 nu_s[];  // [2][NT]
     __shared__ NuTile tw;
-    nu_tile_init(&tw, 12);
+    nu_tile_init(&tw, LN2);
     const int64_t nfft = int64_t(1) << lnfft;
-    const int ln1 = lnfft - 12;
+    const int ln1 = lnfft - LN2;
     const int64_t k1 = blockIdx.x;
     const int r = blockIdx.y;
     const int t = threadIdx.x;
-    const double2* xr = X + (int64_t)r * nfft + (k1 << 12);
+    const double2* xr = X + (int64_t)r * nfft + (k1 << LN2);
     const int64_t pstride = (int64_t)nrow * nfft;
-    auto load_row = [&](int pm, double2 (&dst)[8]) {  // moment pm's row: elements t + 512 q
+    auto load_row = [&](int pm, double2 (&dst)[8]) {  // moment pm's row: elements t + TPB q
         const __amdgpu_buffer_rsrc_t rs =
             __builtin_amdgcn_make_buffer_rsrc((void*)(xr + (int64_t)pm * pstride), (short)0, N * 16, 0x00020000);
 #pragma unroll
@@ -1254,37 +1369,49 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
         bs[q] = {2.0 * b0.j1, 2.0 * b0.j2, b0.iz2};
     }
     load_row(P - 1 - plo, xa);
-    const int m2 = (t & 7) << 6, m3 = (t & 63) << 3, m4 = t;  // stage twiddles in units of w_4096
-    const int z2 = ((t >> 3) << 6) + (t & 7), z3 = ((t >> 6) << 9) + (t & 63);  // stage 2 / 3 output bases
-    // padded bases: element e = base + offset lands at e + e / 8 = (base + base / 8) + (offset + offset / 8) for these
-    const int w1 = 9 * t, w2 = z2 + (z2 >> 3), w3 = z3 + (z3 >> 3), rd = t + (t >> 3);
+    // stage twiddles in units of w_N (stage 4: w_N^{t q})
+    const int m2 = (t & (Ns2 - 1)) * (N / (8 * Ns2)), m3 = (t & (Ns3 - 1)) * (N / (8 * Ns3)), m4 = t;
+    const int z2 = (t / Ns2) * 8 * Ns2 + (t & (Ns2 - 1)), z3 = (t / Ns3) * 8 * Ns3 + (t & (Ns3 - 1));  // outputs
+    // padded bases: element e = base + offset lands at e + e / 8 = (base + base / 8) + (offset + offset / 8 (+1 where
+    // the stage-2 offset 4 q carries into the base's bit 3 at LN2 = 11)) -- compile-time offsets
+    const int w1 = LN2 == 12 ? 9 * t : 4 * t + (t >> 1), w2 = z2 + (z2 >> 3), w3 = z3 + (z3 >> 3), rd = t + (t >> 3);
     __syncthreads();  // tw
     // one moment: v (its row) through the four stages, moment p - 1's loads into nv, then the sum
     auto moment = [&](auto LAST, int p, double2 (&v)[8], double2 (&nv)[8], double2* A, double2* B) {
         constexpr bool last = decltype(LAST)::value;  // p == 0: w_0 = J_0 (1 where z = 0)
         if (p > plo) load_row(p - 1 - plo, nv);
-        nu_dft8(v);  // stage 1 (Ns = 1)
+        if constexpr (LN2 == 12) {
+            nu_dft8(v);  // stage 1 (Ns = 1): element 8 t + q
 #pragma unroll
-        for (int q = 0; q < 8; ++q) A[w1 + q] = v[q];
+            for (int q = 0; q < 8; ++q) A[w1 + q] = v[q];
+        } else {
+            nu_dft4(v[0], v[2], v[4], v[6]);  // stage 1 (R 4, Ns = 1): elements 4 t + q and 4 t + 1024 + q
+            nu_dft4(v[1], v[3], v[5], v[7]);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                A[w1 + q] = v[2 * q];
+                A[w1 + N / 2 + N / 16 + q] = v[2 * q + 1];
+            }
+        }
         __syncthreads();
 #pragma unroll
-        for (int q = 0; q < 8; ++q) v[q] = A[rd + 576 * q];
+        for (int q = 0; q < 8; ++q) v[q] = A[rd + TPB * 9 / 8 * q];
         nu_twiddle<8>(nu_tw_tile(&tw, m2), v);
-        nu_dft8(v);  // stage 2 (Ns = 8)
+        nu_dft8(v);  // stage 2: element z2 + Ns2 q
 #pragma unroll
-        for (int q = 0; q < 8; ++q) B[w2 + 9 * q] = v[q];
+        for (int q = 0; q < 8; ++q) B[w2 + Ns2 * q + (Ns2 == 8 ? q : q >> 1)] = v[q];
         __syncthreads();
 #pragma unroll
-        for (int q = 0; q < 8; ++q) v[q] = B[rd + 576 * q];
+        for (int q = 0; q < 8; ++q) v[q] = B[rd + TPB * 9 / 8 * q];
         nu_twiddle<8>(nu_tw_tile(&tw, m3), v);
-        nu_dft8(v);  // stage 3 (Ns = 64)
+        nu_dft8(v);  // stage 3: element z3 + Ns3 q
 #pragma unroll
-        for (int q = 0; q < 8; ++q) A[w3 + 72 * q] = v[q];
+        for (int q = 0; q < 8; ++q) A[w3 + Ns3 * 9 / 8 * q] = v[q];
         __syncthreads();
 #pragma unroll
-        for (int q = 0; q < 8; ++q) v[q] = A[rd + 576 * q];
+        for (int q = 0; q < 8; ++q) v[q] = A[rd + TPB * 9 / 8 * q];
         nu_twiddle<8>(nu_tw_tile(&tw, m4), v);
-        nu_dft8(v);  // stage 4 (Ns = 512): output position t + 512 q
+        nu_dft8(v);  // stage 4: output position t + TPB q
         const double pp1 = (double)(p + 1);
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
@@ -1816,6 +1943,12 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
     // profiles/r05/ab_r8_ilp.log); CRIMP_NUFFT_R8=0 runs the radix-16 form
     const char* r8_env = getenv("CRIMP_NUFFT_R8");
     const bool rows_r8 = !(r8_env && !strcmp(r8_env, "0"));
+    // CRIMP_NUFFT_ROW2048=1: n = 2^20 as 512 x 2048 (k_nu_cols512, k_nu_rows_combine8<11>), else 256 x 4096. The row
+    // pass gains what the column pass loses (config 3: pass 2 0.160 vs 0.180 ms, pass 1 0.138 vs 0.115 ms per search,
+    // profiles/r06/ab_rows2048_cols512.log), so 4096-element rows stay the default.
+    const char* r2k_env = getenv("CRIMP_NUFFT_ROW2048");
+    const bool row2048 = r2k_env && !strcmp(r2k_env, "1") && rows4096 && rows_r8 && fused_combine;
+    auto row_log = [&](int lnfft) { return row2048 && lnfft == 20 ? 11 : std::min(lnfft, 12); };
     {  // 128 KB of dynamic LDS for k_nu_rows4096_combine, set once per device
         static std::mutex mu;
         static uint64_t done = 0;
@@ -1825,8 +1958,10 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
         if (dev >= 64 || !(done >> dev & 1)) {
             HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_nu_rows4096_combine),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kNuTile * (int)sizeof(double2)));
-            HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_nu_rows4096_combine8),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)kNuRowsLds));
+            HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_nu_rows_combine8<12>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)nu_rows_lds(12)));
+            HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_nu_rows_combine8<11>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)nu_rows_lds(11)));
             if (dev < 64) done |= uint64_t(1) << dev;
         }
     }
@@ -1861,12 +1996,12 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
     HIPCHK(sc.alloc(&Y, (size_t)Bmax));
     HIPCHK(sc.alloc(&CS, (size_t)csmax));
     HIPCHK(sc.alloc(&flagged, (size_t)count));
-    // per-block best trials of the fused finalize (k_nu_rows4096_combine8 blocks of every row batch)
+    // per-block best trials of the fused finalize (k_nu_rows_combine8 blocks of every row batch)
     BestCand* best_part = nullptr;
     int64_t best_count = 0, separate_batches = 0;
     if (best) {
         int64_t nb = 0;
-        for (const NuPlan& pl : plans) nb += (pl.r1 - pl.r0) * (int64_t(1) << std::max(0, pl.lnfft - 12));
+        for (const NuPlan& pl : plans) nb += (pl.r1 - pl.r0) * (int64_t(1) << (pl.lnfft - row_log(pl.lnfft)));
         HIPCHK(sc.alloc(&best_part, (size_t)std::max<int64_t>(nb, 1)));
     }
     // every MFMA (group, row batch, pass)'s slot table, uploaded once before the launches
@@ -1927,7 +2062,7 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
         const int64_t nfft = int64_t(1) << lnfft;
         // FFT shape: one row pass for n <= kNuTile (2^lrow transforms per block), else columns (n1 = n / 4096 <= 4096)
         // then rows of 4096
-        const int ln2 = std::min(lnfft, 12), ln1 = lnfft - ln2;
+        const int ln2 = row_log(lnfft), ln1 = lnfft - ln2;
         const int lcol = 12 - ln1;  // columns per block in pass 1 (n1 * c = 4096)
         const int lrow = 12 - ln2;  // rows per block in pass 2
         const int64_t jbase = pl.j0 + pl.h;
@@ -1936,12 +2071,12 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
             nu_occupied(pl.gmin[(size_t)(k - 1)], pl.gmax[(size_t)(k - 1)], lnfft, ln1, alo, acnt);
         };
         // fused finalize: the last harmonic's row pass forms the powers (NuFinal), for the 4096-row radix-8 path
-        const bool fuse_final = fused_combine && ln2 == 12 && rows4096 && rows_r8 && !nu_final_separate();
+        const bool fuse_final = fused_combine && ln2 >= 11 && rows4096 && rows_r8 && !nu_final_separate();
         bool final_done = false;  // set by fft_combine when it finalized the batch
         auto fft_combine = [&](int k, int64_t rb, int nrow, int64_t tb0, int64_t nbt, double2* W) -> int {
             const int64_t Bp = (int64_t)P * nrow;
             const double plane = 16.0 * (double)Bp * (double)nfft;  // one complex FFT buffer of the batch
-            if (fused_combine && ln2 == 12 && rows4096 && rows_r8) {
+            if (fused_combine && ln2 >= 11 && rows4096 && rows_r8) {
                 // moment chunks of <= nu_pchunk() (default: all P moments in one): pass 1 and pass 2 of a chunk in turn
                 int alo = 0, acnt = 0;
                 if (ln1 > 0) occupied(k, &alo, &acnt);
@@ -1957,6 +2092,10 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
                         if (ln1 == 8) {
                             const int64_t ngroups = Bc << (ln2 - 4);
                             k_nu_cols256<<<(unsigned)std::min<int64_t>(ngroups, 2 * nu_cus()), 256, lds_fft, s>>>(
+                                Win, Y, lnfft, T, alo, acnt, ngroups);
+                        } else if (ln1 == 9) {
+                            const int64_t ngroups = Bc << (ln2 - 3);
+                            k_nu_cols512<<<(unsigned)std::min<int64_t>(ngroups, 2 * nu_cus()), 512, lds_fft, s>>>(
                                 Win, Y, lnfft, T, alo, acnt, ngroups);
                         } else {
                             k_nu_fft_cols<<<dim3((unsigned)(int64_t(1) << (ln2 - lcol)), (unsigned)Bc), 256, lds_fft,
@@ -1989,14 +2128,15 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
                     // earlier harmonics' sums read and the powers written
                     g_nu_work[kNuClsPass2] += cplane + (F.on ? (16.0 * (nharm - 1) + 8.0) * (double)nbt
                                                              : 16.0 * (double)nbt * (phi < P ? 2.0 : 1.0));
-#define CRIMP_P2(PR)                                                                                               \
-    k_nu_rows4096_combine8<PR><<<dim3((unsigned)(int64_t(1) << ln1), (unsigned)nrow), 512, 2 * lds_fft, s>>>(     \
-        Zo, lnfft, phi, plo, phi < P ? 1 : 0, nrow, nf, pl.nseg - 1 - pl.h, pl.h, rb * nf + jbase - (tb0 + first),  \
-        nbt, bc, CS + (int64_t)(k - 1) * nbt, F)
-                    k_nu_rows4096_combine8<<<dim3((unsigned)(int64_t(1) << ln1), (unsigned)nrow), 512, kNuRowsLds,
-                                             s>>>(Zo, lnfft, phi, plo, phi < P ? 1 : 0, nrow, nf, pl.nseg - 1 - pl.h,
-                                                  pl.h, rb * nf + jbase - (tb0 + first), nbt, bc,
-                                                  CS + (int64_t)(k - 1) * nbt, F);
+                    const dim3 g2((unsigned)(int64_t(1) << ln1), (unsigned)nrow);
+                    if (ln2 == 11)
+                        k_nu_rows_combine8<11><<<g2, 256, nu_rows_lds(11), s>>>(
+                            Zo, lnfft, phi, plo, phi < P ? 1 : 0, nrow, nf, pl.nseg - 1 - pl.h, pl.h,
+                            rb * nf + jbase - (tb0 + first), nbt, bc, CS + (int64_t)(k - 1) * nbt, F);
+                    else
+                        k_nu_rows_combine8<12><<<g2, 512, nu_rows_lds(12), s>>>(
+                            Zo, lnfft, phi, plo, phi < P ? 1 : 0, nrow, nf, pl.nseg - 1 - pl.h, pl.h,
+                            rb * nf + jbase - (tb0 + first), nbt, bc, CS + (int64_t)(k - 1) * nbt, F);
                     HIPCHK(hipGetLastError());
                     HIPCHK(span(kNuClsPass2));
                 }
