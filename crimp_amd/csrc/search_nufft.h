@@ -1254,12 +1254,14 @@ struct NuFinal {
 template <int TPB, int NP>
 __device__ __forceinline__ void nu_rows_epilogue(const double2 (&acc)[NP], int64_t k1, int ln1, int64_t nfft,
                                                  int64_t jhi, int64_t h, int64_t tbase, int r, int64_t nf, int64_t nbt,
-                                                 double2* __restrict__ CS, const NuFinal& F, double2* lds) {
+                                                 double2* __restrict__ CS, const NuFinal& F, double2* lds,
+                                                 int pos0 = -1) {
     const int t = threadIdx.x;
+    const int b0 = pos0 < 0 ? t : pos0;  // the thread's first row position (then + TPB q)
     if (!F.on) {
 #pragma unroll
         for (int q = 0; q < NP; ++q) {
-            const int64_t J = k1 + ((int64_t)(t + TPB * q) << ln1);
+            const int64_t J = k1 + ((int64_t)(b0 + TPB * q) << ln1);
             int64_t jc;
             if (J <= jhi)
                 jc = J;
@@ -1275,7 +1277,7 @@ __device__ __forceinline__ void nu_rows_epilogue(const double2 (&acc)[NP], int64
     BestCand bc_ = {-INFINITY, INT64_MAX};
 #pragma unroll
     for (int q = 0; q < NP; ++q) {
-        const int64_t J = k1 + ((int64_t)(t + TPB * q) << ln1);
+        const int64_t J = k1 + ((int64_t)(b0 + TPB * q) << ln1);
         int64_t jc;
         if (J <= jhi)
             jc = J;
@@ -1452,6 +1454,126 @@ __global__ __launch_bounds__(1 << (LN2 - 3)) __attribute__((amdgpu_waves_per_eu(
                                                                 : make_double2(a.y, -a.x);
     }
     nu_rows_epilogue<TPB, 8>(acc, k1, ln1, nfft, jhi, h, tbase, r, nf, nbt, CS, F, nu_s);
+}
+
+// The 4096-element row pass with one cross-wave exchange per moment. Radix-8 decimation in frequency over the input
+// digits n = 512 n3 + 64 n2 + 8 n1 + n0 (outputs k0 + 8 k1 + 64 k2 + 512 k3): stage 1 (over n3, the row as loaded:
+// thread t = m = 64 n2 + 8 n1 + n0) then w_4096^(m k0); one exchange through a 64 KB tile to thread (wave k0, lane
+// m' = 8 n1 + n0), whose wave reads the tile's 8 KB region k0 only; stage 2 (over n2) then w_512^(m' k1); an exchange
+// inside the wave (lane 8 k1 + n0) through its own region of the tile, which no other wave reads; stage 3 (over n1)
+// then w_64^(n0 k2); a second exchange inside the wave (lane 8 k1 + k2); stage 4 (over n0): outputs k3 at positions
+// k0 + 8 k1 + 64 k2 + 512 k3. Two tiles alternate between moments, so one barrier per moment (the cross-wave exchange)
+// suffices: a tile is written again two moments later, after every wave has passed the next moment's barrier and with
+// it left the tile. Every exchange conflict-free (linear or lane-xor layouts); the wave-level exchanges wait only for
+// their own stores. Moment sum as k_nu_rows_combine8 (rotating frame, doubled Bessel state, two moments per iteration).
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k_nu_rows_iw(
+    const double2* X, int lnfft, int P, int plo, int accum, int nrow, int64_t nf, int64_t jhi, int64_t h,
+    int64_t tbase, int64_t nbt, const double* __restrict__ bc, double2* __restrict__ CS, const NuFinal F) {
+    constexpr int N = 4096, TPB = 512;
+    extern __shared__ double2 nu_s[];  // [2][4096]
+    __shared__ NuTile tw;
+    nu_tile_init(&tw, 12);
+    const int64_t nfft = int64_t(1) << lnfft;
+    const int ln1 = lnfft - 12;
+    const int64_t k1b = blockIdx.x;
+    const int r = blockIdx.y;
+    const int t = threadIdx.x, w = t >> 6, L = t & 63, hi3 = L >> 3, lo3 = L & 7;
+    const int pos0 = w + 8 * hi3 + 64 * lo3;  // output positions pos0 + 512 q
+    const double2* xr = X + (int64_t)r * nfft + (k1b << 12);
+    const int64_t pstride = (int64_t)nrow * nfft;
+    auto load_row = [&](int pm, double2 (&dst)[8]) {  // moment pm's row: elements t + 512 q
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc((void*)(xr + (int64_t)pm * pstride), (short)0, N * 16, 0x00020000);
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            dst[q] = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rs, t * 16, TPB * 16 * q, 0));
+    };
+    double2 acc[8], xa[8], xb[8];
+    NuRot bs[8];
+    const int rP = P & 3;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        double2 a0 = make_double2(0.0, 0.0);
+        const int64_t J = k1b + ((int64_t)(pos0 + TPB * q) << ln1);
+        const int64_t jc = J <= jhi ? J : J - nfft;
+        if (accum) {
+            const int64_t tt = tbase + r * nf + jc;
+            if ((J <= jhi || J >= nfft - h) && tt >= 0 && tt < nbt) a0 = CS[tt];
+        }
+        acc[q] = rP == 0 ? a0 : rP == 1 ? make_double2(a0.y, -a0.x) : rP == 2 ? make_double2(-a0.x, -a0.y)
+                                                                        : make_double2(-a0.y, a0.x);
+        const NuBes b0 = nu_bes_start(bc, P, nu_zh(jc, lnfft));
+        bs[q] = {2.0 * b0.j1, 2.0 * b0.j2, b0.iz2};
+    }
+    load_row(P - 1 - plo, xa);
+    // tile offsets: cross-wave store (q 512 + n2 64 + m'), its read (k0 512 + n2 64 + m'), wave-level exchange 1 store
+    // (64 n1 + 8 k1 + n0) / read (64 n1 + 8 k1 + n0, n1 = q), exchange 2 store (64 k2 + 8 k1 + (n0 ^ k2)) / read
+    const int cw = 64 * w + L, cr = 512 * w + L, e1w = 512 * w + 64 * hi3 + lo3, e2w = 512 * w + 8 * hi3,
+              e2r = 512 * w + 64 * lo3 + 8 * hi3;
+    __syncthreads();  // tw
+    auto moment = [&](auto LAST, int p, double2 (&v)[8], double2 (&nv)[8], double2* A) {
+        constexpr bool last = decltype(LAST)::value;
+        if (p > plo) load_row(p - 1 - plo, nv);
+        nu_dft8(v);  // stage 1 (over n3): k0 = q
+        nu_twiddle<8>(nu_tw_tile(&tw, t), v);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) A[cw + 512 * q] = v[q];
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = A[cr + 64 * q];
+        nu_dft8(v);  // stage 2 (over n2): k1 = q
+        nu_twiddle<8>(nu_tw_tile(&tw, 8 * L), v);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) A[e1w + 8 * q] = v[q];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's own stores, before its lanes read them
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = A[cr + 64 * q];
+        nu_dft8(v);  // stage 3 (over n1): k2 = q
+        nu_twiddle<8>(nu_tw_tile(&tw, 64 * lo3), v);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) A[e2w + 64 * q + (lo3 ^ q)] = v[q];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = A[e2r + (q ^ lo3)];
+        nu_dft8(v);  // stage 4 (over n0): k3 = q, position pos0 + 512 q
+        const double pp1 = (double)(p + 1);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const double j = fma(pp1 * bs[q].iz2, bs[q].j1, -bs[q].j2);  // 2 J_p
+            bs[q].j2 = bs[q].j1;
+            bs[q].j1 = j;
+            double wgt = j;
+            // w_0 = J_0, and 1 at z = 0: position 0 of row 0 (pos0 = 0: thread 0)
+            if constexpr (last) wgt = (q == 0 && k1b == 0 && pos0 == 0) ? 1.0 : 0.5 * j;
+            acc[q] = make_double2(fma(wgt, v[q].x, -acc[q].y), fma(wgt, v[q].y, acc[q].x));
+        }
+    };
+    const int pend = plo > 0 ? plo : 1;
+    int p = P - 1;
+    double2* TA = nu_s;
+    double2* TB = nu_s + N;
+    if (p >= pend && ((p - pend + 1) & 1)) {
+        moment(std::false_type(), p, xa, xb, TA);
+        --p;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) xa[q] = xb[q];
+        double2* tt = TA;
+        TA = TB;
+        TB = tt;
+    }
+    for (; p >= pend; p -= 2) {
+        moment(std::false_type(), p, xa, xb, TA);
+        moment(std::false_type(), p - 1, xb, xa, TB);
+    }
+    if (plo == 0) moment(std::true_type(), 0, xa, xb, TA);
+    const int rl = plo & 3;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const double2 a = acc[q];
+        acc[q] = rl == 0 ? a : rl == 1 ? make_double2(-a.y, a.x) : rl == 2 ? make_double2(-a.x, -a.y)
+                                                                : make_double2(a.y, -a.x);
+    }
+    nu_rows_epilogue<TPB, 8>(acc, k1b, ln1, nfft, jhi, h, tbase, r, nf, nbt, CS, F, nu_s, pos0);
 }
 
 // (C_k, S_k) of the trials of one harmonic: position pos = k1 n2 + k2 of the FFT output holds J = k1 + n1 k2
@@ -1949,6 +2071,10 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
     const char* r2k_env = getenv("CRIMP_NUFFT_ROW2048");
     const bool row2048 = r2k_env && !strcmp(r2k_env, "1") && rows4096 && rows_r8 && fused_combine;
     auto row_log = [&](int lnfft) { return row2048 && lnfft == 20 ? 11 : std::min(lnfft, 12); };
+    // 4096-element rows by k_nu_rows_iw (one cross-wave exchange per moment; 0.171 vs 0.180 ms per config-3 search,
+    // profiles/r06/ab_p2_iw.log); CRIMP_NUFFT_P2_IW=0: k_nu_rows_combine8<12> (three block-wide exchanges)
+    const char* iw_env = getenv("CRIMP_NUFFT_P2_IW");
+    const bool p2_iw = !(iw_env && !strcmp(iw_env, "0"));
     {  // 128 KB of dynamic LDS for k_nu_rows4096_combine, set once per device
         static std::mutex mu;
         static uint64_t done = 0;
@@ -1960,6 +2086,8 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
                                        hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kNuTile * (int)sizeof(double2)));
             HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_nu_rows_combine8<12>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)nu_rows_lds(12)));
+            HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_nu_rows_iw),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kNuTile * (int)sizeof(double2)));
             HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_nu_rows_combine8<11>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)nu_rows_lds(11)));
             if (dev < 64) done |= uint64_t(1) << dev;
@@ -2129,7 +2257,11 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
                     g_nu_work[kNuClsPass2] += cplane + (F.on ? (16.0 * (nharm - 1) + 8.0) * (double)nbt
                                                              : 16.0 * (double)nbt * (phi < P ? 2.0 : 1.0));
                     const dim3 g2((unsigned)(int64_t(1) << ln1), (unsigned)nrow);
-                    if (ln2 == 11)
+                    if (ln2 == 12 && p2_iw)
+                        k_nu_rows_iw<<<g2, 512, 2 * lds_fft, s>>>(
+                            Zo, lnfft, phi, plo, phi < P ? 1 : 0, nrow, nf, pl.nseg - 1 - pl.h, pl.h,
+                            rb * nf + jbase - (tb0 + first), nbt, bc, CS + (int64_t)(k - 1) * nbt, F);
+                    else if (ln2 == 11)
                         k_nu_rows_combine8<11><<<g2, 256, nu_rows_lds(11), s>>>(
                             Zo, lnfft, phi, plo, phi < P ? 1 : 0, nrow, nf, pl.nseg - 1 - pl.h, pl.h,
                             rb * nf + jbase - (tb0 + first), nbt, bc, CS + (int64_t)(k - 1) * nbt, F);

@@ -209,8 +209,8 @@ def test_nufft_declines_cells_beyond_32_bits(gpu):
 def test_nufft_fused_pass2_equals_separate_combine(gpu, monkeypatch):
     """FFT pass 2 fused with the moments' Horner sum against pass 2 and k_nu_combine as two kernels
     (CRIMP_NUFFT_FUSED=0), both with the radix-16 row transform (CRIMP_NUFFT_R8=0): the same arithmetic, so
-    bit-identical powers; the default (512-thread radix-8 row pass) and the 4096-row / 256-row-column kernels
-    (k_nu_rows4096_combine, k_nu_rows_combine8, k_nu_cols256; k_nu_cols512 with 2048-element rows at n = 2^20) against
+    bit-identical powers; the default (512-thread radix-8 row pass, k_nu_rows_iw) and the 4096-row / 256-row-column
+    kernels (k_nu_rows4096_combine, k_nu_rows_combine8, k_nu_cols256; k_nu_cols512 with 2048-element rows at n = 2^20) against
     the generic ones (CRIMP_NUFFT_ROWS4096=0) to rounding -- single-pass (n <= 4096) and four-step FFTs, 1-D and 2-D
     grids."""
     from crimp_amd import ops, _native as N
@@ -239,6 +239,7 @@ def test_nufft_fused_pass2_equals_separate_combine(gpu, monkeypatch):
         generic = run(CRIMP_NUFFT_ROWS4096="0")
         close(r16, generic)
         close(run(), generic)
+        close(run(CRIMP_NUFFT_P2_IW="0"), generic)  # three block-wide exchanges per moment (k_nu_rows_combine8<12>)
         if len(f) == 600000:  # n = 2^20 as 512 x 2048 (k_nu_cols512, k_nu_rows_combine8<11>)
             close(run(CRIMP_NUFFT_ROW2048="1"), generic)
 
