@@ -54,7 +54,7 @@ PMC_FILE = os.path.join(ROOT, "profiles", "r04", "pmc_traffic.json")
 PMC_NUFFT_FILE = os.path.join(ROOT, "profiles", "r06", "pmc_nufft_traffic.json")
 # the kernel behind each NUFFT class on the config-3 plan (cell gather, n1 = 256 columns, 4096-element rows)
 NUFFT_CLASS_KERNEL = {"cellstart": "k_nu_cellstart", "spread": "k_nu_gather", "pass1": "k_nu_cols256",
-                      "pass2": "k_nu_rows_combine8", "finalize": "k_nu_finalize"}
+                      "pass2": "k_nu_rows_iw", "finalize": "k_nu_finalize"}
 
 
 def parse():

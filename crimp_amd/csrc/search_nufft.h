@@ -421,24 +421,28 @@ __global__ __launch_bounds__(256) void k_nu_cellstart(const double* __restrict__
             // a wave that holds a pair out of order writes nothing for its photons (a vote, no block barrier: the
             // barrier cost a quarter of the pass; mode 2, A/B: the lanes' own pairs only)
             if (mode == 2 ? ooo : __any(ooo)) continue;
+            // per harmonic the cells of the predecessor and of the pair's two photons, each formed once (the second
+            // photon's range starts at the first one's cell); cells fit 32 bits (nu_plan checks |G| + n < 2^31): one
+            // v_cvt_i32_f64 each, and 32-bit bounds
+            const double up = dp0 * s1, u0 = d0 * s1, u1 = d1 * s1;
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int64_t i = i0 + h;
-                if (i >= n) break;
-                const double u = (h == 0 ? d0 : d1) * s1;
-                const double up = (h == 0 ? dp0 : d0) * s1;
-#pragma unroll
-                for (int j = 0; j < kNuCellK; ++j) {
-                    if (j >= nk) break;
-                    const double kd = (double)(k0 + j);
-                    // cells fit 32 bits (nu_plan checks |G| + n < 2^31): one v_cvt_i32_f64, not the int64 one
-                    const int64_t g = (int)rint(kd * u);
-                    const int64_t gp = i == 0 ? a.gmin[j] - 1 : (int)rint(kd * up);
-                    int64_t* st = start + a.off[j];
-                    const int64_t lo = gp + 1 > a.gmin[j] ? gp + 1 : a.gmin[j];
-                    const int64_t hi = g < a.gmin[j] + a.span[j] - 1 ? g : a.gmin[j] + a.span[j] - 1;
-                    for (int64_t G = lo; G <= hi; ++G) st[G - a.gmin[j]] = i;
-                    if (i == n - 1) st[a.span[j]] = n;
+            for (int j = 0; j < kNuCellK; ++j) {
+                if (j >= nk) break;
+                const double kd = (double)(k0 + j);
+                const int gm = (int)a.gmin[j], gl = (int)(a.gmin[j] + a.span[j] - 1);
+                int64_t* st = start + a.off[j];
+                const int gA = i0 == 0 ? gm - 1 : (int)rint(kd * up);
+                const int gB = (int)rint(kd * u0);
+                if (v0) {  // photon i0 starts the cells (gA, gB]
+                    const int lo = gA + 1 > gm ? gA + 1 : gm, hi = gB < gl ? gB : gl;
+                    for (int G = lo; G <= hi; ++G) st[G - gm] = i0;
+                    if (i0 == n - 1) st[a.span[j]] = n;
+                }
+                if (v1) {  // photon i0 + 1 the cells (gB, gC]
+                    const int gC = (int)rint(kd * u1);
+                    const int lo = gB + 1 > gm ? gB + 1 : gm, hi = gC < gl ? gC : gl;
+                    for (int G = lo; G <= hi; ++G) st[G - gm] = i0 + 1;
+                    if (i0 + 1 == n - 1) st[a.span[j]] = n;
                 }
             }
         }
