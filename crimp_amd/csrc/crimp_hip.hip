@@ -2116,7 +2116,7 @@ static int search_impl(const double* t, int64_t n, double t0, const double* freq
         NuSpecKey key{};
         bool spec_mismatch = false;
         if (nu_try && !f64) {
-            key = nu_spec_key(dtm, n, t0, dfr, nf, twod ? nfd : 0, nharm, first, count, gather_form);
+            key = nu_spec_key(dtm, n, t0, dfr, nf, twod ? nfd : 0, nharm, stat, first, count, gather_form);
             NuExpect ex{};
             if (nu_spec_find(key, nu_hs)) {
                 for (int q = 0; q < 4; ++q) ex.v[q] = nu_hs[q];

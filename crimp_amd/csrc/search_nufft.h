@@ -43,6 +43,11 @@ constexpr int kNuMergeG = 16;      // wrapped cells per merge block
 constexpr int kNuMaxWrap = 32;     // unwrapped cells per wrapped cell (span of the photons over n)
 constexpr int kNuTile = 4096;      // complex elements per FFT block (64 KB of LDS), 16 per thread
 constexpr double kNuEps = 5e-14;   // truncation bound per photon at the grid's edge (below the rounding term kNuRho)
+// Z^2_m with m >= 2: 5e-13. The certificate flags a trial when its power's bound exceeds 1e-6 of the power, and Z^2_m's
+// bound over its power is sum_k (2 |A_k| E + E^2) / sum_k |A_k|^2 -- at E = N (5e-13 + kNuRho) only trials whose every
+// |A_k| is below ~2e-5 N are flagged (none at config 3, P 15 -> 14). Z^2_1 and H keep kNuEps: H = max_m (Z^2_m - 4m + 4)
+// cancels to near 0 on noise, where a larger E flags many more trials for the fp64 fix-up (config 4: 55 at kNuEps).
+constexpr double kNuEpsZm = 5e-13;
 // Rounding bound per photon for the certificate, in units of |A_k|'s scale N: c_i (cis table + fp64 polynomial,
 // angle-addition over <= 8 harmonics: ~20 ulp), the MFMA's fp64 accumulation over <= 256 K-groups per cell run
 // (<= 256 ulp of the run's sum of |terms|, each <= 1), the merge, the FFT (~3 log2 n ulp) and Horner (e^x ulp):
@@ -1762,7 +1767,9 @@ static void launch_gather_r(int64_t blocks, const double* tt, double t0, const i
     const dim3 grid((unsigned)blocks);
 #define NU_GATHER(PPP) \
     k_nu_gather<R, TWOD, PPP><<<grid, 256, 0, s>>>(tt, t0, start, nfft, s1, fch, fcl, c2, nrow, P, S, bad, tab, W)
-    if (P <= 15) {
+    if (P <= 14) {  // Z^2_m (m >= 2) at config-3-like grids (kNuEpsZm)
+        NU_GATHER(14);
+    } else if (P <= 15) {
         NU_GATHER(15);
     } else if (P <= 16) {
         NU_GATHER(16);
@@ -1829,7 +1836,8 @@ struct NuPlan {
 // n and P: among the powers of two n >= nseg (up to 2^24) whose edge truncation (nu_trunc) <= kNuEps within P <= pmax
 // moments, the one with the least FFT work n P; false when none exists or the photons wrap the grid more than
 // kNuMaxWrap times
-static bool nu_plan(NuPlan* pl, double delta, double f0, double dt0, double dtn, int nharm, int64_t nchunk, int pmax) {
+static bool nu_plan(NuPlan* pl, double delta, double f0, double dt0, double dtn, int nharm, int64_t nchunk, int pmax,
+                    double eps) {
     // an ascending progression only: with delta < 0 the cells of the later photons come first (s1 < 0) and every
     // table below would be sized negative (a descending grid takes the exact rule)
     if (!(delta > 0.0) || !std::isfinite(delta) || !std::isfinite(f0)) return false;
@@ -1840,7 +1848,7 @@ static bool nu_plan(NuPlan* pl, double delta, double f0, double dt0, double dtn,
     for (int l = std::max(ilog2(pl->nseg), 6); l <= 24; ++l) {
         const double x = M_PI * (double)std::max<int64_t>(h, pl->nseg - 1 - h) / (double)(int64_t(1) << l);
         int p = 1;
-        while (p <= pmax && nu_trunc(x, p, &invfact) > kNuEps) ++p;
+        while (p <= pmax && nu_trunc(x, p, &invfact) > eps) ++p;
         if (p > pmax) continue;
         if (lnfft == 0 || ((int64_t)p << l) < ((int64_t)P << lnfft)) {
             lnfft = l;
@@ -1907,10 +1915,11 @@ struct NuSpecKey {
     const void* f;
     int64_t n, nf, nfd, first, count;
     double t0;
-    int nharm, dev, gather;
+    int nharm, stat, dev, gather;
     bool operator==(const NuSpecKey& o) const {
         return t == o.t && f == o.f && n == o.n && nf == o.nf && nfd == o.nfd && first == o.first &&
-               count == o.count && t0 == o.t0 && nharm == o.nharm && dev == o.dev && gather == o.gather;
+               count == o.count && t0 == o.t0 && nharm == o.nharm && stat == o.stat && dev == o.dev &&
+               gather == o.gather;
     }
 };
 struct NuSpecEntry {
@@ -1923,8 +1932,9 @@ static bool nu_spec_disabled() {  // CRIMP_NUFFT_PLAN_CACHE=0: every search read
     return e && !strcmp(e, "0");
 }
 static NuSpecKey nu_spec_key(const double* t, int64_t n, double t0, const double* f, int64_t nf, int64_t nfd,
-                             int nharm, int64_t first, int64_t count, bool gather) {
+                             int nharm, int stat, int64_t first, int64_t count, bool gather) {
     NuSpecKey k{};
+    k.stat = stat;
     k.t = t;
     k.f = f;
     k.n = n;
@@ -1995,7 +2005,8 @@ static int nufft_search(Scratch& sc, hipStream_t s, const double* t, double t0, 
         pl.r1 = r1;
         pl.j0 = a;
         pl.nseg = b - a;
-        if (pl.nseg < 64 || !nu_plan(&pl, delta, f0, dt0, dtn, nharm + 1, nchunk, gather_grid ? kNuGatherMaxP : kNuMaxP))
+        if (pl.nseg < 64 || !nu_plan(&pl, delta, f0, dt0, dtn, nharm + 1, nchunk, gather_grid ? kNuGatherMaxP : kNuMaxP,
+                                     stat == 0 && nharm >= 2 ? kNuEpsZm : kNuEps))
             return CRIMP_OK;
         plans.push_back(std::move(pl));
         r = r1;
