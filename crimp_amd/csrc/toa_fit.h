@@ -90,6 +90,24 @@ enum : int { kHNone = 0, kHStore = 1, kHLoad = 2 };
 #define CRIMP_FIT_PROD 8
 #endif
 constexpr int kFitProd = CRIMP_FIT_PROD;  // model values per fp64 log in fit_eval
+// 16 model values per log where that provably stays in the fp64 range: a compile-time Fourier template, whose template
+// part |h| <= sum_j |amp_j| = H, at a pass norm n with n - H >= 2^-60 and n + H <= 2^60 -- a product of 16 model
+// values n + h then lies in [2^-960, 2^960] (2.82 -> 2.70 ms per 1250 config-5 fits, profiles/r06/ab_toa_prod16.log);
+// kFitProd elsewhere. Chosen per pass from (n, template) alone, so a record does not depend on its batch.
+// CRIMP_FIT_PROD16=0: kFitProd everywhere.
+#ifndef CRIMP_FIT_PROD16
+#define CRIMP_FIT_PROD16 1
+#endif
+template <int MODEL, int KF>
+__device__ __forceinline__ int fit_prodlen(const TplDev* __restrict__ T, double n) {
+    if constexpr (CRIMP_FIT_PROD16 && MODEL == CRIMP_MODEL_FOURIER && KF > 0) {
+        double H = 0.0;
+#pragma unroll
+        for (int j = 0; j < KF; ++j) H += fabs(T->amp[j]);
+        if (n - H >= 0x1p-60 && n + H <= 0x1p60) return 16;
+    }
+    return kFitProd;
+}
 // the photon loops load the next photon's time (or cached template part) one iteration ahead, so the load's
 // latency overlaps the current photon's arithmetic (CRIMP_FIT_PREFETCH=0: load at the top of each iteration)
 #ifndef CRIMP_FIT_PREFETCH
@@ -101,10 +119,10 @@ constexpr bool kFitPrefetch = CRIMP_FIT_PREFETCH != 0;
 // Hessian at (n, phi), from one pass over photons x[a, b) (as toafit.ToAFitter.evaluate assembles them).
 // kHStore and kHLoad passes return the LL and the norm derivatives only (gp, hnp, hpp are 0). MODEL and (Fourier) the template
 // size KF are compile-time (KF = 0: K from the template at run time), as in k_toa_grid.
-template <int MODEL, int KF>
-__device__ FitEval fit_eval(const double* __restrict__ x, int64_t a, int64_t b, const TplDev* __restrict__ T, double n,
-                            double phi, double E, const FitCfg& C, FitShared& sh, double* __restrict__ hc = nullptr,
-                            int hmode = kHNone) {
+template <int MODEL, int KF, int PL>  // PL: model values per log (fit_prodlen)
+__device__ FitEval fit_eval_pl(const double* __restrict__ x, int64_t a, int64_t b, const TplDev* __restrict__ T,
+                               double n, double phi, double E, const FitCfg& C, FitShared& sh, double* __restrict__ hc,
+                               int hmode) {
     const int tid = threadIdx.x;
     constexpr int model = MODEL;
     const int K = KF > 0 ? KF : T->K;
@@ -120,7 +138,7 @@ __device__ FitEval fit_eval(const double* __restrict__ x, int64_t a, int64_t b, 
     int np = 0;
     auto lnacc = [&](double mv) {
         pr *= mv;
-        if (++np == kFitProd) {
+        if (++np == PL) {
             acc[0] += log(pr);
             pr = 1.0;
             np = 0;
@@ -228,6 +246,13 @@ __device__ FitEval fit_eval(const double* __restrict__ x, int64_t a, int64_t b, 
     r.hnp = S[4];
     r.hpp = S[5];
     return r;
+}
+template <int MODEL, int KF>
+__device__ FitEval fit_eval(const double* __restrict__ x, int64_t a, int64_t b, const TplDev* __restrict__ T, double n,
+                            double phi, double E, const FitCfg& C, FitShared& sh, double* __restrict__ hc = nullptr,
+                            int hmode = kHNone) {
+    if (fit_prodlen<MODEL, KF>(T, n) == 16) return fit_eval_pl<MODEL, KF, 16>(x, a, b, T, n, phi, E, C, sh, hc, hmode);
+    return fit_eval_pl<MODEL, KF, kFitProd>(x, a, b, T, n, phi, E, C, sh, hc, hmode);
 }
 
 // toafit._newton_step: Levenberg-shifted Newton direction with a trust region (0.05 rad, half the norm). Projected:
@@ -338,9 +363,9 @@ struct FitMom {
     double s[6];  // S_0 .. S_5
     double mn;
 };
-template <int MODEL, int KF>
-__device__ FitMom fit_moments(const double* __restrict__ x, int64_t a, int64_t b, const TplDev* __restrict__ T,
-                              double n, double phi, FitShared& sh) {
+template <int MODEL, int KF, int PL>
+__device__ FitMom fit_moments_pl(const double* __restrict__ x, int64_t a, int64_t b, const TplDev* __restrict__ T,
+                                 double n, double phi, FitShared& sh) {
     const int tid = threadIdx.x;
     constexpr int model = MODEL;
     const int K = KF > 0 ? KF : T->K;
@@ -374,7 +399,7 @@ __device__ FitMom fit_moments(const double* __restrict__ x, int64_t a, int64_t b
         const double mv = n + h;
         const double q = lk_rcp(mv);
         pr *= mv;
-        if (++np == kFitProd) {
+        if (++np == PL) {
             acc[0] += log(pr);
             pr = 1.0;
             np = 0;
@@ -405,6 +430,12 @@ __device__ FitMom fit_moments(const double* __restrict__ x, int64_t a, int64_t b
         if (q < 6) r.s[q] = v; else r.mn = v;
     }
     return r;
+}
+template <int MODEL, int KF>
+__device__ FitMom fit_moments(const double* __restrict__ x, int64_t a, int64_t b, const TplDev* __restrict__ T,
+                              double n, double phi, FitShared& sh) {
+    if (fit_prodlen<MODEL, KF>(T, n) == 16) return fit_moments_pl<MODEL, KF, 16>(x, a, b, T, n, phi, sh);
+    return fit_moments_pl<MODEL, KF, kFitProd>(x, a, b, T, n, phi, sh);
 }
 
 // the profile optimum and LL from one phShift's moments (fit_profile_mom); false where the series does not apply
@@ -453,10 +484,10 @@ __device__ double fit_profile_mom(const double* __restrict__ x, int64_t a, int64
 // Two phShifts' moments in one pass (the 1-sigma scan's step k on both sides, Fourier templates of compile-time
 // size): the photon's sin/cos and harmonic recurrence are formed once, and each phShift's sums repeat
 // fit_moments' per-photon operations, striding and reduction order, so they equal two fit_moments passes.
-template <int KF>
-__device__ __noinline__ void fit_moments2(const double* __restrict__ x, int64_t a, int64_t b,
-                                          const TplDev* __restrict__ T, double n, double phi0, double phi1,
-                                          FitShared& sh, FitMom& m0, FitMom& m1) {
+template <int KF, int PL>
+__device__ __noinline__ void fit_moments2_pl(const double* __restrict__ x, int64_t a, int64_t b,
+                                             const TplDev* __restrict__ T, double n, double phi0, double phi1,
+                                             FitShared& sh, FitMom& m0, FitMom& m1) {
     static_assert(KF > 0, "compile-time template size");
     const int tid = threadIdx.x;
     __syncthreads();  // the previous evaluation's readers are done with sh
@@ -502,7 +533,7 @@ __device__ __noinline__ void fit_moments2(const double* __restrict__ x, int64_t 
         const double q0 = lk_rcp(mv0), q1 = lk_rcp(mv1);
         pr0 *= mv0;
         pr1 *= mv1;
-        if (++np == kFitProd) {
+        if (++np == PL) {
             acc0[0] += log(pr0);
             acc1[0] += log(pr1);
             pr0 = 1.0;
@@ -558,6 +589,15 @@ __device__ __noinline__ void fit_moments2(const double* __restrict__ x, int64_t 
             m1.mn = v1;
         }
     }
+}
+template <int KF>
+__device__ __forceinline__ void fit_moments2(const double* __restrict__ x, int64_t a, int64_t b,
+                                             const TplDev* __restrict__ T, double n, double phi0, double phi1,
+                                             FitShared& sh, FitMom& m0, FitMom& m1) {
+    if (fit_prodlen<CRIMP_MODEL_FOURIER, KF>(T, n) == 16)
+        fit_moments2_pl<KF, 16>(x, a, b, T, n, phi0, phi1, sh, m0, m1);
+    else
+        fit_moments2_pl<KF, kFitProd>(x, a, b, T, n, phi0, phi1, sh, m0, m1);
 }
 
 // ---------------------------------------------------------------- varyAmps (measureToAs.py:305-312)
