@@ -648,18 +648,22 @@ __device__ __forceinline__ void tpl_terms(const TplDev* __restrict__ T, int mode
 template <int KF>
 __device__ __forceinline__ void tpl_terms_fourier(const double (&al)[KF], const double (&be)[KF], double s1, double c1,
                                                   double& h, double& h1, double& h2) {
-    h = 0.0;
-    h1 = 0.0;
-    h2 = 0.0;
+    // harmonic 1 starts the sums (not 0 + term: three adds per photon fewer, the same values up to the sign of zero)
     const double tc = c1 + c1;
     double cj = c1, sj = s1, cp = 1.0, sp = 0.0;
 #pragma unroll
     for (int j = 0; j < KF; ++j) {
         const double tj = fma(al[j], cj, be[j] * sj);
         const double jj = (double)(j + 1);
-        h += tj;
-        h2 = fma(-(jj * jj), tj, h2);
-        h1 = fma(jj, fma(al[j], sj, -(be[j] * cj)), h1);
+        if (j == 0) {
+            h = tj;
+            h2 = -tj;
+            h1 = fma(al[0], sj, -(be[0] * cj));
+        } else {
+            h += tj;
+            h2 = fma(-(jj * jj), tj, h2);
+            h1 = fma(jj, fma(al[j], sj, -(be[j] * cj)), h1);
+        }
         if (j + 1 < KF) {
             const double cn = fma(tc, cj, -cp), sn = fma(tc, sj, -sp);
             cp = cj;
@@ -674,12 +678,12 @@ __device__ __forceinline__ void tpl_terms_fourier(const double (&al)[KF], const 
 template <int KF>
 __device__ __forceinline__ void tpl_value_fourier(const double (&al)[KF], const double (&be)[KF], double s1, double c1,
                                                   double& h) {
-    h = 0.0;
     const double tc = c1 + c1;
     double cj = c1, sj = s1, cp = 1.0, sp = 0.0;
 #pragma unroll
     for (int j = 0; j < KF; ++j) {
-        h += fma(al[j], cj, be[j] * sj);
+        const double tj = fma(al[j], cj, be[j] * sj);
+        h = j == 0 ? tj : h + tj;
         if (j + 1 < KF) {
             const double cn = fma(tc, cj, -cp), sn = fma(tc, sj, -sp);
             cp = cj;

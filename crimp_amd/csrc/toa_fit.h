@@ -518,8 +518,9 @@ __device__ __noinline__ void fit_moments2_pl(const double* __restrict__ x, int64
             double cj = c1, sj = s1, cp = 1.0, sp = 0.0;
 #pragma unroll
             for (int j = 0; j < KF; ++j) {
-                h0 += fma(al0[j], cj, be0[j] * sj);
-                h1 += fma(al1[j], cj, be1[j] * sj);
+                const double t0j = fma(al0[j], cj, be0[j] * sj), t1j = fma(al1[j], cj, be1[j] * sj);
+                h0 = j == 0 ? t0j : h0 + t0j;
+                h1 = j == 0 ? t1j : h1 + t1j;
                 if (j + 1 < KF) {
                     const double cn = fma(tc, cj, -cp), sn = fma(tc, sj, -sp);
                     cp = cj;
