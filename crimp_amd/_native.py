@@ -215,13 +215,18 @@ class Buffers:
     def stream(self):
         if self.device:
             import torch
+            raw = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+            if raw is not None and self.tdev.index is not None:  # the handle itself, no Stream object (~2 us less)
+                return ctypes.c_void_p(raw(self.tdev.index))
             return ctypes.c_void_p(torch.cuda.current_stream(self.tdev).cuda_stream)
         return None
 
     def device_guard(self):
         """Context making the tensors' GPU the current HIP device for the native call (the library allocates its
-        scratch and launches on the current device)."""
+        scratch and launches on the current device); nothing to switch when it already is."""
         if self.device and self.tdev is not None:
             import torch
+            if self.tdev.index is not None and torch.cuda.current_device() == self.tdev.index:
+                return contextlib.nullcontext()
             return torch.cuda.device(self.tdev)
         return contextlib.nullcontext()

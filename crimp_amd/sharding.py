@@ -95,6 +95,8 @@ def sharded_search(time, freq, nharm=2, stat=0, freq_dot=None, gather="all", com
         rank_best = (bv_, bi_)
     else:
         local = compute(time, t0, freq, nharm, stat, freq_dot, first, count)
+    if rank_best is not None and dist is None:  # one process: the call's own best is the answer
+        return rank_best[0], rank_best[1] + first
     dev = _device_for_backend(dist) if dist is not None else (
         local.device if isinstance(local, torch.Tensor) else torch.device("cpu"))
     loc = _as_comm(local, dev)
